@@ -1,0 +1,44 @@
+# Builds the product library udpdk_amd/libudpdk_amd.so (HIP kernels for gfx950 + C-ABI host code
+# + the C udpdk_api.h host layer) and the test-only oracle (oracle/liboracle.so).
+HIPCC     ?= /opt/rocm/bin/hipcc
+CC        ?= gcc
+ARCH      ?= gfx950
+HIPFLAGS  ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Werror -Wno-unused-result
+CFLAGS_H  ?= -O2 -std=gnu11 -fPIC -Wall -Wextra -Werror
+INC       := -Iinclude -Iudpdk_amd/csrc
+LIB       := udpdk_amd/libudpdk_amd.so
+OBJDIR    := build/obj
+
+HIP_SRC   := udpdk_amd/csrc/rx_kernels.hip udpdk_amd/csrc/tx_kernels.hip udpdk_amd/csrc/udpdk_gpu.hip
+C_SRC     := $(wildcard udpdk_amd/csrc/host/*.c)
+HIP_OBJ   := $(patsubst udpdk_amd/csrc/%.hip,$(OBJDIR)/%.o,$(HIP_SRC))
+C_OBJ     := $(patsubst udpdk_amd/csrc/host/%.c,$(OBJDIR)/host/%.o,$(C_SRC))
+HDRS      := include/udpdk_gpu.h include/udpdk_api.h udpdk_amd/csrc/rx_common.h \
+             $(wildcard udpdk_amd/csrc/host/*.h)
+
+all: $(LIB) oracle
+
+$(OBJDIR)/%.o: udpdk_amd/csrc/%.hip $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) $(INC) -c $< -o $@
+
+$(OBJDIR)/host/%.o: udpdk_amd/csrc/host/%.c $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS_H) $(INC) -c $< -o $@
+
+$(LIB): $(HIP_OBJ) $(C_OBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -Wl,--no-undefined -Wl,-soname,libudpdk_amd.so
+
+oracle:
+	$(MAKE) -C oracle
+
+asm: udpdk_amd/csrc/rx_kernels.hip $(HDRS)
+	@mkdir -p build/asm
+	$(HIPCC) $(HIPFLAGS) $(INC) -S --cuda-device-only -o build/asm/rx_kernels.s $<
+	$(HIPCC) $(HIPFLAGS) $(INC) -c -Rpass-analysis=kernel-resource-usage $< -o /dev/null 2> build/asm/rx_resource.txt || true
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean asm

@@ -1,0 +1,249 @@
+"""Benchmark: device-resident RX parse + checksum + port demux (BASELINE.json metric).
+
+A step = one udpdk_gpu_rx call (rx_classify + rx_scan + rx_scatter) over one batch of frames
+already resident in HBM. Default workload = BASELINE.json configs[1]: 1 M synthetic 64 B
+Eth/IPv4/UDP frames, 1 bound port, per GPU. With N GPUs (torchrun) every rank processes its own
+independent shard (seed 0x5EED ^ rank) with no data-path collective: weak scaling.
+
+To keep the 256 MiB Infinity Cache from serving the 64 B batch (≈80 MB) out of cache, the timed
+loop rotates over enough device copies of the batch that a copy is evicted before its reuse
+(> 512 MiB in flight), so every step reads its frames from HBM.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from udpdk_amd import abi, frames as F  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak, MI355X_MICROARCH.md chip table
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--config", type=int, default=2, help="BASELINE.json config number (2..5)")
+    p.add_argument("--frames", type=int, default=None, help="override frames per GPU")
+    p.add_argument("--rotate-mib", type=int, default=640, help="device bytes cycled by the loop")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extra", action="store_true", help="skip the 1500 B / IMIX side lines")
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU time per baseline leg")
+    return p.parse_args()
+
+
+class Rx:
+    """Device-resident copies of one batch plus prebuilt ctypes argument blocks."""
+
+    def __init__(self, ctx: abi.GpuContext, w: F.Workload, rotate_bytes: int):
+        b = w.batch
+        self.ctx, self.w = ctx, w
+        self.n = b.n
+        self.sum_len = int(b.length.astype(np.int64).sum())
+        per_copy = b.frames.nbytes + 10 * b.n
+        self.copies = max(1, math.ceil(rotate_bytes / per_copy)) if rotate_bytes else 1
+        hs = abi.snapshot_from_lists(w.port_lists(), w.n_sockets)
+        ctx.upload_snapshot(hs)
+        self._hs = hs
+        self.args = []
+        for _ in range(self.copies):
+            db = abi.rx_upload(ctx, b.frames, b.offset, b.length)
+            db.frames_bytes = b.frames_bytes
+            out = abi.rx_alloc_out(ctx, b.n, w.n_sockets, b.n)
+            bt = abi.RxBatch(db.frames.ptr, db.frames_bytes, db.offset.ptr, db.length.ptr, None, b.n)
+            ot = abi.RxOut(out.meta.ptr, out.lane_off.ptr, out.lane_pkt.ptr, out.lane_cap)
+            self.args.append((C.byref(bt), C.byref(ot), bt, ot, db, out))
+        self.f = abi.lib().udpdk_gpu_rx
+        self.h = ctx.handle
+
+    def step(self, i: int):
+        a = self.args[i % self.copies]
+        rc = self.f(self.h, a[0], a[1])
+        if rc:
+            raise abi.UdpdkError(f"udpdk_gpu_rx rc={rc}")
+
+    def check(self):
+        rc, st = abi.rx_stats(self.ctx)
+        if rc != 0 or st.counters[abi.V_DELIVERED] != self.n:
+            raise abi.UdpdkError(f"bench batch not fully delivered: rc={rc} "
+                                 f"delivered={st.counters[abi.V_DELIVERED]} n={self.n}")
+        return st
+
+    def classify_bytes(self) -> int:
+        # rx_classify algorithmic bytes per launch: every frame byte + u32 offset + u16 length
+        # read, u32 verdict written, + the tile histogram column (lanes x tiles x 4 B)
+        t, k = abi.geometry(self.n, self.w.n_sockets)
+        return self.sum_len + 6 * self.n + 4 * self.n + 4 * self.w.n_sockets * k
+
+    def pipeline_bytes(self) -> int:
+        # sum(frame_len) + 8 N (descriptor) + 4 N (verdict) + 4 D (lane entry)
+        return self.sum_len + 8 * self.n + 4 * self.n + 4 * self.n + 4 * (self.w.n_sockets + 1)
+
+
+def time_loop(rx: Rx, steps: int, warmup: int, barrier, timing: bool):
+    ctx = rx.ctx
+    for i in range(warmup):
+        rx.step(i)
+    rx.check()
+    ctx.timing(timing)
+    ctx.timing_read()                    # reset accumulators
+    barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        rx.step(warmup + i)
+    ctx.sync()
+    t1 = time.perf_counter()
+    barrier()
+    st = rx.check()
+    ms, n = ctx.timing_read() if timing else ([0.0] * 4, [0] * 4)
+    ctx.timing(False)
+    return (t1 - t0), ms, n, st
+
+
+def cpu_baseline(w: F.Workload, target_s: float):
+    """Oracle (the C restatement, kind "port") on the host cores: 1 thread and min(nproc, 16)
+    threads, one independent shard per pinned thread, with the RX checksum verification."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    b = w.batch
+    bt = O.bindtable_from_lists(w.port_lists())
+    res = {}
+    threads_all = max(1, min(os.cpu_count() or 1, 16))
+    for th in sorted({1, threads_all}):
+        for csum in (True, False):
+            # calibrate reps so each leg takes ~target_s
+            t1 = O.rx_parallel(bt, b.frames, b.frames_bytes, b.offset, b.length, w.n_sockets, csum, th, 1)
+            reps = max(1, int(target_s / max(t1, 1e-6)))
+            secs = O.rx_parallel(bt, b.frames, b.frames_bytes, b.offset, b.length, w.n_sockets, csum, th, reps)
+            res[(th, csum)] = (b.n * reps / secs / 1e6, reps, secs)
+    return res, threads_all
+
+
+def side_config(ctx, cfg: int, steps: int, rotate: int):
+    w = F.config_batch(cfg)
+    rx = Rx(ctx, w, rotate)
+    wall, ms, n, st = time_loop(rx, steps, 5, lambda: None, True)
+    out = {"workload": w.name, "mpkt_s": rx.n * steps / wall / 1e6,
+           "gbps_pipeline": rx.pipeline_bytes() * steps / wall / 1e9,
+           "classify_us": 1e3 * ms[0] / max(1, n[0]),
+           "classify_gbps": rx.classify_bytes() / (ms[0] / max(1, n[0]) / 1e3) / 1e9,
+           "frac_hbm_classify": rx.classify_bytes() / (ms[0] / max(1, n[0]) / 1e3) / 1e9 / HBM_PEAK_GBS,
+           "scan_us": 1e3 * ms[1] / max(1, n[1]), "scatter_us": 1e3 * ms[2] / max(1, n[2])}
+    for a in rx.args:
+        a[4].frames.free(); a[4].offset.free(); a[4].length.free()
+        a[5].meta.free(); a[5].lane_off.free(); a[5].lane_pkt.free()
+    return out
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    import torch
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    ndev = abi.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py needs a GPU (no HIP device visible)")
+    device = local % ndev
+    w = F.config_batch(args.config, n=args.frames, shard=rank)
+    ctx = abi.GpuContext(device, max_frames=max(w.batch.n, 1 << 20), max_lanes=max(w.n_sockets, 1))
+    rx = Rx(ctx, w, args.rotate_mib << 20)
+    wall, ms, n, st = time_loop(rx, args.steps, args.warmup, barrier, True)
+    if dist is not None:
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    total_pkts = rx.n * args.steps * world
+    mpkt_s = total_pkts / wall / 1e6
+    ms_step = 1e3 * wall / args.steps
+    cls_ms = ms[0] / max(1, n[0])
+    cls_bytes = rx.classify_bytes()
+    achieved = cls_bytes / (cls_ms / 1e3) / 1e9
+
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tf):
+        try:
+            with open(tf) as f:
+                traffic = json.load(f).get(w.name, {}).get("rx_classify_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    line = {
+        "metric": "device-resident Mpkt/s + GB/s, RX parse+cksum+port-demux, 64B & 1500B frames",
+        "value": round(mpkt_s, 2),
+        "unit": "Mpkt/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (SURVEY.md §8(d) recipe, seeded per rank)",
+        "config": {"workload": w.name, "baseline_config": args.config, "frames_per_gpu": rx.n,
+                   "frame_bytes_per_gpu": rx.sum_len, "bound_ports": w.n_sockets,
+                   "parallelism": f"shard{world}", "device_copies_rotated": rx.copies},
+        "gbps_pipeline": round(rx.pipeline_bytes() * args.steps * world / wall / 1e9, 1),
+        "kernel_us": {"rx_classify": round(1e3 * cls_ms, 3),
+                      "rx_scan": round(1e3 * ms[1] / max(1, n[1]), 3),
+                      "rx_scatter": round(1e3 * ms[2] / max(1, n[2]), 3)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel": "rx_classify",
+                     "algorithmic_bytes_per_launch": cls_bytes},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res, thr = cpu_baseline(F.config_batch(args.config, n=min(rx.n, 1 << 20)), args.cpu_seconds)
+        v, reps, secs = res[(thr, True)]
+        line["cpu_baseline"] = {
+            "value": round(v, 2), "unit": "Mpkt/s", "cores": thr, "kind": "port",
+            "sample": f"{min(rx.n, 1 << 20)} frames of {w.name} x {reps} passes, {thr} pinned "
+                      f"threads (one shard each), RX checksum verification on",
+            "one_thread": round(res[(1, True)][0], 2),
+            "one_thread_no_csum": round(res[(1, False)][0], 2),
+            f"{thr}_threads_no_csum": round(res[(thr, False)][0], 2),
+        }
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra = []
+        for cfg in (3, 4):
+            if cfg != args.config:
+                try:
+                    extra.append(side_config(ctx, cfg, max(10, args.steps // 4), args.rotate_mib << 20))
+                except Exception as e:   # a side line never hides the main measurement
+                    extra.append({"config": cfg, "error": repr(e)})
+        line["other_configs"] = extra
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,264 @@
+/*
+ * udpdk_gpu.h — C ABI of the MI355X (gfx950) batch datapath.
+ *
+ * This is the drop-in boundary for UDPDK's per-packet hot path. The reference has no plugin
+ * registry (udpdk/Makefile:72-81 localises every non-API symbol), so the replacement points are
+ * the two function bodies the hot path lives in:
+ *
+ *   RX  udpdk_poller.c:516-545 (burst loop) + :316-413 reassemble() + :274-298 enqueue/flush
+ *       -> udpdk_gpu_rx(): one launch sequence over N frames instead of N reassemble() calls,
+ *          producing a verdict word per frame and stable per-socket output lanes (the
+ *          equivalent of exch_slots[s].rx_buffer flushed into exch_slots[s].rx_q).
+ *   TX  udpdk_syscall.c:314-356 (udpdk_sendto header build + rte_ipv4_cksum)
+ *       -> udpdk_gpu_tx_build(): header build + IPv4 checksum + payload copy for N datagrams.
+ *
+ * The bind table walked by reassemble() (udpdk_bind_table.c:152 btable_get_bindings + the list
+ * iterator, list_iterator.c:19-55) is replaced by an immutable flattened snapshot uploaded with
+ * udpdk_gpu_bind_snapshot_upload(); the host bind table (see udpdk_api.h) builds it in list order.
+ *
+ * Conventions
+ *   - Plain C types only; no HIP/torch types cross the boundary. Streams are opaque (void*).
+ *   - Every entry point returns 0 on success or a negative errno (-EINVAL bad arguments,
+ *     -ENOMEM allocation failure, -ENOSPC output capacity exceeded, -EIO HIP failure; the HIP
+ *     error code of the last failure is kept in the context, see udpdk_gpu_last_hip_error()).
+ *     Nothing aborts. (Reference convention: API calls return -1 + errno, udpdk_syscall.c:23-520;
+ *     the datapath itself never reports errors, it logs and drops.)
+ *   - Ports and IPv4 addresses are "raw": the 2/4 wire bytes read as a little-endian host
+ *     integer, exactly how the reference compares and indexes them (udpdk_poller.c:372-373,
+ *     udpdk_bind_table.c:152, udpdk_syscall.c:230).
+ *   - Buffers named *_dev are device pointers (from udpdk_gpu_alloc or any hipMalloc on the
+ *     context's device); buffers named *_host are host pointers.
+ *   - Calls on one context are asynchronous on that context's stream unless stated otherwise.
+ *     One host thread per context; contexts on different devices are independent.
+ */
+#ifndef UDPDK_GPU_H
+#define UDPDK_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UDPDK_GPU_ABI_VERSION 1
+
+/* ---------------------------------------------------------------------------------------------
+ * Per-frame verdict word (one uint32 per frame, written by udpdk_gpu_rx)
+ *
+ *   bits  0..3   verdict (enum udpdk_verdict)
+ *   bit   4      IPv4 header checksum verifies (RFC 1071 over the fixed 20 B at frame offset 14)
+ *   bits  5..6   UDP checksum state (enum udpdk_udp_csum)
+ *   bit   7      UDP length bad: dgram_len < 8 or 34 + dgram_len > frame length
+ *   bit   8      IHL != 5 (the reference parses at fixed offsets regardless, poller.c:336,:372)
+ *   bits  9..15  number of deliveries (fan-out), saturating at 127
+ *   bits 16..31  sockfd of the first delivery (the original mbuf's socket; clones follow it)
+ * ------------------------------------------------------------------------------------------- */
+enum udpdk_verdict {
+    UDPDK_V_DELIVERED = 0, /* >= 1 socket matched (poller.c:391-403)                            */
+    UDPDK_V_NOT_IPV4  = 1, /* !RTE_ETH_IS_IPV4_HDR(ptype) (poller.c:334, :362-366)               */
+    UDPDK_V_FRAG      = 2, /* rte_ipv4_frag_pkt_is_fragmented (poller.c:338); host slow path      */
+    UDPDK_V_NOT_UDP   = 3, /* next_proto_id != 17 (poller.c:368-371)                             */
+    UDPDK_V_NO_BIND   = 4, /* empty bind list for the raw dst port (poller.c:376-380)            */
+    UDPDK_V_NO_MATCH  = 5, /* bind list present, no IP matched (poller.c:406-411)                */
+    UDPDK_V_TRUNC     = 6, /* IPv4 by ptype but shorter than the 42 B Eth/IPv4/UDP header
+                              (the reference would read past data_len; divergence)   */
+    UDPDK_V_BAD_DESC  = 7  /* offset + length beyond frames_bytes: nothing was read              */
+};
+#define UDPDK_N_VERDICTS 8
+
+enum udpdk_udp_csum {
+    UDPDK_UDP_CSUM_NONE = 0, /* dgram_cksum == 0 (RFC 768 "no checksum") or not a UDP verdict */
+    UDPDK_UDP_CSUM_OK   = 1,
+    UDPDK_UDP_CSUM_BAD  = 2
+};
+
+#define UDPDK_META_VERDICT(m)  ((unsigned)(m) & 0xFu)
+#define UDPDK_META_IP_OK(m)    (((unsigned)(m) >> 4) & 1u)
+#define UDPDK_META_UDP_CSUM(m) (((unsigned)(m) >> 5) & 3u)
+#define UDPDK_META_LEN_BAD(m)  (((unsigned)(m) >> 7) & 1u)
+#define UDPDK_META_IHL_NE5(m)  (((unsigned)(m) >> 8) & 1u)
+#define UDPDK_META_FANOUT(m)   (((unsigned)(m) >> 9) & 0x7Fu)
+#define UDPDK_META_SOCKFD(m)   ((unsigned)(m) >> 16)
+
+/* Counters reduced over a whole udpdk_gpu_rx call (replace the per-drop RTE_LOG WARNINGs,
+ * poller.c:363, :369, :378, :410). */
+enum udpdk_rx_counter {
+    UDPDK_C_VERDICT0   = 0,  /* 0..7: frames per verdict                                     */
+    UDPDK_C_DELIVERIES = 8,  /* total (frame, socket) deliveries = lane entries               */
+    UDPDK_C_IP_BAD     = 9,  /* IPv4-gated frames whose header checksum fails                 */
+    UDPDK_C_UDP_OK     = 10,
+    UDPDK_C_UDP_BAD    = 11,
+    UDPDK_C_UDP_NONE   = 12, /* UDP-verdict frames carrying dgram_cksum == 0                  */
+    UDPDK_C_LEN_BAD    = 13,
+    UDPDK_C_IHL_NE5    = 14,
+    UDPDK_C_BYTES      = 15, /* sum of frame lengths                                         */
+    UDPDK_N_COUNTERS   = 16
+};
+
+/* Limits of the GPU path. NUM_SOCKETS_MAX is 1024 in the reference (udpdk_constants.h:12); the
+ * lane count is widened here and bounded by the per-workgroup LDS histogram. */
+#define UDPDK_GPU_MAX_LANES        16384u
+#define UDPDK_GPU_MAX_BINDS        (1u << 20)
+#define UDPDK_GPU_MAX_PORT_BINDS   4095u
+#define UDPDK_UDP_PORTS            65536u     /* UDP_MAX_PORT, udpdk_constants.h:13 */
+
+/* ---------------------------------------------------------------------------------------------
+ * Context
+ * ------------------------------------------------------------------------------------------- */
+typedef struct udpdk_gpu_ctx udpdk_gpu_ctx;
+
+/* Create a context on `device` with its own stream and workspace sized for batches of up to
+ * max_frames frames and up to max_lanes per-socket lanes. Called from udpdk_init(). */
+int  udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes,
+                          udpdk_gpu_ctx **out);
+/* Synchronise and free everything. Called from udpdk_cleanup(). NULL is a no-op. */
+int  udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *ctx);
+int  udpdk_gpu_sync(udpdk_gpu_ctx *ctx);
+int  udpdk_gpu_last_hip_error(const udpdk_gpu_ctx *ctx);
+int  udpdk_gpu_device_count(int *count);
+int  udpdk_gpu_abi_version(void);
+/* The context's HIP stream (hipStream_t) as an opaque pointer. */
+void *udpdk_gpu_stream(udpdk_gpu_ctx *ctx);
+
+/* Device / pinned-host memory helpers on the context's device (so callers need no HIP). */
+int  udpdk_gpu_alloc(udpdk_gpu_ctx *ctx, size_t bytes, void **dev);
+int  udpdk_gpu_free(udpdk_gpu_ctx *ctx, void *dev);
+int  udpdk_gpu_host_alloc(udpdk_gpu_ctx *ctx, size_t bytes, void **host); /* pinned */
+int  udpdk_gpu_host_free(udpdk_gpu_ctx *ctx, void *host);
+int  udpdk_gpu_memset(udpdk_gpu_ctx *ctx, void *dev, int value, size_t bytes);       /* async */
+int  udpdk_gpu_h2d(udpdk_gpu_ctx *ctx, void *dev, const void *host, size_t bytes);   /* async */
+int  udpdk_gpu_d2h(udpdk_gpu_ctx *ctx, void *host, const void *dev, size_t bytes);   /* async */
+
+/* ---------------------------------------------------------------------------------------------
+ * Bind snapshot (replaces sock_bind_table[65536] of list<bind_info>, udpdk_bind_table.c:17-18,
+ * walked at poller.c:376-405). Bindings of one raw port are contiguous and in list order
+ * (head -> tail: ANY bindings lpush'ed, specific ones rpush'ed, udpdk_bind_table.c:119-124).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+    uint32_t ip;      /* raw IPv4 (bind_info.ip_addr.s_addr, udpdk_types.h:33); 0 = INADDR_ANY */
+    int32_t  sockfd;  /* bind_info.sockfd (udpdk_types.h:32), 0..65535                         */
+    uint32_t reuse;   /* bind_info.reuse_addr || bind_info.reuse_port (poller.c:396)            */
+} udpdk_binding_t;
+
+/* Socket slot state needed by TX header build (exch_slot_info, udpdk_types.h:40-47). */
+typedef struct {
+    uint32_t ip;       /* raw bound IPv4, 0 = ANY                                              */
+    uint32_t udp_port; /* raw bound UDP port (low 16 bits)                                     */
+    uint32_t bound;    /* slot did bind (explicitly or by sendto auto-bind)                    */
+} udpdk_slot_t;
+
+typedef struct {
+    const uint32_t        *port_first;  /* [65536] index of the port's first binding          */
+    const uint16_t        *port_count;  /* [65536] bindings on the port (0 = none)            */
+    const udpdk_binding_t *binds;       /* [n_binds]                                          */
+    uint32_t               n_binds;
+    uint32_t               n_lanes;     /* > max(sockfd & lane_mask) over all bindings        */
+    uint32_t               lane_mask;   /* 0xFFFFFFFF: lanes keyed by full sockfd;
+                                           0xFF: compat mode, the reference's (uint8_t) slot
+                                           index (poller.c:294, :393)           */
+    const udpdk_slot_t    *slots;       /* [n_slots] for TX, may be NULL                      */
+    uint32_t               n_slots;
+    uint64_t               version;     /* bumped by every bind/close on the host             */
+} udpdk_bind_snapshot_t;
+
+/* Upload (host arrays -> device, synchronous on the context stream). */
+int udpdk_gpu_bind_snapshot_upload(udpdk_gpu_ctx *ctx, const udpdk_bind_snapshot_t *snap);
+
+/* ---------------------------------------------------------------------------------------------
+ * RX: parse + validate + checksum + port demux + per-socket lanes
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+    const uint8_t  *frames_dev;   /* frame bytes (rte_pktmbuf_mtod, Ethernet first, no FCS),
+                                     16-byte aligned base                                      */
+    uint64_t        frames_bytes; /* < 2^32                                                    */
+    const uint32_t *offset_dev;   /* [n] byte offset of each frame in frames_dev               */
+    const uint16_t *length_dev;   /* [n] data_len of each frame                                */
+    const uint32_t *ptype_dev;    /* [n] mbuf packet_type, or NULL: derived from ether_type
+                                     (0x0800 -> L2_ETHER|L3_IPV4|L4_UDP, else L2_ETHER)        */
+    uint32_t        n;
+} udpdk_rx_batch_t;
+
+typedef struct {
+    uint32_t *meta_dev;      /* [n] verdict words                                             */
+    uint32_t *lane_off_dev;  /* [n_lanes + 1] exclusive prefix of per-lane delivery counts    */
+    uint32_t *lane_pkt_dev;  /* [lane_cap] frame indices grouped by lane, arrival order kept  */
+    uint32_t  lane_cap;
+} udpdk_rx_out_t;
+
+typedef struct {
+    uint64_t counters[UDPDK_N_COUNTERS];
+    uint32_t deliveries;     /* == lane_off[n_lanes]                                           */
+    uint32_t overflow;       /* deliveries > lane_cap: lane_pkt holds only the first lane_cap  */
+} udpdk_rx_stats_t;
+
+/* Enqueue the RX pipeline for one batch on the context stream (async). */
+int udpdk_gpu_rx(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch, const udpdk_rx_out_t *out);
+/* Wait for the last udpdk_gpu_rx and read its counters. Returns -ENOSPC on lane overflow. */
+int udpdk_gpu_rx_stats(udpdk_gpu_ctx *ctx, udpdk_rx_stats_t *stats);
+
+/* End-to-end variant for host-resident batches (the real poller's situation: frames arrive in
+ * host mbufs): pinned staging, H2D, the RX pipeline, D2H of meta and lanes. Synchronous.
+ * frames_host etc. follow udpdk_rx_batch_t; outputs are host arrays. */
+int udpdk_gpu_rx_host(udpdk_gpu_ctx *ctx,
+                      const uint8_t *frames_host, uint64_t frames_bytes,
+                      const uint32_t *offset_host, const uint16_t *length_host,
+                      const uint32_t *ptype_host, uint32_t n,
+                      uint32_t *meta_host, uint32_t *lane_off_host,
+                      uint32_t *lane_pkt_host, uint32_t lane_cap,
+                      udpdk_rx_stats_t *stats);
+
+/* ---------------------------------------------------------------------------------------------
+ * TX: Eth/IPv4/UDP header build + rte_ipv4_cksum + payload copy (udpdk_syscall.c:314-356)
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+    uint8_t  src_mac[6];     /* config.src_mac_addr ([port0] mac_addr, udpdk_args.c:21-49)     */
+    uint8_t  dst_mac[6];     /* config.dst_mac_addr ([port0_dst] mac_addr)                     */
+    uint32_t src_ip;         /* config.src_ip_addr, raw                                        */
+} udpdk_tx_config_t;
+
+typedef struct {
+    const uint8_t  *payload_dev;     /* payload bytes                                          */
+    uint64_t        payload_bytes;
+    const uint32_t *payload_off_dev; /* [n]                                                    */
+    const uint16_t *payload_len_dev; /* [n] sendto len, <= 65507                               */
+    const int32_t  *sockfd_dev;      /* [n] sending socket (slot table from the snapshot)      */
+    const uint32_t *dst_ip_dev;      /* [n] raw dest_addr->sin_addr                            */
+    const uint16_t *dst_port_dev;    /* [n] raw dest_addr->sin_port                            */
+    uint32_t        n;
+} udpdk_tx_batch_t;
+
+typedef struct {
+    uint8_t        *frames_dev;      /* output frames                                          */
+    uint64_t        frames_bytes;    /* capacity                                               */
+    const uint32_t *frame_off_dev;   /* [n] where frame i starts (len_i + 42 bytes)            */
+} udpdk_tx_out_t;
+
+int udpdk_gpu_tx_build(udpdk_gpu_ctx *ctx, const udpdk_tx_config_t *cfg,
+                       const udpdk_tx_batch_t *batch, const udpdk_tx_out_t *out);
+
+/* ---------------------------------------------------------------------------------------------
+ * Timing (for bench.py / the roofline): when enabled, udpdk_gpu_rx records HIP events around
+ * each of its kernels on the context stream; read back accumulated device milliseconds.
+ * ------------------------------------------------------------------------------------------- */
+enum udpdk_gpu_kernel_id {
+    UDPDK_K_RX_CLASSIFY = 0,   /* parse + checksums + demux + tile histograms (dominant)      */
+    UDPDK_K_RX_SCAN     = 1,   /* lane offsets (one or three launches)                         */
+    UDPDK_K_RX_SCATTER  = 2,   /* stable per-lane compaction                                   */
+    UDPDK_K_TX_BUILD    = 3,
+    UDPDK_N_KERNEL_IDS  = 4
+};
+int udpdk_gpu_timing_enable(udpdk_gpu_ctx *ctx, int enable);
+/* Synchronises; ms[k] = accumulated device ms, launches[k] = number of timed calls. Resets. */
+int udpdk_gpu_timing_read(udpdk_gpu_ctx *ctx, double ms[UDPDK_N_KERNEL_IDS],
+                          uint32_t launches[UDPDK_N_KERNEL_IDS]);
+
+/* Tile geometry the RX pipeline will use for (n, n_lanes): frames per tile and tile count. */
+int udpdk_gpu_rx_geometry(uint32_t n, uint32_t n_lanes, uint32_t *tile_frames,
+                          uint32_t *n_tiles);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* UDPDK_GPU_H */

@@ -1,0 +1,137 @@
+"""ctypes binding of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference hot path (see udpdk_oracle.h). Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg load this module; the product library
+never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run `make -C oracle`")
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        L.oracle_btable_new.restype = P
+        L.oracle_btable_free.argtypes = [P]
+        L.oracle_btable_add.argtypes = [P, C.c_int, C.c_uint32, C.c_uint32, C.c_int]
+        L.oracle_btable_del.argtypes = [P, C.c_int, C.c_uint32]
+        L.oracle_btable_free_port.argtypes = [P]
+        L.oracle_btable_port_len.argtypes = [P, C.c_uint32]
+        L.oracle_btable_port_at.argtypes = [P, C.c_uint32, C.c_int, C.POINTER(C.c_int),
+                                            C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
+        L.oracle_rx.restype = C.c_int64
+        L.oracle_rx.argtypes = [P, P, C.c_uint64, P, P, P, C.c_uint32, C.c_uint32, C.c_uint32,
+                                C.c_int, P, P, P, C.c_uint32, P]
+        L.oracle_rx_parallel.restype = C.c_double
+        L.oracle_rx_parallel.argtypes = [P, P, C.c_uint64, P, P, C.c_uint32, C.c_uint32,
+                                         C.c_uint32, C.c_int, C.c_int, C.c_int]
+        L.oracle_rte_ipv4_cksum.restype = C.c_uint16
+        L.oracle_rte_ipv4_cksum.argtypes = [P]
+        L.oracle_tx_frame.argtypes = [P, P, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32,
+                                      C.c_uint32, C.c_uint32, P, C.c_uint32, P]
+        _lib = L
+    return _lib
+
+
+class BindTable:
+    """sock_bind_table restated (udpdk_bind_table.c)."""
+
+    def __init__(self):
+        self.h = C.c_void_p(lib().oracle_btable_new())
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_btable_free(self.h)
+            self.h = None
+
+    def add(self, sockfd: int, ip_raw: int, port_raw: int, opts: int) -> int:
+        return lib().oracle_btable_add(self.h, sockfd, ip_raw, port_raw, opts)
+
+    def delete(self, sockfd: int, port_raw: int):
+        lib().oracle_btable_del(self.h, sockfd, port_raw)
+
+    def free_port(self) -> int:
+        return lib().oracle_btable_free_port(self.h)
+
+    def port_list(self, port_raw: int) -> list[tuple[int, int, int]]:
+        out = []
+        n = lib().oracle_btable_port_len(self.h, port_raw)
+        s, ip, r = C.c_int(), C.c_uint32(), C.c_int()
+        for i in range(n):
+            lib().oracle_btable_port_at(self.h, port_raw, i, C.byref(s), C.byref(ip), C.byref(r))
+            out.append((ip.value, s.value, r.value))
+        return out
+
+
+def rx(bt: BindTable, frames: np.ndarray, frames_bytes: int, offset: np.ndarray, length: np.ndarray,
+       ptype: np.ndarray | None, n_lanes: int, lane_mask: int = 0xFFFFFFFF, do_csum: bool = True,
+       lane_cap: int | None = None):
+    """Returns (meta, lane_off, lane_pkt, counters)."""
+    n = len(offset)
+    offset = np.ascontiguousarray(offset, np.uint32)
+    length = np.ascontiguousarray(length, np.uint16)
+    meta = np.zeros(max(1, n), np.uint32)
+    loff = np.zeros(n_lanes + 1, np.uint32)
+    cap = lane_cap if lane_cap is not None else max(1, n * 8)
+    pkt = np.zeros(cap, np.uint32)
+    cnt = np.zeros(16, np.uint64)
+    pt = np.ascontiguousarray(ptype, np.uint32) if ptype is not None else None
+    d = lib().oracle_rx(bt.h, frames.ctypes.data, frames_bytes, offset.ctypes.data,
+                        length.ctypes.data, pt.ctypes.data if pt is not None else None, n,
+                        lane_mask, n_lanes, int(do_csum), meta.ctypes.data, loff.ctypes.data,
+                        pkt.ctypes.data, cap, cnt.ctypes.data)
+    if d < 0:
+        raise RuntimeError("oracle_rx failed (lane capacity or key out of range)")
+    return meta[:n], loff, pkt[:d], cnt
+
+
+def rx_parallel(bt: BindTable, frames: np.ndarray, frames_bytes: int, offset: np.ndarray,
+                length: np.ndarray, n_lanes: int, do_csum: bool, threads: int, reps: int) -> float:
+    offset = np.ascontiguousarray(offset, np.uint32)
+    length = np.ascontiguousarray(length, np.uint16)
+    return lib().oracle_rx_parallel(bt.h, frames.ctypes.data, frames_bytes, offset.ctypes.data,
+                                     length.ctypes.data, len(offset), 0xFFFFFFFF, n_lanes,
+                                     int(do_csum), threads, reps)
+
+
+def ipv4_cksum(hdr20: bytes) -> int:
+    b = C.create_string_buffer(hdr20, 20)
+    return lib().oracle_rte_ipv4_cksum(b)
+
+
+def tx_frame(src_mac: bytes, dst_mac: bytes, cfg_src_ip: int, slot_bound: int, slot_ip: int,
+             slot_port: int, dst_ip: int, dst_port: int, payload: bytes) -> bytes:
+    out = C.create_string_buffer(len(payload) + 42)
+    pb = C.create_string_buffer(payload, max(1, len(payload)))
+    lib().oracle_tx_frame(C.create_string_buffer(src_mac, 6), C.create_string_buffer(dst_mac, 6),
+                          cfg_src_ip, slot_bound, slot_ip, slot_port, dst_ip, dst_port, pb,
+                          len(payload), out)
+    return out.raw
+
+
+def bindtable_from_lists(port_lists: dict[int, list[tuple[int, int, int]]]) -> BindTable:
+    """Replay bindings so that each port's list ends up in the given order. ANY bindings are
+    lpush'ed, specific ones rpush'ed, so replaying ANY entries in reverse list order first and the
+    specific ones in list order reproduces any list whose ANY entries precede the specific ones."""
+    bt = BindTable()
+    for p, lst in port_lists.items():
+        anys = [x for x in lst if x[0] == 0]
+        specs = [x for x in lst if x[0] != 0]
+        assert lst == anys + specs, "list order not reachable through bind()"
+        for ip, s, reuse in reversed(anys):
+            assert bt.add(s, ip, p, 15 if reuse else 0) == 0
+        for ip, s, reuse in specs:
+            assert bt.add(s, ip, p, 15 if reuse else 0) == 0
+    return bt

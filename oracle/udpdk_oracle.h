@@ -1,0 +1,74 @@
+/*
+ * udpdk_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, CPU-only restatement of the reference UDPDK hot path (leoll2/UDPDK @ v1) used as the
+ * parity checker for the HIP datapath and as bench.py's cpu_baseline ("port"). Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it; the product library
+ * (udpdk_amd/libudpdk_amd.so) never links or calls it.
+ *
+ * Pinning: the reference itself is unbuildable here (it needs DPDK 20.05; deps/dpdk is an empty
+ * submodule) so this restatement is pinned by the TX golden vectors and RX behaviour probes that
+ * SURVEY.md §8.G / §8(a) recorded from the reference's own code, and by published RFC 1071
+ * checksum examples (tests/golden/). See DESIGN.md "Oracle and parity".
+ */
+#ifndef UDPDK_ORACLE_H
+#define UDPDK_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_btable oracle_btable;
+
+/* Bind table: sock_bind_table[65536] of lists (udpdk_bind_table.c:17-30). */
+oracle_btable *oracle_btable_new(void);
+void           oracle_btable_free(oracle_btable *bt);
+/* btable_add_binding (udpdk_bind_table.c:92-126): 0 ok, -1 if btable_can_bind refuses. */
+int            oracle_btable_add(oracle_btable *bt, int sockfd, uint32_t ip_raw, uint32_t port_raw,
+                                 int opts);
+/* btable_del_binding (udpdk_bind_table.c:129-149). */
+void           oracle_btable_del(oracle_btable *bt, int sockfd, uint32_t port_raw);
+/* btable_get_free_port (udpdk_bind_table.c:33-42). */
+int            oracle_btable_free_port(const oracle_btable *bt);
+/* Number of bindings on a raw port, and the i-th in list order (head -> tail). */
+int            oracle_btable_port_len(const oracle_btable *bt, uint32_t port_raw);
+int            oracle_btable_port_at(const oracle_btable *bt, uint32_t port_raw, int i,
+                                     int *sockfd, uint32_t *ip_raw, int *reuse);
+
+/* RX over a batch, in the reference's structure: 128-frame bursts (poller.c:517, BURST_SIZE),
+ * reassemble() per frame (poller.c:316-413), per-slot rx_buffer appends (poller.c:294-298) and a
+ * per-burst flush of every slot in index order (poller.c:537-541, :274-292).
+ * Lanes are keyed by (sockfd & lane_mask). Writes meta[n] in the udpdk_gpu.h word format,
+ * lane_off[n_lanes+1], lane_pkt[<= lane_cap], counters[16].
+ * do_csum = 0 skips the (new, non-reference) checksum verification for the baseline timing.
+ * Returns the number of deliveries, or -1 if lane_cap was too small / a key >= n_lanes. */
+int64_t oracle_rx(const oracle_btable *bt, const uint8_t *frames, uint64_t frames_bytes,
+                  const uint32_t *offset, const uint16_t *length, const uint32_t *ptype,
+                  uint32_t n, uint32_t lane_mask, uint32_t n_lanes, int do_csum,
+                  uint32_t *meta, uint32_t *lane_off, uint32_t *lane_pkt, uint32_t lane_cap,
+                  uint64_t counters[16]);
+
+/* CPU baseline: nthreads pinned threads, thread t runs oracle_rx over its contiguous slice of
+ * the batch (one independent shard per thread) `reps` times. Returns wall seconds. */
+double  oracle_rx_parallel(const oracle_btable *bt, const uint8_t *frames, uint64_t frames_bytes,
+                           const uint32_t *offset, const uint16_t *length, uint32_t n,
+                           uint32_t lane_mask, uint32_t n_lanes, int do_csum, int nthreads,
+                           int reps);
+
+/* DPDK 20.05 rte_raw_cksum + rte_ipv4_cksum over a 20-byte header (called udpdk_syscall.c:337). */
+uint16_t oracle_rte_ipv4_cksum(const uint8_t hdr[20]);
+
+/* udpdk_sendto header build + payload (udpdk_syscall.c:314-356). Writes len + 42 bytes.
+ * slot_bound/slot_ip/slot_port: exch_zone_desc->slots[sockfd] after any auto-bind. */
+void oracle_tx_frame(const uint8_t src_mac[6], const uint8_t dst_mac[6], uint32_t cfg_src_ip,
+                     int slot_bound, uint32_t slot_ip, uint32_t slot_port,
+                     uint32_t dst_ip, uint32_t dst_port, const uint8_t *payload, uint32_t len,
+                     uint8_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,197 @@
+"""Pins the oracle (and the product's CPU TX path) to the golden fixtures: the reference's own
+outputs recorded by the survey (TX V1-V5, RX behaviour probes) and published RFC 1071 examples.
+CPU only."""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import oracle as O
+from udpdk_amd import abi, frames as F
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    with open(os.path.join(HERE, name)) as f:
+        return json.load(f)
+
+
+def _fold(s):
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return s
+
+
+# ---- checksums --------------------------------------------------------------------------------
+def test_rfc1071_vectors():
+    for v in _load("checksum_vectors.json"):
+        b = bytes.fromhex(v["bytes"])
+        be = sum(struct.unpack(f">{len(b) // 2}H", b))
+        if "sum_be" in v:
+            assert _fold(be) == v["sum_be"]
+        assert (~_fold(be)) & 0xFFFF == v["cksum_be"]
+
+
+def test_oracle_rte_ipv4_cksum_known_answer():
+    v = [x for x in _load("checksum_vectors.json") if x["id"] == "ipv4-b861"][0]
+    hdr = bytes.fromhex(v["bytes"])
+    c = O.ipv4_cksum(hdr)          # host u16; stored little-endian -> wire bytes b8 61
+    assert struct.pack("<H", c) == struct.pack(">H", v["cksum_be"])
+
+
+def test_oracle_rte_ipv4_cksum_0xffff_quirk():
+    # raw sum 0xffff is returned unchanged (V3's header)
+    hdr = bytes.fromhex("4500005c00000000401100 00ac1f6402ac1fbe50".replace(" ", ""))
+    assert O.ipv4_cksum(hdr) == 0xFFFF
+
+
+# ---- TX golden vectors ---------------------------------------------------------------------------
+def _payload(n):
+    return bytes((i * 7 + 3) & 0xFF for i in range(n))
+
+
+def test_oracle_tx_vectors():
+    g = _load("tx_vectors.json")
+    cfg = g["config"]
+    for v in g["vectors"]:
+        # slot state after the setup: explicit binds, or the auto-bind raw port the survey saw
+        slots = {}
+        bound = {}
+        for step in v["setup"]:
+            if step[0] == "bind":
+                bound[step[1]] = (abi.raw_ip(step[2]), abi.raw_port(step[3]))
+        s = v["send"]["sock"]
+        if s in bound:
+            sb, sip, sport = 1, bound[s][0], bound[s][1]
+        else:   # auto-bind to ANY on the lowest free raw port
+            bt = O.BindTable()
+            for k, (ip, port) in bound.items():
+                assert bt.add(k, ip, port, 0) == 0
+            for step in v["setup"]:
+                if step[0] == "autobind":
+                    assert bt.add(step[1], 0, bt.free_port(), 0) == 0
+            sb, sip, sport = 1, 0, bt.free_port()
+        pl = _payload(v["send"]["len"])
+        fr = O.tx_frame(bytes.fromhex(cfg["src_mac"]), bytes.fromhex(cfg["dst_mac"]),
+                        abi.raw_ip(cfg["src_ip"]), sb, sip, sport, abi.raw_ip(v["send"]["dst"]),
+                        abi.raw_port(v["send"]["port"]), pl)
+        assert len(fr) == v["pkt_len"], v["id"]
+        assert fr[:42].hex() == v["hdr"], v["id"]
+        assert fr[42:] == pl
+        del slots
+
+
+def test_product_cpu_tx_vectors(host_api):
+    """udpdk_build_frame (the product's sendto header build) against the same vectors, including
+    the auto-bind path (V4/V5)."""
+    g = _load("tx_vectors.json")
+    cfg = g["config"]
+    for v in g["vectors"]:
+        host_api.reset()
+        host_api.config_set(bytes.fromhex(cfg["src_mac"]), bytes.fromhex(cfg["dst_mac"]), cfg["src_ip"])
+        for step in v["setup"]:
+            if step[0] == "socket":
+                assert host_api.socket() >= 0
+            elif step[0] == "bind":
+                assert host_api.bind(step[1], step[2], step[3]) == 0
+            elif step[0] == "autobind":
+                host_api.build_frame(step[1], b"x", "172.31.100.1", 10001)
+        pl = _payload(v["send"]["len"])
+        fr = host_api.build_frame(v["send"]["sock"], pl, v["send"]["dst"], v["send"]["port"])
+        assert len(fr) == v["pkt_len"], v["id"]
+        assert fr[:42].hex() == v["hdr"], v["id"]
+        assert fr[42:] == pl
+
+
+# ---- RX behaviour probes ---------------------------------------------------------------------
+def _probe_batch(p, rng):
+    kw = dict(dport=10001, dst_ip=p.get("dst_ip", "172.31.100.1"), payload_len=22)
+    if "ethertype" in p:
+        kw["ethertype"] = p["ethertype"]
+    if "frag" in p:
+        kw["frag"] = p["frag"]
+    if "proto" in p:
+        kw["proto"] = p["proto"]
+    f = F.make_frame(rng, **kw)
+    buf = np.zeros(256, np.uint8)
+    buf[:len(f)] = np.frombuffer(f, np.uint8)
+    return buf, len(f)
+
+
+def test_oracle_rx_probes():
+    rng = np.random.default_rng(0)
+    for p in _load("rx_probes.json")["frames"]:
+        buf, n = _probe_batch(p, rng)
+        lists = {}
+        if "binds" in p:
+            lists = {abi.raw_port(10001): []}
+            bt = O.BindTable()
+            for s, ip, opts in p["binds"]:
+                assert bt.add(s, abi.raw_ip(ip), abi.raw_port(10001), opts) == 0
+        else:
+            bt = O.bindtable_from_lists({abi.raw_port(10001): [(0, 0, 0)]})
+        pt = np.array([p["ptype"]], np.uint32) if "ptype" in p else None
+        meta, loff, pkt, _ = O.rx(bt, buf, n, np.array([0], np.uint32), np.array([n], np.uint16),
+                                  pt, 16)
+        assert abi.VERDICT_NAMES[int(abi.meta_verdict(meta[0]))] == p["expect_verdict"], p["id"]
+        if "expect_deliveries" in p:
+            got = [lane for lane in range(16) for _ in range(loff[lane + 1] - loff[lane])]
+            assert sorted(got) == sorted(p["expect_deliveries"]), p["id"]
+            if p["expect_deliveries"]:
+                assert int(abi.meta_sockfd(meta[0])) == p["expect_deliveries"][0], p["id"]
+                assert int(abi.meta_fanout(meta[0])) == len(p["expect_deliveries"]), p["id"]
+        del lists
+
+
+@pytest.mark.parametrize("probe", _load("rx_probes.json")["alias"])
+def test_oracle_uint8_slot_aliasing(probe):
+    n = probe["n_sockets"]
+    lists = {abi.raw_port(10000 + i): [(0, i, 0)] for i in range(n)}
+    bt = O.bindtable_from_lists(lists)
+    rng = np.random.default_rng(1)
+    out = bytearray()
+    offs = []
+    for i in range(n):
+        f = F.make_frame(rng, dport=10000 + i)
+        offs.append(len(out))
+        out += f
+    buf = np.zeros(len(out) + 256, np.uint8)
+    buf[:len(out)] = np.frombuffer(bytes(out), np.uint8)
+    lens = np.full(n, 64, np.uint16)
+    meta, loff, pkt, _ = O.rx(bt, buf, len(out), np.array(offs, np.uint32), lens, None, 256, 0xFF)
+    socks = abi.meta_sockfd(meta)
+    aliased = int(np.sum(socks >= 256))
+    assert aliased == probe["aliased"]
+    # compat lanes: lane k holds every frame whose sockfd & 0xff == k (the reference's rx_buffer)
+    for k in range(256):
+        want = np.nonzero((socks & 0xFF) == k)[0]
+        assert np.array_equal(pkt[loff[k]:loff[k + 1]], want)
+
+
+def test_sockopt_probes(host_api):
+    for p in _load("rx_probes.json")["sockopt"]:
+        host_api.reset()
+        s = host_api.socket()
+        opt = abi.SO_REUSEPORT if p["set"] == "SO_REUSEPORT" else abi.SO_REUSEADDR
+        assert host_api.setsockopt(s, abi.SOL_SOCKET, opt, 1) == 0
+        assert host_api.getsockopt(s, abi.SOL_SOCKET, abi.SO_REUSEADDR) == (0, p["get_SO_REUSEADDR"])
+        assert host_api.getsockopt(s, abi.SOL_SOCKET, abi.SO_REUSEPORT) == (0, p["get_SO_REUSEPORT"])
+
+
+def test_oracle_regression_fixture():
+    """The oracle still produces what it produced when rx_mixed.npz was written."""
+    z = np.load(os.path.join(HERE, "rx_mixed.npz"))
+    lists = {}
+    for p, ip, s, r in z["lists"]:
+        lists.setdefault(int(p), []).append((int(ip), int(s), int(r)))
+    bt = O.bindtable_from_lists(lists)
+    fr = np.zeros(len(z["frames"]) + 256, np.uint8)
+    fr[:len(z["frames"])] = z["frames"]
+    meta, loff, pkt, cnt = O.rx(bt, fr, len(z["frames"]), z["offset"], z["length"], z["ptype"], 4)
+    assert np.array_equal(meta, z["meta"])
+    assert np.array_equal(loff, z["lane_off"])
+    assert np.array_equal(pkt, z["lane_pkt"])
+    assert np.array_equal(cnt, z["counters"])

@@ -1,0 +1,189 @@
+"""RX parity: the HIP pipeline (through the C ABI) against the oracle, bit for bit — verdict
+words, per-lane delivery lists and counters — on seeded inputs; plus full-size property checks.
+"""
+import errno
+
+import numpy as np
+import pytest
+
+import oracle as O
+from udpdk_amd import abi, frames as F
+
+pytestmark = pytest.mark.gpu
+
+IP1, IP9 = "172.31.100.1", "172.31.100.9"
+
+
+def _rx_both(ctx, batch, lists, n_lanes, lane_mask=0xFFFFFFFF, lane_cap=None):
+    hs = abi.snapshot_from_lists(lists, n_lanes, lane_mask)
+    ctx.upload_snapshot(hs)
+    bt = O.bindtable_from_lists(lists)
+    want = O.rx(bt, batch.frames, batch.frames_bytes, batch.offset, batch.length, batch.ptype,
+                n_lanes, lane_mask)
+    db = abi.rx_upload(ctx, batch.frames, batch.offset, batch.length, batch.ptype)
+    db.frames_bytes = batch.frames_bytes
+    cap = lane_cap if lane_cap is not None else max(1, batch.n * 4)
+    out = abi.rx_alloc_out(ctx, batch.n, n_lanes, cap)
+    got = abi.rx_run(ctx, db, out)
+    for b in (db.frames, db.offset, db.length, db.ptype, out.meta, out.lane_off, out.lane_pkt):
+        if b is not None:
+            b.free()
+    return want, got
+
+
+def _assert_same(want, got, ctx=""):
+    wm, wl, wp, wc = want
+    gm, gl, gp, gc, rc = got
+    assert rc == 0, ctx
+    bad = np.nonzero(wm != gm)[0]
+    assert len(bad) == 0, f"{ctx}: {len(bad)} verdict words differ, first {bad[:5]} " \
+                          f"want {[hex(x) for x in wm[bad[:5]]]} got {[hex(x) for x in gm[bad[:5]]]}"
+    assert np.array_equal(wl, gl), ctx
+    assert np.array_equal(wp, gp), ctx
+    assert np.array_equal(wc, gc), f"{ctx}: counters {wc} vs {gc}"
+
+
+MIXED_LISTS = {
+    abi.raw_port(10001): [(0, 0, 0)],
+    abi.raw_port(10002): [(abi.raw_ip(IP1), 1, 1), (abi.raw_ip(IP1), 2, 1)],    # REUSEPORT fan-out
+    abi.raw_port(10003): [(abi.raw_ip(IP9), 3, 0)],                          # specific, no match
+    abi.raw_port(10004): [(0, 4, 1), (abi.raw_ip(IP1), 5, 1)],               # ANY + specific clone
+    abi.raw_port(10005): [(0, 6, 0), (abi.raw_ip(IP1), 7, 1)],               # ANY swallows (Q3)
+}
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("with_ptype", [False, True])
+def test_mixed_batches(gpu_ctx, seed, with_ptype):
+    b = F.mixed_batch(seed, 3000, [10001, 10002, 10003, 10004, 10005], [9, 20000, 65535],
+                      [IP1, IP9], with_ptype=with_ptype)
+    want, got = _rx_both(gpu_ctx, b, MIXED_LISTS, 8)
+    _assert_same(want, got, f"seed={seed} ptype={with_ptype}")
+    # the batch really covers every verdict class
+    assert set(np.unique(abi.meta_verdict(want[0]))) >= {0, 1, 2, 3, 4, 5, 6}
+
+
+def test_fixture_batch(gpu_ctx):
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "rx_mixed.npz"))
+    lists = {}
+    for p, ip, s, r in z["lists"]:
+        lists.setdefault(int(p), []).append((int(ip), int(s), int(r)))
+    fr = np.zeros(len(z["frames"]) + 256, np.uint8)
+    fr[:len(z["frames"])] = z["frames"]
+    b = F.Batch(fr, z["offset"], z["length"], len(z["frames"]), z["ptype"])
+    want, got = _rx_both(gpu_ctx, b, lists, 4)
+    _assert_same(want, got, "fixture")
+    assert np.array_equal(got[0], z["meta"])
+    assert np.array_equal(got[2], z["lane_pkt"])
+
+
+def test_compat_uint8_lanes(gpu_ctx):
+    """Compat mode: lanes keyed by (uint8_t)sockfd exactly like exch_slots[(uint8_t)fd]."""
+    n = 600
+    lists = {abi.raw_port(10000 + i): [(0, i, 0)] for i in range(n)}
+    rng = np.random.default_rng(5)
+    ports = 10000 + rng.integers(0, n, 20000)
+    b = F.build_frames(np.full(len(ports), 64, np.uint32), ports, 9)
+    want, got = _rx_both(gpu_ctx, b, lists, 256, 0xFF)
+    _assert_same(want, got, "compat")
+    assert int(np.sum(abi.meta_sockfd(got[0]) >= 256)) > 0
+
+
+@pytest.mark.parametrize("cfg,n", [(2, 70001), (3, 20000), (4, 50000), (5, 100000), (1, 4096)])
+def test_configs_reduced(gpu_ctx, cfg, n):
+    w = F.config_batch(cfg, n=n)
+    want, got = _rx_both(gpu_ctx, w.batch, w.port_lists(), w.n_sockets)
+    _assert_same(want, got, w.name)
+    assert int(want[3][abi.V_DELIVERED]) == n
+
+
+@pytest.mark.parametrize("cfg", [2, 3])
+def test_configs_full_size(gpu_ctx, cfg):
+    """BASELINE.json sizes (1 M frames): exact against the oracle plus properties."""
+    w = F.config_batch(cfg)
+    want, got = _rx_both(gpu_ctx, w.batch, w.port_lists(), w.n_sockets)
+    _assert_same(want, got, w.name)
+    meta, loff, pkt = got[0], got[1], got[2]
+    assert np.all(abi.meta_verdict(meta) == abi.V_DELIVERED)
+    assert np.all(abi.meta_udp(meta) == abi.UDP_OK)
+    assert np.all((meta >> 4) & 1)
+    assert np.array_equal(pkt, np.arange(w.batch.n, dtype=np.uint32))   # one lane, arrival order
+
+
+def test_zipf_4096_full(gpu_ctx):
+    w = F.config_batch(5)
+    want, got = _rx_both(gpu_ctx, w.batch, w.port_lists(), w.n_sockets)
+    _assert_same(want, got, w.name)
+    # stability: every lane is strictly increasing
+    loff, pkt = got[1], got[2]
+    d = np.diff(pkt.astype(np.int64))
+    starts = loff[1:-1].astype(np.int64) - 1
+    mask = np.ones(len(d), bool)
+    mask[starts[(starts >= 0) & (starts < len(d))]] = False
+    assert np.all(d[mask] > 0)
+
+
+def test_edge_sizes(gpu_ctx):
+    lists = {abi.raw_port(10001): [(0, 0, 0)]}
+    for n in [1, 63, 64, 65, 1023, 1024, 1025, 4097]:
+        b = F.build_frames(np.full(n, 64, np.uint32), np.full(n, 10001, np.uint32), n)
+        want, got = _rx_both(gpu_ctx, b, lists, 1)
+        _assert_same(want, got, f"n={n}")
+
+
+def test_empty_batch(gpu_ctx):
+    lists = {abi.raw_port(10001): [(0, 0, 0)]}
+    hs = abi.snapshot_from_lists(lists, 3)
+    gpu_ctx.upload_snapshot(hs)
+    b = abi.RxDeviceBatch(gpu_ctx.alloc(256), 0, gpu_ctx.alloc(4), gpu_ctx.alloc(4), None, 0)
+    out = abi.rx_alloc_out(gpu_ctx, 0, 3, 4)
+    meta, loff, pkt, cnt, rc = abi.rx_run(gpu_ctx, b, out)
+    assert rc == 0 and np.all(loff == 0) and len(pkt) == 0 and np.all(cnt == 0)
+
+
+def test_bad_descriptors(gpu_ctx):
+    """offset + length beyond frames_bytes: verdict BAD_DESC, nothing read."""
+    lists = {abi.raw_port(10001): [(0, 0, 0)]}
+    b = F.build_frames(np.full(100, 64, np.uint32), np.full(100, 10001, np.uint32), 3)
+    b.offset[7] = b.frames_bytes - 10
+    b.offset[50] = 0xFFFFFF00
+    b.length[60] = 65535
+    want, got = _rx_both(gpu_ctx, b, lists, 1)
+    _assert_same(want, got, "bad desc")
+    assert abi.meta_verdict(got[0])[[7, 50, 60]].tolist() == [abi.V_BAD_DESC] * 3
+
+
+def test_lane_overflow(gpu_ctx):
+    lists = {abi.raw_port(10001): [(0, 0, 0)]}
+    b = F.build_frames(np.full(1000, 64, np.uint32), np.full(1000, 10001, np.uint32), 3)
+    hs = abi.snapshot_from_lists(lists, 1)
+    gpu_ctx.upload_snapshot(hs)
+    db = abi.rx_upload(gpu_ctx, b.frames, b.offset, b.length)
+    db.frames_bytes = b.frames_bytes
+    out = abi.rx_alloc_out(gpu_ctx, 1000, 1, 100)
+    meta, loff, pkt, cnt, rc = abi.rx_run(gpu_ctx, db, out)
+    assert rc == -errno.ENOSPC
+    assert loff[1] == 1000 and np.array_equal(pkt, np.arange(100))
+
+
+def test_rx_host_end_to_end(gpu_ctx):
+    """udpdk_gpu_rx_host: host batch in, host results out (pinned staging + H2D + D2H)."""
+    import ctypes as C
+    b = F.mixed_batch(11, 2000, [10001, 10002, 10003, 10004, 10005], [9, 20000], [IP1, IP9])
+    hs = abi.snapshot_from_lists(MIXED_LISTS, 8)
+    gpu_ctx.upload_snapshot(hs)
+    bt = O.bindtable_from_lists(MIXED_LISTS)
+    wm, wl, wp, wc = O.rx(bt, b.frames, b.frames_bytes, b.offset, b.length, None, 8)
+    meta = np.zeros(b.n, np.uint32)
+    loff = np.zeros(9, np.uint32)
+    pkt = np.zeros(b.n * 4, np.uint32)
+    st = abi.RxStats()
+    rc = abi.lib().udpdk_gpu_rx_host(gpu_ctx.handle, b.frames.ctypes.data, b.frames_bytes,
+                                     b.offset.ctypes.data, b.length.ctypes.data, None, b.n,
+                                     meta.ctypes.data, loff.ctypes.data, pkt.ctypes.data,
+                                     len(pkt), C.byref(st))
+    assert rc == 0
+    assert np.array_equal(meta, wm) and np.array_equal(loff, wl)
+    assert np.array_equal(pkt[:st.deliveries], wp)
+    assert np.array_equal(np.array(st.counters[:], np.uint64), wc)

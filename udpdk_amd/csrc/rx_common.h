@@ -1,0 +1,115 @@
+// rx_common.h — kernel argument blocks and launch constants shared by the HIP kernels and the
+// C-ABI host code (udpdk_gpu.hip). Device-internal; not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace udpdk {
+
+constexpr int RX_BLOCK  = 256;              // rx_classify workgroup (4 waves)
+constexpr int RX_WAVES  = RX_BLOCK / 64;
+constexpr int RX_UNROLL = 4;                // 16-byte chunk loads in flight per lane
+constexpr uint32_t RX_TILE_MIN = 1024;      // frames per tile (histogram granularity)
+constexpr uint32_t RX_TILE_MAX = 16384;
+constexpr uint32_t RX_HIST_CAP = 1u << 21;  // target bound on lanes x tiles
+
+constexpr int SCAN_BLOCK = 256;
+constexpr uint32_t SCAN_CHUNK = 4096;       // elements per workgroup in the 3-pass scan
+constexpr uint32_t SCAN_SMALL_MAX = 16384;  // single-workgroup scan up to this many elements
+
+constexpr int TX_BLOCK = 256;
+
+// rx_classify LDS carve (one dynamic array, 16-byte aligned offsets: cdna_hip_programming.md
+// Guideline 17): per wave a 64 B header window per frame (80 B stride spreads the lane-per-frame
+// dword reads over banks), five 64-entry per-frame arrays, then block counters and the tile's
+// per-lane histogram.
+constexpr int HDR_STRIDE  = 80;
+constexpr int HDR_BYTES   = RX_WAVES * 64 * HDR_STRIDE;
+constexpr int WAVE_ARRAYS = 5;                    // chunk start, offset, length, ip sum, udp sum
+constexpr int ARR_BYTES   = RX_WAVES * WAVE_ARRAYS * 64 * 4;
+constexpr int CNT_OFF     = HDR_BYTES + ARR_BYTES;
+constexpr int HIST_OFF    = CNT_OFF + 64;
+
+__host__ __device__ constexpr uint32_t classify_lds_bytes(uint32_t n_lanes)
+{
+    return (uint32_t)HIST_OFF + 4u * n_lanes;
+}
+
+// Packed snapshot entry per raw port: (index of first binding << 12) | count (<= 4095).
+// Binding: x = raw IPv4, y = sockfd | reuse << 31.
+struct RxArgs {
+    const uint8_t  *frames;
+    const uint32_t *offset;
+    const uint16_t *length;
+    const uint32_t *ptype;
+    const uint32_t *port_tab;
+    const uint2    *binds;
+    uint32_t *meta;
+    uint32_t *hist;       // [n_lanes][n_tiles]
+    uint32_t *tile_cnt;   // [n_tiles][16]
+    uint32_t frames_bytes;
+    uint32_t rsrc_bytes;  // buffer-resource range (frames_bytes rounded up to 16)
+    uint32_t n;
+    uint32_t tile_frames;
+    uint32_t n_tiles;
+    uint32_t lane_mask;
+    uint32_t n_lanes;
+};
+
+struct ScanArgs {
+    uint32_t *hist;
+    uint32_t *partial;
+    uint32_t *lane_off;
+    const uint32_t *tile_cnt;
+    unsigned long long *counters;
+    uint32_t *total;
+    uint32_t n_elems;
+    uint32_t n_tiles;
+    uint32_t n_lanes;
+};
+
+struct ScatterArgs {
+    const uint32_t *meta;
+    const uint32_t *base;  // scanned hist
+    const uint8_t  *frames;
+    const uint32_t *offset;
+    const uint32_t *port_tab;
+    const uint2    *binds;
+    uint32_t *lane_pkt;
+    uint32_t n;
+    uint32_t tile_frames;
+    uint32_t n_tiles;
+    uint32_t n_lanes;
+    uint32_t lane_mask;
+    uint32_t key_bits;
+    uint32_t lane_cap;
+};
+
+struct TxArgs {
+    const uint8_t  *payload;
+    const uint32_t *payload_off;
+    const uint16_t *payload_len;
+    const int32_t  *sockfd;
+    const uint32_t *dst_ip;
+    const uint16_t *dst_port;
+    const uint32_t *frame_off;
+    const uint4    *slots;     // x = ip, y = udp_port, z = bound
+    uint8_t *frames;
+    uint32_t n;
+    uint32_t n_slots;
+    uint32_t payload_bytes;
+    uint32_t payload_rsrc;
+    uint32_t frames_bytes;
+    uint32_t src_ip;
+    uint32_t mac_lo[3];        // 12 MAC bytes: dst(6) src(6) as three LE dwords
+};
+
+__global__ void rx_classify(RxArgs a);
+__global__ void rx_scan_small(ScanArgs a);
+__global__ void rx_scan_reduce(ScanArgs a);
+__global__ void rx_scan_top(ScanArgs a, uint32_t n_part);
+__global__ void rx_scan_down(ScanArgs a);
+__global__ void rx_scatter(ScatterArgs a);
+__global__ void tx_build(TxArgs a);
+
+} // namespace udpdk

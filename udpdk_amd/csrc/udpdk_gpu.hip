@@ -1,0 +1,607 @@
+// udpdk_gpu.hip — host side of the C ABI declared in include/udpdk_gpu.h.
+//
+// Owns the per-device context (stream, bind snapshot, workspace, pinned readback) and enqueues
+// the RX and TX kernels. No hidden synchronisation on the RX/TX enqueue path: everything stays
+// on the context stream, so a caller may capture udpdk_gpu_rx into a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+#include "udpdk_gpu.h"
+#include "rx_common.h"
+
+using namespace udpdk;
+
+namespace {
+
+constexpr int EVENT_SETS = 256;   // timed calls buffered between two timing reads
+
+struct TimingSet {
+    hipEvent_t ev[4];             // classify start, classify end, scan end, scatter end
+};
+
+} // namespace
+
+struct udpdk_gpu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int last_err = 0;
+    uint32_t max_frames = 0, max_lanes = 0;
+
+    // bind snapshot (device)
+    uint32_t *port_tab = nullptr;       // [65536]
+    uint2 *binds = nullptr;
+    uint32_t binds_cap = 0;
+    uint4 *slots = nullptr;
+    uint32_t slots_cap = 0, n_slots = 0;
+    uint32_t n_lanes = 1, lane_mask = 0xFFFFFFFFu, key_bits = 0, max_fanout = 0;
+    bool have_snapshot = false;
+
+    // RX workspace
+    uint32_t *hist = nullptr;
+    size_t hist_cap = 0;
+    uint32_t *partial = nullptr;
+    size_t partial_cap = 0;
+    uint32_t *tile_cnt = nullptr;
+    size_t tiles_cap = 0;
+    unsigned long long *counters = nullptr;   // [16]
+    uint32_t *total = nullptr;
+    unsigned long long *h_counters = nullptr; // pinned
+    uint32_t *h_total = nullptr;              // pinned
+    hipEvent_t done = nullptr;
+    uint32_t last_lane_cap = 0;
+    bool pending = false;
+
+    // end-to-end staging (lazy)
+    uint8_t *st_frames_d = nullptr; size_t st_frames_dcap = 0;
+    uint8_t *st_frames_h = nullptr; size_t st_frames_hcap = 0;
+    uint8_t *st_desc_d = nullptr; size_t st_desc_dcap = 0;
+    uint8_t *st_desc_h = nullptr; size_t st_desc_hcap = 0;
+    uint8_t *st_out_d = nullptr; size_t st_out_cap = 0;
+
+    // timing
+    bool timing = false;
+    TimingSet *sets = nullptr;
+    int n_sets_used = 0;
+    double ms[UDPDK_N_KERNEL_IDS] = {0, 0, 0, 0};
+    uint32_t launches[UDPDK_N_KERNEL_IDS] = {0, 0, 0, 0};
+};
+
+#define HIPC(ctx, expr)                                                      \
+    do {                                                                     \
+        hipError_t e_ = (expr);                                              \
+        if (e_ != hipSuccess) {                                              \
+            if (ctx) (ctx)->last_err = (int)e_;                              \
+            return -EIO;                                                     \
+        }                                                                    \
+    } while (0)
+
+namespace {
+
+uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+void geometry(uint32_t n, uint32_t lanes, uint32_t *T, uint32_t *tiles)
+{
+    uint32_t t = RX_TILE_MIN;
+    while (t < RX_TILE_MAX && (uint64_t)ceil_div(n, t) * lanes > RX_HIST_CAP) t *= 2;
+    *T = t;
+    *tiles = std::max<uint32_t>(1u, ceil_div(n, t));
+}
+
+int fold_timing(udpdk_gpu_ctx *c)
+{
+    if (!c->n_sets_used) return 0;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < c->n_sets_used; ++i) {
+        float a = 0, b = 0, d = 0;
+        HIPC(c, hipEventElapsedTime(&a, c->sets[i].ev[0], c->sets[i].ev[1]));
+        HIPC(c, hipEventElapsedTime(&b, c->sets[i].ev[1], c->sets[i].ev[2]));
+        HIPC(c, hipEventElapsedTime(&d, c->sets[i].ev[2], c->sets[i].ev[3]));
+        c->ms[UDPDK_K_RX_CLASSIFY] += a;
+        c->ms[UDPDK_K_RX_SCAN] += b;
+        c->ms[UDPDK_K_RX_SCATTER] += d;
+        c->launches[UDPDK_K_RX_CLASSIFY]++;
+        c->launches[UDPDK_K_RX_SCAN]++;
+        c->launches[UDPDK_K_RX_SCATTER]++;
+    }
+    c->n_sets_used = 0;
+    return 0;
+}
+
+int ensure_dev(udpdk_gpu_ctx *c, void **p, size_t *cap, size_t need)
+{
+    if (*cap >= need) return 0;
+    if (*p) HIPC(c, hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIPC(c, hipMalloc(p, need));
+    *cap = need;
+    return 0;
+}
+
+int ensure_host(udpdk_gpu_ctx *c, void **p, size_t *cap, size_t need)
+{
+    if (*cap >= need) return 0;
+    if (*p) HIPC(c, hipHostFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIPC(c, hipHostMalloc(p, need, hipHostMallocDefault));
+    *cap = need;
+    return 0;
+}
+
+} // namespace
+
+extern "C" {
+
+int udpdk_gpu_abi_version(void) { return UDPDK_GPU_ABI_VERSION; }
+
+int udpdk_gpu_device_count(int *count)
+{
+    if (!count) return -EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return 0;
+}
+
+int udpdk_gpu_rx_geometry(uint32_t n, uint32_t n_lanes, uint32_t *tile_frames, uint32_t *n_tiles)
+{
+    if (!tile_frames || !n_tiles || n_lanes == 0) return -EINVAL;
+    geometry(n, n_lanes, tile_frames, n_tiles);
+    return 0;
+}
+
+int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, udpdk_gpu_ctx **out)
+{
+    if (!out || max_lanes == 0 || max_lanes > UDPDK_GPU_MAX_LANES || max_frames == 0) return -EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return -ENODEV;
+    udpdk_gpu_ctx *c = new (std::nothrow) udpdk_gpu_ctx();
+    if (!c) return -ENOMEM;
+    c->device = device;
+    c->max_frames = max_frames;
+    c->max_lanes = max_lanes;
+    int rc = -EIO;
+    do {
+        if (hipSetDevice(device) != hipSuccess) break;
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) break;
+        if (hipMalloc((void **)&c->port_tab, UDPDK_UDP_PORTS * 4) != hipSuccess) break;
+        if (hipMemset(c->port_tab, 0, UDPDK_UDP_PORTS * 4) != hipSuccess) break;
+        const uint64_t e_cap = std::max<uint64_t>((uint64_t)RX_HIST_CAP + max_lanes,
+                                                  (uint64_t)ceil_div(max_frames, RX_TILE_MAX) * max_lanes);
+        c->hist_cap = e_cap;
+        if (hipMalloc((void **)&c->hist, e_cap * 4) != hipSuccess) break;
+        c->partial_cap = ceil_div(e_cap, SCAN_CHUNK) + 1;
+        if (hipMalloc((void **)&c->partial, c->partial_cap * 4) != hipSuccess) break;
+        c->tiles_cap = ceil_div(max_frames, RX_TILE_MIN) + 1;
+        if (hipMalloc((void **)&c->tile_cnt, c->tiles_cap * UDPDK_N_COUNTERS * 4) != hipSuccess) break;
+        if (hipMalloc((void **)&c->counters, UDPDK_N_COUNTERS * 8) != hipSuccess) break;
+        if (hipMalloc((void **)&c->total, 64) != hipSuccess) break;
+        if (hipHostMalloc((void **)&c->h_counters, UDPDK_N_COUNTERS * 8, hipHostMallocDefault) != hipSuccess) break;
+        if (hipHostMalloc((void **)&c->h_total, 64, hipHostMallocDefault) != hipSuccess) break;
+        if (hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) break;
+        // rx_classify needs up to 90 KiB of dynamic LDS at 16384 lanes
+        if (hipFuncSetAttribute((const void *)rx_classify, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess) break;
+        if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess) break;
+        rc = 0;
+    } while (0);
+    if (rc) {
+        (void)hipGetLastError();
+        udpdk_gpu_ctx_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return 0;
+}
+
+int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
+{
+    if (!c) return 0;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void *dev[] = {c->port_tab, c->binds, c->slots, c->hist, c->partial, c->tile_cnt,
+                   c->counters, c->total, c->st_frames_d, c->st_desc_d, c->st_out_d};
+    for (void *p : dev) if (p) (void)hipFree(p);
+    void *host[] = {c->h_counters, c->h_total, c->st_frames_h, c->st_desc_h};
+    for (void *p : host) if (p) (void)hipHostFree(p);
+    if (c->sets) {
+        for (int i = 0; i < EVENT_SETS; ++i)
+            for (int k = 0; k < 4; ++k) (void)hipEventDestroy(c->sets[i].ev[k]);
+        delete[] c->sets;
+    }
+    if (c->done) (void)hipEventDestroy(c->done);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+int udpdk_gpu_sync(udpdk_gpu_ctx *c)
+{
+    if (!c) return -EINVAL;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int udpdk_gpu_last_hip_error(const udpdk_gpu_ctx *c) { return c ? c->last_err : 0; }
+
+void *udpdk_gpu_stream(udpdk_gpu_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int udpdk_gpu_alloc(udpdk_gpu_ctx *c, size_t bytes, void **dev)
+{
+    if (!c || !dev) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    // round up so 16-byte chunk loads past the last frame stay inside the allocation
+    const size_t b = ((bytes ? bytes : 1) + 255) & ~(size_t)255;
+    if (hipMalloc(dev, b) != hipSuccess) { (void)hipGetLastError(); *dev = nullptr; return -ENOMEM; }
+    return 0;
+}
+
+int udpdk_gpu_free(udpdk_gpu_ctx *c, void *dev)
+{
+    if (!c) return -EINVAL;
+    if (dev) HIPC(c, hipFree(dev));
+    return 0;
+}
+
+int udpdk_gpu_host_alloc(udpdk_gpu_ctx *c, size_t bytes, void **host)
+{
+    if (!c || !host) return -EINVAL;
+    if (hipHostMalloc(host, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        *host = nullptr;
+        return -ENOMEM;
+    }
+    return 0;
+}
+
+int udpdk_gpu_host_free(udpdk_gpu_ctx *c, void *host)
+{
+    if (!c) return -EINVAL;
+    if (host) HIPC(c, hipHostFree(host));
+    return 0;
+}
+
+int udpdk_gpu_memset(udpdk_gpu_ctx *c, void *dev, int value, size_t bytes)
+{
+    if (!c || (!dev && bytes)) return -EINVAL;
+    if (bytes) HIPC(c, hipMemsetAsync(dev, value, bytes, c->stream));
+    return 0;
+}
+
+int udpdk_gpu_h2d(udpdk_gpu_ctx *c, void *dev, const void *host, size_t bytes)
+{
+    if (!c || ((!dev || !host) && bytes)) return -EINVAL;
+    if (bytes) HIPC(c, hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, c->stream));
+    return 0;
+}
+
+int udpdk_gpu_d2h(udpdk_gpu_ctx *c, void *host, const void *dev, size_t bytes)
+{
+    if (!c || ((!dev || !host) && bytes)) return -EINVAL;
+    if (bytes) HIPC(c, hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, c->stream));
+    return 0;
+}
+
+int udpdk_gpu_bind_snapshot_upload(udpdk_gpu_ctx *c, const udpdk_bind_snapshot_t *s)
+{
+    if (!c || !s || !s->port_first || !s->port_count || (s->n_binds && !s->binds)) return -EINVAL;
+    if (s->n_lanes == 0 || s->n_lanes > c->max_lanes || s->n_binds > UDPDK_GPU_MAX_BINDS) return -EINVAL;
+    if (s->n_slots && !s->slots) return -EINVAL;
+    std::vector<uint32_t> tab(UDPDK_UDP_PORTS, 0u);
+    uint32_t maxfan = 0;
+    for (uint32_t p = 0; p < UDPDK_UDP_PORTS; ++p) {
+        const uint32_t cnt = s->port_count[p];
+        if (!cnt) continue;
+        const uint32_t first = s->port_first[p];
+        if (cnt > UDPDK_GPU_MAX_PORT_BINDS || (uint64_t)first + cnt > s->n_binds) return -EINVAL;
+        tab[p] = (first << 12) | cnt;
+        maxfan = std::max(maxfan, cnt);
+    }
+    std::vector<uint2> b(s->n_binds ? s->n_binds : 1);
+    for (uint32_t i = 0; i < s->n_binds; ++i) {
+        const udpdk_binding_t &x = s->binds[i];
+        if (x.sockfd < 0 || x.sockfd > 0xFFFF) return -EINVAL;
+        if (((uint32_t)x.sockfd & s->lane_mask) >= s->n_lanes) return -EINVAL;
+        b[i] = make_uint2(x.ip, (uint32_t)x.sockfd | (x.reuse ? 0x80000000u : 0u));
+    }
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    if (s->n_binds > c->binds_cap) {
+        if (c->binds) HIPC(c, hipFree(c->binds));
+        c->binds = nullptr;
+        c->binds_cap = 0;
+        HIPC(c, hipMalloc((void **)&c->binds, (size_t)s->n_binds * sizeof(uint2)));
+        c->binds_cap = s->n_binds;
+    }
+    if (!c->binds) {
+        HIPC(c, hipMalloc((void **)&c->binds, sizeof(uint2)));
+        c->binds_cap = 1;
+    }
+    HIPC(c, hipMemcpy(c->port_tab, tab.data(), UDPDK_UDP_PORTS * 4, hipMemcpyHostToDevice));
+    if (s->n_binds)
+        HIPC(c, hipMemcpy(c->binds, b.data(), (size_t)s->n_binds * sizeof(uint2), hipMemcpyHostToDevice));
+    if (s->n_slots) {
+        if (s->n_slots > c->slots_cap) {
+            if (c->slots) HIPC(c, hipFree(c->slots));
+            c->slots = nullptr;
+            HIPC(c, hipMalloc((void **)&c->slots, (size_t)s->n_slots * sizeof(uint4)));
+            c->slots_cap = s->n_slots;
+        }
+        std::vector<uint4> sl(s->n_slots);
+        for (uint32_t i = 0; i < s->n_slots; ++i)
+            sl[i] = make_uint4(s->slots[i].ip, s->slots[i].udp_port & 0xFFFFu, s->slots[i].bound ? 1u : 0u, 0u);
+        HIPC(c, hipMemcpy(c->slots, sl.data(), (size_t)s->n_slots * sizeof(uint4), hipMemcpyHostToDevice));
+    }
+    c->n_slots = s->n_slots;
+    c->n_lanes = s->n_lanes;
+    c->lane_mask = s->lane_mask;
+    uint32_t kb = 0;
+    while ((1u << kb) < s->n_lanes) ++kb;
+    c->key_bits = kb;
+    c->max_fanout = maxfan;
+    c->have_snapshot = true;
+    return 0;
+}
+
+int udpdk_gpu_timing_enable(udpdk_gpu_ctx *c, int enable)
+{
+    if (!c) return -EINVAL;
+    if (enable && !c->sets) {
+        c->sets = new (std::nothrow) TimingSet[EVENT_SETS];
+        if (!c->sets) return -ENOMEM;
+        for (int i = 0; i < EVENT_SETS; ++i)
+            for (int k = 0; k < 4; ++k) HIPC(c, hipEventCreate(&c->sets[i].ev[k]));
+    }
+    c->timing = enable != 0;
+    return 0;
+}
+
+int udpdk_gpu_timing_read(udpdk_gpu_ctx *c, double ms[UDPDK_N_KERNEL_IDS],
+                          uint32_t launches[UDPDK_N_KERNEL_IDS])
+{
+    if (!c) return -EINVAL;
+    int rc = fold_timing(c);
+    if (rc) return rc;
+    for (int k = 0; k < UDPDK_N_KERNEL_IDS; ++k) {
+        if (ms) ms[k] = c->ms[k];
+        if (launches) launches[k] = c->launches[k];
+        c->ms[k] = 0;
+        c->launches[k] = 0;
+    }
+    return 0;
+}
+
+int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_out_t *o)
+{
+    if (!c || !bt || !o || !c->have_snapshot) return -EINVAL;
+    if (bt->n > c->max_frames || bt->frames_bytes >= (1ull << 32)) return -EINVAL;
+    if (bt->n && (!bt->frames_dev || !bt->offset_dev || !bt->length_dev)) return -EINVAL;
+    if (((uintptr_t)bt->frames_dev & 15u) != 0) return -EINVAL;
+    if (!o->meta_dev && bt->n) return -EINVAL;
+    if (!o->lane_off_dev || (!o->lane_pkt_dev && o->lane_cap)) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    const uint32_t S = c->n_lanes;
+    c->last_lane_cap = o->lane_cap;
+    c->pending = true;
+    TimingSet *ts = nullptr;
+    if (c->timing) {
+        if (c->n_sets_used == EVENT_SETS) { int rc = fold_timing(c); if (rc) return rc; }
+        ts = &c->sets[c->n_sets_used++];
+    }
+    if (bt->n == 0) {
+        HIPC(c, hipMemsetAsync(o->lane_off_dev, 0, (size_t)(S + 1) * 4, c->stream));
+        HIPC(c, hipMemsetAsync(c->counters, 0, UDPDK_N_COUNTERS * 8, c->stream));
+        HIPC(c, hipMemsetAsync(c->total, 0, 4, c->stream));
+        if (ts) for (int k = 0; k < 4; ++k) HIPC(c, hipEventRecord(ts->ev[k], c->stream));
+    } else {
+        uint32_t T, tiles;
+        geometry(bt->n, S, &T, &tiles);
+        const uint64_t E = (uint64_t)S * tiles;
+        if (E > c->hist_cap || tiles > c->tiles_cap) return -EINVAL;
+
+        RxArgs ra;
+        ra.frames = bt->frames_dev;
+        ra.offset = bt->offset_dev;
+        ra.length = bt->length_dev;
+        ra.ptype = bt->ptype_dev;
+        ra.port_tab = c->port_tab;
+        ra.binds = c->binds;
+        ra.meta = o->meta_dev;
+        ra.hist = c->hist;
+        ra.tile_cnt = c->tile_cnt;
+        ra.frames_bytes = (uint32_t)bt->frames_bytes;
+        ra.rsrc_bytes = (uint32_t)std::min<uint64_t>((bt->frames_bytes + 15) & ~15ull, 0xFFFFFFFFull);
+        ra.n = bt->n;
+        ra.tile_frames = T;
+        ra.n_tiles = tiles;
+        ra.lane_mask = c->lane_mask;
+        ra.n_lanes = S;
+
+        if (ts) HIPC(c, hipEventRecord(ts->ev[0], c->stream));
+        hipLaunchKernelGGL(rx_classify, dim3(tiles), dim3(RX_BLOCK), classify_lds_bytes(S), c->stream, ra);
+        HIPC(c, hipGetLastError());
+        if (ts) HIPC(c, hipEventRecord(ts->ev[1], c->stream));
+
+        ScanArgs sa;
+        sa.hist = c->hist;
+        sa.partial = c->partial;
+        sa.lane_off = o->lane_off_dev;
+        sa.tile_cnt = c->tile_cnt;
+        sa.counters = c->counters;
+        sa.total = c->total;
+        sa.n_elems = (uint32_t)E;
+        sa.n_tiles = tiles;
+        sa.n_lanes = S;
+        if (E <= SCAN_SMALL_MAX) {
+            hipLaunchKernelGGL(rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 0, c->stream, sa);
+            HIPC(c, hipGetLastError());
+        } else {
+            const uint32_t nb = ceil_div(E, SCAN_CHUNK);
+            hipLaunchKernelGGL(rx_scan_reduce, dim3(nb), dim3(SCAN_BLOCK), 0, c->stream, sa);
+            HIPC(c, hipGetLastError());
+            hipLaunchKernelGGL(rx_scan_top, dim3(1), dim3(SCAN_BLOCK), 0, c->stream, sa, nb);
+            HIPC(c, hipGetLastError());
+            hipLaunchKernelGGL(rx_scan_down, dim3(nb), dim3(SCAN_BLOCK), 0, c->stream, sa);
+            HIPC(c, hipGetLastError());
+        }
+        if (ts) HIPC(c, hipEventRecord(ts->ev[2], c->stream));
+
+        ScatterArgs xa;
+        xa.meta = o->meta_dev;
+        xa.base = c->hist;
+        xa.frames = bt->frames_dev;
+        xa.offset = bt->offset_dev;
+        xa.port_tab = c->port_tab;
+        xa.binds = c->binds;
+        xa.lane_pkt = o->lane_pkt_dev;
+        xa.n = bt->n;
+        xa.tile_frames = T;
+        xa.n_tiles = tiles;
+        xa.n_lanes = S;
+        xa.lane_mask = c->lane_mask;
+        xa.key_bits = c->key_bits;
+        xa.lane_cap = o->lane_cap;
+        hipLaunchKernelGGL(rx_scatter, dim3(tiles), dim3(64), 4u * S, c->stream, xa);
+        HIPC(c, hipGetLastError());
+        if (ts) HIPC(c, hipEventRecord(ts->ev[3], c->stream));
+    }
+    HIPC(c, hipMemcpyAsync(c->h_counters, c->counters, UDPDK_N_COUNTERS * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(c->h_total, c->total, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipEventRecord(c->done, c->stream));
+    return 0;
+}
+
+int udpdk_gpu_rx_stats(udpdk_gpu_ctx *c, udpdk_rx_stats_t *st)
+{
+    if (!c || !st) return -EINVAL;
+    if (!c->pending) return -EINVAL;
+    HIPC(c, hipEventSynchronize(c->done));
+    for (int k = 0; k < UDPDK_N_COUNTERS; ++k) st->counters[k] = c->h_counters[k];
+    st->deliveries = *c->h_total;
+    st->overflow = st->deliveries > c->last_lane_cap ? 1u : 0u;
+    return st->overflow ? -ENOSPC : 0;
+}
+
+int udpdk_gpu_rx_host(udpdk_gpu_ctx *c, const uint8_t *frames_host, uint64_t frames_bytes,
+                      const uint32_t *offset_host, const uint16_t *length_host,
+                      const uint32_t *ptype_host, uint32_t n, uint32_t *meta_host,
+                      uint32_t *lane_off_host, uint32_t *lane_pkt_host, uint32_t lane_cap,
+                      udpdk_rx_stats_t *stats)
+{
+    if (!c || !stats || !lane_off_host || n > c->max_frames) return -EINVAL;
+    if (n && (!frames_host || !offset_host || !length_host || !meta_host)) return -EINVAL;
+    if (lane_cap && !lane_pkt_host) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    const size_t fb = ((size_t)frames_bytes + 255) & ~(size_t)255;
+    const size_t desc = (size_t)n * 10 + 64;
+    const size_t outb = (size_t)n * 4 + (size_t)(c->n_lanes + 1) * 4 + (size_t)lane_cap * 4 + 64;
+    int rc;
+    // The frames are expected in pinned memory (DPDK hugepage mbufs registered with the
+    // runtime); pageable input is copied into a pinned staging buffer first.
+    hipPointerAttribute_t attr;
+    const bool pinned = n && hipPointerGetAttributes(&attr, frames_host) == hipSuccess &&
+                        attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    if ((rc = ensure_dev(c, (void **)&c->st_frames_d, &c->st_frames_dcap, fb ? fb : 256))) return rc;
+    if (n && !pinned &&
+        (rc = ensure_host(c, (void **)&c->st_frames_h, &c->st_frames_hcap, fb ? fb : 256))) return rc;
+    if ((rc = ensure_dev(c, (void **)&c->st_desc_d, &c->st_desc_dcap, desc))) return rc;
+    if ((rc = ensure_host(c, (void **)&c->st_desc_h, &c->st_desc_hcap, desc))) return rc;
+    if ((rc = ensure_dev(c, (void **)&c->st_out_d, &c->st_out_cap, outb))) return rc;
+    const uint8_t *src = frames_host;
+    if (n && !pinned) {
+        memcpy(c->st_frames_h, frames_host, frames_bytes);
+        src = c->st_frames_h;
+    }
+    uint8_t *dh = c->st_desc_h;
+    memcpy(dh, offset_host, (size_t)n * 4);
+    memcpy(dh + (size_t)n * 4, length_host, (size_t)n * 2);
+    const size_t pt_off = ((size_t)n * 6 + 15) & ~(size_t)15;
+    if (ptype_host) memcpy(dh + pt_off, ptype_host, (size_t)n * 4);
+    if (n) HIPC(c, hipMemcpyAsync(c->st_frames_d, src, frames_bytes, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->st_desc_d, dh, pt_off + (ptype_host ? (size_t)n * 4 : 0),
+                           hipMemcpyHostToDevice, c->stream));
+
+    uint32_t *meta_d = (uint32_t *)c->st_out_d;
+    uint32_t *off_d = meta_d + n;
+    uint32_t *pkt_d = off_d + c->n_lanes + 1;
+    udpdk_rx_batch_t b = {c->st_frames_d, frames_bytes, (const uint32_t *)c->st_desc_d,
+                          (const uint16_t *)(c->st_desc_d + (size_t)n * 4),
+                          ptype_host ? (const uint32_t *)(c->st_desc_d + pt_off) : nullptr, n};
+    udpdk_rx_out_t o = {meta_d, off_d, pkt_d, lane_cap};
+    if ((rc = udpdk_gpu_rx(c, &b, &o))) return rc;
+    if (n) HIPC(c, hipMemcpyAsync(meta_host, meta_d, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(lane_off_host, off_d, (size_t)(c->n_lanes + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+    rc = udpdk_gpu_rx_stats(c, stats);
+    const uint32_t d = std::min(stats->deliveries, lane_cap);
+    if (d) HIPC(c, hipMemcpyAsync(lane_pkt_host, pkt_d, (size_t)d * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return rc;
+}
+
+int udpdk_gpu_tx_build(udpdk_gpu_ctx *c, const udpdk_tx_config_t *cfg, const udpdk_tx_batch_t *bt,
+                       const udpdk_tx_out_t *o)
+{
+    if (!c || !cfg || !bt || !o) return -EINVAL;
+    if (!bt->n) return 0;
+    if (!bt->payload_dev || !bt->payload_off_dev || !bt->payload_len_dev || !bt->sockfd_dev ||
+        !bt->dst_ip_dev || !bt->dst_port_dev || !o->frames_dev || !o->frame_off_dev) return -EINVAL;
+    if (!c->slots || !c->n_slots) return -EINVAL;
+    if (bt->payload_bytes >= (1ull << 32) || o->frames_bytes >= (1ull << 32)) return -EINVAL;
+    if (((uintptr_t)o->frames_dev & 15u) || ((uintptr_t)bt->payload_dev & 15u)) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    TxArgs ta;
+    ta.payload = bt->payload_dev;
+    ta.payload_off = bt->payload_off_dev;
+    ta.payload_len = bt->payload_len_dev;
+    ta.sockfd = bt->sockfd_dev;
+    ta.dst_ip = bt->dst_ip_dev;
+    ta.dst_port = bt->dst_port_dev;
+    ta.frame_off = o->frame_off_dev;
+    ta.slots = c->slots;
+    ta.frames = o->frames_dev;
+    ta.n = bt->n;
+    ta.n_slots = c->n_slots;
+    ta.payload_bytes = (uint32_t)bt->payload_bytes;
+    ta.payload_rsrc = (uint32_t)std::min<uint64_t>((bt->payload_bytes + 15) & ~15ull, 0xFFFFFFFFull);
+    ta.frames_bytes = (uint32_t)o->frames_bytes;
+    ta.src_ip = cfg->src_ip;
+    uint8_t mac[12];
+    memcpy(mac, cfg->dst_mac, 6);   // Ethernet d_addr first (udpdk_syscall.c:317)
+    memcpy(mac + 6, cfg->src_mac, 6);
+    memcpy(ta.mac_lo, mac, 12);
+    const uint32_t groups = ceil_div(bt->n, 64);
+    const uint32_t grid = std::min<uint32_t>(ceil_div(groups, TX_BLOCK / 64), 4096);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->timing) {
+        HIPC(c, hipEventCreate(&e0));
+        HIPC(c, hipEventCreate(&e1));
+        HIPC(c, hipEventRecord(e0, c->stream));
+    }
+    hipLaunchKernelGGL(tx_build, dim3(grid), dim3(TX_BLOCK), 0, c->stream, ta);
+    HIPC(c, hipGetLastError());
+    if (c->timing) {
+        HIPC(c, hipEventRecord(e1, c->stream));
+        HIPC(c, hipEventSynchronize(e1));
+        float ms = 0;
+        HIPC(c, hipEventElapsedTime(&ms, e0, e1));
+        c->ms[UDPDK_K_TX_BUILD] += ms;
+        c->launches[UDPDK_K_TX_BUILD]++;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    return 0;
+}
+
+} // extern "C"
