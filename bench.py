@@ -169,7 +169,7 @@ def main():
         raise SystemExit("bench.py needs a GPU (no HIP device visible)")
     device = local % ndev
     w = F.config_batch(args.config, n=args.frames, shard=rank)
-    ctx = abi.GpuContext(device, max_frames=max(w.batch.n, 1 << 20), max_lanes=max(w.n_sockets, 1))
+    ctx = abi.GpuContext(device, max_frames=max(w.batch.n, 1 << 22), max_lanes=4096)
     rx = Rx(ctx, w, args.rotate_mib << 20)
     wall, ms, n, st = time_loop(rx, args.steps, args.warmup, barrier, True)
     if dist is not None:

@@ -21,32 +21,44 @@ constexpr int TX_BLOCK = 256;
 
 // rx_classify LDS carve (one dynamic array, 16-byte aligned offsets: cdna_hip_programming.md
 // Guideline 17): per wave a 64 B header window per frame (80 B stride spreads the lane-per-frame
-// dword reads over banks), five 64-entry per-frame arrays, then block counters and the tile's
-// per-lane histogram.
+// dword reads over banks) and three 64-entry chunk-map arrays; block counters + misc words; then
+// either per-step delivered masks/counts (fused single-lane path) or the per-lane histogram.
 constexpr int HDR_STRIDE  = 80;
 constexpr int HDR_BYTES   = RX_WAVES * 64 * HDR_STRIDE;
-constexpr int WAVE_ARRAYS = 5;                    // chunk start, offset, length, ip sum, udp sum
+constexpr int WAVE_ARRAYS = 3;                    // chunk start, offset, length
 constexpr int ARR_BYTES   = RX_WAVES * WAVE_ARRAYS * 64 * 4;
 constexpr int CNT_OFF     = HDR_BYTES + ARR_BYTES;
-constexpr int HIST_OFF    = CNT_OFF + 64;
+constexpr int TAIL_OFF    = CNT_OFF + 80;         // 16 counters + 4 misc words
 
-__host__ __device__ constexpr uint32_t classify_lds_bytes(uint32_t n_lanes)
+__host__ __device__ constexpr uint32_t classify_lds_bytes(bool fused, uint32_t n_lanes,
+                                                          uint32_t steps)
 {
-    return (uint32_t)HIST_OFF + 4u * n_lanes;
+    return (uint32_t)TAIL_OFF + (fused ? 12u * steps : 4u * n_lanes);
 }
 
-// Packed snapshot entry per raw port: (index of first binding << 12) | count (<= 4095).
-// Binding: x = raw IPv4, y = sockfd | reuse << 31.
+// Port table entry (16 B per raw port): x = bindings on the port, y = index of the first in the
+// binding array, z/w = the first binding itself (ip, sockfd | reuse << 31), so single-binding
+// ports demultiplex with one load. Binding array entries: x = raw IPv4, y = sockfd | reuse << 31.
 struct RxArgs {
     const uint8_t  *frames;
     const uint32_t *offset;
     const uint16_t *length;
     const uint32_t *ptype;
-    const uint32_t *port_tab;
+    const uint4    *port_tab;
     const uint2    *binds;
     uint32_t *meta;
-    uint32_t *hist;       // [n_lanes][n_tiles]
-    uint32_t *tile_cnt;   // [n_tiles][16]
+    uint32_t *hist;       // [n_lanes][n_tiles]            (general path)
+    uint32_t *tile_cnt;   // [n_tiles][16]                 (general path)
+    unsigned long long *lb_state;   // [n_tiles][16] look-back granules (fused path)
+    uint32_t *ticket;     // dynamic tile order            (fused path)
+    uint32_t *err;        // = epoch of a call whose look-back timed out
+    uint32_t *lane_pkt;   // fused path writes the lane directly
+    uint32_t *lane_off;
+    unsigned long long *counters;
+    uint32_t *total;
+    uint32_t lane_cap;
+    uint32_t epoch;
+    uint32_t key_bits;
     uint32_t frames_bytes;
     uint32_t rsrc_bytes;  // buffer-resource range (frames_bytes rounded up to 16)
     uint32_t n;
@@ -73,7 +85,7 @@ struct ScatterArgs {
     const uint32_t *base;  // scanned hist
     const uint8_t  *frames;
     const uint32_t *offset;
-    const uint32_t *port_tab;
+    const uint4    *port_tab;
     const uint2    *binds;
     uint32_t *lane_pkt;
     uint32_t n;
@@ -104,7 +116,7 @@ struct TxArgs {
     uint32_t mac_lo[3];        // 12 MAC bytes: dst(6) src(6) as three LE dwords
 };
 
-__global__ void rx_classify(RxArgs a);
+template <bool FUSED> __global__ void rx_classify(RxArgs a);
 __global__ void rx_scan_small(ScanArgs a);
 __global__ void rx_scan_reduce(ScanArgs a);
 __global__ void rx_scan_top(ScanArgs a, uint32_t n_part);

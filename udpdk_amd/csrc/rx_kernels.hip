@@ -2,23 +2,26 @@
 //
 // Replaces, for a batch of N frames, N calls of reassemble() (udpdk_poller.c:316-413) from the
 // burst loop (udpdk_poller.c:516-545) plus the per-socket rx_buffer appends and ring flushes
-// (udpdk_poller.c:274-298). Three stages, all integer/byte work bound by HBM:
+// (udpdk_poller.c:274-298). All integer/byte work, bound by HBM:
 //
-//   rx_classify  one workgroup per tile of T frames. Frames are read once, as 16-byte chunks
-//                assigned to lanes so that a wave-instruction reads 1 KiB of consecutive bytes
-//                whatever the frame sizes. The first 64 B window of every frame is staged in
-//                LDS and parsed by the frame's lane; the RFC 1071 sums of the IPv4 header and
-//                the whole UDP datagram are accumulated per frame in LDS. Demux walks the
-//                flattened bind snapshot. Writes one verdict word per frame and the tile's
-//                per-lane delivery histogram (lane-major: hist[lane][tile]).
-//   rx_scan      exclusive scan of the lane-major histogram: hist[lane][tile] becomes the
-//                position of the tile's first delivery in that lane; lane_off falls out as
-//                hist[lane][0]. One launch when small, reduce/top/down-sweep otherwise.
-//   rx_scatter   one wave per tile walks its frames in order and writes each delivery at its
-//                stable position (wave multi-split by ballots, LDS running cursor per lane).
+//   rx_classify<FUSED>  one workgroup per tile of T frames, each wave walking 64-frame steps.
+//       Frames are read once as 16-byte chunks swept across lanes, so a wave-instruction reads
+//       1 KiB of consecutive bytes whatever the frame sizes. The first 64 B window of each frame
+//       is staged in LDS and parsed by the frame's lane; the UDP datagram sum is reduced per
+//       frame with a wave prefix scan over chunk sums (no LDS atomics); the IPv4 header sum comes
+//       from the parsed header. Steps are software-pipelined: the next step's descriptors and
+//       chunk loads are in flight while the current step is parsed and demultiplexed.
+//       Demux reads one 16-byte port-table entry (first binding inline) per frame.
+//       FUSED (one lane, fan-out <= 1: the single bound socket of apps/pktgen): tiles take a
+//       ticket, chain a decoupled look-back over tiles for the lane position and the 16 counters
+//       (8-byte {tag, value} granules, agent scope), and write the lane directly: one launch.
+//       General: writes the tile's per-lane delivery histogram (lane-major, hist[lane][tile]).
+//   rx_scan     exclusive scan of the lane-major histogram -> per-(lane, tile) start positions,
+//       lane_off, and the counter reduction. One launch when small, reduce/top/down otherwise.
+//   rx_scatter  one wave per tile writes each delivery at its stable position.
 //
-// Bytes per frame: frame_len (every byte is summed) + 6 (offset u32 + length u16) + 4 (verdict)
-// in rx_classify; + 4 (verdict re-read) + 4 per delivery in rx_scatter.
+// Algorithmic bytes per frame in rx_classify: frame_len + 6 (u32 offset + u16 length) + 4
+// (verdict word) [+ 4 lane entry when FUSED].
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,18 +41,16 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_wave_barrier();
 }
 
-// Exclusive prefix sum across the wave; *total = sum over all 64 lanes.
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total)
+// Inclusive prefix sum across the wave.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
 {
     const uint32_t lane = lane_id();
-    uint32_t x = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= (uint32_t)d) x += y;
+        const uint32_t y = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v += y;
     }
-    *total = __shfl(x, 63, 64);
-    return x - v;
+    return v;
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
@@ -59,27 +60,25 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
     return v;
 }
 
-// Bytes [a, e) of a 16-byte chunk as four dword masks (a, e clamped to [0, 16]).
+// Bytes [a, e) of a 16-byte chunk as a dword mask for dword i (a, e clamped to [0, 16]).
 __device__ __forceinline__ uint32_t dword_window(int a, int e, int i)
 {
-    int la = min(max(a - 4 * i, 0), 4);
-    int le = min(max(e - 4 * i, 0), 4);
-    uint32_t hm = le >= 4 ? 0xFFFFFFFFu : ((1u << (8 * le)) - 1u);
-    uint32_t lm = la >= 4 ? 0xFFFFFFFFu : ((1u << (8 * la)) - 1u);
+    const int la = min(max(a - 4 * i, 0), 4);
+    const int le = min(max(e - 4 * i, 0), 4);
+    const uint32_t hm = le >= 4 ? 0xFFFFFFFFu : ((1u << (8 * le)) - 1u);
+    const uint32_t lm = la >= 4 ? 0xFFFFFFFFu : ((1u << (8 * la)) - 1u);
     return hm & ~lm;
 }
 
-// Sum of the 16-bit halves of the masked dwords: <= 8 * 0xFFFF per chunk.
-__device__ __forceinline__ uint32_t masked_sum16(const uint32_t d[4], int a, int e)
+__device__ __forceinline__ uint32_t sum16(uint32_t v) { return (v & 0xFFFFu) + (v >> 16); }
+
+// Sum of the 16-bit halves of the bytes [a, e) of the chunk: <= 8 * 0xFFFF.
+__device__ __forceinline__ uint32_t chunk_sum(const uint4 d, int a, int e)
 {
-    if (e <= a) return 0;
-    uint32_t s = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        uint32_t v = d[i] & dword_window(a, e, i);
-        s += (v & 0xFFFFu) + (v >> 16);
-    }
-    return s;
+    if (e <= a) return 0u;
+    if (a <= 0 && e >= 16) return sum16(d.x) + sum16(d.y) + sum16(d.z) + sum16(d.w);
+    return sum16(d.x & dword_window(a, e, 0)) + sum16(d.y & dword_window(a, e, 1)) +
+           sum16(d.z & dword_window(a, e, 2)) + sum16(d.w & dword_window(a, e, 3));
 }
 
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
@@ -97,205 +96,383 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint3
                                              0x00020000);
 }
 
+__device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// 8-byte look-back granules: tag (epoch << 2 | kind) in the top 26 bits, value in the low 38.
+constexpr uint32_t LB_AGG = 1u, LB_INCL = 2u;
+constexpr int LB_VALUE_BITS = 38;
+constexpr unsigned long long LB_VALUE_MASK = (1ull << LB_VALUE_BITS) - 1ull;
+
 // ------------------------------------------------------------------------------------------
 // rx_classify
 // ------------------------------------------------------------------------------------------
+template <bool FUSED>
 __global__ void __launch_bounds__(RX_BLOCK)
 rx_classify(RxArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+    const uint32_t steps = a.tile_frames / 64;
 
-    uint8_t  *hdr  = smem + w * 64 * HDR_STRIDE;
-    uint32_t *arr  = reinterpret_cast<uint32_t *>(smem + HDR_BYTES) + w * WAVE_ARRAYS * 64;
-    uint32_t *l_cs = arr, *l_off = arr + 64, *l_len = arr + 128, *l_ip = arr + 192,
-             *l_udp = arr + 256;
-    uint32_t *cnt  = reinterpret_cast<uint32_t *>(smem + CNT_OFF);
-    uint32_t *hist = reinterpret_cast<uint32_t *>(smem + HIST_OFF);
+    uint8_t *hdr = smem + w * 64 * HDR_STRIDE;
+    uint32_t *arr = reinterpret_cast<uint32_t *>(smem + HDR_BYTES) + w * WAVE_ARRAYS * 64;
+    uint32_t *l_cs = arr, *l_off = arr + 64, *l_len = arr + 128;
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + CNT_OFF);
+    uint32_t *misc = cnt + UDPDK_N_COUNTERS;                 // [0] tile, [1..2] lane base
+    uint8_t *tail = smem + TAIL_OFF;
+    // FUSED: per-step delivered masks and counts; general: per-lane histogram
+    unsigned long long *smask = reinterpret_cast<unsigned long long *>(tail);
+    uint32_t *scnt = reinterpret_cast<uint32_t *>(tail + 8 * steps);
+    uint32_t *hist = reinterpret_cast<uint32_t *>(tail);
 
-    for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK) hist[s] = 0;
+    if (FUSED) {
+        if (tid == 0) {
+            const uint32_t t = atomicAdd(a.ticket, 1u);
+            if (t == a.n_tiles - 1u) atomicExch(a.ticket, 0u);  // every block has its ticket
+            misc[0] = t;
+        }
+    } else {
+        for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK) hist[s] = 0;
+    }
     if (tid < UDPDK_N_COUNTERS) cnt[tid] = 0;
     __syncthreads();
+    const uint32_t tile = FUSED ? misc[0] : xcd_remap(blockIdx.x, gridDim.x);
 
     const __amdgpu_buffer_rsrc_t fr = make_rsrc(a.frames, a.rsrc_bytes);
     const uint32_t t0 = tile * a.tile_frames;
     const uint32_t t1 = min(a.n, t0 + a.tile_frames);
-    const uint32_t steps = a.tile_frames / 64;
 
-    for (uint32_t st = w; st < steps; st += RX_WAVES) {
+    // per-lane counters (reduced once per tile)
+    uint32_t cv[UDPDK_N_COUNTERS];
+#pragma unroll
+    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) cv[c] = 0;
+
+    // ---- software pipeline state ----
+    uint32_t st = w;
+    uint32_t c_off = 0, c_len = 0;     // descriptors of step st (frame lane)
+    uint32_t n_off = 0, n_len = 0;     // descriptors of step st + RX_WAVES
+    auto load_desc = [&](uint32_t s, uint32_t &o, uint32_t &l) {
+        const uint32_t p = t0 + s * 64 + lane;
+        const bool v = s < steps && p < t1;
+        o = v ? a.offset[p] : 0u;
+        l = v ? (uint32_t)a.length[p] : 0u;
+    };
+    uint32_t total = 0, my_cs = 0, my_nch = 0;
+    uint4 R[RX_UNROLL];
+    uint32_t Rq[RX_UNROLL];
+    // set up step s: chunk map in LDS, iteration-0 chunk loads in flight
+    auto setup = [&](uint32_t s, uint32_t o, uint32_t l) {
+        const uint32_t p = t0 + s * 64 + lane;
+        const bool v = p < t1;
+        const bool bad = v && ((uint64_t)o + l > (uint64_t)a.frames_bytes);
+        my_nch = (v && !bad && l) ? (((o & 15u) + l + 15u) >> 4) : 0u;
+        const uint32_t inc = wave_incl_scan(my_nch);
+        my_cs = inc - my_nch;
+        total = __shfl(inc, 63, 64);
+        l_cs[lane] = my_cs;
+        l_off[lane] = o;
+        l_len[lane] = l;
+        wave_sync();
+#pragma unroll
+        for (int u = 0; u < RX_UNROLL; ++u) {
+            const uint32_t k = u * 64 + lane;
+            uint32_t q = 0;
+#pragma unroll
+            for (int sft = 32; sft >= 1; sft >>= 1)
+                if (l_cs[q + sft] <= k) q += sft;
+            Rq[u] = q;
+            R[u] = k < total ? load16(fr, (l_off[q] & ~15u) + 16u * (k - l_cs[q])) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    // consume the chunks in R (iteration starting at chunk k0): header windows + UDP sums
+    auto consume = [&](uint32_t k0, uint32_t &usum) {
+#pragma unroll
+        for (int u = 0; u < RX_UNROLL; ++u) {
+            const uint32_t base = k0 + u * 64;
+            const uint32_t k = base + lane;
+            const uint32_t q = Rq[u];
+            uint32_t part = 0;
+            if (k < total) {
+                const uint32_t j = k - l_cs[q];
+                const uint32_t fo = l_off[q];
+                if (j < 4)
+                    *reinterpret_cast<uint4 *>(hdr + q * HDR_STRIDE + 16 * j) = R[u];
+                const int rel = (int)(((fo & ~15u) + 16u * j) - fo);
+                part = chunk_sum(R[u], 34 - rel, (int)l_len[q] - rel);
+            }
+            const uint32_t P = wave_incl_scan(part);
+            // this frame's chunks inside [base, base + 64)
+            const uint32_t lo = max(my_cs, base), hi = min(my_cs + my_nch, base + 64u);
+            const uint32_t ph = __shfl(P, (int)((hi > base ? hi - 1u - base : 0u) & 63u), 64);
+            const uint32_t pl = __shfl(P, (int)((lo > base ? lo - 1u - base : 0u) & 63u), 64);
+            if (lo < hi) usum += ph - (lo > base ? pl : 0u);
+        }
+    };
+
+    if (st < steps) {
+        load_desc(st, c_off, c_len);
+        setup(st, c_off, c_len);
+        if (st + RX_WAVES < steps) load_desc(st + RX_WAVES, n_off, n_len);
+    }
+
+    while (st < steps) {
         const uint32_t p = t0 + st * 64 + lane;
         const bool valid = p < t1;
-        const uint32_t off = valid ? a.offset[p] : 0u;
-        const uint32_t len = valid ? (uint32_t)a.length[p] : 0u;
+        const uint32_t off = c_off, len = c_len;
         const bool bad_desc = valid && ((uint64_t)off + len > (uint64_t)a.frames_bytes);
-        const uint32_t nch = (valid && !bad_desc && len) ? (((off & 15u) + len + 15u) >> 4) : 0u;
-        uint32_t total;
-        const uint32_t cs = wave_excl_scan(nch, &total);
-        l_cs[lane] = cs;
-        l_off[lane] = off;
-        l_len[lane] = len;
-        l_ip[lane] = 0;
-        l_udp[lane] = 0;
-        wave_sync();
 
-        // ---- chunk sweep: lane k of the sweep reads the k-th 16-byte chunk of this step ----
-        for (uint32_t k0 = 0; k0 < total; k0 += 64 * RX_UNROLL) {
-            uint32_t d[RX_UNROLL][4];
-            uint32_t q[RX_UNROLL], j[RX_UNROLL];
-            int rel[RX_UNROLL];
+        // ---- finish the chunk sweep of step st ----
+        uint32_t usum = 0;
+        consume(0, usum);
+        for (uint32_t k0 = 64 * RX_UNROLL; k0 < total; k0 += 64 * RX_UNROLL) {
 #pragma unroll
             for (int u = 0; u < RX_UNROLL; ++u) {
                 const uint32_t k = k0 + u * 64 + lane;
-                // last frame whose first chunk index is <= k (frames with no chunk are skipped)
-                uint32_t qq = 0;
+                uint32_t q = 0;
 #pragma unroll
                 for (int sft = 32; sft >= 1; sft >>= 1)
-                    if (l_cs[qq + sft] <= k) qq += sft;
-                q[u] = qq;
-                j[u] = k - l_cs[qq];
-                const uint32_t fo = l_off[qq];
-                const uint32_t base = (fo & ~15u) + 16u * j[u];
-                rel[u] = (int)(base - fo);
-                if (k < total) {
-                    auto v = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)base, 0, 0);
-                    d[u][0] = v[0]; d[u][1] = v[1]; d[u][2] = v[2]; d[u][3] = v[3];
-                } else {
-                    d[u][0] = d[u][1] = d[u][2] = d[u][3] = 0u;
-                }
+                    if (l_cs[q + sft] <= k) q += sft;
+                Rq[u] = q;
+                R[u] = k < total ? load16(fr, (l_off[q] & ~15u) + 16u * (k - l_cs[q])) : make_uint4(0, 0, 0, 0);
             }
-#pragma unroll
-            for (int u = 0; u < RX_UNROLL; ++u) {
-                const uint32_t k = k0 + u * 64 + lane;
-                if (k >= total) continue;
-                const uint32_t qq = q[u];
-                if (j[u] < 4) {
-                    uint32_t *hw = reinterpret_cast<uint32_t *>(hdr + qq * HDR_STRIDE + 16 * j[u]);
-                    *reinterpret_cast<uint4 *>(hw) = make_uint4(d[u][0], d[u][1], d[u][2], d[u][3]);
-                }
-                const int r = rel[u];
-                const int flen = (int)l_len[qq];
-                const uint32_t ip = masked_sum16(d[u], 14 - r, 34 - r);
-                const uint32_t ud = masked_sum16(d[u], 34 - r, flen - r);
-                if (ip) atomicAdd(&l_ip[qq], ip);
-                if (ud) atomicAdd(&l_udp[qq], ud);
-            }
+            consume(k0, usum);
         }
         wave_sync();
 
+        // ---- start the next step of this wave: its loads overlap the parse below ----
+        const uint32_t nst = st + RX_WAVES;
+        if (nst < steps) {
+            setup(nst, n_off, n_len);
+            c_off = n_off;
+            c_len = n_len;
+            if (nst + RX_WAVES < steps) load_desc(nst + RX_WAVES, n_off, n_len);
+        }
+
         // ---- per-frame parse (lane = frame) from the staged 64-byte window ----
         uint32_t word = 0, verdict = UDPDK_V_BAD_DESC, fan = 0, first = 0;
-        bool ip_bad = false, udp_ok = false, udp_bad = false, udp_none = false, len_bad = false,
-             ihl_ne5 = false;
         if (valid && !bad_desc) {
             const uint32_t sh = off & 15u;
-            const uint32_t *hw = reinterpret_cast<const uint32_t *>(hdr + lane * HDR_STRIDE +
-                                                                   (sh & ~3u));
+            const uint32_t *hw = reinterpret_cast<const uint32_t *>(hdr + lane * HDR_STRIDE + (sh & ~3u));
             uint32_t raw[12], h[11];
 #pragma unroll
             for (int i = 0; i < 12; ++i) raw[i] = hw[i];
 #pragma unroll
             for (int i = 0; i < 11; ++i) h[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh & 3u);
             // h[i] = frame bytes 4i .. 4i+3 (little-endian)
+            cv[UDPDK_C_BYTES] += len;
             uint32_t pt;
             if (a.ptype) pt = a.ptype[p];
             else pt = len >= 14 ? (((h[3] & 0xFFFFu) == 0x0008u) ? 0x211u : 0x1u) : 0u;
             if (!(pt & 0x10u)) {
-                verdict = UDPDK_V_NOT_IPV4;               // udpdk_poller.c:334, :362-366
+                verdict = UDPDK_V_NOT_IPV4;                       // udpdk_poller.c:334, :362-366
             } else if (len < 42) {
                 verdict = UDPDK_V_TRUNC;
             } else {
-                const uint32_t ipsum = l_ip[lane];
-                const bool ip_ok = ipsum != 0u && (ipsum % 65535u) == 0u;
-                ip_bad = !ip_ok;
-                ihl_ne5 = ((h[3] >> 16) & 0x0Fu) != 5u;
+                // IPv4 header checksum over the fixed 20 bytes at offset 14 (RFC 1071)
+                const uint32_t ipraw = (h[3] >> 16) + sum16(h[4]) + sum16(h[5]) + sum16(h[6]) +
+                                       sum16(h[7]) + (h[8] & 0xFFFFu);
+                const bool ip_ok = ipraw != 0u && (ipraw % 65535u) == 0u;
+                const bool ihl_ne5 = ((h[3] >> 16) & 0x0Fu) != 5u;
+                cv[UDPDK_C_IP_BAD] += ip_ok ? 0u : 1u;
+                cv[UDPDK_C_IHL_NE5] += ihl_ne5 ? 1u : 0u;
                 word |= (ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8;
                 const uint32_t frag = ((h[5] & 0xFFu) << 8) | ((h[5] >> 8) & 0xFFu);
                 if ((frag & 0x2000u) || (frag & 0x1FFFu)) {
-                    verdict = UDPDK_V_FRAG;               // udpdk_poller.c:338
+                    verdict = UDPDK_V_FRAG;                       // udpdk_poller.c:338
                 } else if ((h[5] >> 24) != 17u) {
-                    verdict = UDPDK_V_NOT_UDP;            // udpdk_poller.c:368-371
+                    verdict = UDPDK_V_NOT_UDP;                    // udpdk_poller.c:368-371
                 } else {
                     const uint32_t src = (h[6] >> 16) | (h[7] << 16);
                     const uint32_t dip = (h[7] >> 16) | (h[8] << 16);   // poller.c:373
                     const uint32_t dport = h[9] & 0xFFFFu;               // poller.c:372
+                    // issue the demux load first: it overlaps the checksum arithmetic
+                    const uint4 e = a.port_tab[dport];
                     const uint32_t ulen_raw = h[9] >> 16;
                     const uint32_t ulen = ((ulen_raw & 0xFFu) << 8) | (ulen_raw >> 8);
                     const uint32_t ucks = h[10] & 0xFFFFu;
-                    len_bad = ulen < 8u || 34u + ulen > len;
+                    const bool len_bad = ulen < 8u || 34u + ulen > len;
                     uint32_t state;
                     if (ucks == 0u) {
                         state = UDPDK_UDP_CSUM_NONE;
                     } else if (len_bad) {
                         state = UDPDK_UDP_CSUM_BAD;
                     } else {
-                        uint32_t s = l_udp[lane] % 65535u;
-                        if (34u + ulen < len) {            // Ethernet padding after the datagram
+                        uint32_t s = usum % 65535u;
+                        if (34u + ulen < len) {                    // Ethernet padding after the datagram
                             uint32_t pad = 0;
                             for (uint32_t b = off + 34u + ulen; b < off + len; ++b)
                                 pad += (uint32_t)a.frames[b] << (8u * (b & 1u));
                             s = (s + 65535u - pad % 65535u) % 65535u;
                         }
-                        if (off & 1u) s = (s * 256u) % 65535u;           // odd start: swap bytes
+                        if (off & 1u) s = (s * 256u) % 65535u;   // odd start: words byte-swapped
                         const uint32_t pseudo = (src & 0xFFFFu) + (src >> 16) + (dip & 0xFFFFu) +
                                                 (dip >> 16) + 0x1100u + ulen_raw;
-                        state = ((s + pseudo) % 65535u) == 0u ? UDPDK_UDP_CSUM_OK
-                                                             : UDPDK_UDP_CSUM_BAD;
+                        state = ((s + pseudo) % 65535u) == 0u ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD;
                     }
-                    udp_ok = state == UDPDK_UDP_CSUM_OK;
-                    udp_bad = state == UDPDK_UDP_CSUM_BAD;
-                    udp_none = state == UDPDK_UDP_CSUM_NONE;
+                    cv[UDPDK_C_UDP_OK] += state == UDPDK_UDP_CSUM_OK ? 1u : 0u;
+                    cv[UDPDK_C_UDP_BAD] += state == UDPDK_UDP_CSUM_BAD ? 1u : 0u;
+                    cv[UDPDK_C_UDP_NONE] += state == UDPDK_UDP_CSUM_NONE ? 1u : 0u;
+                    cv[UDPDK_C_LEN_BAD] += len_bad ? 1u : 0u;
                     word |= state << 5 | (len_bad ? 1u : 0u) << 7;
 
                     // ---- demux: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
-                    const uint32_t e = a.port_tab[dport];
-                    const uint32_t nb = e & 0xFFFu;
-                    if (nb == 0u) {
+                    if (e.x == 0u) {
                         verdict = UDPDK_V_NO_BIND;
                     } else {
-                        const uint32_t b0 = e >> 12;
-                        for (uint32_t i = 0; i < nb; ++i) {
-                            const uint2 b = a.binds[b0 + i];
-                            if (dip == b.x || b.x == 0u) {                // poller.c:391
-                                const uint32_t sock = b.y & 0x7FFFFFFFu;
-                                atomicAdd(&hist[sock & a.lane_mask], 1u);   // poller.c:393
+                        uint32_t bip = e.z, bsr = e.w;
+                        for (uint32_t i = 0;;) {
+                            if (dip == bip || bip == 0u) {                // poller.c:391
+                                const uint32_t sock = bsr & 0x7FFFFFFFu;
+                                if (!FUSED && fan > 0)
+                                    atomicAdd(&hist[sock & a.lane_mask], 1u); // clones (rare)
                                 if (fan == 0) first = sock;
                                 ++fan;
-                                if (!(b.y >> 31)) break;                 // poller.c:396-403
+                                if (!(bsr >> 31)) break;                 // poller.c:396-403
                             }
+                            if (++i >= e.x) break;
+                            const uint2 b = a.binds[e.y + i];
+                            bip = b.x;
+                            bsr = b.y;
                         }
                         verdict = fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
                     }
                 }
             }
         }
-        word |= verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
-        if (valid) a.meta[p] = word;
-
-        // ---- per-tile counters via ballots (no per-frame logging, cf. poller.c:363-410) ----
-        uint32_t cv[UDPDK_N_COUNTERS];
+        if (valid) {
+            word |= verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
+            a.meta[p] = word;
 #pragma unroll
-        for (int v = 0; v < UDPDK_N_VERDICTS; ++v)
-            cv[v] = (uint32_t)__popcll(__ballot(valid && verdict == (uint32_t)v));
-        cv[UDPDK_C_DELIVERIES] = wave_sum(valid ? fan : 0u);
-        cv[UDPDK_C_IP_BAD] = (uint32_t)__popcll(__ballot(valid && ip_bad));
-        cv[UDPDK_C_UDP_OK] = (uint32_t)__popcll(__ballot(valid && udp_ok));
-        cv[UDPDK_C_UDP_BAD] = (uint32_t)__popcll(__ballot(valid && udp_bad));
-        cv[UDPDK_C_UDP_NONE] = (uint32_t)__popcll(__ballot(valid && udp_none));
-        cv[UDPDK_C_LEN_BAD] = (uint32_t)__popcll(__ballot(valid && len_bad));
-        cv[UDPDK_C_IHL_NE5] = (uint32_t)__popcll(__ballot(valid && ihl_ne5));
-        cv[UDPDK_C_BYTES] = wave_sum(valid && !bad_desc ? len : 0u);
-        if (lane == 0) {
-#pragma unroll
-            for (int c = 0; c < UDPDK_N_COUNTERS; ++c)
-                if (cv[c]) atomicAdd(&cnt[c], cv[c]);
+            for (int v = 0; v < UDPDK_N_VERDICTS; ++v) cv[v] += verdict == (uint32_t)v ? 1u : 0u;
+            cv[UDPDK_C_DELIVERIES] += fan;
+        }
+        const bool delivered = valid && fan > 0u;
+        if (FUSED) {
+            const unsigned long long m = __ballot(delivered);
+            if (lane == 0) {
+                smask[st] = m;
+                scnt[st] = (uint32_t)__popcll(m);
+            }
+        } else {
+            // first delivery of every frame into the tile histogram; small key spaces are
+            // aggregated with a wave multi-split first (all 64 lanes may share one lane)
+            const uint32_t key = first & a.lane_mask;
+            if (a.key_bits <= 4u) {
+                unsigned long long peers = __ballot(delivered);
+                for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
+                    const bool kb = (key >> bit) & 1u;
+                    const unsigned long long bal = __ballot(kb);
+                    peers &= kb ? bal : ~bal;
+                }
+                if (delivered && lane == (uint32_t)__ffsll((long long)peers) - 1u)
+                    atomicAdd(&hist[key], (uint32_t)__popcll(peers));
+            } else if (delivered) {
+                atomicAdd(&hist[key], 1u);
+            }
         }
         wave_sync();
+        st = nst;
+    }
+
+    // ---- tile counters ----
+#pragma unroll
+    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) {
+        const uint32_t s = wave_sum(cv[c]);
+        if (lane == 0 && s) atomicAdd(&cnt[c], s);
     }
     __syncthreads();
-    for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK) a.hist[(size_t)s * a.n_tiles + tile] = hist[s];
-    if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = cnt[tid];
+
+    if (!FUSED) {
+        for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK)
+            a.hist[(size_t)s * a.n_tiles + tile] = hist[s];
+        if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = cnt[tid];
+        return;
+    }
+
+    // ---- FUSED: step prefix, decoupled look-back over tiles, lane writes ----
+    if (w == 0) {
+        // exclusive prefix of per-step delivered counts (steps <= 256: 4 per lane)
+        uint32_t v[4], s4 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t si = lane * 4 + i;
+            v[i] = si < steps ? scnt[si] : 0u;
+            s4 += v[i];
+        }
+        uint32_t run = wave_incl_scan(s4) - s4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t si = lane * 4 + i;
+            if (si < steps) scnt[si] = run;
+            run += v[i];
+        }
+        // look-back: lanes 0..15 carry the 16 counters (lane 8 = deliveries = lane position)
+        unsigned long long *state = reinterpret_cast<unsigned long long *>(a.lb_state);
+        const unsigned long long agg = lane < UDPDK_N_COUNTERS ? cnt[lane] : 0ull;
+        const unsigned long long tagA = (unsigned long long)((a.epoch << 2) | LB_AGG) << LB_VALUE_BITS;
+        const unsigned long long tagI = (unsigned long long)((a.epoch << 2) | LB_INCL) << LB_VALUE_BITS;
+        if (lane < UDPDK_N_COUNTERS)
+            __hip_atomic_store(&state[(size_t)tile * UDPDK_N_COUNTERS + lane], tagA | agg,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long excl = 0;
+        bool timeout = false;
+        for (int32_t pt = (int32_t)tile - 1; pt >= 0; --pt) {
+            unsigned long long x = 0;
+            uint32_t kind = 0;
+            for (uint32_t spins = 0;; ++spins) {
+                x = lane < UDPDK_N_COUNTERS
+                        ? __hip_atomic_load(&state[(size_t)pt * UDPDK_N_COUNTERS + lane],
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : 0ull;
+                const uint32_t tg = (uint32_t)(x >> LB_VALUE_BITS);
+                const bool mine = lane >= UDPDK_N_COUNTERS || (tg >> 2) == a.epoch;
+                const unsigned long long incl = __ballot(lane < UDPDK_N_COUNTERS && mine && (tg & 3u) == LB_INCL);
+                const unsigned long long aggm = __ballot(lane < UDPDK_N_COUNTERS && mine && (tg & 3u) == LB_AGG);
+                const unsigned long long need = (1ull << UDPDK_N_COUNTERS) - 1ull;
+                if (incl == need) { kind = LB_INCL; break; }
+                if (aggm == need) { kind = LB_AGG; break; }
+                if (spins > (1u << 22)) { timeout = true; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (timeout) break;
+            excl += x & LB_VALUE_MASK;
+            if (kind == LB_INCL) break;
+        }
+        if (timeout && lane == 0) atomicExch(a.err, a.epoch);
+        if (lane < UDPDK_N_COUNTERS)
+            __hip_atomic_store(&state[(size_t)tile * UDPDK_N_COUNTERS + lane],
+                               tagI | ((excl + agg) & LB_VALUE_MASK), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t base = (uint32_t)__shfl((uint32_t)excl, UDPDK_C_DELIVERIES, 64);
+        if (lane == 0) misc[1] = base;
+        if (tile == a.n_tiles - 1u) {                       // last tile holds the totals
+            if (lane < UDPDK_N_COUNTERS) a.counters[lane] = excl + agg;
+            const uint32_t tot = (uint32_t)__shfl((uint32_t)(excl + agg), UDPDK_C_DELIVERIES, 64);
+            if (lane == 0) {
+                a.lane_off[0] = 0u;
+                a.lane_off[1] = tot;
+                *a.total = tot;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t base = misc[1];
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (uint32_t s = w; s < steps; s += RX_WAVES) {
+        const unsigned long long m = smask[s];
+        if ((m >> lane) & 1ull) {
+            const uint32_t pos = base + scnt[s] + (uint32_t)__popcll(m & lt);
+            if (pos < a.lane_cap) a.lane_pkt[pos] = t0 + s * 64 + lane;
+        }
+    }
 }
+
+template __global__ void rx_classify<false>(RxArgs);
+template __global__ void rx_classify<true>(RxArgs);
 
 // ------------------------------------------------------------------------------------------
 // rx_scan: exclusive scan of hist[E] (lane-major) in place; lane_off; counter reduction
@@ -303,9 +480,8 @@ rx_classify(RxArgs a)
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds16, uint32_t *total)
 {
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t wt;
-    const uint32_t x = wave_excl_scan(v, &wt);
-    if (lane == 0) lds16[w] = wt;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) lds16[w] = inc;
     __syncthreads();
     uint32_t pre = 0, tot = 0;
     for (uint32_t i = 0; i < nw; ++i) {
@@ -315,31 +491,49 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds16,
     }
     __syncthreads();
     *total = tot;
-    return pre + x;
+    return pre + inc - v;
 }
 
-// Counter reduction over tiles: counters[c] = sum_t tile_cnt[t][c] (64-bit).
+// counters[c] = sum over tiles of tile_cnt[t][c] (64-bit): each thread sums whole rows.
 __device__ void reduce_counters(const uint32_t *tile_cnt, uint32_t n_tiles,
                                 unsigned long long *counters, unsigned long long *lds)
 {
-    const uint32_t tid = threadIdx.x;
-    if (tid < UDPDK_N_COUNTERS) lds[tid] = 0;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    unsigned long long s[UDPDK_N_COUNTERS];
+#pragma unroll
+    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) s[c] = 0;
+    const uint4 *rows = reinterpret_cast<const uint4 *>(tile_cnt);
+#pragma unroll 2
+    for (uint32_t t = tid; t < n_tiles; t += blockDim.x) {
+        const uint4 r0 = rows[t * 4 + 0], r1 = rows[t * 4 + 1], r2 = rows[t * 4 + 2], r3 = rows[t * 4 + 3];
+        s[0] += r0.x; s[1] += r0.y; s[2] += r0.z; s[3] += r0.w;
+        s[4] += r1.x; s[5] += r1.y; s[6] += r1.z; s[7] += r1.w;
+        s[8] += r2.x; s[9] += r2.y; s[10] += r2.z; s[11] += r2.w;
+        s[12] += r3.x; s[13] += r3.y; s[14] += r3.z; s[15] += r3.w;
+    }
+    if (tid < UDPDK_N_COUNTERS * 16) lds[tid] = 0;
     __syncthreads();
-    const uint32_t c = tid % UDPDK_N_COUNTERS;
-    unsigned long long s = 0;
-    for (uint32_t t = tid / UDPDK_N_COUNTERS; t < n_tiles; t += blockDim.x / UDPDK_N_COUNTERS)
-        s += tile_cnt[(size_t)t * UDPDK_N_COUNTERS + c];
-    atomicAdd(&lds[c], s);
+#pragma unroll
+    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) {
+        unsigned long long v = s[c];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        if (lane == 0) lds[w * UDPDK_N_COUNTERS + c] = v;
+    }
     __syncthreads();
-    if (tid < UDPDK_N_COUNTERS) counters[tid] = lds[tid];
+    if (tid < UDPDK_N_COUNTERS) {
+        unsigned long long t = 0;
+        for (uint32_t i = 0; i < blockDim.x / 64; ++i) t += lds[i * UDPDK_N_COUNTERS + tid];
+        counters[tid] = t;
+    }
 }
 
-// Small case: one workgroup of SCAN_BLOCK threads, E <= SCAN_BLOCK * SCAN_SMALL_PER.
+// Small case: one workgroup of SCAN_BLOCK threads, E <= SCAN_SMALL_MAX.
 __global__ void __launch_bounds__(SCAN_BLOCK)
 rx_scan_small(ScanArgs a)
 {
     __shared__ uint32_t lds16[SCAN_BLOCK / 64];
-    __shared__ unsigned long long lcnt[UDPDK_N_COUNTERS];
+    __shared__ unsigned long long lcnt[UDPDK_N_COUNTERS * 16];
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (a.n_elems + SCAN_BLOCK - 1) / SCAN_BLOCK;
     const uint32_t i0 = tid * per, i1 = min(a.n_elems, i0 + per);
@@ -383,7 +577,7 @@ __global__ void __launch_bounds__(SCAN_BLOCK)
 rx_scan_top(ScanArgs a, uint32_t n_part)
 {
     __shared__ uint32_t lds16[SCAN_BLOCK / 64];
-    __shared__ unsigned long long lcnt[UDPDK_N_COUNTERS];
+    __shared__ unsigned long long lcnt[UDPDK_N_COUNTERS * 16];
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (n_part + SCAN_BLOCK - 1) / SCAN_BLOCK;
     const uint32_t i0 = tid * per, i1 = min(n_part, i0 + per);
@@ -431,14 +625,6 @@ rx_scan_down(ScanArgs a)
 // ------------------------------------------------------------------------------------------
 // rx_scatter: stable per-lane compaction, one wave per tile
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lane_cursor(uint32_t *cur, const ScatterArgs &a, uint32_t key,
-                                                uint32_t tile)
-{
-    uint32_t c = cur[key];
-    if (c == 0xFFFFFFFFu) c = a.base[(size_t)key * a.n_tiles + tile];
-    return c;
-}
-
 __global__ void __launch_bounds__(64)
 rx_scatter(ScatterArgs a)
 {
@@ -446,65 +632,80 @@ rx_scatter(ScatterArgs a)
     uint32_t *cur = reinterpret_cast<uint32_t *>(smem);   // running position per lane
     const uint32_t lane = lane_id();
     const uint32_t tile = blockIdx.x;
-    for (uint32_t s = lane; s < a.n_lanes; s += 64) cur[s] = 0xFFFFFFFFu;
+    // cursor of every lane for this tile (independent loads, one latency)
+#pragma unroll 8
+    for (uint32_t s = lane; s < a.n_lanes; s += 64) cur[s] = a.base[(size_t)s * a.n_tiles + tile];
     wave_sync();
     const uint32_t t0 = tile * a.tile_frames;
     const uint32_t t1 = min(a.n, t0 + a.tile_frames);
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
 
-    for (uint32_t f0 = t0; f0 < t1; f0 += 64) {
-        const uint32_t p = f0 + lane;
-        const bool valid = p < t1;
-        const uint32_t m = valid ? a.meta[p] : 0u;
-        const bool deliver = valid && UDPDK_META_VERDICT(m) == UDPDK_V_DELIVERED;
-        const uint32_t fan = UDPDK_META_FANOUT(m);
-        const uint64_t multi = __ballot(deliver && fan > 1u);
-        if (multi == 0ull) {
-            // fast path: one delivery per frame. Wave multi-split on the lane key.
-            const uint32_t key = UDPDK_META_SOCKFD(m) & a.lane_mask;
-            uint64_t peers = __ballot(deliver);
-            for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
-                const bool kb = (key >> bit) & 1u;
-                const uint64_t bal = __ballot(kb);
-                peers &= kb ? bal : ~bal;
-            }
-            const uint32_t leader = deliver ? (uint32_t)__ffsll((long long)peers) - 1u : 64u;
-            uint32_t c = 0;
-            if (deliver && lane == leader) {
-                c = lane_cursor(cur, a, key, tile);
-                cur[key] = c + (uint32_t)__popcll(peers);
-            }
-            c = __shfl(c, deliver ? (int)leader : 0, 64);
-            const uint32_t pos = c + (uint32_t)__popcll(peers & lt_mask);
-            if (deliver && pos < a.lane_cap) a.lane_pkt[pos] = p;
-        } else {
-            // fan-out path (SO_REUSEADDR/SO_REUSEPORT clones, poller.c:396-399): deliveries in
-            // frame order, then list order, re-derived from the frame header. Serial in lane 0.
-            if (lane == 0) {
-                for (uint32_t i = 0; i < 64 && f0 + i < t1; ++i) {
-                    const uint32_t mi = a.meta[f0 + i];
+    constexpr int PF = 8;                                 // verdict words prefetched per lane
+    for (uint32_t g0 = t0; g0 < t1; g0 += 64 * PF) {
+        uint32_t mv[PF];
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const uint32_t p = g0 + i * 64 + lane;
+            mv[i] = p < t1 ? a.meta[p] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const uint32_t f0 = g0 + i * 64;
+            if (f0 >= t1) break;
+            const uint32_t p = f0 + lane;
+            const bool valid = p < t1;
+            const uint32_t m = mv[i];
+            const bool deliver = valid && UDPDK_META_VERDICT(m) == UDPDK_V_DELIVERED;
+            const uint32_t fan = UDPDK_META_FANOUT(m);
+            const unsigned long long multi = __ballot(deliver && fan > 1u);
+            if (multi == 0ull) {
+                // one delivery per frame: wave multi-split on the lane key
+                const uint32_t key = UDPDK_META_SOCKFD(m) & a.lane_mask;
+                unsigned long long peers = __ballot(deliver);
+                for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
+                    const bool kb = (key >> bit) & 1u;
+                    const unsigned long long bal = __ballot(kb);
+                    peers &= kb ? bal : ~bal;
+                }
+                const uint32_t leader = deliver ? (uint32_t)__ffsll((long long)peers) - 1u : 64u;
+                uint32_t c = 0;
+                if (deliver && lane == leader) {
+                    c = cur[key];
+                    cur[key] = c + (uint32_t)__popcll(peers);
+                }
+                c = __shfl(c, deliver ? (int)leader : 0, 64);
+                const uint32_t pos = c + (uint32_t)__popcll(peers & lt_mask);
+                if (deliver && pos < a.lane_cap) a.lane_pkt[pos] = p;
+            } else if (lane == 0) {
+                // fan-out (SO_REUSEADDR/SO_REUSEPORT clones, poller.c:396-399): deliveries in
+                // frame order then list order, re-derived from the frame header. Serial.
+                for (uint32_t q = 0; q < 64 && f0 + q < t1; ++q) {
+                    const uint32_t fp = f0 + q;
+                    const uint32_t mi = a.meta[fp];
                     if (UDPDK_META_VERDICT(mi) != UDPDK_V_DELIVERED) continue;
-                    const uint32_t fp = f0 + i;
                     const uint8_t *f = a.frames + a.offset[fp];
                     const uint32_t dport = (uint32_t)f[36] | ((uint32_t)f[37] << 8);
                     const uint32_t dip = (uint32_t)f[30] | ((uint32_t)f[31] << 8) |
                                          ((uint32_t)f[32] << 16) | ((uint32_t)f[33] << 24);
-                    const uint32_t e = a.port_tab[dport];
-                    const uint32_t nb = e & 0xFFFu, b0 = e >> 12;
-                    for (uint32_t k = 0; k < nb; ++k) {
-                        const uint2 b = a.binds[b0 + k];
-                        if (dip == b.x || b.x == 0u) {
-                            const uint32_t key = (b.y & 0x7FFFFFFFu) & a.lane_mask;
-                            const uint32_t c = lane_cursor(cur, a, key, tile);
+                    const uint4 e = a.port_tab[dport];
+                    uint32_t bip = e.z, bsr = e.w;
+                    for (uint32_t k = 0;;) {
+                        if (dip == bip || bip == 0u) {
+                            const uint32_t key = (bsr & 0x7FFFFFFFu) & a.lane_mask;
+                            const uint32_t c = cur[key];
                             cur[key] = c + 1u;
                             if (c < a.lane_cap) a.lane_pkt[c] = fp;
-                            if (!(b.y >> 31)) break;
+                            if (!(bsr >> 31)) break;
                         }
+                        if (++k >= e.x) break;
+                        const uint2 b = a.binds[e.y + k];
+                        bip = b.x;
+                        bsr = b.y;
                     }
                 }
             }
+            wave_sync();
         }
-        wave_sync();
     }
 }
 

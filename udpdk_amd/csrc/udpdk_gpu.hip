@@ -22,6 +22,13 @@ using namespace udpdk;
 namespace {
 
 constexpr int EVENT_SETS = 256;   // timed calls buffered between two timing reads
+constexpr uint32_t EPOCH_MAX = 1u << 24;   // look-back tag width (rx_kernels.hip)
+
+struct DevResult {
+    unsigned long long counters[UDPDK_N_COUNTERS];
+    uint32_t total;
+    uint32_t err;
+};
 
 struct TimingSet {
     hipEvent_t ev[4];             // classify start, classify end, scan end, scatter end
@@ -36,7 +43,7 @@ struct udpdk_gpu_ctx {
     uint32_t max_frames = 0, max_lanes = 0;
 
     // bind snapshot (device)
-    uint32_t *port_tab = nullptr;       // [65536]
+    uint4 *port_tab = nullptr;          // [65536]
     uint2 *binds = nullptr;
     uint32_t binds_cap = 0;
     uint4 *slots = nullptr;
@@ -51,10 +58,12 @@ struct udpdk_gpu_ctx {
     size_t partial_cap = 0;
     uint32_t *tile_cnt = nullptr;
     size_t tiles_cap = 0;
-    unsigned long long *counters = nullptr;   // [16]
-    uint32_t *total = nullptr;
-    unsigned long long *h_counters = nullptr; // pinned
-    uint32_t *h_total = nullptr;              // pinned
+    DevResult *res = nullptr;                 // counters, total, err (device)
+    DevResult *h_res = nullptr;               // pinned mirror, filled by udpdk_gpu_rx_stats
+    unsigned long long *lb_state = nullptr;   // fused path look-back granules [tiles][16]
+    uint32_t *ticket = nullptr;
+    uint32_t epoch = 0;
+    uint32_t last_epoch = 0;
     hipEvent_t done = nullptr;
     uint32_t last_lane_cap = 0;
     bool pending = false;
@@ -174,8 +183,8 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
     do {
         if (hipSetDevice(device) != hipSuccess) break;
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) break;
-        if (hipMalloc((void **)&c->port_tab, UDPDK_UDP_PORTS * 4) != hipSuccess) break;
-        if (hipMemset(c->port_tab, 0, UDPDK_UDP_PORTS * 4) != hipSuccess) break;
+        if (hipMalloc((void **)&c->port_tab, UDPDK_UDP_PORTS * sizeof(uint4)) != hipSuccess) break;
+        if (hipMemset(c->port_tab, 0, UDPDK_UDP_PORTS * sizeof(uint4)) != hipSuccess) break;
         const uint64_t e_cap = std::max<uint64_t>((uint64_t)RX_HIST_CAP + max_lanes,
                                                   (uint64_t)ceil_div(max_frames, RX_TILE_MAX) * max_lanes);
         c->hist_cap = e_cap;
@@ -184,13 +193,18 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
         if (hipMalloc((void **)&c->partial, c->partial_cap * 4) != hipSuccess) break;
         c->tiles_cap = ceil_div(max_frames, RX_TILE_MIN) + 1;
         if (hipMalloc((void **)&c->tile_cnt, c->tiles_cap * UDPDK_N_COUNTERS * 4) != hipSuccess) break;
-        if (hipMalloc((void **)&c->counters, UDPDK_N_COUNTERS * 8) != hipSuccess) break;
-        if (hipMalloc((void **)&c->total, 64) != hipSuccess) break;
-        if (hipHostMalloc((void **)&c->h_counters, UDPDK_N_COUNTERS * 8, hipHostMallocDefault) != hipSuccess) break;
-        if (hipHostMalloc((void **)&c->h_total, 64, hipHostMallocDefault) != hipSuccess) break;
+        if (hipMalloc((void **)&c->res, sizeof(DevResult)) != hipSuccess) break;
+        if (hipMemset(c->res, 0, sizeof(DevResult)) != hipSuccess) break;
+        if (hipHostMalloc((void **)&c->h_res, sizeof(DevResult), hipHostMallocDefault) != hipSuccess) break;
+        if (hipMalloc((void **)&c->lb_state, c->tiles_cap * UDPDK_N_COUNTERS * 8) != hipSuccess) break;
+        if (hipMemset(c->lb_state, 0, c->tiles_cap * UDPDK_N_COUNTERS * 8) != hipSuccess) break;
+        if (hipMalloc((void **)&c->ticket, 64) != hipSuccess) break;
+        if (hipMemset(c->ticket, 0, 64) != hipSuccess) break;
         if (hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) break;
         // rx_classify needs up to 90 KiB of dynamic LDS at 16384 lanes
-        if (hipFuncSetAttribute((const void *)rx_classify, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void *)rx_classify<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess) break;
+        if (hipFuncSetAttribute((const void *)rx_classify<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) break;
@@ -211,9 +225,9 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *dev[] = {c->port_tab, c->binds, c->slots, c->hist, c->partial, c->tile_cnt,
-                   c->counters, c->total, c->st_frames_d, c->st_desc_d, c->st_out_d};
+                   c->res, c->lb_state, c->ticket, c->st_frames_d, c->st_desc_d, c->st_out_d};
     for (void *p : dev) if (p) (void)hipFree(p);
-    void *host[] = {c->h_counters, c->h_total, c->st_frames_h, c->st_desc_h};
+    void *host[] = {c->h_res, c->st_frames_h, c->st_desc_h};
     for (void *p : host) if (p) (void)hipHostFree(p);
     if (c->sets) {
         for (int i = 0; i < EVENT_SETS; ++i)
@@ -298,14 +312,15 @@ int udpdk_gpu_bind_snapshot_upload(udpdk_gpu_ctx *c, const udpdk_bind_snapshot_t
     if (!c || !s || !s->port_first || !s->port_count || (s->n_binds && !s->binds)) return -EINVAL;
     if (s->n_lanes == 0 || s->n_lanes > c->max_lanes || s->n_binds > UDPDK_GPU_MAX_BINDS) return -EINVAL;
     if (s->n_slots && !s->slots) return -EINVAL;
-    std::vector<uint32_t> tab(UDPDK_UDP_PORTS, 0u);
+    std::vector<uint4> tab(UDPDK_UDP_PORTS, make_uint4(0, 0, 0, 0));
     uint32_t maxfan = 0;
     for (uint32_t p = 0; p < UDPDK_UDP_PORTS; ++p) {
         const uint32_t cnt = s->port_count[p];
         if (!cnt) continue;
         const uint32_t first = s->port_first[p];
         if (cnt > UDPDK_GPU_MAX_PORT_BINDS || (uint64_t)first + cnt > s->n_binds) return -EINVAL;
-        tab[p] = (first << 12) | cnt;
+        const udpdk_binding_t &b0 = s->binds[first];
+        tab[p] = make_uint4(cnt, first, b0.ip, (uint32_t)b0.sockfd | (b0.reuse ? 0x80000000u : 0u));
         maxfan = std::max(maxfan, cnt);
     }
     std::vector<uint2> b(s->n_binds ? s->n_binds : 1);
@@ -328,7 +343,7 @@ int udpdk_gpu_bind_snapshot_upload(udpdk_gpu_ctx *c, const udpdk_bind_snapshot_t
         HIPC(c, hipMalloc((void **)&c->binds, sizeof(uint2)));
         c->binds_cap = 1;
     }
-    HIPC(c, hipMemcpy(c->port_tab, tab.data(), UDPDK_UDP_PORTS * 4, hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(c->port_tab, tab.data(), UDPDK_UDP_PORTS * sizeof(uint4), hipMemcpyHostToDevice));
     if (s->n_binds)
         HIPC(c, hipMemcpy(c->binds, b.data(), (size_t)s->n_binds * sizeof(uint2), hipMemcpyHostToDevice));
     if (s->n_slots) {
@@ -392,92 +407,120 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     if (!o->lane_off_dev || (!o->lane_pkt_dev && o->lane_cap)) return -EINVAL;
     HIPC(c, hipSetDevice(c->device));
     const uint32_t S = c->n_lanes;
-    c->last_lane_cap = o->lane_cap;
-    c->pending = true;
     TimingSet *ts = nullptr;
     if (c->timing) {
         if (c->n_sets_used == EVENT_SETS) { int rc = fold_timing(c); if (rc) return rc; }
         ts = &c->sets[c->n_sets_used++];
     }
+    c->last_lane_cap = o->lane_cap;
+    c->pending = true;
     if (bt->n == 0) {
         HIPC(c, hipMemsetAsync(o->lane_off_dev, 0, (size_t)(S + 1) * 4, c->stream));
-        HIPC(c, hipMemsetAsync(c->counters, 0, UDPDK_N_COUNTERS * 8, c->stream));
-        HIPC(c, hipMemsetAsync(c->total, 0, 4, c->stream));
+        HIPC(c, hipMemsetAsync(c->res, 0, sizeof(DevResult), c->stream));
+        c->last_epoch = 0;
         if (ts) for (int k = 0; k < 4; ++k) HIPC(c, hipEventRecord(ts->ev[k], c->stream));
-    } else {
-        uint32_t T, tiles;
-        geometry(bt->n, S, &T, &tiles);
-        const uint64_t E = (uint64_t)S * tiles;
-        if (E > c->hist_cap || tiles > c->tiles_cap) return -EINVAL;
-
-        RxArgs ra;
-        ra.frames = bt->frames_dev;
-        ra.offset = bt->offset_dev;
-        ra.length = bt->length_dev;
-        ra.ptype = bt->ptype_dev;
-        ra.port_tab = c->port_tab;
-        ra.binds = c->binds;
-        ra.meta = o->meta_dev;
-        ra.hist = c->hist;
-        ra.tile_cnt = c->tile_cnt;
-        ra.frames_bytes = (uint32_t)bt->frames_bytes;
-        ra.rsrc_bytes = (uint32_t)std::min<uint64_t>((bt->frames_bytes + 15) & ~15ull, 0xFFFFFFFFull);
-        ra.n = bt->n;
-        ra.tile_frames = T;
-        ra.n_tiles = tiles;
-        ra.lane_mask = c->lane_mask;
-        ra.n_lanes = S;
-
-        if (ts) HIPC(c, hipEventRecord(ts->ev[0], c->stream));
-        hipLaunchKernelGGL(rx_classify, dim3(tiles), dim3(RX_BLOCK), classify_lds_bytes(S), c->stream, ra);
-        HIPC(c, hipGetLastError());
-        if (ts) HIPC(c, hipEventRecord(ts->ev[1], c->stream));
-
-        ScanArgs sa;
-        sa.hist = c->hist;
-        sa.partial = c->partial;
-        sa.lane_off = o->lane_off_dev;
-        sa.tile_cnt = c->tile_cnt;
-        sa.counters = c->counters;
-        sa.total = c->total;
-        sa.n_elems = (uint32_t)E;
-        sa.n_tiles = tiles;
-        sa.n_lanes = S;
-        if (E <= SCAN_SMALL_MAX) {
-            hipLaunchKernelGGL(rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 0, c->stream, sa);
-            HIPC(c, hipGetLastError());
-        } else {
-            const uint32_t nb = ceil_div(E, SCAN_CHUNK);
-            hipLaunchKernelGGL(rx_scan_reduce, dim3(nb), dim3(SCAN_BLOCK), 0, c->stream, sa);
-            HIPC(c, hipGetLastError());
-            hipLaunchKernelGGL(rx_scan_top, dim3(1), dim3(SCAN_BLOCK), 0, c->stream, sa, nb);
-            HIPC(c, hipGetLastError());
-            hipLaunchKernelGGL(rx_scan_down, dim3(nb), dim3(SCAN_BLOCK), 0, c->stream, sa);
-            HIPC(c, hipGetLastError());
-        }
-        if (ts) HIPC(c, hipEventRecord(ts->ev[2], c->stream));
-
-        ScatterArgs xa;
-        xa.meta = o->meta_dev;
-        xa.base = c->hist;
-        xa.frames = bt->frames_dev;
-        xa.offset = bt->offset_dev;
-        xa.port_tab = c->port_tab;
-        xa.binds = c->binds;
-        xa.lane_pkt = o->lane_pkt_dev;
-        xa.n = bt->n;
-        xa.tile_frames = T;
-        xa.n_tiles = tiles;
-        xa.n_lanes = S;
-        xa.lane_mask = c->lane_mask;
-        xa.key_bits = c->key_bits;
-        xa.lane_cap = o->lane_cap;
-        hipLaunchKernelGGL(rx_scatter, dim3(tiles), dim3(64), 4u * S, c->stream, xa);
-        HIPC(c, hipGetLastError());
-        if (ts) HIPC(c, hipEventRecord(ts->ev[3], c->stream));
+        HIPC(c, hipEventRecord(c->done, c->stream));
+        return 0;
     }
-    HIPC(c, hipMemcpyAsync(c->h_counters, c->counters, UDPDK_N_COUNTERS * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipMemcpyAsync(c->h_total, c->total, 4, hipMemcpyDeviceToHost, c->stream));
+    uint32_t T, tiles;
+    geometry(bt->n, S, &T, &tiles);
+    const uint64_t E = (uint64_t)S * tiles;
+    if (E > c->hist_cap || tiles > c->tiles_cap) return -EINVAL;
+    const bool fused = S == 1 && c->max_fanout <= 1;
+
+    if (fused) {
+        if (++c->epoch >= EPOCH_MAX) {      // tag space exhausted: clear stale granules
+            HIPC(c, hipMemsetAsync(c->lb_state, 0, c->tiles_cap * UDPDK_N_COUNTERS * 8, c->stream));
+            c->epoch = 1;
+        }
+    }
+    c->last_epoch = fused ? c->epoch : 0;
+
+    RxArgs ra;
+    memset(&ra, 0, sizeof(ra));
+    ra.frames = bt->frames_dev;
+    ra.offset = bt->offset_dev;
+    ra.length = bt->length_dev;
+    ra.ptype = bt->ptype_dev;
+    ra.port_tab = c->port_tab;
+    ra.binds = c->binds;
+    ra.meta = o->meta_dev;
+    ra.hist = c->hist;
+    ra.tile_cnt = c->tile_cnt;
+    ra.lb_state = c->lb_state;
+    ra.ticket = c->ticket;
+    ra.err = &c->res->err;
+    ra.lane_pkt = o->lane_pkt_dev;
+    ra.lane_off = o->lane_off_dev;
+    ra.counters = c->res->counters;
+    ra.total = &c->res->total;
+    ra.lane_cap = o->lane_cap;
+    ra.epoch = c->epoch;
+    ra.key_bits = c->key_bits;
+    ra.frames_bytes = (uint32_t)bt->frames_bytes;
+    ra.rsrc_bytes = (uint32_t)std::min<uint64_t>((bt->frames_bytes + 15) & ~15ull, 0xFFFFFFFFull);
+    ra.n = bt->n;
+    ra.tile_frames = T;
+    ra.n_tiles = tiles;
+    ra.lane_mask = c->lane_mask;
+    ra.n_lanes = S;
+
+    if (ts) HIPC(c, hipEventRecord(ts->ev[0], c->stream));
+    if (fused) {
+        hipLaunchKernelGGL(rx_classify<true>, dim3(tiles), dim3(RX_BLOCK),
+                           classify_lds_bytes(true, S, T / 64), c->stream, ra);
+        HIPC(c, hipGetLastError());
+        if (ts) for (int k = 1; k < 4; ++k) HIPC(c, hipEventRecord(ts->ev[k], c->stream));
+        HIPC(c, hipEventRecord(c->done, c->stream));
+        return 0;
+    }
+    hipLaunchKernelGGL(rx_classify<false>, dim3(tiles), dim3(RX_BLOCK),
+                       classify_lds_bytes(false, S, T / 64), c->stream, ra);
+    HIPC(c, hipGetLastError());
+    if (ts) HIPC(c, hipEventRecord(ts->ev[1], c->stream));
+
+    ScanArgs sa;
+    sa.hist = c->hist;
+    sa.partial = c->partial;
+    sa.lane_off = o->lane_off_dev;
+    sa.tile_cnt = c->tile_cnt;
+    sa.counters = c->res->counters;
+    sa.total = &c->res->total;
+    sa.n_elems = (uint32_t)E;
+    sa.n_tiles = tiles;
+    sa.n_lanes = S;
+    if (E <= SCAN_SMALL_MAX) {
+        hipLaunchKernelGGL(rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 0, c->stream, sa);
+        HIPC(c, hipGetLastError());
+    } else {
+        const uint32_t nb = ceil_div(E, SCAN_CHUNK);
+        hipLaunchKernelGGL(rx_scan_reduce, dim3(nb), dim3(SCAN_BLOCK), 0, c->stream, sa);
+        HIPC(c, hipGetLastError());
+        hipLaunchKernelGGL(rx_scan_top, dim3(1), dim3(SCAN_BLOCK), 0, c->stream, sa, nb);
+        HIPC(c, hipGetLastError());
+        hipLaunchKernelGGL(rx_scan_down, dim3(nb), dim3(SCAN_BLOCK), 0, c->stream, sa);
+        HIPC(c, hipGetLastError());
+    }
+    if (ts) HIPC(c, hipEventRecord(ts->ev[2], c->stream));
+
+    ScatterArgs xa;
+    xa.meta = o->meta_dev;
+    xa.base = c->hist;
+    xa.frames = bt->frames_dev;
+    xa.offset = bt->offset_dev;
+    xa.port_tab = c->port_tab;
+    xa.binds = c->binds;
+    xa.lane_pkt = o->lane_pkt_dev;
+    xa.n = bt->n;
+    xa.tile_frames = T;
+    xa.n_tiles = tiles;
+    xa.n_lanes = S;
+    xa.lane_mask = c->lane_mask;
+    xa.key_bits = c->key_bits;
+    xa.lane_cap = o->lane_cap;
+    hipLaunchKernelGGL(rx_scatter, dim3(tiles), dim3(64), 4u * S, c->stream, xa);
+    HIPC(c, hipGetLastError());
+    if (ts) HIPC(c, hipEventRecord(ts->ev[3], c->stream));
     HIPC(c, hipEventRecord(c->done, c->stream));
     return 0;
 }
@@ -486,10 +529,14 @@ int udpdk_gpu_rx_stats(udpdk_gpu_ctx *c, udpdk_rx_stats_t *st)
 {
     if (!c || !st) return -EINVAL;
     if (!c->pending) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
     HIPC(c, hipEventSynchronize(c->done));
-    for (int k = 0; k < UDPDK_N_COUNTERS; ++k) st->counters[k] = c->h_counters[k];
-    st->deliveries = *c->h_total;
+    HIPC(c, hipMemcpyAsync(c->h_res, c->res, sizeof(DevResult), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < UDPDK_N_COUNTERS; ++k) st->counters[k] = c->h_res->counters[k];
+    st->deliveries = c->h_res->total;
     st->overflow = st->deliveries > c->last_lane_cap ? 1u : 0u;
+    if (c->last_epoch && c->h_res->err == c->last_epoch) return -EIO;   // look-back timed out
     return st->overflow ? -ENOSPC : 0;
 }
 
