@@ -84,7 +84,10 @@ class Rx:
 
     def classify_bytes(self) -> int:
         # rx_classify algorithmic bytes per launch: every frame byte + u32 offset + u16 length
-        # read, u32 verdict written, + the tile histogram column (lanes x tiles x 4 B)
+        # read, u32 verdict written; the fused single-lane kernel also writes the lane entry
+        # (4 B per delivery), the general one the tile histogram column (lanes x tiles x 4 B)
+        if self.w.n_sockets == 1:
+            return self.sum_len + 6 * self.n + 4 * self.n + 4 * self.n
         t, k = abi.geometry(self.n, self.w.n_sockets)
         return self.sum_len + 6 * self.n + 4 * self.n + 4 * self.w.n_sockets * k
 
