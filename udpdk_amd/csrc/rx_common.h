@@ -51,6 +51,7 @@ struct RxArgs {
     uint32_t *tile_cnt;   // [n_tiles][16]                 (general path)
     unsigned long long *lb_state;   // [n_tiles][16] look-back granules (fused path)
     uint32_t *ticket;     // dynamic tile order            (fused path)
+    uint32_t *done;       // tiles finished: the last one reduces the counters (fused path)
     uint32_t *err;        // = epoch of a call whose look-back timed out
     uint32_t *lane_pkt;   // fused path writes the lane directly
     uint32_t *lane_off;

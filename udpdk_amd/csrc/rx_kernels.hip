@@ -13,8 +13,9 @@
 //       chunk loads are in flight while the current step is parsed and demultiplexed.
 //       Demux reads one 16-byte port-table entry (first binding inline) per frame.
 //       FUSED (one lane, fan-out <= 1: the single bound socket of apps/pktgen): tiles take a
-//       ticket, chain a decoupled look-back over tiles for the lane position and the 16 counters
-//       (8-byte {tag, value} granules, agent scope), and write the lane directly: one launch.
+//       ticket (dynamic order), find their lane position by a decoupled look-back over tiles
+//       (8-byte {tag, value} granules at agent scope, 64 predecessors inspected per round),
+//       write the lane directly, and the last tile to finish reduces the counters: one launch.
 //       General: writes the tile's per-lane delivery histogram (lane-major, hist[lane][tile]).
 //   rx_scan     exclusive scan of the lane-major histogram -> per-(lane, tile) start positions,
 //       lane_off, and the counter reduction. One launch when small, reduce/top/down otherwise.
@@ -106,6 +107,40 @@ __device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
 constexpr uint32_t LB_AGG = 1u, LB_INCL = 2u;
 constexpr int LB_VALUE_BITS = 38;
 constexpr unsigned long long LB_VALUE_MASK = (1ull << LB_VALUE_BITS) - 1ull;
+
+// counters[c] = sum over tiles of tile_cnt[t][c] (64-bit): each thread sums whole rows.
+__device__ void reduce_counters(const uint32_t *tile_cnt, uint32_t n_tiles,
+                                unsigned long long *counters, unsigned long long *lds)
+{
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    unsigned long long s[UDPDK_N_COUNTERS];
+#pragma unroll
+    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) s[c] = 0;
+    const uint4 *rows = reinterpret_cast<const uint4 *>(tile_cnt);
+#pragma unroll 2
+    for (uint32_t t = tid; t < n_tiles; t += blockDim.x) {
+        const uint4 r0 = rows[t * 4 + 0], r1 = rows[t * 4 + 1], r2 = rows[t * 4 + 2], r3 = rows[t * 4 + 3];
+        s[0] += r0.x; s[1] += r0.y; s[2] += r0.z; s[3] += r0.w;
+        s[4] += r1.x; s[5] += r1.y; s[6] += r1.z; s[7] += r1.w;
+        s[8] += r2.x; s[9] += r2.y; s[10] += r2.z; s[11] += r2.w;
+        s[12] += r3.x; s[13] += r3.y; s[14] += r3.z; s[15] += r3.w;
+    }
+    if (tid < UDPDK_N_COUNTERS * 16) lds[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) {
+        unsigned long long v = s[c];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        if (lane == 0) lds[w * UDPDK_N_COUNTERS + c] = v;
+    }
+    __syncthreads();
+    if (tid < UDPDK_N_COUNTERS) {
+        unsigned long long t = 0;
+        for (uint32_t i = 0; i < blockDim.x / 64; ++i) t += lds[i * UDPDK_N_COUNTERS + tid];
+        counters[tid] = t;
+    }
+}
 
 // ------------------------------------------------------------------------------------------
 // rx_classify
@@ -410,53 +445,48 @@ rx_classify(RxArgs a)
             if (si < steps) scnt[si] = run;
             run += v[i];
         }
-        // look-back: lanes 0..15 carry the 16 counters (lane 8 = deliveries = lane position)
-        unsigned long long *state = reinterpret_cast<unsigned long long *>(a.lb_state);
-        const unsigned long long agg = lane < UDPDK_N_COUNTERS ? cnt[lane] : 0ull;
+        // Decoupled look-back on the tile's delivery count: publish the aggregate, then each
+        // lane inspects one of the 64 nearest predecessors per round (8-byte {tag, value}
+        // granules written and read at agent scope; the data is the flag).
+        unsigned long long *state = a.lb_state;
+        const unsigned long long agg = cnt[UDPDK_C_DELIVERIES];
         const unsigned long long tagA = (unsigned long long)((a.epoch << 2) | LB_AGG) << LB_VALUE_BITS;
         const unsigned long long tagI = (unsigned long long)((a.epoch << 2) | LB_INCL) << LB_VALUE_BITS;
-        if (lane < UDPDK_N_COUNTERS)
-            __hip_atomic_store(&state[(size_t)tile * UDPDK_N_COUNTERS + lane], tagA | agg,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0)
+            __hip_atomic_store(&state[tile], tagA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned long long excl = 0;
         bool timeout = false;
-        for (int32_t pt = (int32_t)tile - 1; pt >= 0; --pt) {
+        for (int32_t wb = (int32_t)tile - 1; wb >= 0 && !timeout; wb -= 64) {
+            const int32_t pt = wb - (int32_t)lane;
             unsigned long long x = 0;
-            uint32_t kind = 0;
+            uint32_t first_incl = 64;
             for (uint32_t spins = 0;; ++spins) {
-                x = lane < UDPDK_N_COUNTERS
-                        ? __hip_atomic_load(&state[(size_t)pt * UDPDK_N_COUNTERS + lane],
-                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                        : 0ull;
-                const uint32_t tg = (uint32_t)(x >> LB_VALUE_BITS);
-                const bool mine = lane >= UDPDK_N_COUNTERS || (tg >> 2) == a.epoch;
-                const unsigned long long incl = __ballot(lane < UDPDK_N_COUNTERS && mine && (tg & 3u) == LB_INCL);
-                const unsigned long long aggm = __ballot(lane < UDPDK_N_COUNTERS && mine && (tg & 3u) == LB_AGG);
-                const unsigned long long need = (1ull << UDPDK_N_COUNTERS) - 1ull;
-                if (incl == need) { kind = LB_INCL; break; }
-                if (aggm == need) { kind = LB_AGG; break; }
+                uint32_t kind = LB_INCL;                   // before tile 0: an inclusive zero
+                x = 0;
+                if (pt >= 0) {
+                    x = __hip_atomic_load(&state[pt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t tg = (uint32_t)(x >> LB_VALUE_BITS);
+                    kind = (tg >> 2) == a.epoch ? (tg & 3u) : 0u;
+                }
+                const unsigned long long incl = __ballot(kind == LB_INCL);
+                const unsigned long long ready = __ballot(kind != 0u);
+                first_incl = incl ? (uint32_t)__ffsll((long long)incl) - 1u : 64u;
+                const unsigned long long need = first_incl >= 63u ? ~0ull : ((2ull << first_incl) - 1ull);
+                if ((ready & need) == need) break;
                 if (spins > (1u << 22)) { timeout = true; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
-            if (timeout) break;
-            excl += x & LB_VALUE_MASK;
-            if (kind == LB_INCL) break;
+            unsigned long long val = lane <= first_incl ? (x & LB_VALUE_MASK) : 0ull;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
+            excl += val;
+            if (first_incl < 64u) break;
         }
         if (timeout && lane == 0) atomicExch(a.err, a.epoch);
-        if (lane < UDPDK_N_COUNTERS)
-            __hip_atomic_store(&state[(size_t)tile * UDPDK_N_COUNTERS + lane],
-                               tagI | ((excl + agg) & LB_VALUE_MASK), __ATOMIC_RELAXED,
+        if (lane == 0) {
+            __hip_atomic_store(&state[tile], tagI | ((excl + agg) & LB_VALUE_MASK), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t base = (uint32_t)__shfl((uint32_t)excl, UDPDK_C_DELIVERIES, 64);
-        if (lane == 0) misc[1] = base;
-        if (tile == a.n_tiles - 1u) {                       // last tile holds the totals
-            if (lane < UDPDK_N_COUNTERS) a.counters[lane] = excl + agg;
-            const uint32_t tot = (uint32_t)__shfl((uint32_t)(excl + agg), UDPDK_C_DELIVERIES, 64);
-            if (lane == 0) {
-                a.lane_off[0] = 0u;
-                a.lane_off[1] = tot;
-                *a.total = tot;
-            }
+            misc[1] = (uint32_t)excl;
         }
     }
     __syncthreads();
@@ -468,6 +498,31 @@ rx_classify(RxArgs a)
             const uint32_t pos = base + scnt[s] + (uint32_t)__popcll(m & lt);
             if (pos < a.lane_cap) a.lane_pkt[pos] = t0 + s * 64 + lane;
         }
+    }
+
+    // ---- counters: rows published with release, the last-arriving tile reduces them ----
+    if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = cnt[tid];
+    if (w == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t prev = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        misc[2] = prev;
+        if (prev == a.n_tiles - 1u) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (misc[2] != a.n_tiles - 1u) return;
+    reduce_counters(a.tile_cnt, a.n_tiles, a.counters, reinterpret_cast<unsigned long long *>(smem));
+    if (tid == 0) {
+        const uint32_t tot = (uint32_t)a.counters[UDPDK_C_DELIVERIES];
+        a.lane_off[0] = 0u;
+        a.lane_off[1] = tot;
+        *a.total = tot;
+        *a.done = 0u;                                    // ready for the next launch
     }
 }
 
@@ -492,40 +547,6 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds16,
     __syncthreads();
     *total = tot;
     return pre + inc - v;
-}
-
-// counters[c] = sum over tiles of tile_cnt[t][c] (64-bit): each thread sums whole rows.
-__device__ void reduce_counters(const uint32_t *tile_cnt, uint32_t n_tiles,
-                                unsigned long long *counters, unsigned long long *lds)
-{
-    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    unsigned long long s[UDPDK_N_COUNTERS];
-#pragma unroll
-    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) s[c] = 0;
-    const uint4 *rows = reinterpret_cast<const uint4 *>(tile_cnt);
-#pragma unroll 2
-    for (uint32_t t = tid; t < n_tiles; t += blockDim.x) {
-        const uint4 r0 = rows[t * 4 + 0], r1 = rows[t * 4 + 1], r2 = rows[t * 4 + 2], r3 = rows[t * 4 + 3];
-        s[0] += r0.x; s[1] += r0.y; s[2] += r0.z; s[3] += r0.w;
-        s[4] += r1.x; s[5] += r1.y; s[6] += r1.z; s[7] += r1.w;
-        s[8] += r2.x; s[9] += r2.y; s[10] += r2.z; s[11] += r2.w;
-        s[12] += r3.x; s[13] += r3.y; s[14] += r3.z; s[15] += r3.w;
-    }
-    if (tid < UDPDK_N_COUNTERS * 16) lds[tid] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) {
-        unsigned long long v = s[c];
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-        if (lane == 0) lds[w * UDPDK_N_COUNTERS + c] = v;
-    }
-    __syncthreads();
-    if (tid < UDPDK_N_COUNTERS) {
-        unsigned long long t = 0;
-        for (uint32_t i = 0; i < blockDim.x / 64; ++i) t += lds[i * UDPDK_N_COUNTERS + tid];
-        counters[tid] = t;
-    }
 }
 
 // Small case: one workgroup of SCAN_BLOCK threads, E <= SCAN_SMALL_MAX.

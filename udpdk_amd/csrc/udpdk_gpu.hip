@@ -449,6 +449,7 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     ra.tile_cnt = c->tile_cnt;
     ra.lb_state = c->lb_state;
     ra.ticket = c->ticket;
+    ra.done = c->ticket + 1;
     ra.err = &c->res->err;
     ra.lane_pkt = o->lane_pkt_dev;
     ra.lane_off = o->lane_off_dev;
