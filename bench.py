@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1500 B / IMIX side lines")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU time per baseline leg")
+    p.add_argument("--timing-every", type=int, default=8,
+                   help="record per-kernel HIP events on every Nth timed step (sampling)")
     return p.parse_args()
 
 
@@ -96,7 +98,8 @@ class Rx:
         return self.sum_len + 8 * self.n + 4 * self.n + 4 * self.n + 4 * (self.w.n_sockets + 1)
 
 
-def time_loop(rx: Rx, steps: int, warmup: int, barrier, timing: bool):
+def time_loop(rx: Rx, steps: int, warmup: int, barrier, timing: int):
+    """timing = N: kernel events on every Nth step of the timed region (0 = none)."""
     ctx = rx.ctx
     for i in range(warmup):
         rx.step(i)
@@ -113,7 +116,7 @@ def time_loop(rx: Rx, steps: int, warmup: int, barrier, timing: bool):
     barrier()
     st = rx.check()
     ms, n = ctx.timing_read() if timing else ([0.0] * 4, [0] * 4)
-    ctx.timing(False)
+    ctx.timing(0)
     return (t1 - t0), ms, n, st
 
 
@@ -139,7 +142,7 @@ def cpu_baseline(w: F.Workload, target_s: float):
 def side_config(ctx, cfg: int, steps: int, rotate: int):
     w = F.config_batch(cfg)
     rx = Rx(ctx, w, rotate)
-    wall, ms, n, st = time_loop(rx, steps, 5, lambda: None, True)
+    wall, ms, n, st = time_loop(rx, steps, 5, lambda: None, 4)
     out = {"workload": w.name, "mpkt_s": rx.n * steps / wall / 1e6,
            "gbps_pipeline": rx.pipeline_bytes() * steps / wall / 1e9,
            "classify_us": 1e3 * ms[0] / max(1, n[0]),
@@ -174,7 +177,7 @@ def main():
     w = F.config_batch(args.config, n=args.frames, shard=rank)
     ctx = abi.GpuContext(device, max_frames=max(w.batch.n, 1 << 22), max_lanes=4096)
     rx = Rx(ctx, w, args.rotate_mib << 20)
-    wall, ms, n, st = time_loop(rx, args.steps, args.warmup, barrier, True)
+    wall, ms, n, st = time_loop(rx, args.steps, args.warmup, barrier, args.timing_every)
     if dist is not None:
         t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

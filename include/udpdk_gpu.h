@@ -238,8 +238,10 @@ int udpdk_gpu_tx_build(udpdk_gpu_ctx *ctx, const udpdk_tx_config_t *cfg,
                        const udpdk_tx_batch_t *batch, const udpdk_tx_out_t *out);
 
 /* ---------------------------------------------------------------------------------------------
- * Timing (for bench.py / the roofline): when enabled, udpdk_gpu_rx records HIP events around
- * each of its kernels on the context stream; read back accumulated device milliseconds.
+ * Timing (for bench.py / the roofline): udpdk_gpu_rx records HIP events around each of its
+ * kernels on the context stream on every `enable`-th call (0 = off, 1 = every call; sampling
+ * keeps the ~10 us host cost of an event record off most calls); read back the accumulated
+ * device milliseconds and the number of timed calls.
  * ------------------------------------------------------------------------------------------- */
 enum udpdk_gpu_kernel_id {
     UDPDK_K_RX_CLASSIFY = 0,   /* parse + checksums + demux + tile histograms (dominant)      */

@@ -23,7 +23,7 @@ for lanes in (1, 1024):
     ot = abi.RxOut(out.meta.ptr, out.lane_off.ptr, out.lane_pkt.ptr, n)
     import ctypes as C
     pb, po = C.byref(bt), C.byref(ot)
-    for timing in (False, True):
+    for timing in (0, 1, 8):
         ctx.timing(timing)
         for _ in range(50):
             L.udpdk_gpu_rx(ctx.handle, pb, po)
@@ -38,5 +38,5 @@ for lanes in (1, 1024):
         ms, cnt = ctx.timing_read() if timing else ([0] * 4, [0] * 4)
         print(f"lanes={lanes} timing={timing}: enqueue {1e6 * t_enq / K:.2f} us/call, "
               f"wall {1e6 * t_all / K:.2f} us/call, gpu classify {1e3 * ms[0] / max(1, cnt[0]):.2f} us")
-    ctx.timing(False)
+    ctx.timing(0)
 ctx.close()

@@ -292,8 +292,9 @@ class GpuContext:
         _check(lib().udpdk_gpu_bind_snapshot_upload(self.handle, C.byref(hs.snap)),
                "udpdk_gpu_bind_snapshot_upload")
 
-    def timing(self, enable: bool):
-        _check(lib().udpdk_gpu_timing_enable(self.handle, int(enable)), "timing_enable")
+    def timing(self, every: int):
+        """0 = off, N = record kernel events on every Nth udpdk_gpu_rx call."""
+        _check(lib().udpdk_gpu_timing_enable(self.handle, int(every)), "timing_enable")
 
     def timing_read(self):
         ms = (C.c_double * 4)()

@@ -20,14 +20,12 @@ constexpr uint32_t SCAN_SMALL_MAX = 16384;  // single-workgroup scan up to this 
 constexpr int TX_BLOCK = 256;
 
 // rx_classify LDS carve (one dynamic array, 16-byte aligned offsets: cdna_hip_programming.md
-// Guideline 17): per wave a 64 B header window per frame (80 B stride spreads the lane-per-frame
-// dword reads over banks) and three 64-entry chunk-map arrays; block counters + misc words; then
-// either per-step delivered masks/counts (fused single-lane path) or the per-lane histogram.
-constexpr int HDR_STRIDE  = 80;
-constexpr int HDR_BYTES   = RX_WAVES * 64 * HDR_STRIDE;
+// Guideline 17): per wave three 64-entry chunk-map arrays for the tail sweep; block counters +
+// misc words; then per-step delivered masks/counts (fused single-lane path) or the per-lane
+// histogram (general path).
 constexpr int WAVE_ARRAYS = 3;                    // chunk start, offset, length
 constexpr int ARR_BYTES   = RX_WAVES * WAVE_ARRAYS * 64 * 4;
-constexpr int CNT_OFF     = HDR_BYTES + ARR_BYTES;
+constexpr int CNT_OFF     = ARR_BYTES;
 constexpr int TAIL_OFF    = CNT_OFF + 80;         // 16 counters + 4 misc words
 
 __host__ __device__ constexpr uint32_t classify_lds_bytes(bool fused, uint32_t n_lanes,

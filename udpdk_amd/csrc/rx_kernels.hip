@@ -145,6 +145,40 @@ __device__ void reduce_counters(const uint32_t *tile_cnt, uint32_t n_tiles,
 // ------------------------------------------------------------------------------------------
 // rx_classify
 // ------------------------------------------------------------------------------------------
+// Bytes [lo, hi) of the little-endian dword holding frame bytes [base, base + 4), as a mask.
+__device__ __forceinline__ uint32_t byte_mask(int lo, int hi, int base)
+{
+    const int la = min(max(lo - base, 0), 4);
+    const int le = min(max(hi - base, 0), 4);
+    const uint32_t hm = le >= 4 ? 0xFFFFFFFFu : ((1u << (8 * le)) - 1u);
+    const uint32_t lm = la >= 4 ? 0xFFFFFFFFu : ((1u << (8 * la)) - 1u);
+    return hm & ~lm;
+}
+
+// m[lane] ? b : a, as one v_cndmask_b32 with an SGPR-pair lane mask.
+__device__ __forceinline__ uint32_t lane_select(unsigned long long m, uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+
+// Inclusive wave64 prefix sum on the DPP network (row shifts + row broadcasts; no LDS traffic).
+__device__ __forceinline__ uint32_t scan_dpp(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return v;
+}
+
+struct Win {
+    uint4 c0, c1, c2, c3, c4;
+};
+
 template <bool FUSED>
 __global__ void __launch_bounds__(RX_BLOCK)
 rx_classify(RxArgs a)
@@ -153,11 +187,10 @@ rx_classify(RxArgs a)
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t steps = a.tile_frames / 64;
 
-    uint8_t *hdr = smem + w * 64 * HDR_STRIDE;
-    uint32_t *arr = reinterpret_cast<uint32_t *>(smem + HDR_BYTES) + w * WAVE_ARRAYS * 64;
+    uint32_t *arr = reinterpret_cast<uint32_t *>(smem) + w * WAVE_ARRAYS * 64;
     uint32_t *l_cs = arr, *l_off = arr + 64, *l_len = arr + 128;
     uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + CNT_OFF);
-    uint32_t *misc = cnt + UDPDK_N_COUNTERS;                 // [0] tile, [1..2] lane base
+    uint32_t *misc = cnt + UDPDK_N_COUNTERS;                 // [0] tile, [1] lane base, [2] arrival
     uint8_t *tail = smem + TAIL_OFF;
     // FUSED: per-step delivered masks and counts; general: per-lane histogram
     unsigned long long *smask = reinterpret_cast<unsigned long long *>(tail);
@@ -181,122 +214,115 @@ rx_classify(RxArgs a)
     const uint32_t t0 = tile * a.tile_frames;
     const uint32_t t1 = min(a.n, t0 + a.tile_frames);
 
-    // per-lane counters (reduced once per tile)
-    uint32_t cv[UDPDK_N_COUNTERS];
+    uint32_t cv[UDPDK_N_COUNTERS];                          // per-lane counters
 #pragma unroll
     for (int c = 0; c < UDPDK_N_COUNTERS; ++c) cv[c] = 0;
 
-    // ---- software pipeline state ----
-    uint32_t st = w;
-    uint32_t c_off = 0, c_len = 0;     // descriptors of step st (frame lane)
-    uint32_t n_off = 0, n_len = 0;     // descriptors of step st + RX_WAVES
     auto load_desc = [&](uint32_t s, uint32_t &o, uint32_t &l) {
         const uint32_t p = t0 + s * 64 + lane;
         const bool v = s < steps && p < t1;
         o = v ? a.offset[p] : 0u;
         l = v ? (uint32_t)a.length[p] : 0u;
     };
-    uint32_t total = 0, my_cs = 0, my_nch = 0;
-    uint4 R[RX_UNROLL];
-    uint32_t Rq[RX_UNROLL];
-    // set up step s: chunk map in LDS, iteration-0 chunk loads in flight
-    auto setup = [&](uint32_t s, uint32_t o, uint32_t l) {
+    // The frame's header window: 5 aligned 16-byte chunks from (off & ~15) hold frame bytes
+    // [0, 64] whatever the alignment. One lane per frame.
+    auto load_win = [&](uint32_t s, uint32_t o, uint32_t l) -> Win {
         const uint32_t p = t0 + s * 64 + lane;
-        const bool v = p < t1;
-        const bool bad = v && ((uint64_t)o + l > (uint64_t)a.frames_bytes);
-        my_nch = (v && !bad && l) ? (((o & 15u) + l + 15u) >> 4) : 0u;
-        const uint32_t inc = wave_incl_scan(my_nch);
-        my_cs = inc - my_nch;
-        total = __shfl(inc, 63, 64);
-        l_cs[lane] = my_cs;
-        l_off[lane] = o;
-        l_len[lane] = l;
-        wave_sync();
-#pragma unroll
-        for (int u = 0; u < RX_UNROLL; ++u) {
-            const uint32_t k = u * 64 + lane;
-            uint32_t q = 0;
-#pragma unroll
-            for (int sft = 32; sft >= 1; sft >>= 1)
-                if (l_cs[q + sft] <= k) q += sft;
-            Rq[u] = q;
-            R[u] = k < total ? load16(fr, (l_off[q] & ~15u) + 16u * (k - l_cs[q])) : make_uint4(0, 0, 0, 0);
-        }
-    };
-    // consume the chunks in R (iteration starting at chunk k0): header windows + UDP sums
-    auto consume = [&](uint32_t k0, uint32_t &usum) {
-#pragma unroll
-        for (int u = 0; u < RX_UNROLL; ++u) {
-            const uint32_t base = k0 + u * 64;
-            const uint32_t k = base + lane;
-            const uint32_t q = Rq[u];
-            uint32_t part = 0;
-            if (k < total) {
-                const uint32_t j = k - l_cs[q];
-                const uint32_t fo = l_off[q];
-                if (j < 4)
-                    *reinterpret_cast<uint4 *>(hdr + q * HDR_STRIDE + 16 * j) = R[u];
-                const int rel = (int)(((fo & ~15u) + 16u * j) - fo);
-                part = chunk_sum(R[u], 34 - rel, (int)l_len[q] - rel);
-            }
-            const uint32_t P = wave_incl_scan(part);
-            // this frame's chunks inside [base, base + 64)
-            const uint32_t lo = max(my_cs, base), hi = min(my_cs + my_nch, base + 64u);
-            const uint32_t ph = __shfl(P, (int)((hi > base ? hi - 1u - base : 0u) & 63u), 64);
-            const uint32_t pl = __shfl(P, (int)((lo > base ? lo - 1u - base : 0u) & 63u), 64);
-            if (lo < hi) usum += ph - (lo > base ? pl : 0u);
-        }
+        const bool ok = s < steps && p < t1 && l != 0u && (uint64_t)o + l <= (uint64_t)a.frames_bytes;
+        const uint32_t nw = ok ? min(5u, ((o & 15u) + l + 15u) >> 4) : 0u;
+        const uint32_t ab = o & ~15u;
+        Win r;
+        r.c0 = nw > 0u ? load16(fr, ab) : make_uint4(0, 0, 0, 0);
+        r.c1 = nw > 1u ? load16(fr, ab + 16u) : make_uint4(0, 0, 0, 0);
+        r.c2 = nw > 2u ? load16(fr, ab + 32u) : make_uint4(0, 0, 0, 0);
+        r.c3 = nw > 3u ? load16(fr, ab + 48u) : make_uint4(0, 0, 0, 0);
+        r.c4 = nw > 4u ? load16(fr, ab + 64u) : make_uint4(0, 0, 0, 0);
+        return r;
     };
 
-    if (st < steps) {
-        load_desc(st, c_off, c_len);
-        setup(st, c_off, c_len);
-        if (st + RX_WAVES < steps) load_desc(st + RX_WAVES, n_off, n_len);
-    }
+    uint32_t st = w;
+    uint32_t c_off = 0, c_len = 0, n_off = 0, n_len = 0;
+    load_desc(st, c_off, c_len);
+    Win W = load_win(st, c_off, c_len);
+    load_desc(st + RX_WAVES, n_off, n_len);
 
     while (st < steps) {
         const uint32_t p = t0 + st * 64 + lane;
         const bool valid = p < t1;
         const uint32_t off = c_off, len = c_len;
         const bool bad_desc = valid && ((uint64_t)off + len > (uint64_t)a.frames_bytes);
+        const bool good = valid && !bad_desc;
 
-        // ---- finish the chunk sweep of step st ----
-        uint32_t usum = 0;
-        consume(0, usum);
-        for (uint32_t k0 = 64 * RX_UNROLL; k0 < total; k0 += 64 * RX_UNROLL) {
-#pragma unroll
-            for (int u = 0; u < RX_UNROLL; ++u) {
-                const uint32_t k = k0 + u * 64 + lane;
-                uint32_t q = 0;
-#pragma unroll
-                for (int sft = 32; sft >= 1; sft >>= 1)
-                    if (l_cs[q + sft] <= k) q += sft;
-                Rq[u] = q;
-                R[u] = k < total ? load16(fr, (l_off[q] & ~15u) + 16u * (k - l_cs[q])) : make_uint4(0, 0, 0, 0);
-            }
-            consume(k0, usum);
-        }
-        wave_sync();
-
-        // ---- start the next step of this wave: its loads overlap the parse below ----
+        // ---- next step of this wave: window loads in flight during this step ----
         const uint32_t nst = st + RX_WAVES;
-        if (nst < steps) {
-            setup(nst, n_off, n_len);
-            c_off = n_off;
-            c_len = n_len;
-            if (nst + RX_WAVES < steps) load_desc(nst + RX_WAVES, n_off, n_len);
+        const Win NW = load_win(nst, n_off, n_len);
+        uint32_t nn_off, nn_len;
+        load_desc(nst + RX_WAVES, nn_off, nn_len);
+
+        // ---- tail sweep: UDP bytes at frame offsets >= 64, as chunks swept across lanes ----
+        const uint32_t my_nt = (good && len > 64u) ? ((((off + 64u) & 15u) + (len - 64u) + 15u) >> 4) : 0u;
+        const uint32_t inc = scan_dpp(my_nt);
+        const uint32_t my_cs = inc - my_nt;
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        uint32_t tsum = 0;                                  // absolute-address word parity
+        if (total) {
+            l_cs[lane] = my_cs;
+            l_off[lane] = off;
+            l_len[lane] = len;
+            wave_sync();
+            for (uint32_t k0 = 0; k0 < total; k0 += 64 * RX_UNROLL) {
+                uint4 R[RX_UNROLL];
+                uint32_t Rq[RX_UNROLL];
+#pragma unroll
+                for (int u = 0; u < RX_UNROLL; ++u) {
+                    const uint32_t k = k0 + u * 64 + lane;
+                    uint32_t q = 0;
+#pragma unroll
+                    for (int sft = 32; sft >= 1; sft >>= 1)
+                        if (l_cs[q + sft] <= k) q += sft;
+                    Rq[u] = q;
+                    R[u] = k < total ? load16(fr, ((l_off[q] + 64u) & ~15u) + 16u * (k - l_cs[q]))
+                                     : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < RX_UNROLL; ++u) {
+                    const uint32_t base = k0 + u * 64;
+                    const uint32_t k = base + lane;
+                    uint32_t part = 0;
+                    if (k < total) {
+                        const uint32_t q = Rq[u], fo = l_off[q];
+                        const int rel = (int)((((fo + 64u) & ~15u) + 16u * (k - l_cs[q])) - fo);
+                        part = chunk_sum(R[u], 64 - rel, (int)l_len[q] - rel);
+                    }
+                    const uint32_t P = scan_dpp(part);
+                    const uint32_t lo = max(my_cs, base), hi = min(my_cs + my_nt, base + 64u);
+                    const uint32_t ph = __shfl(P, (int)((hi > base ? hi - 1u - base : 0u) & 63u), 64);
+                    const uint32_t pl = __shfl(P, (int)((lo > base ? lo - 1u - base : 0u) & 63u), 64);
+                    if (lo < hi) tsum += ph - (lo > base ? pl : 0u);
+                }
+            }
+            wave_sync();
         }
 
-        // ---- per-frame parse (lane = frame) from the staged 64-byte window ----
+        // ---- parse (lane = frame) from the window registers ----
         uint32_t word = 0, verdict = UDPDK_V_BAD_DESC, fan = 0, first = 0;
-        if (valid && !bad_desc) {
-            const uint32_t sh = off & 15u;
-            const uint32_t *hw = reinterpret_cast<const uint32_t *>(hdr + lane * HDR_STRIDE + (sh & ~3u));
-            uint32_t raw[12], h[11];
+        if (good) {
+            const uint32_t sh = off & 15u, s3 = sh & 3u;
+            uint32_t wd[20], w1[19], w2[17], h[16];
+            const uint4 wc[5] = {W.c0, W.c1, W.c2, W.c3, W.c4};
 #pragma unroll
-            for (int i = 0; i < 12; ++i) raw[i] = hw[i];
+            for (int i = 0; i < 5; ++i) {
+                wd[4 * i] = wc[i].x; wd[4 * i + 1] = wc[i].y; wd[4 * i + 2] = wc[i].z; wd[4 * i + 3] = wc[i].w;
+            }
+            // shift by (sh >> 2) dwords with lane-mask selects (a plain ?: here is turned into a
+            // scratch-indexed array by the compiler)
+            const unsigned long long m4 = __ballot((sh & 4u) != 0u), m8 = __ballot((sh & 8u) != 0u);
 #pragma unroll
-            for (int i = 0; i < 11; ++i) h[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh & 3u);
+            for (int i = 0; i < 19; ++i) w1[i] = lane_select(m4, wd[i], wd[i + 1]);
+#pragma unroll
+            for (int i = 0; i < 17; ++i) w2[i] = lane_select(m8, w1[i], w1[i + 2]);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) h[i] = __builtin_amdgcn_alignbyte(w2[i + 1], w2[i], s3);
             // h[i] = frame bytes 4i .. 4i+3 (little-endian)
             cv[UDPDK_C_BYTES] += len;
             uint32_t pt;
@@ -324,8 +350,7 @@ rx_classify(RxArgs a)
                     const uint32_t src = (h[6] >> 16) | (h[7] << 16);
                     const uint32_t dip = (h[7] >> 16) | (h[8] << 16);   // poller.c:373
                     const uint32_t dport = h[9] & 0xFFFFu;               // poller.c:372
-                    // issue the demux load first: it overlaps the checksum arithmetic
-                    const uint4 e = a.port_tab[dport];
+                    const uint4 e = a.port_tab[dport];                   // overlaps the sums below
                     const uint32_t ulen_raw = h[9] >> 16;
                     const uint32_t ulen = ((ulen_raw & 0xFFu) << 8) | (ulen_raw >> 8);
                     const uint32_t ucks = h[10] & 0xFFFFu;
@@ -336,14 +361,26 @@ rx_classify(RxArgs a)
                     } else if (len_bad) {
                         state = UDPDK_UDP_CSUM_BAD;
                     } else {
-                        uint32_t s = usum % 65535u;
+                        // frame bytes [34, min(len, 64)) from the window (frame-relative words)
+                        uint32_t ws = 0;
+                        if (len >= 64u) {
+                            ws = (h[8] >> 16);
+#pragma unroll
+                            for (int i = 9; i < 16; ++i) ws += sum16(h[i]);
+                        } else {
+#pragma unroll
+                            for (int i = 8; i < 16; ++i) ws += sum16(h[i] & byte_mask(34, (int)len, 4 * i));
+                        }
+                        uint32_t s = ws % 65535u;
+                        // tail bytes [64, len): absolute-address words, byte-swapped at odd starts
+                        const uint32_t t = tsum % 65535u;
+                        s = (s + ((off & 1u) ? (t * 256u) % 65535u : t)) % 65535u;
                         if (34u + ulen < len) {                    // Ethernet padding after the datagram
                             uint32_t pad = 0;
-                            for (uint32_t b = off + 34u + ulen; b < off + len; ++b)
-                                pad += (uint32_t)a.frames[b] << (8u * (b & 1u));
+                            for (uint32_t r = 34u + ulen; r < len; ++r)
+                                pad += (uint32_t)a.frames[off + r] << (8u * (r & 1u));
                             s = (s + 65535u - pad % 65535u) % 65535u;
                         }
-                        if (off & 1u) s = (s * 256u) % 65535u;   // odd start: words byte-swapped
                         const uint32_t pseudo = (src & 0xFFFFu) + (src >> 16) + (dip & 0xFFFFu) +
                                                 (dip >> 16) + 0x1100u + ulen_raw;
                         state = ((s + pseudo) % 65535u) == 0u ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD;
@@ -409,7 +446,11 @@ rx_classify(RxArgs a)
                 atomicAdd(&hist[key], 1u);
             }
         }
-        wave_sync();
+        W = NW;
+        c_off = n_off;
+        c_len = n_len;
+        n_off = nn_off;
+        n_len = nn_len;
         st = nst;
     }
 

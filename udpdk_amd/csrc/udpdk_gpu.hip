@@ -76,7 +76,8 @@ struct udpdk_gpu_ctx {
     uint8_t *st_out_d = nullptr; size_t st_out_cap = 0;
 
     // timing
-    bool timing = false;
+    uint32_t timing_every = 0;                // 0 off, N: events on every Nth call
+    uint64_t timing_calls = 0;
     TimingSet *sets = nullptr;
     int n_sets_used = 0;
     double ms[UDPDK_N_KERNEL_IDS] = {0, 0, 0, 0};
@@ -378,7 +379,8 @@ int udpdk_gpu_timing_enable(udpdk_gpu_ctx *c, int enable)
         for (int i = 0; i < EVENT_SETS; ++i)
             for (int k = 0; k < 4; ++k) HIPC(c, hipEventCreate(&c->sets[i].ev[k]));
     }
-    c->timing = enable != 0;
+    c->timing_every = enable > 0 ? (uint32_t)enable : 0u;
+    c->timing_calls = 0;
     return 0;
 }
 
@@ -408,7 +410,7 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     HIPC(c, hipSetDevice(c->device));
     const uint32_t S = c->n_lanes;
     TimingSet *ts = nullptr;
-    if (c->timing) {
+    if (c->timing_every && (c->timing_calls++ % c->timing_every) == 0) {
         if (c->n_sets_used == EVENT_SETS) { int rc = fold_timing(c); if (rc) return rc; }
         ts = &c->sets[c->n_sets_used++];
     }
@@ -632,14 +634,14 @@ int udpdk_gpu_tx_build(udpdk_gpu_ctx *c, const udpdk_tx_config_t *cfg, const udp
     const uint32_t groups = ceil_div(bt->n, 64);
     const uint32_t grid = std::min<uint32_t>(ceil_div(groups, TX_BLOCK / 64), 4096);
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (c->timing) {
+    if (c->timing_every) {
         HIPC(c, hipEventCreate(&e0));
         HIPC(c, hipEventCreate(&e1));
         HIPC(c, hipEventRecord(e0, c->stream));
     }
     hipLaunchKernelGGL(tx_build, dim3(grid), dim3(TX_BLOCK), 0, c->stream, ta);
     HIPC(c, hipGetLastError());
-    if (c->timing) {
+    if (c->timing_every) {
         HIPC(c, hipEventRecord(e1, c->stream));
         HIPC(c, hipEventSynchronize(e1));
         float ms = 0;
