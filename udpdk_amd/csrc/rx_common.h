@@ -46,7 +46,7 @@ struct RxArgs {
     const uint2    *binds;
     uint32_t *meta;
     uint32_t *hist;       // [n_lanes][n_tiles]            (general path)
-    uint32_t *tile_cnt;   // [n_tiles][16]                 (general path)
+    uint32_t *tile_cnt;   // [n_tiles][16] per-tile counters
     unsigned long long *lb_state;   // [n_tiles][16] look-back granules (fused path)
     uint32_t *ticket;     // dynamic tile order            (fused path)
     uint32_t *done;       // tiles finished: the last one reduces the counters (fused path)

@@ -36,9 +36,12 @@ namespace udpdk {
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
+// Orders LDS accesses of one wave across lanes. The hardware executes a wave's DS instructions
+// in order, so only the compiler must be kept from reordering them; a wavefront-scope fence
+// would also emit vmcnt(0) and drain every prefetch in flight.
 __device__ __forceinline__ void wave_sync()
 {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    asm volatile("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -109,6 +112,8 @@ constexpr int LB_VALUE_BITS = 38;
 constexpr unsigned long long LB_VALUE_MASK = (1ull << LB_VALUE_BITS) - 1ull;
 
 // counters[c] = sum over tiles of tile_cnt[t][c] (64-bit): each thread sums whole rows.
+// SC1: rows handed off inside the launch are read with agent-scope (sc1) loads.
+template <bool SC1 = false>
 __device__ void reduce_counters(const uint32_t *tile_cnt, uint32_t n_tiles,
                                 unsigned long long *counters, unsigned long long *lds)
 {
@@ -117,13 +122,22 @@ __device__ void reduce_counters(const uint32_t *tile_cnt, uint32_t n_tiles,
 #pragma unroll
     for (int c = 0; c < UDPDK_N_COUNTERS; ++c) s[c] = 0;
     const uint4 *rows = reinterpret_cast<const uint4 *>(tile_cnt);
+    if (SC1) {
+        for (uint32_t t = tid; t < n_tiles; t += blockDim.x) {
+#pragma unroll
+            for (int c = 0; c < UDPDK_N_COUNTERS; ++c)
+                s[c] += __hip_atomic_load(&tile_cnt[(size_t)t * UDPDK_N_COUNTERS + c], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else {
 #pragma unroll 2
-    for (uint32_t t = tid; t < n_tiles; t += blockDim.x) {
-        const uint4 r0 = rows[t * 4 + 0], r1 = rows[t * 4 + 1], r2 = rows[t * 4 + 2], r3 = rows[t * 4 + 3];
-        s[0] += r0.x; s[1] += r0.y; s[2] += r0.z; s[3] += r0.w;
-        s[4] += r1.x; s[5] += r1.y; s[6] += r1.z; s[7] += r1.w;
-        s[8] += r2.x; s[9] += r2.y; s[10] += r2.z; s[11] += r2.w;
-        s[12] += r3.x; s[13] += r3.y; s[14] += r3.z; s[15] += r3.w;
+        for (uint32_t t = tid; t < n_tiles; t += blockDim.x) {
+            const uint4 r0 = rows[t * 4 + 0], r1 = rows[t * 4 + 1], r2 = rows[t * 4 + 2], r3 = rows[t * 4 + 3];
+            s[0] += r0.x; s[1] += r0.y; s[2] += r0.z; s[3] += r0.w;
+            s[4] += r1.x; s[5] += r1.y; s[6] += r1.z; s[7] += r1.w;
+            s[8] += r2.x; s[9] += r2.y; s[10] += r2.z; s[11] += r2.w;
+            s[12] += r3.x; s[13] += r3.y; s[14] += r3.z; s[15] += r3.w;
+        }
     }
     if (tid < UDPDK_N_COUNTERS * 16) lds[tid] = 0;
     __syncthreads();
@@ -176,8 +190,27 @@ __device__ __forceinline__ uint32_t scan_dpp(uint32_t v)
 }
 
 struct Win {
-    uint4 c0, c1, c2, c3, c4;
+    uint4 c0, c1, c2, c3;
+    uint32_t c4;                     // only the first dword of the fifth chunk is ever needed
 };
+
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+
+// 16-byte global load the compiler does not see as a load: it cannot sink it into the branch
+// that uses it (and wait there). The destination is only valid after wait_vm<N>(), N = number
+// of vector-memory operations issued after it (cdna_hip_programming.md §5.7 item 1).
+__device__ __forceinline__ v4u32 asm_load16(const void *p)
+{
+    v4u32 r;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+    return r;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm(v4u32 &r)
+{
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r) : "n"(N) : "memory");
+}
 
 template <bool FUSED>
 __global__ void __launch_bounds__(RX_BLOCK)
@@ -218,33 +251,44 @@ rx_classify(RxArgs a)
 #pragma unroll
     for (int c = 0; c < UDPDK_N_COUNTERS; ++c) cv[c] = 0;
 
-    auto load_desc = [&](uint32_t s, uint32_t &o, uint32_t &l) {
+    // Loads are unconditional (clamped index / range-checked buffer offsets): a load under a
+    // lane condition makes the compiler wait for it at the end of the branch, which would drain
+    // the prefetch pipeline every step.
+    const uint32_t plast = a.n - 1u;
+    auto load_desc = [&](uint32_t s, uint32_t &o, uint32_t &l, uint32_t &t) {
         const uint32_t p = t0 + s * 64 + lane;
         const bool v = s < steps && p < t1;
-        o = v ? a.offset[p] : 0u;
-        l = v ? (uint32_t)a.length[p] : 0u;
+        const uint32_t pc = min(p, plast);
+        const uint32_t o_ = a.offset[pc];
+        const uint32_t l_ = a.length[pc];
+        const uint32_t t_ = a.ptype ? a.ptype[pc] : 0u;
+        o = v ? o_ : 0u;
+        l = v ? l_ : 0u;
+        t = v ? t_ : 0u;
     };
-    // The frame's header window: 5 aligned 16-byte chunks from (off & ~15) hold frame bytes
-    // [0, 64] whatever the alignment. One lane per frame.
+    // The frame's header window: 5 aligned 16-byte chunks from ((off + 12) & ~15) hold frame
+    // bytes [12, 64] whatever the alignment (bytes 0-11, the MAC addresses, are never read).
+    // One lane per frame.
     auto load_win = [&](uint32_t s, uint32_t o, uint32_t l) -> Win {
         const uint32_t p = t0 + s * 64 + lane;
         const bool ok = s < steps && p < t1 && l != 0u && (uint64_t)o + l <= (uint64_t)a.frames_bytes;
-        const uint32_t nw = ok ? min(5u, ((o & 15u) + l + 15u) >> 4) : 0u;
-        const uint32_t ab = o & ~15u;
+        // bytes past the frame are never used (parse and sums mask by length); out-of-range
+        // offsets of the range-checked buffer read zero
+        const uint32_t ab = ok ? ((o + 12u) & ~15u) : 0u;
         Win r;
-        r.c0 = nw > 0u ? load16(fr, ab) : make_uint4(0, 0, 0, 0);
-        r.c1 = nw > 1u ? load16(fr, ab + 16u) : make_uint4(0, 0, 0, 0);
-        r.c2 = nw > 2u ? load16(fr, ab + 32u) : make_uint4(0, 0, 0, 0);
-        r.c3 = nw > 3u ? load16(fr, ab + 48u) : make_uint4(0, 0, 0, 0);
-        r.c4 = nw > 4u ? load16(fr, ab + 64u) : make_uint4(0, 0, 0, 0);
+        r.c0 = load16(fr, ab);
+        r.c1 = load16(fr, ab + 16u);
+        r.c2 = load16(fr, ab + 32u);
+        r.c3 = load16(fr, ab + 48u);
+        r.c4 = __builtin_amdgcn_raw_buffer_load_b32(fr, (int)(ab + 64u), 0, 0);
         return r;
     };
 
     uint32_t st = w;
-    uint32_t c_off = 0, c_len = 0, n_off = 0, n_len = 0;
-    load_desc(st, c_off, c_len);
+    uint32_t c_off = 0, c_len = 0, c_pt = 0, n_off = 0, n_len = 0, n_pt = 0;
+    load_desc(st, c_off, c_len, c_pt);
     Win W = load_win(st, c_off, c_len);
-    load_desc(st + RX_WAVES, n_off, n_len);
+    load_desc(st + RX_WAVES, n_off, n_len, n_pt);
 
     while (st < steps) {
         const uint32_t p = t0 + st * 64 + lane;
@@ -253,11 +297,44 @@ rx_classify(RxArgs a)
         const bool bad_desc = valid && ((uint64_t)off + len > (uint64_t)a.frames_bytes);
         const bool good = valid && !bad_desc;
 
-        // ---- next step of this wave: window loads in flight during this step ----
+        // ---- header fields from the window registers (lane = frame) ----
+        uint32_t g[13];                                     // g[i] = frame bytes 12+4i .. 15+4i
+        {
+            const uint32_t sh = (off + 12u) & 15u, s3 = sh & 3u;
+            uint32_t wd[17], w1[16], w2[14];
+            const uint4 wc[4] = {W.c0, W.c1, W.c2, W.c3};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                wd[4 * i] = wc[i].x; wd[4 * i + 1] = wc[i].y; wd[4 * i + 2] = wc[i].z; wd[4 * i + 3] = wc[i].w;
+            }
+            wd[16] = W.c4;
+            // shift by (sh >> 2) dwords with lane-mask selects (a plain ?: here is turned into a
+            // scratch-indexed array by the compiler)
+            const unsigned long long m4 = __ballot((sh & 4u) != 0u), m8 = __ballot((sh & 8u) != 0u);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w1[i] = lane_select(m4, wd[i], wd[i + 1]);
+#pragma unroll
+            for (int i = 0; i < 14; ++i) w2[i] = lane_select(m8, w1[i], w1[i + 2]);
+#pragma unroll
+            for (int i = 0; i < 13; ++i) g[i] = __builtin_amdgcn_alignbyte(w2[i + 1], w2[i], s3);
+        }
+        const uint32_t pt = !good ? 0u : a.ptype ? c_pt
+                          : (len >= 14 ? (((g[0] & 0xFFFFu) == 0x0008u) ? 0x211u : 0x1u) : 0u);
+        const uint32_t frag = ((g[2] & 0xFFu) << 8) | ((g[2] >> 8) & 0xFFu);
+        const bool is_udp = good && (pt & 0x10u) && len >= 42u && !(frag & 0x3FFFu) && (g[2] >> 24) == 17u;
+        const uint32_t dport = g[6] & 0xFFFFu;                   // poller.c:372
+        // The demux load goes out before the next step's loads, and is waited for only where it
+        // is used, so the next step's window loads stay in flight across this step.
+        v4u32 ev = asm_load16(a.port_tab + dport);
+
+        // ---- next step of this wave: window loads stay in flight across this step ----
         const uint32_t nst = st + RX_WAVES;
         const Win NW = load_win(nst, n_off, n_len);
-        uint32_t nn_off, nn_len;
-        load_desc(nst + RX_WAVES, nn_off, nn_len);
+        uint32_t nn_off, nn_len, nn_pt;
+        load_desc(nst + RX_WAVES, nn_off, nn_len, nn_pt);
+        // issued after the demux load: 5 window loads + 2 descriptor loads (+1 with ptype)
+        wait_vm<7>(ev);
+        const uint4 e = is_udp ? make_uint4(ev[0], ev[1], ev[2], ev[3]) : make_uint4(0, 0, 0, 0);
 
         // ---- tail sweep: UDP bytes at frame offsets >= 64, as chunks swept across lanes ----
         const uint32_t my_nt = (good && len > 64u) ? ((((off + 64u) & 15u) + (len - 64u) + 15u) >> 4) : 0u;
@@ -273,16 +350,22 @@ rx_classify(RxArgs a)
             for (uint32_t k0 = 0; k0 < total; k0 += 64 * RX_UNROLL) {
                 uint4 R[RX_UNROLL];
                 uint32_t Rq[RX_UNROLL];
+                // binary searches of the RX_UNROLL sub-iterations in lockstep (one LDS wait per level)
+#pragma unroll
+                for (int u = 0; u < RX_UNROLL; ++u) Rq[u] = 0;
+#pragma unroll
+                for (int sft = 32; sft >= 1; sft >>= 1) {
+                    uint32_t c[RX_UNROLL];
+#pragma unroll
+                    for (int u = 0; u < RX_UNROLL; ++u) c[u] = l_cs[Rq[u] + sft];
+#pragma unroll
+                    for (int u = 0; u < RX_UNROLL; ++u)
+                        if (c[u] <= k0 + u * 64 + lane) Rq[u] += sft;
+                }
 #pragma unroll
                 for (int u = 0; u < RX_UNROLL; ++u) {
-                    const uint32_t k = k0 + u * 64 + lane;
-                    uint32_t q = 0;
-#pragma unroll
-                    for (int sft = 32; sft >= 1; sft >>= 1)
-                        if (l_cs[q + sft] <= k) q += sft;
-                    Rq[u] = q;
-                    R[u] = k < total ? load16(fr, ((l_off[q] + 64u) & ~15u) + 16u * (k - l_cs[q]))
-                                     : make_uint4(0, 0, 0, 0);
+                    const uint32_t k = k0 + u * 64 + lane, q = Rq[u];
+                    R[u] = load16(fr, k < total ? ((l_off[q] + 64u) & ~15u) + 16u * (k - l_cs[q]) : 0u);
                 }
 #pragma unroll
                 for (int u = 0; u < RX_UNROLL; ++u) {
@@ -304,56 +387,33 @@ rx_classify(RxArgs a)
             wave_sync();
         }
 
-        // ---- parse (lane = frame) from the window registers ----
+        // ---- verdict, checksums, demux ----
         uint32_t word = 0, verdict = UDPDK_V_BAD_DESC, fan = 0, first = 0;
         if (good) {
-            const uint32_t sh = off & 15u, s3 = sh & 3u;
-            uint32_t wd[20], w1[19], w2[17], h[16];
-            const uint4 wc[5] = {W.c0, W.c1, W.c2, W.c3, W.c4};
-#pragma unroll
-            for (int i = 0; i < 5; ++i) {
-                wd[4 * i] = wc[i].x; wd[4 * i + 1] = wc[i].y; wd[4 * i + 2] = wc[i].z; wd[4 * i + 3] = wc[i].w;
-            }
-            // shift by (sh >> 2) dwords with lane-mask selects (a plain ?: here is turned into a
-            // scratch-indexed array by the compiler)
-            const unsigned long long m4 = __ballot((sh & 4u) != 0u), m8 = __ballot((sh & 8u) != 0u);
-#pragma unroll
-            for (int i = 0; i < 19; ++i) w1[i] = lane_select(m4, wd[i], wd[i + 1]);
-#pragma unroll
-            for (int i = 0; i < 17; ++i) w2[i] = lane_select(m8, w1[i], w1[i + 2]);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) h[i] = __builtin_amdgcn_alignbyte(w2[i + 1], w2[i], s3);
-            // h[i] = frame bytes 4i .. 4i+3 (little-endian)
             cv[UDPDK_C_BYTES] += len;
-            uint32_t pt;
-            if (a.ptype) pt = a.ptype[p];
-            else pt = len >= 14 ? (((h[3] & 0xFFFFu) == 0x0008u) ? 0x211u : 0x1u) : 0u;
             if (!(pt & 0x10u)) {
                 verdict = UDPDK_V_NOT_IPV4;                       // udpdk_poller.c:334, :362-366
             } else if (len < 42) {
                 verdict = UDPDK_V_TRUNC;
             } else {
                 // IPv4 header checksum over the fixed 20 bytes at offset 14 (RFC 1071)
-                const uint32_t ipraw = (h[3] >> 16) + sum16(h[4]) + sum16(h[5]) + sum16(h[6]) +
-                                       sum16(h[7]) + (h[8] & 0xFFFFu);
+                const uint32_t ipraw = (g[0] >> 16) + sum16(g[1]) + sum16(g[2]) + sum16(g[3]) +
+                                       sum16(g[4]) + (g[5] & 0xFFFFu);
                 const bool ip_ok = ipraw != 0u && (ipraw % 65535u) == 0u;
-                const bool ihl_ne5 = ((h[3] >> 16) & 0x0Fu) != 5u;
+                const bool ihl_ne5 = ((g[0] >> 16) & 0x0Fu) != 5u;
                 cv[UDPDK_C_IP_BAD] += ip_ok ? 0u : 1u;
                 cv[UDPDK_C_IHL_NE5] += ihl_ne5 ? 1u : 0u;
                 word |= (ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8;
-                const uint32_t frag = ((h[5] & 0xFFu) << 8) | ((h[5] >> 8) & 0xFFu);
-                if ((frag & 0x2000u) || (frag & 0x1FFFu)) {
+                if (frag & 0x3FFFu) {
                     verdict = UDPDK_V_FRAG;                       // udpdk_poller.c:338
-                } else if ((h[5] >> 24) != 17u) {
+                } else if ((g[2] >> 24) != 17u) {
                     verdict = UDPDK_V_NOT_UDP;                    // udpdk_poller.c:368-371
                 } else {
-                    const uint32_t src = (h[6] >> 16) | (h[7] << 16);
-                    const uint32_t dip = (h[7] >> 16) | (h[8] << 16);   // poller.c:373
-                    const uint32_t dport = h[9] & 0xFFFFu;               // poller.c:372
-                    const uint4 e = a.port_tab[dport];                   // overlaps the sums below
-                    const uint32_t ulen_raw = h[9] >> 16;
+                    const uint32_t src = (g[3] >> 16) | (g[4] << 16);
+                    const uint32_t dip = (g[4] >> 16) | (g[5] << 16);   // poller.c:373
+                    const uint32_t ulen_raw = g[6] >> 16;
                     const uint32_t ulen = ((ulen_raw & 0xFFu) << 8) | (ulen_raw >> 8);
-                    const uint32_t ucks = h[10] & 0xFFFFu;
+                    const uint32_t ucks = g[7] & 0xFFFFu;
                     const bool len_bad = ulen < 8u || 34u + ulen > len;
                     uint32_t state;
                     if (ucks == 0u) {
@@ -364,12 +424,12 @@ rx_classify(RxArgs a)
                         // frame bytes [34, min(len, 64)) from the window (frame-relative words)
                         uint32_t ws = 0;
                         if (len >= 64u) {
-                            ws = (h[8] >> 16);
+                            ws = (g[5] >> 16);
 #pragma unroll
-                            for (int i = 9; i < 16; ++i) ws += sum16(h[i]);
+                            for (int i = 6; i < 13; ++i) ws += sum16(g[i]);
                         } else {
 #pragma unroll
-                            for (int i = 8; i < 16; ++i) ws += sum16(h[i] & byte_mask(34, (int)len, 4 * i));
+                            for (int i = 5; i < 13; ++i) ws += sum16(g[i] & byte_mask(34, (int)len, 12 + 4 * i));
                         }
                         uint32_t s = ws % 65535u;
                         // tail bytes [64, len): absolute-address words, byte-swapped at odd starts
@@ -449,8 +509,10 @@ rx_classify(RxArgs a)
         W = NW;
         c_off = n_off;
         c_len = n_len;
+        c_pt = n_pt;
         n_off = nn_off;
         n_len = nn_len;
+        n_pt = nn_pt;
         st = nst;
     }
 
@@ -541,23 +603,20 @@ rx_classify(RxArgs a)
         }
     }
 
-    // ---- counters: rows published with release, the last-arriving tile reduces them ----
-    if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = cnt[tid];
-    if (w == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // ---- counters: write-through (sc1) rows, drained, then one agent-scope ticket add; the
+    // last-arriving tile reads every row with sc1 loads (no fences: MI355X_MICROARCH.md
+    // "Hand-offs measured with sc1 loads", first row) ----
+    if (w == 0) {
+        if (lane < UDPDK_N_COUNTERS)
+            __hip_atomic_store(&a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + lane], cnt[lane],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t prev = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        misc[2] = prev;
-        if (prev == a.n_tiles - 1u) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        if (lane == 0)
+            misc[2] = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (misc[2] != a.n_tiles - 1u) return;
-    reduce_counters(a.tile_cnt, a.n_tiles, a.counters, reinterpret_cast<unsigned long long *>(smem));
+    reduce_counters<true>(a.tile_cnt, a.n_tiles, a.counters, reinterpret_cast<unsigned long long *>(smem));
     if (tid == 0) {
         const uint32_t tot = (uint32_t)a.counters[UDPDK_C_DELIVERIES];
         a.lane_off[0] = 0u;
