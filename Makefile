@@ -32,6 +32,17 @@ $(LIB): $(HIP_OBJ) $(C_OBJ)
 oracle:
 	$(MAKE) -C oracle
 
+# diagnostic library with per-phase s_memtime stamps (tools/stamps.py); never used by tests/bench
+STAMP_LIB := tools/diag/libudpdk_amd.so
+STAMP_OBJ := $(patsubst udpdk_amd/csrc/%.hip,build/stamps/%.o,$(HIP_SRC))
+stamps: $(STAMP_LIB)
+build/stamps/%.o: udpdk_amd/csrc/%.hip $(HDRS)
+	@mkdir -p build/stamps
+	$(HIPCC) $(HIPFLAGS) -DUDPDK_STAMPS $(INC) -c $< -o $@
+$(STAMP_LIB): $(STAMP_OBJ) $(C_OBJ)
+	@mkdir -p tools/diag
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -Wl,--no-undefined
+
 asm: udpdk_amd/csrc/rx_kernels.hip $(HDRS)
 	@mkdir -p build/asm
 	$(HIPCC) $(HIPFLAGS) $(INC) -S --cuda-device-only -o build/asm/rx_kernels.s $<
@@ -41,4 +52,4 @@ clean:
 	rm -rf build $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean asm
+.PHONY: all oracle clean asm stamps

@@ -1,0 +1,35 @@
+"""Per-phase cycle stamps of rx_classify (diagnostic build, make stamps). Prints the mean cycles
+per workgroup (wave 0) spent in each phase, for a tiny batch (latency) and a full batch."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["UDPDK_LIB_OVERRIDE"] = os.path.join(ROOT, "tools", "diag", "libudpdk_amd.so")
+sys.path.insert(0, ROOT)
+import numpy as np
+from udpdk_amd import abi, frames as F
+
+PH = ["prologue", "funnel+fields", "issue next", "wait demux", "tail sweep", "verdict/csum/demux",
+      "meta/ctr/hist", "tile ctr", "lookback", "lane writes", "ctr publish", "steps"]
+L = abi.lib()
+L.udpdk_gpu_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
+ctx = abi.GpuContext(0, max_frames=1 << 22, max_lanes=4096)
+dbg = ctx.alloc(16 * 8 * 8192)
+L.udpdk_gpu_debug_buffer(ctx.handle, C.c_void_p(dbg.ptr))
+for cfg, n in [(2, 4096), (2, None), (4, 65536), (3, 65536)]:
+    w = F.config_batch(cfg, n=n)
+    ctx.upload_snapshot(abi.snapshot_from_lists(w.port_lists(), w.n_sockets))
+    db = abi.rx_upload(ctx, w.batch.frames, w.batch.offset, w.batch.length)
+    db.frames_bytes = w.batch.frames_bytes
+    out = abi.rx_alloc_out(ctx, w.batch.n, w.n_sockets, w.batch.n)
+    for _ in range(3):
+        abi.rx_run(ctx, db, out)
+    _, tiles = abi.geometry(w.batch.n, w.n_sockets)
+    d = ctx.download(dbg, np.uint64, 16 * tiles).reshape(tiles, 16).astype(np.float64)
+    print(f"{w.name} n={w.batch.n} tiles={tiles}")
+    for k, name in enumerate(PH):
+        print(f"   {name:20s} mean {d[:, k].mean():12.0f}  max {d[:, k].max():12.0f}")
+    for b in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt):
+        b.free()
+ctx.close()

@@ -15,7 +15,7 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libudpdk_amd.so")
+LIB_PATH = os.environ.get("UDPDK_LIB_OVERRIDE") or os.path.join(_HERE, "libudpdk_amd.so")
 
 # ---- constants mirrored from include/udpdk_gpu.h -------------------------------------------
 V_DELIVERED, V_NOT_IPV4, V_FRAG, V_NOT_UDP, V_NO_BIND, V_NO_MATCH, V_TRUNC, V_BAD_DESC = range(8)

@@ -55,6 +55,7 @@ struct RxArgs {
     uint32_t *lane_off;
     unsigned long long *counters;
     uint32_t *total;
+    unsigned long long *dbg;        // diagnostic stamps (UDPDK_STAMPS builds), may be null
     uint32_t lane_cap;
     uint32_t epoch;
     uint32_t key_bits;

@@ -106,6 +106,21 @@ __device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
+// Diagnostic build (-DUDPDK_STAMPS): wave 0 of every workgroup accumulates s_memtime cycles per
+// phase into a.dbg[block][16]. Stamps never feed an output (cdna_hip_programming.md §7).
+#ifdef UDPDK_STAMPS
+#define STAMP(k)                                                                 \
+    do {                                                                         \
+        if (w == 0) {                                                            \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+            st_acc[k] += t_ - st_last;                                           \
+            st_last = t_;                                                        \
+        }                                                                        \
+    } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+
 // 8-byte look-back granules: tag (epoch << 2 | kind) in the top 26 bits, value in the low 38.
 constexpr uint32_t LB_AGG = 1u, LB_INCL = 2u;
 constexpr int LB_VALUE_BITS = 38;
@@ -219,6 +234,9 @@ rx_classify(RxArgs a)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t steps = a.tile_frames / 64;
+#ifdef UDPDK_STAMPS
+    unsigned long long st_acc[16] = {0}, st_last = __builtin_amdgcn_s_memtime();
+#endif
 
     uint32_t *arr = reinterpret_cast<uint32_t *>(smem) + w * WAVE_ARRAYS * 64;
     uint32_t *l_cs = arr, *l_off = arr + 64, *l_len = arr + 128;
@@ -289,6 +307,7 @@ rx_classify(RxArgs a)
     load_desc(st, c_off, c_len, c_pt);
     Win W = load_win(st, c_off, c_len);
     load_desc(st + RX_WAVES, n_off, n_len, n_pt);
+    STAMP(0);
 
     while (st < steps) {
         const uint32_t p = t0 + st * 64 + lane;
@@ -325,6 +344,7 @@ rx_classify(RxArgs a)
         const uint32_t dport = g[6] & 0xFFFFu;                   // poller.c:372
         // The demux load goes out before the next step's loads, and is waited for only where it
         // is used, so the next step's window loads stay in flight across this step.
+        STAMP(1);
         v4u32 ev = asm_load16(a.port_tab + dport);
 
         // ---- next step of this wave: window loads stay in flight across this step ----
@@ -332,8 +352,10 @@ rx_classify(RxArgs a)
         const Win NW = load_win(nst, n_off, n_len);
         uint32_t nn_off, nn_len, nn_pt;
         load_desc(nst + RX_WAVES, nn_off, nn_len, nn_pt);
+        STAMP(2);
         // issued after the demux load: 5 window loads + 2 descriptor loads (+1 with ptype)
         wait_vm<7>(ev);
+        STAMP(3);
         const uint4 e = is_udp ? make_uint4(ev[0], ev[1], ev[2], ev[3]) : make_uint4(0, 0, 0, 0);
 
         // ---- tail sweep: UDP bytes at frame offsets >= 64, as chunks swept across lanes ----
@@ -387,6 +409,7 @@ rx_classify(RxArgs a)
             wave_sync();
         }
 
+        STAMP(4);
         // ---- verdict, checksums, demux ----
         uint32_t word = 0, verdict = UDPDK_V_BAD_DESC, fan = 0, first = 0;
         if (good) {
@@ -475,6 +498,7 @@ rx_classify(RxArgs a)
                 }
             }
         }
+        STAMP(5);
         if (valid) {
             word |= verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
             a.meta[p] = word;
@@ -506,6 +530,10 @@ rx_classify(RxArgs a)
                 atomicAdd(&hist[key], 1u);
             }
         }
+        STAMP(6);
+#ifdef UDPDK_STAMPS
+        st_acc[11] += 1;
+#endif
         W = NW;
         c_off = n_off;
         c_len = n_len;
@@ -523,6 +551,10 @@ rx_classify(RxArgs a)
         if (lane == 0 && s) atomicAdd(&cnt[c], s);
     }
     __syncthreads();
+    STAMP(7);
+#ifdef UDPDK_STAMPS
+    if (!FUSED && a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
+#endif
 
     if (!FUSED) {
         for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK)
@@ -593,6 +625,7 @@ rx_classify(RxArgs a)
         }
     }
     __syncthreads();
+    STAMP(8);
     const uint32_t base = misc[1];
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (uint32_t s = w; s < steps; s += RX_WAVES) {
@@ -603,6 +636,7 @@ rx_classify(RxArgs a)
         }
     }
 
+    STAMP(9);
     // ---- counters: write-through (sc1) rows, drained, then one agent-scope ticket add; the
     // last-arriving tile reads every row with sc1 loads (no fences: MI355X_MICROARCH.md
     // "Hand-offs measured with sc1 loads", first row) ----
@@ -615,6 +649,10 @@ rx_classify(RxArgs a)
             misc[2] = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    STAMP(10);
+#ifdef UDPDK_STAMPS
+    if (a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
+#endif
     if (misc[2] != a.n_tiles - 1u) return;
     reduce_counters<true>(a.tile_cnt, a.n_tiles, a.counters, reinterpret_cast<unsigned long long *>(smem));
     if (tid == 0) {

@@ -75,6 +75,8 @@ struct udpdk_gpu_ctx {
     uint8_t *st_desc_h = nullptr; size_t st_desc_hcap = 0;
     uint8_t *st_out_d = nullptr; size_t st_out_cap = 0;
 
+    unsigned long long *dbg = nullptr;        // diagnostic stamp buffer (UDPDK_STAMPS builds)
+
     // timing
     uint32_t timing_every = 0;                // 0 off, N: events on every Nth call
     uint64_t timing_calls = 0;
@@ -458,6 +460,7 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     ra.counters = c->res->counters;
     ra.total = &c->res->total;
     ra.lane_cap = o->lane_cap;
+    ra.dbg = c->dbg;
     ra.epoch = c->epoch;
     ra.key_bits = c->key_bits;
     ra.frames_bytes = (uint32_t)bt->frames_bytes;
@@ -653,5 +656,15 @@ int udpdk_gpu_tx_build(udpdk_gpu_ctx *c, const udpdk_tx_config_t *cfg, const udp
     }
     return 0;
 }
+
+#ifdef UDPDK_STAMPS
+// Diagnostic builds only (not part of the ABI headers): per-workgroup phase stamps.
+int udpdk_gpu_debug_buffer(udpdk_gpu_ctx *c, void *dev)
+{
+    if (!c) return -EINVAL;
+    c->dbg = (unsigned long long *)dev;
+    return 0;
+}
+#endif
 
 } // extern "C"
