@@ -155,6 +155,44 @@ def side_config(ctx, cfg: int, steps: int, rotate: int):
     return out
 
 
+def end_to_end(ctx, cfg: int, reps: int):
+    """Host-resident batch through udpdk_gpu_rx_host: frames already in pinned host memory (DPDK
+    hugepage mbufs registered with the runtime), H2D of frames + descriptors, the RX pipeline,
+    D2H of verdicts and lanes, synchronous per batch. PCIe-inclusive; never the headline value."""
+    w = F.config_batch(cfg)
+    b = w.batch
+    ctx.upload_snapshot(abi.snapshot_from_lists(w.port_lists(), w.n_sockets))
+    L = abi.lib()
+
+    def pinned(nbytes, dtype):
+        p = C.c_void_p()
+        abi._check(L.udpdk_gpu_host_alloc(ctx.handle, max(16, nbytes), C.byref(p)), "host_alloc")
+        arr = np.ctypeslib.as_array((C.c_uint8 * max(16, nbytes)).from_address(p.value))
+        return p, arr[:nbytes].view(dtype)
+    held = []
+    pf, fr = pinned(b.frames_bytes, np.uint8); held.append(pf)
+    fr[:] = b.frames[:b.frames_bytes]
+    po, meta = pinned(4 * b.n, np.uint32); held.append(po)
+    pl, loff = pinned(4 * (w.n_sockets + 1), np.uint32); held.append(pl)
+    pp, pkt = pinned(4 * b.n, np.uint32); held.append(pp)
+    st = abi.RxStats()
+
+    def once():
+        abi._check(L.udpdk_gpu_rx_host(ctx.handle, pf.value, b.frames_bytes, b.offset.ctypes.data,
+                                       b.length.ctypes.data, None, b.n, po.value, pl.value, pp.value,
+                                       b.n, C.byref(st)), "udpdk_gpu_rx_host")
+    once()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    dt = (time.perf_counter() - t0) / reps
+    for p in held:
+        L.udpdk_gpu_host_free(ctx.handle, p)
+    return {"workload": w.name, "mpkt_s": round(b.n / dt / 1e6, 1),
+            "frame_gbps": round(int(b.length.sum()) / dt / 1e9, 2), "ms_per_batch": round(dt * 1e3, 3),
+            "path": "pinned host frames -> H2D -> rx pipeline -> D2H meta+lanes, synchronous"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,6 +282,13 @@ def main():
                 except Exception as e:   # a side line never hides the main measurement
                     extra.append({"config": cfg, "error": repr(e)})
         line["other_configs"] = extra
+        e2e = []
+        for cfg in (2, 3, 4):
+            try:
+                e2e.append(end_to_end(ctx, cfg, 10))
+            except Exception as e:
+                e2e.append({"config": cfg, "error": repr(e)})
+        line["end_to_end"] = e2e
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -11,7 +11,7 @@ import numpy as np
 from udpdk_amd import abi, frames as F
 
 PH = ["prologue", "funnel+fields", "issue next", "wait demux", "tail sweep", "verdict/csum/demux",
-      "meta/ctr/hist", "tile ctr", "lookback", "lane writes", "ctr publish", "steps"]
+      "meta/ctr/hist", "tile ctr", "lookback", "ctr publish", "lane writes", "steps"]
 L = abi.lib()
 L.udpdk_gpu_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 ctx = abi.GpuContext(0, max_frames=1 << 22, max_lanes=4096)
@@ -30,6 +30,23 @@ for cfg, n in [(2, 4096), (2, None), (4, 65536), (3, 65536)]:
     print(f"{w.name} n={w.batch.n} tiles={tiles}")
     for k, name in enumerate(PH):
         print(f"   {name:20s} mean {d[:, k].mean():12.0f}  max {d[:, k].max():12.0f}")
+    # timeline from the chip-synchronous 100 MHz realtime stamps (slots 12-13)
+    raw = ctx.download(dbg, np.uint64, 16 * tiles).reshape(tiles, 16)
+    st0 = raw[:, 12].astype(np.int64) - int(raw[:, 12].min())
+    en0 = raw[:, 13].astype(np.int64) - int(raw[:, 12].min())
+    dur = en0 - st0
+    pct = lambda x: " ".join(f"{np.percentile(x, q) / 100:.2f}" for q in (0, 10, 50, 90, 100))
+    print(f"   span {en0.max() / 100:.2f} us; start us p0/10/50/90/100: {pct(st0)}; "
+          f"duration us: {pct(dur)}")
+    xcc = (raw[:, 14] >> 32).astype(np.int64) & 0xF
+    for x in np.unique(xcc)[:8]:
+        m = xcc == x
+        print(f"     xcc {x}: wgs {m.sum():5d} start p50 {np.median(st0[m]) / 100:.2f} "
+              f"end max {en0[m].max() / 100:.2f}")
+    tl = raw[:, 15].astype(np.int64)
+    order = np.argsort(tl)
+    print(f"   tile order: start of tile k vs k: corr {np.corrcoef(tl, st0)[0, 1]:.3f}; "
+          f"end(last tile) {en0[order[-1]] / 100:.2f} us")
     for b in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt):
         b.free()
 ctx.close()

@@ -76,6 +76,14 @@ __device__ __forceinline__ uint32_t dword_window(int a, int e, int i)
 
 __device__ __forceinline__ uint32_t sum16(uint32_t v) { return (v & 0xFFFFu) + (v >> 16); }
 
+// One's-complement fold of a 32-bit sum of 16-bit words to [0, 0xffff] (0xffff is -0: a valid
+// RFC 1071 sum folds to 0xffff; only an all-zero input folds to 0).
+__device__ __forceinline__ uint32_t fold32(uint32_t x)
+{
+    x = (x & 0xFFFFu) + (x >> 16);
+    return (x & 0xFFFFu) + (x >> 16);
+}
+
 // Sum of the 16-bit halves of the bytes [a, e) of the chunk: <= 8 * 0xFFFF.
 __device__ __forceinline__ uint32_t chunk_sum(const uint4 d, int a, int e)
 {
@@ -116,6 +124,14 @@ __device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
             st_acc[k] += t_ - st_last;                                           \
             st_last = t_;                                                        \
         }                                                                        \
+    } while (0)
+// slots 12-15: realtime (100 MHz, chip-synchronous) at entry and exit, HW_ID | XCC_ID << 32, tile
+#define STAMP_END()                                                                   \
+    do {                                                                              \
+        st_acc[13] = __builtin_amdgcn_s_memrealtime();                                \
+        st_acc[14] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |  \
+                     ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32); \
+        st_acc[15] = tile;                                                            \
     } while (0)
 #else
 #define STAMP(k) do {} while (0)
@@ -236,6 +252,7 @@ rx_classify(RxArgs a)
     const uint32_t steps = a.tile_frames / 64;
 #ifdef UDPDK_STAMPS
     unsigned long long st_acc[16] = {0}, st_last = __builtin_amdgcn_s_memtime();
+    st_acc[12] = __builtin_amdgcn_s_memrealtime();
 #endif
 
     uint32_t *arr = reinterpret_cast<uint32_t *>(smem) + w * WAVE_ARRAYS * 64;
@@ -265,9 +282,11 @@ rx_classify(RxArgs a)
     const uint32_t t0 = tile * a.tile_frames;
     const uint32_t t1 = min(a.n, t0 + a.tile_frames);
 
-    uint32_t cv[UDPDK_N_COUNTERS];                          // per-lane counters
+    // counters: wave-uniform (ballot popcounts, kept in SGPRs) + the per-lane byte sum
+    uint32_t sc[UDPDK_N_COUNTERS];
 #pragma unroll
-    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) cv[c] = 0;
+    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) sc[c] = 0;
+    uint32_t lane_bytes = 0;
 
     // Loads are unconditional (clamped index / range-checked buffer offsets): a load under a
     // lane condition makes the compiler wait for it at the end of the branch, which would drain
@@ -412,8 +431,10 @@ rx_classify(RxArgs a)
         STAMP(4);
         // ---- verdict, checksums, demux ----
         uint32_t word = 0, verdict = UDPDK_V_BAD_DESC, fan = 0, first = 0;
+        bool f_ip_bad = false, f_ihl = false, f_len_bad = false;
+        uint32_t f_udp = 3u;                                 // 3 = not a UDP verdict
         if (good) {
-            cv[UDPDK_C_BYTES] += len;
+            lane_bytes += len;
             if (!(pt & 0x10u)) {
                 verdict = UDPDK_V_NOT_IPV4;                       // udpdk_poller.c:334, :362-366
             } else if (len < 42) {
@@ -422,10 +443,10 @@ rx_classify(RxArgs a)
                 // IPv4 header checksum over the fixed 20 bytes at offset 14 (RFC 1071)
                 const uint32_t ipraw = (g[0] >> 16) + sum16(g[1]) + sum16(g[2]) + sum16(g[3]) +
                                        sum16(g[4]) + (g[5] & 0xFFFFu);
-                const bool ip_ok = ipraw != 0u && (ipraw % 65535u) == 0u;
+                const bool ip_ok = fold32(ipraw) == 0xFFFFu;
                 const bool ihl_ne5 = ((g[0] >> 16) & 0x0Fu) != 5u;
-                cv[UDPDK_C_IP_BAD] += ip_ok ? 0u : 1u;
-                cv[UDPDK_C_IHL_NE5] += ihl_ne5 ? 1u : 0u;
+                f_ip_bad = !ip_ok;
+                f_ihl = ihl_ne5;
                 word |= (ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8;
                 if (frag & 0x3FFFu) {
                     verdict = UDPDK_V_FRAG;                       // udpdk_poller.c:338
@@ -454,24 +475,21 @@ rx_classify(RxArgs a)
 #pragma unroll
                             for (int i = 5; i < 13; ++i) ws += sum16(g[i] & byte_mask(34, (int)len, 12 + 4 * i));
                         }
-                        uint32_t s = ws % 65535u;
                         // tail bytes [64, len): absolute-address words, byte-swapped at odd starts
-                        const uint32_t t = tsum % 65535u;
-                        s = (s + ((off & 1u) ? (t * 256u) % 65535u : t)) % 65535u;
+                        uint32_t t = fold32(tsum);
+                        if (off & 1u) t = ((t & 0xFFu) << 8) | (t >> 8);
+                        uint32_t s = ws + t + (src & 0xFFFFu) + (src >> 16) + (dip & 0xFFFFu) +
+                                     (dip >> 16) + 0x1100u + ulen_raw;   // + pseudo-header
                         if (34u + ulen < len) {                    // Ethernet padding after the datagram
                             uint32_t pad = 0;
                             for (uint32_t r = 34u + ulen; r < len; ++r)
                                 pad += (uint32_t)a.frames[off + r] << (8u * (r & 1u));
-                            s = (s + 65535u - pad % 65535u) % 65535u;
+                            s += 0xFFFFu - fold32(pad);            // one's-complement subtraction
                         }
-                        const uint32_t pseudo = (src & 0xFFFFu) + (src >> 16) + (dip & 0xFFFFu) +
-                                                (dip >> 16) + 0x1100u + ulen_raw;
-                        state = ((s + pseudo) % 65535u) == 0u ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD;
+                        state = fold32(s) == 0xFFFFu ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD;
                     }
-                    cv[UDPDK_C_UDP_OK] += state == UDPDK_UDP_CSUM_OK ? 1u : 0u;
-                    cv[UDPDK_C_UDP_BAD] += state == UDPDK_UDP_CSUM_BAD ? 1u : 0u;
-                    cv[UDPDK_C_UDP_NONE] += state == UDPDK_UDP_CSUM_NONE ? 1u : 0u;
-                    cv[UDPDK_C_LEN_BAD] += len_bad ? 1u : 0u;
+                    f_udp = state;
+                    f_len_bad = len_bad;
                     word |= state << 5 | (len_bad ? 1u : 0u) << 7;
 
                     // ---- demux: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
@@ -502,10 +520,18 @@ rx_classify(RxArgs a)
         if (valid) {
             word |= verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
             a.meta[p] = word;
-#pragma unroll
-            for (int v = 0; v < UDPDK_N_VERDICTS; ++v) cv[v] += verdict == (uint32_t)v ? 1u : 0u;
-            cv[UDPDK_C_DELIVERIES] += fan;
         }
+#pragma unroll
+        for (int v = 0; v < UDPDK_N_VERDICTS; ++v)
+            sc[v] += (uint32_t)__popcll(__ballot(valid && verdict == (uint32_t)v));
+        sc[UDPDK_C_IP_BAD] += (uint32_t)__popcll(__ballot(f_ip_bad));
+        sc[UDPDK_C_IHL_NE5] += (uint32_t)__popcll(__ballot(f_ihl));
+        sc[UDPDK_C_UDP_OK] += (uint32_t)__popcll(__ballot(f_udp == UDPDK_UDP_CSUM_OK));
+        sc[UDPDK_C_UDP_BAD] += (uint32_t)__popcll(__ballot(f_udp == UDPDK_UDP_CSUM_BAD));
+        sc[UDPDK_C_UDP_NONE] += (uint32_t)__popcll(__ballot(f_udp == UDPDK_UDP_CSUM_NONE));
+        sc[UDPDK_C_LEN_BAD] += (uint32_t)__popcll(__ballot(f_len_bad));
+        if (__ballot(fan > 1u)) sc[UDPDK_C_DELIVERIES] += wave_sum(fan);   // clones (rare)
+        else sc[UDPDK_C_DELIVERIES] += (uint32_t)__popcll(__ballot(fan != 0u));
         const bool delivered = valid && fan > 0u;
         if (FUSED) {
             const unsigned long long m = __ballot(delivered);
@@ -545,14 +571,16 @@ rx_classify(RxArgs a)
     }
 
     // ---- tile counters ----
+    sc[UDPDK_C_BYTES] = (uint32_t)__builtin_amdgcn_readlane((int)scan_dpp(lane_bytes), 63);
+    if (lane == 0) {
 #pragma unroll
-    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) {
-        const uint32_t s = wave_sum(cv[c]);
-        if (lane == 0 && s) atomicAdd(&cnt[c], s);
+        for (int c = 0; c < UDPDK_N_COUNTERS; ++c)
+            if (sc[c]) atomicAdd(&cnt[c], sc[c]);
     }
     __syncthreads();
     STAMP(7);
 #ifdef UDPDK_STAMPS
+    if (!FUSED) STAMP_END();
     if (!FUSED && a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
 #endif
 
@@ -563,8 +591,17 @@ rx_classify(RxArgs a)
         return;
     }
 
-    // ---- FUSED: step prefix, decoupled look-back over tiles, lane writes ----
+    // ---- FUSED: decoupled look-back over tiles, counters, lane writes ----
     if (w == 0) {
+        // Decoupled look-back on the tile's delivery count: publish the aggregate at once, then
+        // each lane inspects one of the 64 nearest predecessors per round (8-byte {tag, value}
+        // granules written and read at agent scope; the data is the flag).
+        unsigned long long *state = a.lb_state;
+        const unsigned long long agg = cnt[UDPDK_C_DELIVERIES];
+        const unsigned long long tagA = (unsigned long long)((a.epoch << 2) | LB_AGG) << LB_VALUE_BITS;
+        const unsigned long long tagI = (unsigned long long)((a.epoch << 2) | LB_INCL) << LB_VALUE_BITS;
+        if (lane == 0)
+            __hip_atomic_store(&state[tile], tagA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // exclusive prefix of per-step delivered counts (steps <= 256: 4 per lane)
         uint32_t v[4], s4 = 0;
 #pragma unroll
@@ -573,22 +610,13 @@ rx_classify(RxArgs a)
             v[i] = si < steps ? scnt[si] : 0u;
             s4 += v[i];
         }
-        uint32_t run = wave_incl_scan(s4) - s4;
+        uint32_t run = scan_dpp(s4) - s4;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint32_t si = lane * 4 + i;
             if (si < steps) scnt[si] = run;
             run += v[i];
         }
-        // Decoupled look-back on the tile's delivery count: publish the aggregate, then each
-        // lane inspects one of the 64 nearest predecessors per round (8-byte {tag, value}
-        // granules written and read at agent scope; the data is the flag).
-        unsigned long long *state = a.lb_state;
-        const unsigned long long agg = cnt[UDPDK_C_DELIVERIES];
-        const unsigned long long tagA = (unsigned long long)((a.epoch << 2) | LB_AGG) << LB_VALUE_BITS;
-        const unsigned long long tagI = (unsigned long long)((a.epoch << 2) | LB_INCL) << LB_VALUE_BITS;
-        if (lane == 0)
-            __hip_atomic_store(&state[tile], tagA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned long long excl = 0;
         bool timeout = false;
         for (int32_t wb = (int32_t)tile - 1; wb >= 0 && !timeout; wb -= 64) {
@@ -623,9 +651,19 @@ rx_classify(RxArgs a)
                                __HIP_MEMORY_SCOPE_AGENT);
             misc[1] = (uint32_t)excl;
         }
+        STAMP(8);
+        // counters: write-through (sc1) row, drained, then one agent-scope ticket add; the
+        // last-arriving tile reads every row with sc1 loads (no fences: MI355X_MICROARCH.md
+        // "Hand-offs measured with sc1 loads", first row)
+        if (lane < UDPDK_N_COUNTERS)
+            __hip_atomic_store(&a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + lane], cnt[lane],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+            misc[2] = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        STAMP(9);
     }
     __syncthreads();
-    STAMP(8);
     const uint32_t base = misc[1];
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (uint32_t s = w; s < steps; s += RX_WAVES) {
@@ -635,22 +673,9 @@ rx_classify(RxArgs a)
             if (pos < a.lane_cap) a.lane_pkt[pos] = t0 + s * 64 + lane;
         }
     }
-
-    STAMP(9);
-    // ---- counters: write-through (sc1) rows, drained, then one agent-scope ticket add; the
-    // last-arriving tile reads every row with sc1 loads (no fences: MI355X_MICROARCH.md
-    // "Hand-offs measured with sc1 loads", first row) ----
-    if (w == 0) {
-        if (lane < UDPDK_N_COUNTERS)
-            __hip_atomic_store(&a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + lane], cnt[lane],
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-            misc[2] = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
     STAMP(10);
 #ifdef UDPDK_STAMPS
+    STAMP_END();
     if (a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
 #endif
     if (misc[2] != a.n_tiles - 1u) return;
