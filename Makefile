@@ -45,7 +45,7 @@ $(STAMP_LIB): $(STAMP_OBJ) $(C_OBJ)
 
 asm: udpdk_amd/csrc/rx_kernels.hip $(HDRS)
 	@mkdir -p build/asm
-	$(HIPCC) $(HIPFLAGS) $(INC) -S --cuda-device-only -o build/asm/rx_kernels.s $<
+	$(HIPCC) $(HIPFLAGS) -Wno-unused-command-line-argument $(INC) -S --cuda-device-only -o build/asm/rx_kernels.s $<
 	$(HIPCC) $(HIPFLAGS) $(INC) -c -Rpass-analysis=kernel-resource-usage $< -o /dev/null 2> build/asm/rx_resource.txt || true
 
 clean:

@@ -1,7 +1,9 @@
 """Benchmark: device-resident RX parse + checksum + port demux (BASELINE.json metric).
 
-A step = one udpdk_gpu_rx call (rx_classify + rx_scan + rx_scatter) over one batch of frames
-already resident in HBM. Default workload = BASELINE.json configs[1]: 1 M synthetic 64 B
+A step = one udpdk_gpu_rx call over one batch of frames already resident in HBM (single-lane
+batches: the fused rx_classify alone; otherwise rx_classify + rx_scan + rx_scatter). The timed
+region carries no per-launch events: its GPU time comes from two events on the library stream
+around all K steps, so kernel durations agree with rocprofv3's kernel trace. Default workload = BASELINE.json configs[1]: 1 M synthetic 64 B
 Eth/IPv4/UDP frames, 1 bound port, per GPU. With N GPUs (torchrun) every rank processes its own
 independent shard (seed 0x5EED ^ rank) with no data-path collective: weak scaling.
 
@@ -42,8 +44,6 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1500 B / IMIX side lines")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU time per baseline leg")
-    p.add_argument("--timing-every", type=int, default=8,
-                   help="record per-kernel HIP events on every Nth timed step (sampling)")
     return p.parse_args()
 
 
@@ -98,26 +98,80 @@ class Rx:
         return self.sum_len + 8 * self.n + 4 * self.n + 4 * self.n + 4 * (self.w.n_sockets + 1)
 
 
-def time_loop(rx: Rx, steps: int, warmup: int, barrier, timing: int):
-    """timing = N: kernel events on every Nth step of the timed region (0 = none)."""
+class HipEvents:
+    """Two timing events on the library's stream (libamdhip64 through ctypes): the GPU time of
+    the whole timed region, with no per-launch events inside it (an event pair around a single
+    launch adds the dispatch latency that back-to-back launches hide)."""
+
+    def __init__(self, ctx: abi.GpuContext):
+        self.hip = C.CDLL("libamdhip64.so")
+        self.stream = C.c_void_p(abi.lib().udpdk_gpu_stream(ctx.handle))
+        self.ev = [C.c_void_p(), C.c_void_p()]
+        for e in self.ev:
+            if self.hip.hipEventCreate(C.byref(e)) != 0:
+                raise RuntimeError("hipEventCreate failed")
+
+    def record(self, i: int):
+        if self.hip.hipEventRecord(self.ev[i], self.stream) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def elapsed_ms(self) -> float:
+        self.hip.hipEventSynchronize(self.ev[1])
+        ms = C.c_float()
+        if self.hip.hipEventElapsedTime(C.byref(ms), self.ev[0], self.ev[1]) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return float(ms.value)
+
+    def close(self):
+        for e in self.ev:
+            self.hip.hipEventDestroy(e)
+
+
+def time_loop(rx: Rx, steps: int, warmup: int, barrier, split_steps: int):
+    """Timed region: `steps` back-to-back udpdk_gpu_rx calls between a barrier + sync on each
+    side (host wall clock) and two events on the library stream (GPU time). Afterwards, outside
+    the timed region, `split_steps` calls with per-kernel events give the pipeline's kernel split
+    (general path only; the fused path is one kernel)."""
     ctx = rx.ctx
+    ev = HipEvents(ctx)
     for i in range(warmup):
         rx.step(i)
     rx.check()
-    ctx.timing(timing)
-    ctx.timing_read()                    # reset accumulators
+    ctx.timing(0)
     barrier()
     ctx.sync()
     t0 = time.perf_counter()
+    ev.record(0)
     for i in range(steps):
         rx.step(warmup + i)
+    ev.record(1)
     ctx.sync()
     t1 = time.perf_counter()
     barrier()
+    gpu_ms = ev.elapsed_ms()
+    ev.close()
     st = rx.check()
-    ms, n = ctx.timing_read() if timing else ([0.0] * 4, [0] * 4)
-    ctx.timing(0)
-    return (t1 - t0), ms, n, st
+    split = None
+    if split_steps and rx.w.n_sockets > 1:
+        ctx.timing(1)
+        ctx.timing_read()
+        for i in range(split_steps):
+            rx.step(i)
+        ctx.sync()
+        ms, n = ctx.timing_read()
+        ctx.timing(0)
+        per = [ms[k] / max(1, n[k]) for k in range(3)]
+        split = [x / max(1e-12, sum(per)) for x in per]
+    return (t1 - t0), gpu_ms / steps, split, st
+
+
+def kernel_times(rx: Rx, gpu_step_ms: float, split):
+    """Per-launch kernel times (us): the fused single-lane path is one kernel per step, so its
+    duration is the GPU time per step; the general path's step is divided by the event split."""
+    us = 1e3 * gpu_step_ms
+    if split is None:
+        return {"rx_classify": us, "rx_scan": 0.0, "rx_scatter": 0.0}
+    return {"rx_classify": us * split[0], "rx_scan": us * split[1], "rx_scatter": us * split[2]}
 
 
 def cpu_baseline(w: F.Workload, target_s: float):
@@ -142,13 +196,15 @@ def cpu_baseline(w: F.Workload, target_s: float):
 def side_config(ctx, cfg: int, steps: int, rotate: int):
     w = F.config_batch(cfg)
     rx = Rx(ctx, w, rotate)
-    wall, ms, n, st = time_loop(rx, steps, 5, lambda: None, 4)
-    out = {"workload": w.name, "mpkt_s": rx.n * steps / wall / 1e6,
-           "gbps_pipeline": rx.pipeline_bytes() * steps / wall / 1e9,
-           "classify_us": 1e3 * ms[0] / max(1, n[0]),
-           "classify_gbps": rx.classify_bytes() / (ms[0] / max(1, n[0]) / 1e3) / 1e9,
-           "frac_hbm_classify": rx.classify_bytes() / (ms[0] / max(1, n[0]) / 1e3) / 1e9 / HBM_PEAK_GBS,
-           "scan_us": 1e3 * ms[1] / max(1, n[1]), "scatter_us": 1e3 * ms[2] / max(1, n[2])}
+    wall, gpu_step, split, st = time_loop(rx, steps, 5, lambda: None, 20)
+    kt = kernel_times(rx, gpu_step, split)
+    cls_gbps = rx.classify_bytes() / (kt["rx_classify"] / 1e6) / 1e9
+    out = {"workload": w.name, "mpkt_s": round(rx.n * steps / wall / 1e6, 1),
+           "gbps_pipeline": round(rx.pipeline_bytes() * steps / wall / 1e9, 1),
+           "gpu_us_per_step": round(1e3 * gpu_step, 2),
+           "kernel_us": {k: round(v, 2) for k, v in kt.items()},
+           "classify_gbps": round(cls_gbps, 1),
+           "frac_hbm_classify": round(cls_gbps / HBM_PEAK_GBS, 4)}
     for a in rx.args:
         a[4].frames.free(); a[4].offset.free(); a[4].length.free()
         a[5].meta.free(); a[5].lane_off.free(); a[5].lane_pkt.free()
@@ -215,7 +271,8 @@ def main():
     w = F.config_batch(args.config, n=args.frames, shard=rank)
     ctx = abi.GpuContext(device, max_frames=max(w.batch.n, 1 << 22), max_lanes=4096)
     rx = Rx(ctx, w, args.rotate_mib << 20)
-    wall, ms, n, st = time_loop(rx, args.steps, args.warmup, barrier, args.timing_every)
+    wall, gpu_step, split, st = time_loop(rx, args.steps, args.warmup, barrier, 20)
+    kt = kernel_times(rx, gpu_step, split)
     if dist is not None:
         t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -223,9 +280,8 @@ def main():
     total_pkts = rx.n * args.steps * world
     mpkt_s = total_pkts / wall / 1e6
     ms_step = 1e3 * wall / args.steps
-    cls_ms = ms[0] / max(1, n[0])
     cls_bytes = rx.classify_bytes()
-    achieved = cls_bytes / (cls_ms / 1e3) / 1e9
+    achieved = cls_bytes / (kt["rx_classify"] / 1e6) / 1e9
 
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
@@ -253,9 +309,8 @@ def main():
                    "frame_bytes_per_gpu": rx.sum_len, "bound_ports": w.n_sockets,
                    "parallelism": f"shard{world}", "device_copies_rotated": rx.copies},
         "gbps_pipeline": round(rx.pipeline_bytes() * args.steps * world / wall / 1e9, 1),
-        "kernel_us": {"rx_classify": round(1e3 * cls_ms, 3),
-                      "rx_scan": round(1e3 * ms[1] / max(1, n[1]), 3),
-                      "rx_scatter": round(1e3 * ms[2] / max(1, n[2]), 3)},
+        "gpu_us_per_step": round(1e3 * gpu_step, 3),
+        "kernel_us": {k: round(v, 3) for k, v in kt.items()},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": "rx_classify",

@@ -15,13 +15,14 @@ PH = ["prologue", "funnel+fields", "issue next", "wait demux", "tail sweep", "ve
 L = abi.lib()
 L.udpdk_gpu_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 ctx = abi.GpuContext(0, max_frames=1 << 22, max_lanes=4096)
-dbg = ctx.alloc(16 * 8 * 8192)
+dbg = ctx.alloc(16 * 8 * 8192 + 64)
 L.udpdk_gpu_debug_buffer(ctx.handle, C.c_void_p(dbg.ptr))
 for cfg, n in [(2, 4096), (2, None), (4, 65536), (3, 65536)]:
     w = F.config_batch(cfg, n=n)
     ctx.upload_snapshot(abi.snapshot_from_lists(w.port_lists(), w.n_sockets))
     db = abi.rx_upload(ctx, w.batch.frames, w.batch.offset, w.batch.length)
     db.frames_bytes = w.batch.frames_bytes
+    L.udpdk_gpu_memset(ctx.handle, C.c_void_p(dbg.ptr), 0, 16 * 8 * 8192 + 64)
     out = abi.rx_alloc_out(ctx, w.batch.n, w.n_sockets, w.batch.n)
     for _ in range(3):
         abi.rx_run(ctx, db, out)
@@ -43,6 +44,20 @@ for cfg, n in [(2, 4096), (2, None), (4, 65536), (3, 65536)]:
         m = xcc == x
         print(f"     xcc {x}: wgs {m.sum():5d} start p50 {np.median(st0[m]) / 100:.2f} "
               f"end max {en0[m].max() / 100:.2f}")
+    fin, fst = [int(x) for x in ctx.download(dbg, np.uint64, 16 * tiles + 2)[-2:]]
+    if fin:
+        print(f"   last-tile counter reduction {(fst - int(raw[:, 12].min())) / 100:.2f} .. "
+              f"{(fin - int(raw[:, 12].min())) / 100:.2f} us "
+              f"(last WG exit stamp {en0.max() / 100:.2f} us)")
+    hw = raw[:, 14].astype(np.int64)
+    cu = ((hw >> 32) & 0xF) << 16 | ((hw >> 8) & 0xF) | ((hw >> 12) & 1) << 4 | ((hw >> 13) & 7) << 5
+    ucu, inv, per = np.unique(cu, return_inverse=True, return_counts=True)
+    simd = (hw >> 4) & 3
+    print(f"   CUs used {len(ucu)}; WGs per CU min/median/max {per.min()}/{int(np.median(per))}/"
+          f"{per.max()}; wave0 SIMD histogram {np.bincount(simd, minlength=4).tolist()}")
+    late = st0 > 500                                   # started > 5 us after the first
+    if late.any():
+        print(f"   late WGs {late.sum()}: on CUs holding {np.bincount(per[inv[late]]).nonzero()[0].tolist()} WGs")
     tl = raw[:, 15].astype(np.int64)
     order = np.argsort(tl)
     print(f"   tile order: start of tile k vs k: corr {np.corrcoef(tl, st0)[0, 1]:.3f}; "

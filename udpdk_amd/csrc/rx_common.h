@@ -10,6 +10,8 @@ constexpr int RX_BLOCK  = 256;              // rx_classify workgroup (4 waves)
 constexpr int RX_WAVES  = RX_BLOCK / 64;
 constexpr int RX_UNROLL = 4;                // 16-byte chunk loads in flight per lane
 constexpr uint32_t RX_TILE_MIN = 1024;      // frames per tile (histogram granularity)
+constexpr uint32_t RX_TILE_ONE_LANE = 2048; // single-lane batches: fewer, longer tiles (the fused
+                                            // path's per-tile look-back and publish amortise better)
 constexpr uint32_t RX_TILE_MAX = 16384;
 constexpr uint32_t RX_HIST_CAP = 1u << 21;  // target bound on lanes x tiles
 
@@ -25,8 +27,10 @@ constexpr int TX_BLOCK = 256;
 // histogram (general path).
 constexpr int WAVE_ARRAYS = 3;                    // chunk start, offset, length
 constexpr int ARR_BYTES   = RX_WAVES * WAVE_ARRAYS * 64 * 4;
-constexpr int CNT_OFF     = ARR_BYTES;
-constexpr int TAIL_OFF    = CNT_OFF + 80;         // 16 counters + 4 misc words
+constexpr int CNT_OFF     = ARR_BYTES;            // [RX_WAVES][16] per-wave counter rows
+constexpr int MISC_OFF    = CNT_OFF + RX_WAVES * 16 * 4;   // 4 misc words
+constexpr int LBV_OFF     = MISC_OFF + 16;        // [2][RX_WAVES] u64 look-back partial sums
+constexpr int TAIL_OFF    = LBV_OFF + 2 * RX_WAVES * 8;
 
 __host__ __device__ constexpr uint32_t classify_lds_bytes(bool fused, uint32_t n_lanes,
                                                           uint32_t steps)

@@ -142,48 +142,34 @@ constexpr uint32_t LB_AGG = 1u, LB_INCL = 2u;
 constexpr int LB_VALUE_BITS = 38;
 constexpr unsigned long long LB_VALUE_MASK = (1ull << LB_VALUE_BITS) - 1ull;
 
-// counters[c] = sum over tiles of tile_cnt[t][c] (64-bit): each thread sums whole rows.
-// SC1: rows handed off inside the launch are read with agent-scope (sc1) loads.
+// counters[c] = sum over tiles of tile_cnt[t][c] (64-bit). Thread (g, c) = (tid / 16, tid % 16)
+// sums counter c of rows g, g + G, ... (each pass of the block reads 16 whole rows, coalesced);
+// two xor-shuffles fold the 4 row groups of a wave, LDS the waves. lds: >= 16 * waves u64.
 template <bool SC1 = false>
 __device__ void reduce_counters(const uint32_t *tile_cnt, uint32_t n_tiles,
                                 unsigned long long *counters, unsigned long long *lds)
 {
-    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    unsigned long long s[UDPDK_N_COUNTERS];
-#pragma unroll
-    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) s[c] = 0;
-    const uint4 *rows = reinterpret_cast<const uint4 *>(tile_cnt);
-    if (SC1) {
-        for (uint32_t t = tid; t < n_tiles; t += blockDim.x) {
-#pragma unroll
-            for (int c = 0; c < UDPDK_N_COUNTERS; ++c)
-                s[c] += __hip_atomic_load(&tile_cnt[(size_t)t * UDPDK_N_COUNTERS + c], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-        }
-    } else {
-#pragma unroll 2
-        for (uint32_t t = tid; t < n_tiles; t += blockDim.x) {
-            const uint4 r0 = rows[t * 4 + 0], r1 = rows[t * 4 + 1], r2 = rows[t * 4 + 2], r3 = rows[t * 4 + 3];
-            s[0] += r0.x; s[1] += r0.y; s[2] += r0.z; s[3] += r0.w;
-            s[4] += r1.x; s[5] += r1.y; s[6] += r1.z; s[7] += r1.w;
-            s[8] += r2.x; s[9] += r2.y; s[10] += r2.z; s[11] += r2.w;
-            s[12] += r3.x; s[13] += r3.y; s[14] += r3.z; s[15] += r3.w;
-        }
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6, nw = blockDim.x >> 6;
+    const uint32_t c = tid & 15u, G = blockDim.x >> 4;
+    unsigned long long s = 0;
+    uint32_t t = tid >> 4;
+    auto ld = [&](uint32_t row) -> uint32_t {
+        const uint32_t *p = &tile_cnt[(size_t)row * UDPDK_N_COUNTERS + c];
+        return SC1 ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+    };
+    for (; t + 3u * G < n_tiles; t += 4u * G) {
+        const uint32_t v0 = ld(t), v1 = ld(t + G), v2 = ld(t + 2u * G), v3 = ld(t + 3u * G);
+        s += (unsigned long long)v0 + v1 + v2 + v3;
     }
-    if (tid < UDPDK_N_COUNTERS * 16) lds[tid] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) {
-        unsigned long long v = s[c];
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-        if (lane == 0) lds[w * UDPDK_N_COUNTERS + c] = v;
-    }
+    for (; t < n_tiles; t += G) s += ld(t);
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (lane < 16) lds[w * 16 + lane] = s;
     __syncthreads();
     if (tid < UDPDK_N_COUNTERS) {
-        unsigned long long t = 0;
-        for (uint32_t i = 0; i < blockDim.x / 64; ++i) t += lds[i * UDPDK_N_COUNTERS + tid];
-        counters[tid] = t;
+        unsigned long long r = 0;
+        for (uint32_t i = 0; i < nw; ++i) r += lds[i * 16 + tid];
+        counters[tid] = r;
     }
 }
 
@@ -257,8 +243,10 @@ rx_classify(RxArgs a)
 
     uint32_t *arr = reinterpret_cast<uint32_t *>(smem) + w * WAVE_ARRAYS * 64;
     uint32_t *l_cs = arr, *l_off = arr + 64, *l_len = arr + 128;
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + CNT_OFF);
-    uint32_t *misc = cnt + UDPDK_N_COUNTERS;                 // [0] tile, [1] lane base, [2] arrival
+    uint32_t *cntw = reinterpret_cast<uint32_t *>(smem + CNT_OFF);    // [wave][counter]
+    uint32_t *misc = reinterpret_cast<uint32_t *>(smem + MISC_OFF);   // [0] tile, [2] arrival,
+                                                                       // [3] look-back INCL wave
+    unsigned long long *lbv = reinterpret_cast<unsigned long long *>(smem + LBV_OFF);
     uint8_t *tail = smem + TAIL_OFF;
     // FUSED: per-step delivered masks and counts; general: per-lane histogram
     unsigned long long *smask = reinterpret_cast<unsigned long long *>(tail);
@@ -274,7 +262,7 @@ rx_classify(RxArgs a)
     } else {
         for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK) hist[s] = 0;
     }
-    if (tid < UDPDK_N_COUNTERS) cnt[tid] = 0;
+    if (tid == 0) misc[3] = RX_WAVES;
     __syncthreads();
     const uint32_t tile = FUSED ? misc[0] : xcd_remap(blockIdx.x, gridDim.x);
 
@@ -282,11 +270,9 @@ rx_classify(RxArgs a)
     const uint32_t t0 = tile * a.tile_frames;
     const uint32_t t1 = min(a.n, t0 + a.tile_frames);
 
-    // counters: wave-uniform (ballot popcounts, kept in SGPRs) + the per-lane byte sum
-    uint32_t sc[UDPDK_N_COUNTERS];
-#pragma unroll
-    for (int c = 0; c < UDPDK_N_COUNTERS; ++c) sc[c] = 0;
-    uint32_t lane_bytes = 0;
+    // counters: per-lane packed 8-bit fields (verdicts 0-3 / 4-7, flag counters), deliveries
+    // and bytes; reduced across the wave once per tile
+    uint32_t acc_v0 = 0, acc_v1 = 0, acc_f0 = 0, acc_f1 = 0, acc_fan = 0, lane_bytes = 0;
 
     // Loads are unconditional (clamped index / range-checked buffer offsets): a load under a
     // lane condition makes the compiler wait for it at the end of the branch, which would drain
@@ -379,11 +365,11 @@ rx_classify(RxArgs a)
 
         // ---- tail sweep: UDP bytes at frame offsets >= 64, as chunks swept across lanes ----
         const uint32_t my_nt = (good && len > 64u) ? ((((off + 64u) & 15u) + (len - 64u) + 15u) >> 4) : 0u;
-        const uint32_t inc = scan_dpp(my_nt);
-        const uint32_t my_cs = inc - my_nt;
-        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         uint32_t tsum = 0;                                  // absolute-address word parity
-        if (total) {
+        if (__ballot(my_nt != 0u)) {
+            const uint32_t inc = scan_dpp(my_nt);
+            const uint32_t my_cs = inc - my_nt;
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
             l_cs[lane] = my_cs;
             l_off[lane] = off;
             l_len[lane] = len;
@@ -429,109 +415,92 @@ rx_classify(RxArgs a)
         }
 
         STAMP(4);
-        // ---- verdict, checksums, demux ----
-        uint32_t word = 0, verdict = UDPDK_V_BAD_DESC, fan = 0, first = 0;
-        bool f_ip_bad = false, f_ihl = false, f_len_bad = false;
-        uint32_t f_udp = 3u;                                 // 3 = not a UDP verdict
-        if (good) {
-            lane_bytes += len;
-            if (!(pt & 0x10u)) {
-                verdict = UDPDK_V_NOT_IPV4;                       // udpdk_poller.c:334, :362-366
-            } else if (len < 42) {
-                verdict = UDPDK_V_TRUNC;
-            } else {
-                // IPv4 header checksum over the fixed 20 bytes at offset 14 (RFC 1071)
-                const uint32_t ipraw = (g[0] >> 16) + sum16(g[1]) + sum16(g[2]) + sum16(g[3]) +
-                                       sum16(g[4]) + (g[5] & 0xFFFFu);
-                const bool ip_ok = fold32(ipraw) == 0xFFFFu;
-                const bool ihl_ne5 = ((g[0] >> 16) & 0x0Fu) != 5u;
-                f_ip_bad = !ip_ok;
-                f_ihl = ihl_ne5;
-                word |= (ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8;
-                if (frag & 0x3FFFu) {
-                    verdict = UDPDK_V_FRAG;                       // udpdk_poller.c:338
-                } else if ((g[2] >> 24) != 17u) {
-                    verdict = UDPDK_V_NOT_UDP;                    // udpdk_poller.c:368-371
-                } else {
-                    const uint32_t src = (g[3] >> 16) | (g[4] << 16);
-                    const uint32_t dip = (g[4] >> 16) | (g[5] << 16);   // poller.c:373
-                    const uint32_t ulen_raw = g[6] >> 16;
-                    const uint32_t ulen = ((ulen_raw & 0xFFu) << 8) | (ulen_raw >> 8);
-                    const uint32_t ucks = g[7] & 0xFFFFu;
-                    const bool len_bad = ulen < 8u || 34u + ulen > len;
-                    uint32_t state;
-                    if (ucks == 0u) {
-                        state = UDPDK_UDP_CSUM_NONE;
-                    } else if (len_bad) {
-                        state = UDPDK_UDP_CSUM_BAD;
-                    } else {
-                        // frame bytes [34, min(len, 64)) from the window (frame-relative words)
-                        uint32_t ws = 0;
-                        if (len >= 64u) {
-                            ws = (g[5] >> 16);
+        // ---- verdict, checksums, demux (select-based; rare cases behind wave-uniform tests) ----
+        const bool ipv4 = good && (pt & 0x10u);                   // udpdk_poller.c:334, :362-366
+        const bool l3 = ipv4 && len >= 42u;
+        const bool fragd = (frag & 0x3FFFu) != 0u;                // udpdk_poller.c:338
+        // IPv4 header checksum over the fixed 20 bytes at offset 14 (RFC 1071)
+        const uint32_t ipraw = (g[0] >> 16) + sum16(g[1]) + sum16(g[2]) + sum16(g[3]) +
+                               sum16(g[4]) + (g[5] & 0xFFFFu);
+        const bool ip_ok = fold32(ipraw) == 0xFFFFu;
+        const bool ihl_ne5 = ((g[0] >> 16) & 0x0Fu) != 5u;
+        const uint32_t src = (g[3] >> 16) | (g[4] << 16);
+        const uint32_t dip = (g[4] >> 16) | (g[5] << 16);         // poller.c:373
+        const uint32_t ulen_raw = g[6] >> 16;
+        const uint32_t ulen = ((ulen_raw & 0xFFu) << 8) | (ulen_raw >> 8);
+        const uint32_t ucks = g[7] & 0xFFFFu;
+        const bool len_bad = ulen < 8u || 34u + ulen > len;
+        // frame bytes [34, min(len, 64)) from the window (frame-relative words)
+        uint32_t ws = g[5] >> 16;
 #pragma unroll
-                            for (int i = 6; i < 13; ++i) ws += sum16(g[i]);
-                        } else {
+        for (int i = 6; i < 13; ++i) ws += sum16(g[i]);
+        if (__ballot(is_udp && len < 64u)) {
+            uint32_t wm = 0;
 #pragma unroll
-                            for (int i = 5; i < 13; ++i) ws += sum16(g[i] & byte_mask(34, (int)len, 12 + 4 * i));
-                        }
-                        // tail bytes [64, len): absolute-address words, byte-swapped at odd starts
-                        uint32_t t = fold32(tsum);
-                        if (off & 1u) t = ((t & 0xFFu) << 8) | (t >> 8);
-                        uint32_t s = ws + t + (src & 0xFFFFu) + (src >> 16) + (dip & 0xFFFFu) +
-                                     (dip >> 16) + 0x1100u + ulen_raw;   // + pseudo-header
-                        if (34u + ulen < len) {                    // Ethernet padding after the datagram
-                            uint32_t pad = 0;
-                            for (uint32_t r = 34u + ulen; r < len; ++r)
-                                pad += (uint32_t)a.frames[off + r] << (8u * (r & 1u));
-                            s += 0xFFFFu - fold32(pad);            // one's-complement subtraction
-                        }
-                        state = fold32(s) == 0xFFFFu ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD;
-                    }
-                    f_udp = state;
-                    f_len_bad = len_bad;
-                    word |= state << 5 | (len_bad ? 1u : 0u) << 7;
+            for (int i = 5; i < 13; ++i) wm += sum16(g[i] & byte_mask(34, (int)len, 12 + 4 * i));
+            ws = len < 64u ? wm : ws;
+        }
+        // tail bytes [64, len): absolute-address words, byte-swapped at odd starts
+        uint32_t tf = fold32(tsum);
+        tf = (off & 1u) ? (((tf & 0xFFu) << 8) | (tf >> 8)) : tf;
+        uint32_t us = ws + tf + (src & 0xFFFFu) + (src >> 16) + (dip & 0xFFFFu) + (dip >> 16) +
+                      0x1100u + ulen_raw;                         // + pseudo-header
+        const bool need_pad = is_udp && ucks != 0u && !len_bad && 34u + ulen < len;
+        if (__ballot(need_pad)) {                                 // Ethernet padding after the datagram
+            if (need_pad) {
+                uint32_t pad = 0;
+                for (uint32_t r = 34u + ulen; r < len; ++r)
+                    pad += (uint32_t)a.frames[off + r] << (8u * (r & 1u));
+                us += 0xFFFFu - fold32(pad);                      // one's-complement subtraction
+            }
+        }
+        const uint32_t state = ucks == 0u ? UDPDK_UDP_CSUM_NONE
+                             : (len_bad || fold32(us) != 0xFFFFu) ? UDPDK_UDP_CSUM_BAD
+                                                                   : UDPDK_UDP_CSUM_OK;
 
-                    // ---- demux: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
-                    if (e.x == 0u) {
-                        verdict = UDPDK_V_NO_BIND;
-                    } else {
-                        uint32_t bip = e.z, bsr = e.w;
-                        for (uint32_t i = 0;;) {
-                            if (dip == bip || bip == 0u) {                // poller.c:391
-                                const uint32_t sock = bsr & 0x7FFFFFFFu;
-                                if (!FUSED && fan > 0)
-                                    atomicAdd(&hist[sock & a.lane_mask], 1u); // clones (rare)
-                                if (fan == 0) first = sock;
-                                ++fan;
-                                if (!(bsr >> 31)) break;                 // poller.c:396-403
-                            }
-                            if (++i >= e.x) break;
-                            const uint2 b = a.binds[e.y + i];
-                            bip = b.x;
-                            bsr = b.y;
-                        }
-                        verdict = fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
+        // ---- demux: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
+        // the port entry carries the first binding; later ones only for ports with several
+        const bool match0 = e.x != 0u && (dip == e.z || e.z == 0u);     // poller.c:391
+        uint32_t fan = match0 ? 1u : 0u;
+        uint32_t first = match0 ? (e.w & 0x7FFFFFFFu) : 0u;
+        const bool walk = e.x > 1u && !(match0 && !(e.w >> 31));        // poller.c:396-403
+        if (__ballot(walk)) {
+            if (walk) {
+                for (uint32_t i = 1; i < e.x; ++i) {
+                    const uint2 b = a.binds[e.y + i];
+                    if (dip == b.x || b.x == 0u) {
+                        const uint32_t sock = b.y & 0x7FFFFFFFu;
+                        if (!FUSED && fan > 0)
+                            atomicAdd(&hist[sock & a.lane_mask], 1u);   // clones (rare)
+                        if (fan == 0) first = sock;
+                        ++fan;
+                        if (!(b.y >> 31)) break;
                     }
                 }
             }
         }
+        const uint32_t verdict = !good ? UDPDK_V_BAD_DESC
+                               : !ipv4 ? UDPDK_V_NOT_IPV4
+                               : !l3 ? UDPDK_V_TRUNC
+                               : fragd ? UDPDK_V_FRAG
+                               : (g[2] >> 24) != 17u ? UDPDK_V_NOT_UDP   // udpdk_poller.c:368-371
+                               : e.x == 0u ? UDPDK_V_NO_BIND
+                               : fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
         STAMP(5);
-        if (valid) {
-            word |= verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
-            a.meta[p] = word;
-        }
-#pragma unroll
-        for (int v = 0; v < UDPDK_N_VERDICTS; ++v)
-            sc[v] += (uint32_t)__popcll(__ballot(valid && verdict == (uint32_t)v));
-        sc[UDPDK_C_IP_BAD] += (uint32_t)__popcll(__ballot(f_ip_bad));
-        sc[UDPDK_C_IHL_NE5] += (uint32_t)__popcll(__ballot(f_ihl));
-        sc[UDPDK_C_UDP_OK] += (uint32_t)__popcll(__ballot(f_udp == UDPDK_UDP_CSUM_OK));
-        sc[UDPDK_C_UDP_BAD] += (uint32_t)__popcll(__ballot(f_udp == UDPDK_UDP_CSUM_BAD));
-        sc[UDPDK_C_UDP_NONE] += (uint32_t)__popcll(__ballot(f_udp == UDPDK_UDP_CSUM_NONE));
-        sc[UDPDK_C_LEN_BAD] += (uint32_t)__popcll(__ballot(f_len_bad));
-        if (__ballot(fan > 1u)) sc[UDPDK_C_DELIVERIES] += wave_sum(fan);   // clones (rare)
-        else sc[UDPDK_C_DELIVERIES] += (uint32_t)__popcll(__ballot(fan != 0u));
+        const uint32_t l3f = l3 ? ((ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8) : 0u;
+        const uint32_t udpf = is_udp ? (state << 5 | (len_bad ? 1u : 0u) << 7) : 0u;
+        if (valid)
+            a.meta[p] = verdict | l3f | udpf | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
+        // per-lane packed counters (8-bit fields; a lane sees <= 64 frames per tile)
+        const uint32_t vinc = valid ? 1u << (8u * (verdict & 3u)) : 0u;
+        acc_v0 += verdict < 4u ? vinc : 0u;
+        acc_v1 += verdict < 4u ? 0u : vinc;
+        acc_f0 += (l3 && !ip_ok ? 1u : 0u) | (l3 && ihl_ne5 ? 0x100u : 0u) |
+                  (is_udp && state == UDPDK_UDP_CSUM_OK ? 0x10000u : 0u) |
+                  (is_udp && state == UDPDK_UDP_CSUM_BAD ? 0x1000000u : 0u);
+        acc_f1 += (is_udp && state == UDPDK_UDP_CSUM_NONE ? 1u : 0u) | (is_udp && len_bad ? 0x100u : 0u);
+        acc_fan += fan;
+        if (good) lane_bytes += len;
         const bool delivered = valid && fan > 0u;
         if (FUSED) {
             const unsigned long long m = __ballot(delivered);
@@ -570,15 +539,40 @@ rx_classify(RxArgs a)
         st = nst;
     }
 
-    // ---- tile counters ----
-    sc[UDPDK_C_BYTES] = (uint32_t)__builtin_amdgcn_readlane((int)scan_dpp(lane_bytes), 63);
-    if (lane == 0) {
+    // ---- tile counters: one row per wave (lanes 0-15), summed by the readers ----
+    uint32_t sc[UDPDK_N_COUNTERS];
+    {
+        auto wsum = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)scan_dpp(v), 63); };
+        const uint32_t packed[4] = {acc_v0, acc_v1, acc_f0, acc_f1};
+        const int field[4][4] = {{0, 1, 2, 3}, {4, 5, 6, 7},
+                                 {UDPDK_C_IP_BAD, UDPDK_C_IHL_NE5, UDPDK_C_UDP_OK, UDPDK_C_UDP_BAD},
+                                 {UDPDK_C_UDP_NONE, UDPDK_C_LEN_BAD, -1, -1}};
 #pragma unroll
-        for (int c = 0; c < UDPDK_N_COUNTERS; ++c)
-            if (sc[c]) atomicAdd(&cnt[c], sc[c]);
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t ev = wsum(packed[k] & 0x00FF00FFu);        // 16-bit sums: no carry
+            const uint32_t od = wsum((packed[k] >> 8) & 0x00FF00FFu);
+            if (field[k][0] >= 0) sc[field[k][0]] = ev & 0xFFFFu;
+            if (field[k][1] >= 0) sc[field[k][1]] = od & 0xFFFFu;
+            if (field[k][2] >= 0) sc[field[k][2]] = ev >> 16;
+            if (field[k][3] >= 0) sc[field[k][3]] = od >> 16;
+        }
+        sc[UDPDK_C_DELIVERIES] = wsum(acc_fan);
+        sc[UDPDK_C_BYTES] = wsum(lane_bytes);
+    }
+    {
+        uint32_t row = 0;
+#pragma unroll
+        for (int c = 0; c < UDPDK_N_COUNTERS; ++c) row = lane == (uint32_t)c ? sc[c] : row;
+        if (lane < UDPDK_N_COUNTERS) cntw[w * 16 + lane] = row;
     }
     __syncthreads();
     STAMP(7);
+    auto tile_counter = [&](uint32_t c) -> uint32_t {
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < RX_WAVES; ++i) v += cntw[i * 16 + c];
+        return v;
+    };
 #ifdef UDPDK_STAMPS
     if (!FUSED) STAMP_END();
     if (!FUSED && a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
@@ -587,21 +581,23 @@ rx_classify(RxArgs a)
     if (!FUSED) {
         for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK)
             a.hist[(size_t)s * a.n_tiles + tile] = hist[s];
-        if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = cnt[tid];
+        if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = tile_counter(tid);
         return;
     }
 
     // ---- FUSED: decoupled look-back over tiles, counters, lane writes ----
+    // The tile's delivery count is published at once (8-byte {tag, value} granules written and
+    // read at agent scope; the data is the flag); then all four waves look back together, wave w
+    // over predecessors [tile - 64 (w + 1), tile - 64 w) of the current round, each until its
+    // window is ready up to its nearest inclusive granule. A wave stops early once a nearer wave
+    // has found an inclusive granule (its window is then beyond the prefix).
+    unsigned long long *state = a.lb_state;
+    const unsigned long long agg = tile_counter(UDPDK_C_DELIVERIES);
+    const unsigned long long tagA = (unsigned long long)((a.epoch << 2) | LB_AGG) << LB_VALUE_BITS;
+    const unsigned long long tagI = (unsigned long long)((a.epoch << 2) | LB_INCL) << LB_VALUE_BITS;
+    if (tid == 0)
+        __hip_atomic_store(&state[tile], tagA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (w == 0) {
-        // Decoupled look-back on the tile's delivery count: publish the aggregate at once, then
-        // each lane inspects one of the 64 nearest predecessors per round (8-byte {tag, value}
-        // granules written and read at agent scope; the data is the flag).
-        unsigned long long *state = a.lb_state;
-        const unsigned long long agg = cnt[UDPDK_C_DELIVERIES];
-        const unsigned long long tagA = (unsigned long long)((a.epoch << 2) | LB_AGG) << LB_VALUE_BITS;
-        const unsigned long long tagI = (unsigned long long)((a.epoch << 2) | LB_INCL) << LB_VALUE_BITS;
-        if (lane == 0)
-            __hip_atomic_store(&state[tile], tagA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // exclusive prefix of per-step delivered counts (steps <= 256: 4 per lane)
         uint32_t v[4], s4 = 0;
 #pragma unroll
@@ -617,68 +613,85 @@ rx_classify(RxArgs a)
             if (si < steps) scnt[si] = run;
             run += v[i];
         }
-        unsigned long long excl = 0;
-        bool timeout = false;
-        for (int32_t wb = (int32_t)tile - 1; wb >= 0 && !timeout; wb -= 64) {
-            const int32_t pt = wb - (int32_t)lane;
-            unsigned long long x = 0;
-            uint32_t first_incl = 64;
-            for (uint32_t spins = 0;; ++spins) {
-                uint32_t kind = LB_INCL;                   // before tile 0: an inclusive zero
-                x = 0;
-                if (pt >= 0) {
-                    x = __hip_atomic_load(&state[pt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t tg = (uint32_t)(x >> LB_VALUE_BITS);
-                    kind = (tg >> 2) == a.epoch ? (tg & 3u) : 0u;
-                }
-                const unsigned long long incl = __ballot(kind == LB_INCL);
-                const unsigned long long ready = __ballot(kind != 0u);
-                first_incl = incl ? (uint32_t)__ffsll((long long)incl) - 1u : 64u;
-                const unsigned long long need = first_incl >= 63u ? ~0ull : ((2ull << first_incl) - 1ull);
-                if ((ready & need) == need) break;
-                if (spins > (1u << 22)) { timeout = true; break; }
-                __builtin_amdgcn_s_sleep(1);
+    }
+    unsigned long long excl = 0;
+    bool timeout = false;
+    for (int32_t base = (int32_t)tile - 1, round = 0;; base -= RX_BLOCK, ++round) {
+        const int32_t pt = base - (int32_t)tid;
+        unsigned long long x = 0;
+        uint32_t first_incl = 64;
+        bool counted = true;
+        for (uint32_t spins = 0;; ++spins) {
+            uint32_t kind = LB_INCL;                       // before tile 0: an inclusive zero
+            x = 0;
+            if (pt >= 0) {
+                x = __hip_atomic_load(&state[pt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t tg = (uint32_t)(x >> LB_VALUE_BITS);
+                kind = (tg >> 2) == a.epoch ? (tg & 3u) : 0u;
             }
-            unsigned long long val = lane <= first_incl ? (x & LB_VALUE_MASK) : 0ull;
+            const unsigned long long incl = __ballot(kind == LB_INCL);
+            const unsigned long long ready = __ballot(kind != 0u);
+            first_incl = incl ? (uint32_t)__ffsll((long long)incl) - 1u : 64u;
+            const unsigned long long need = first_incl >= 63u ? ~0ull : ((2ull << first_incl) - 1ull);
+            if ((ready & need) == need) break;
+            if (__hip_atomic_load(&misc[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < w) {
+                counted = false;                            // beyond the prefix: not needed
+                break;
+            }
+            if (spins > (1u << 22)) { timeout = true; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (counted && first_incl < 64u && lane == 0)
+            __hip_atomic_fetch_min(&misc[3], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        unsigned long long val = counted && lane <= first_incl ? (x & LB_VALUE_MASK) : 0ull;
 #pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
-            excl += val;
-            if (first_incl < 64u) break;
-        }
-        if (timeout && lane == 0) atomicExch(a.err, a.epoch);
-        if (lane == 0) {
-            __hip_atomic_store(&state[tile], tagI | ((excl + agg) & LB_VALUE_MASK), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            misc[1] = (uint32_t)excl;
-        }
-        STAMP(8);
-        // counters: write-through (sc1) row, drained, then one agent-scope ticket add; the
-        // last-arriving tile reads every row with sc1 loads (no fences: MI355X_MICROARCH.md
-        // "Hand-offs measured with sc1 loads", first row)
+        for (int d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
+        if (lane == 0) lbv[(round & 1) * RX_WAVES + w] = val;
+        __syncthreads();
+        const uint32_t f = misc[3];
+#pragma unroll
+        for (int i = 0; i < RX_WAVES; ++i)
+            if ((uint32_t)i <= f) excl += lbv[(round & 1) * RX_WAVES + i];
+        if (f < RX_WAVES) break;
+    }
+    if (timeout) atomicExch(a.err, a.epoch);
+    if (tid == 0)
+        __hip_atomic_store(&state[tile], tagI | ((excl + agg) & LB_VALUE_MASK), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    STAMP(8);
+    // counters: write-through (sc1) row, drained, then one agent-scope ticket add whose return
+    // is awaited only after the lane writes; the last-arriving tile reads every row with sc1
+    // loads (no fences: MI355X_MICROARCH.md "Hand-offs measured with sc1 loads", first row)
+    uint32_t arrival = 0;
+    if (w == 0) {
         if (lane < UDPDK_N_COUNTERS)
-            __hip_atomic_store(&a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + lane], cnt[lane],
+            __hip_atomic_store(&a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + lane], tile_counter(lane),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
-            misc[2] = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        STAMP(9);
+            arrival = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __syncthreads();
-    const uint32_t base = misc[1];
+    STAMP(9);
+    const uint32_t lbase = (uint32_t)excl;
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (uint32_t s = w; s < steps; s += RX_WAVES) {
         const unsigned long long m = smask[s];
         if ((m >> lane) & 1ull) {
-            const uint32_t pos = base + scnt[s] + (uint32_t)__popcll(m & lt);
+            const uint32_t pos = lbase + scnt[s] + (uint32_t)__popcll(m & lt);
             if (pos < a.lane_cap) a.lane_pkt[pos] = t0 + s * 64 + lane;
         }
     }
+    if (tid == 0) misc[2] = arrival;
     STAMP(10);
 #ifdef UDPDK_STAMPS
     STAMP_END();
     if (a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
 #endif
+    __syncthreads();
     if (misc[2] != a.n_tiles - 1u) return;
+#ifdef UDPDK_STAMPS
+    if (a.dbg && tid == 0) a.dbg[(size_t)a.n_tiles * 16 + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     reduce_counters<true>(a.tile_cnt, a.n_tiles, a.counters, reinterpret_cast<unsigned long long *>(smem));
     if (tid == 0) {
         const uint32_t tot = (uint32_t)a.counters[UDPDK_C_DELIVERIES];
@@ -686,6 +699,9 @@ rx_classify(RxArgs a)
         a.lane_off[1] = tot;
         *a.total = tot;
         *a.done = 0u;                                    // ready for the next launch
+#ifdef UDPDK_STAMPS
+        if (a.dbg) a.dbg[(size_t)a.n_tiles * 16] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
 }
 

@@ -49,6 +49,7 @@ struct udpdk_gpu_ctx {
     uint4 *slots = nullptr;
     uint32_t slots_cap = 0, n_slots = 0;
     uint32_t n_lanes = 1, lane_mask = 0xFFFFFFFFu, key_bits = 0, max_fanout = 0;
+    uint32_t fused_tile = 0;   // UDPDK_FUSED_TILE (diagnostic): fused-path tile size override
     bool have_snapshot = false;
 
     // RX workspace
@@ -101,7 +102,7 @@ uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); 
 
 void geometry(uint32_t n, uint32_t lanes, uint32_t *T, uint32_t *tiles)
 {
-    uint32_t t = RX_TILE_MIN;
+    uint32_t t = lanes == 1 ? RX_TILE_ONE_LANE : RX_TILE_MIN;
     while (t < RX_TILE_MAX && (uint64_t)ceil_div(n, t) * lanes > RX_HIST_CAP) t *= 2;
     *T = t;
     *tiles = std::max<uint32_t>(1u, ceil_div(n, t));
@@ -182,6 +183,10 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
     c->device = device;
     c->max_frames = max_frames;
     c->max_lanes = max_lanes;
+    if (const char *e = getenv("UDPDK_FUSED_TILE")) {
+        const uint32_t t = (uint32_t)atoi(e);
+        if (t >= RX_TILE_MIN && t <= RX_TILE_MAX && (t & (t - 1)) == 0) c->fused_tile = t;
+    }
     int rc = -EIO;
     do {
         if (hipSetDevice(device) != hipSuccess) break;
@@ -428,6 +433,10 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     }
     uint32_t T, tiles;
     geometry(bt->n, S, &T, &tiles);
+    if (S == 1 && c->max_fanout <= 1 && c->fused_tile > T) {   // diagnostic override
+        T = c->fused_tile;
+        tiles = std::max<uint32_t>(1u, ceil_div(bt->n, T));
+    }
     const uint64_t E = (uint64_t)S * tiles;
     if (E > c->hist_cap || tiles > c->tiles_cap) return -EINVAL;
     const bool fused = S == 1 && c->max_fanout <= 1;
