@@ -1,9 +1,10 @@
 """Benchmark: device-resident RX parse + checksum + port demux (BASELINE.json metric).
 
 A step = one udpdk_gpu_rx call over one batch of frames already resident in HBM (single-lane
-batches: the fused rx_classify alone; otherwise rx_classify + rx_scan + rx_scatter). The timed
-region carries no per-launch events: its GPU time comes from two events on the library stream
-around all K steps, so kernel durations agree with rocprofv3's kernel trace. Default workload = BASELINE.json configs[1]: 1 M synthetic 64 B
+batches: rx_classify + rx_compact1; otherwise rx_classify + rx_scan + rx_scatter). The timed
+region's GPU time comes from two events on the library stream around all K steps; per-kernel
+durations from events carried by the kernel dispatches themselves (hipExtLaunchKernelGGL), so
+they agree with rocprofv3's kernel trace. Default workload = BASELINE.json configs[1]: 1 M synthetic 64 B
 Eth/IPv4/UDP frames, 1 bound port, per GPU. With N GPUs (torchrun) every rank processes its own
 independent shard (seed 0x5EED ^ rank) with no data-path collective: weak scaling.
 
@@ -44,6 +45,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1500 B / IMIX side lines")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU time per baseline leg")
+    p.add_argument("--timing-every", type=int, default=1,
+                   help="per-kernel timing on every Nth call (dispatch-carried events)")
     return p.parse_args()
 
 
@@ -86,10 +89,7 @@ class Rx:
 
     def classify_bytes(self) -> int:
         # rx_classify algorithmic bytes per launch: every frame byte + u32 offset + u16 length
-        # read, u32 verdict written; the fused single-lane kernel also writes the lane entry
-        # (4 B per delivery), the general one the tile histogram column (lanes x tiles x 4 B)
-        if self.w.n_sockets == 1:
-            return self.sum_len + 6 * self.n + 4 * self.n + 4 * self.n
+        # read, u32 verdict written, plus the tile histogram column (lanes x tiles x 4 B)
         t, k = abi.geometry(self.n, self.w.n_sockets)
         return self.sum_len + 6 * self.n + 4 * self.n + 4 * self.w.n_sockets * k
 
@@ -127,17 +127,18 @@ class HipEvents:
             self.hip.hipEventDestroy(e)
 
 
-def time_loop(rx: Rx, steps: int, warmup: int, barrier, split_steps: int):
+def time_loop(rx: Rx, steps: int, warmup: int, barrier, timing_every: int):
     """Timed region: `steps` back-to-back udpdk_gpu_rx calls between a barrier + sync on each
-    side (host wall clock) and two events on the library stream (GPU time). Afterwards, outside
-    the timed region, `split_steps` calls with per-kernel events give the pipeline's kernel split
-    (general path only; the fused path is one kernel)."""
+    side (host wall clock) and two events on the library stream (GPU time). Per-kernel
+    durations come from the library's timing mode, whose events ride on the kernel dispatches
+    themselves (no marker packets between kernels), on every `timing_every`-th call."""
     ctx = rx.ctx
     ev = HipEvents(ctx)
     for i in range(warmup):
         rx.step(i)
     rx.check()
-    ctx.timing(0)
+    ctx.timing(timing_every)
+    ctx.timing_read()                    # reset accumulators
     barrier()
     ctx.sync()
     t0 = time.perf_counter()
@@ -151,27 +152,11 @@ def time_loop(rx: Rx, steps: int, warmup: int, barrier, split_steps: int):
     gpu_ms = ev.elapsed_ms()
     ev.close()
     st = rx.check()
-    split = None
-    if split_steps and rx.w.n_sockets > 1:
-        ctx.timing(1)
-        ctx.timing_read()
-        for i in range(split_steps):
-            rx.step(i)
-        ctx.sync()
-        ms, n = ctx.timing_read()
-        ctx.timing(0)
-        per = [ms[k] / max(1, n[k]) for k in range(3)]
-        split = [x / max(1e-12, sum(per)) for x in per]
-    return (t1 - t0), gpu_ms / steps, split, st
-
-
-def kernel_times(rx: Rx, gpu_step_ms: float, split):
-    """Per-launch kernel times (us): the fused single-lane path is one kernel per step, so its
-    duration is the GPU time per step; the general path's step is divided by the event split."""
-    us = 1e3 * gpu_step_ms
-    if split is None:
-        return {"rx_classify": us, "rx_scan": 0.0, "rx_scatter": 0.0}
-    return {"rx_classify": us * split[0], "rx_scan": us * split[1], "rx_scatter": us * split[2]}
+    ms, n = ctx.timing_read() if timing_every else ([0.0] * 4, [0] * 4)
+    ctx.timing(0)
+    kt = {name: 1e3 * ms[k] / n[k] for k, name in
+          enumerate(("rx_classify", "rx_scan", "rx_scatter")) if n[k]}
+    return (t1 - t0), gpu_ms / steps, kt, st
 
 
 def cpu_baseline(w: F.Workload, target_s: float):
@@ -196,9 +181,8 @@ def cpu_baseline(w: F.Workload, target_s: float):
 def side_config(ctx, cfg: int, steps: int, rotate: int):
     w = F.config_batch(cfg)
     rx = Rx(ctx, w, rotate)
-    wall, gpu_step, split, st = time_loop(rx, steps, 5, lambda: None, 20)
-    kt = kernel_times(rx, gpu_step, split)
-    cls_gbps = rx.classify_bytes() / (kt["rx_classify"] / 1e6) / 1e9
+    wall, gpu_step, kt, st = time_loop(rx, steps, 5, lambda: None, 1)
+    cls_gbps = rx.classify_bytes() / (kt.get("rx_classify", 1e3 * gpu_step) / 1e6) / 1e9
     out = {"workload": w.name, "mpkt_s": round(rx.n * steps / wall / 1e6, 1),
            "gbps_pipeline": round(rx.pipeline_bytes() * steps / wall / 1e9, 1),
            "gpu_us_per_step": round(1e3 * gpu_step, 2),
@@ -271,8 +255,7 @@ def main():
     w = F.config_batch(args.config, n=args.frames, shard=rank)
     ctx = abi.GpuContext(device, max_frames=max(w.batch.n, 1 << 22), max_lanes=4096)
     rx = Rx(ctx, w, args.rotate_mib << 20)
-    wall, gpu_step, split, st = time_loop(rx, args.steps, args.warmup, barrier, 20)
-    kt = kernel_times(rx, gpu_step, split)
+    wall, gpu_step, kt, st = time_loop(rx, args.steps, args.warmup, barrier, args.timing_every)
     if dist is not None:
         t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -281,7 +264,8 @@ def main():
     mpkt_s = total_pkts / wall / 1e6
     ms_step = 1e3 * wall / args.steps
     cls_bytes = rx.classify_bytes()
-    achieved = cls_bytes / (kt["rx_classify"] / 1e6) / 1e9
+    cls_us = kt.get("rx_classify", 1e3 * gpu_step)     # timing off: the whole step, an upper bound
+    achieved = cls_bytes / (cls_us / 1e6) / 1e9
 
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")

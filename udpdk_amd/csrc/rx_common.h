@@ -22,20 +22,16 @@ constexpr uint32_t SCAN_SMALL_MAX = 16384;  // single-workgroup scan up to this 
 constexpr int TX_BLOCK = 256;
 
 // rx_classify LDS carve (one dynamic array, 16-byte aligned offsets: cdna_hip_programming.md
-// Guideline 17): per wave three 64-entry chunk-map arrays for the tail sweep; block counters +
-// misc words; then per-step delivered masks/counts (fused single-lane path) or the per-lane
-// histogram (general path).
+// Guideline 17): per wave three 64-entry chunk-map arrays for the tail sweep; per-wave counter
+// rows; the tile's per-lane delivery histogram.
 constexpr int WAVE_ARRAYS = 3;                    // chunk start, offset, length
 constexpr int ARR_BYTES   = RX_WAVES * WAVE_ARRAYS * 64 * 4;
 constexpr int CNT_OFF     = ARR_BYTES;            // [RX_WAVES][16] per-wave counter rows
-constexpr int MISC_OFF    = CNT_OFF + RX_WAVES * 16 * 4;   // 4 misc words
-constexpr int LBV_OFF     = MISC_OFF + 16;        // [2][RX_WAVES] u64 look-back partial sums
-constexpr int TAIL_OFF    = LBV_OFF + 2 * RX_WAVES * 8;
+constexpr int HIST_OFF    = CNT_OFF + RX_WAVES * 16 * 4;
 
-__host__ __device__ constexpr uint32_t classify_lds_bytes(bool fused, uint32_t n_lanes,
-                                                          uint32_t steps)
+__host__ __device__ constexpr uint32_t classify_lds_bytes(uint32_t n_lanes)
 {
-    return (uint32_t)TAIL_OFF + (fused ? 12u * steps : 4u * n_lanes);
+    return (uint32_t)HIST_OFF + 4u * n_lanes;
 }
 
 // Port table entry (16 B per raw port): x = bindings on the port, y = index of the first in the
@@ -49,19 +45,9 @@ struct RxArgs {
     const uint4    *port_tab;
     const uint2    *binds;
     uint32_t *meta;
-    uint32_t *hist;       // [n_lanes][n_tiles]            (general path)
+    uint32_t *hist;       // [n_lanes][n_tiles] per-tile per-lane delivery counts
     uint32_t *tile_cnt;   // [n_tiles][16] per-tile counters
-    unsigned long long *lb_state;   // [n_tiles][16] look-back granules (fused path)
-    uint32_t *ticket;     // dynamic tile order            (fused path)
-    uint32_t *done;       // tiles finished: the last one reduces the counters (fused path)
-    uint32_t *err;        // = epoch of a call whose look-back timed out
-    uint32_t *lane_pkt;   // fused path writes the lane directly
-    uint32_t *lane_off;
-    unsigned long long *counters;
-    uint32_t *total;
     unsigned long long *dbg;        // diagnostic stamps (UDPDK_STAMPS builds), may be null
-    uint32_t lane_cap;
-    uint32_t epoch;
     uint32_t key_bits;
     uint32_t frames_bytes;
     uint32_t rsrc_bytes;  // buffer-resource range (frames_bytes rounded up to 16)
@@ -76,8 +62,6 @@ struct ScanArgs {
     uint32_t *hist;
     uint32_t *partial;
     uint32_t *lane_off;
-    const uint32_t *tile_cnt;
-    unsigned long long *counters;
     uint32_t *total;
     uint32_t n_elems;
     uint32_t n_tiles;
@@ -101,6 +85,20 @@ struct ScatterArgs {
     uint32_t lane_cap;
 };
 
+// Single-lane compaction (rx_compact1): lane_pkt = indices of delivered frames in frame order,
+// from the classify kernel's verdict words and per-tile delivery counts (hist, one lane).
+struct Compact1Args {
+    const uint32_t *meta;
+    const uint32_t *tile_count;   // [n_tiles] deliveries per tile
+    uint32_t *lane_pkt;
+    uint32_t *lane_off;           // [2]
+    uint32_t *total;
+    uint32_t n;
+    uint32_t tile_frames;
+    uint32_t n_tiles;
+    uint32_t lane_cap;
+};
+
 struct TxArgs {
     const uint8_t  *payload;
     const uint32_t *payload_off;
@@ -120,12 +118,14 @@ struct TxArgs {
     uint32_t mac_lo[3];        // 12 MAC bytes: dst(6) src(6) as three LE dwords
 };
 
-template <bool FUSED> __global__ void rx_classify(RxArgs a);
+__global__ void rx_classify(RxArgs a);
 __global__ void rx_scan_small(ScanArgs a);
 __global__ void rx_scan_reduce(ScanArgs a);
 __global__ void rx_scan_top(ScanArgs a, uint32_t n_part);
 __global__ void rx_scan_down(ScanArgs a);
 __global__ void rx_scatter(ScatterArgs a);
+__global__ void rx_compact1(Compact1Args a);
+__global__ void rx_counters(const uint32_t *tile_cnt, uint32_t n_tiles, unsigned long long *counters);
 __global__ void tx_build(TxArgs a);
 
 } // namespace udpdk

@@ -4,25 +4,26 @@
 // burst loop (udpdk_poller.c:516-545) plus the per-socket rx_buffer appends and ring flushes
 // (udpdk_poller.c:274-298). All integer/byte work, bound by HBM:
 //
-//   rx_classify<FUSED>  one workgroup per tile of T frames, each wave walking 64-frame steps.
-//       Frames are read once as 16-byte chunks swept across lanes, so a wave-instruction reads
-//       1 KiB of consecutive bytes whatever the frame sizes. The first 64 B window of each frame
-//       is staged in LDS and parsed by the frame's lane; the UDP datagram sum is reduced per
-//       frame with a wave prefix scan over chunk sums (no LDS atomics); the IPv4 header sum comes
-//       from the parsed header. Steps are software-pipelined: the next step's descriptors and
-//       chunk loads are in flight while the current step is parsed and demultiplexed.
-//       Demux reads one 16-byte port-table entry (first binding inline) per frame.
-//       FUSED (one lane, fan-out <= 1: the single bound socket of apps/pktgen): tiles take a
-//       ticket (dynamic order), find their lane position by a decoupled look-back over tiles
-//       (8-byte {tag, value} granules at agent scope, 64 predecessors inspected per round),
-//       write the lane directly, and the last tile to finish reduces the counters: one launch.
-//       General: writes the tile's per-lane delivery histogram (lane-major, hist[lane][tile]).
-//   rx_scan     exclusive scan of the lane-major histogram -> per-(lane, tile) start positions,
-//       lane_off, and the counter reduction. One launch when small, reduce/top/down otherwise.
-//   rx_scatter  one wave per tile writes each delivery at its stable position.
+//   rx_classify  one workgroup (4 waves) per tile of T frames, lane = frame, each wave walking
+//       64-frame steps, software-pipelined one step ahead (the next step's descriptors and
+//       header windows are in flight while the current step is parsed).
+//       Header window: 4 x 16 B + 4 B aligned loads covering frame bytes [12, 64], funnel-
+//       shifted into 13 frame-relative dwords with lane-mask selects + alignbyte.
+//       Bytes >= 64 (the rest of the UDP datagram): 16-byte chunks swept across the wave's
+//       lanes (a wave-instruction reads consecutive bytes whatever the frame sizes), chunk sums
+//       reduced per frame by a DPP prefix scan.
+//       Demux: one 16-byte port-table entry per frame (first binding inline), the binding list
+//       only for ports with several. Writes the verdict word, the tile's per-lane delivery
+//       histogram (lane-major hist[lane][tile]) and the tile's counter row.
+//   rx_compact1  single lane without fan-out (the one bound socket of apps/pktgen): per tile,
+//       base = sum of the predecessors' counts, ballots over the verdict words, lane writes.
+//   rx_scan + rx_scatter  general case: exclusive scan of the lane-major histogram (one launch
+//       when small, reduce/top/down otherwise), then one wave per tile writes each delivery at
+//       its stable position.
+//   rx_counters  on demand (udpdk_gpu_rx_stats): sum of the per-tile counter rows.
 //
 // Algorithmic bytes per frame in rx_classify: frame_len + 6 (u32 offset + u16 length) + 4
-// (verdict word) [+ 4 lane entry when FUSED].
+// (verdict word), + 4 per (lane, tile) histogram entry.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -137,17 +138,12 @@ __device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
 #define STAMP(k) do {} while (0)
 #endif
 
-// 8-byte look-back granules: tag (epoch << 2 | kind) in the top 26 bits, value in the low 38.
-constexpr uint32_t LB_AGG = 1u, LB_INCL = 2u;
-constexpr int LB_VALUE_BITS = 38;
-constexpr unsigned long long LB_VALUE_MASK = (1ull << LB_VALUE_BITS) - 1ull;
 
 // counters[c] = sum over tiles of tile_cnt[t][c] (64-bit). Thread (g, c) = (tid / 16, tid % 16)
 // sums counter c of rows g, g + G, ... (each pass of the block reads 16 whole rows, coalesced);
 // two xor-shuffles fold the 4 row groups of a wave, LDS the waves. lds: >= 16 * waves u64.
-template <bool SC1 = false>
-__device__ void reduce_counters(const uint32_t *tile_cnt, uint32_t n_tiles,
-                                unsigned long long *counters, unsigned long long *lds)
+__device__ unsigned long long reduce_counters(const uint32_t *tile_cnt, uint32_t n_tiles,
+                                              unsigned long long *counters, unsigned long long *lds)
 {
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6, nw = blockDim.x >> 6;
     const uint32_t c = tid & 15u, G = blockDim.x >> 4;
@@ -155,7 +151,7 @@ __device__ void reduce_counters(const uint32_t *tile_cnt, uint32_t n_tiles,
     uint32_t t = tid >> 4;
     auto ld = [&](uint32_t row) -> uint32_t {
         const uint32_t *p = &tile_cnt[(size_t)row * UDPDK_N_COUNTERS + c];
-        return SC1 ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+        return *p;
     };
     for (; t + 3u * G < n_tiles; t += 4u * G) {
         const uint32_t v0 = ld(t), v1 = ld(t + G), v2 = ld(t + 2u * G), v3 = ld(t + 3u * G);
@@ -166,11 +162,12 @@ __device__ void reduce_counters(const uint32_t *tile_cnt, uint32_t n_tiles,
     s += __shfl_xor(s, 32, 64);
     if (lane < 16) lds[w * 16 + lane] = s;
     __syncthreads();
+    unsigned long long r = 0;
     if (tid < UDPDK_N_COUNTERS) {
-        unsigned long long r = 0;
         for (uint32_t i = 0; i < nw; ++i) r += lds[i * 16 + tid];
         counters[tid] = r;
     }
+    return r;                                               // counter tid, for tid < 16
 }
 
 // ------------------------------------------------------------------------------------------
@@ -229,7 +226,6 @@ __device__ __forceinline__ void wait_vm(v4u32 &r)
     asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r) : "n"(N) : "memory");
 }
 
-template <bool FUSED>
 __global__ void __launch_bounds__(RX_BLOCK)
 rx_classify(RxArgs a)
 {
@@ -244,27 +240,11 @@ rx_classify(RxArgs a)
     uint32_t *arr = reinterpret_cast<uint32_t *>(smem) + w * WAVE_ARRAYS * 64;
     uint32_t *l_cs = arr, *l_off = arr + 64, *l_len = arr + 128;
     uint32_t *cntw = reinterpret_cast<uint32_t *>(smem + CNT_OFF);    // [wave][counter]
-    uint32_t *misc = reinterpret_cast<uint32_t *>(smem + MISC_OFF);   // [0] tile, [2] arrival,
-                                                                       // [3] look-back INCL wave
-    unsigned long long *lbv = reinterpret_cast<unsigned long long *>(smem + LBV_OFF);
-    uint8_t *tail = smem + TAIL_OFF;
-    // FUSED: per-step delivered masks and counts; general: per-lane histogram
-    unsigned long long *smask = reinterpret_cast<unsigned long long *>(tail);
-    uint32_t *scnt = reinterpret_cast<uint32_t *>(tail + 8 * steps);
-    uint32_t *hist = reinterpret_cast<uint32_t *>(tail);
+    uint32_t *hist = reinterpret_cast<uint32_t *>(smem + HIST_OFF);   // [n_lanes] this tile
 
-    if (FUSED) {
-        if (tid == 0) {
-            const uint32_t t = atomicAdd(a.ticket, 1u);
-            if (t == a.n_tiles - 1u) atomicExch(a.ticket, 0u);  // every block has its ticket
-            misc[0] = t;
-        }
-    } else {
-        for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK) hist[s] = 0;
-    }
-    if (tid == 0) misc[3] = RX_WAVES;
+    for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK) hist[s] = 0;
     __syncthreads();
-    const uint32_t tile = FUSED ? misc[0] : xcd_remap(blockIdx.x, gridDim.x);
+    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
 
     const __amdgpu_buffer_rsrc_t fr = make_rsrc(a.frames, a.rsrc_bytes);
     const uint32_t t0 = tile * a.tile_frames;
@@ -470,7 +450,7 @@ rx_classify(RxArgs a)
                     const uint2 b = a.binds[e.y + i];
                     if (dip == b.x || b.x == 0u) {
                         const uint32_t sock = b.y & 0x7FFFFFFFu;
-                        if (!FUSED && fan > 0)
+                        if (fan > 0)
                             atomicAdd(&hist[sock & a.lane_mask], 1u);   // clones (rare)
                         if (fan == 0) first = sock;
                         ++fan;
@@ -502,33 +482,22 @@ rx_classify(RxArgs a)
         acc_fan += fan;
         if (good) lane_bytes += len;
         const bool delivered = valid && fan > 0u;
-        if (FUSED) {
-            const unsigned long long m = __ballot(delivered);
-            if (lane == 0) {
-                smask[st] = m;
-                scnt[st] = (uint32_t)__popcll(m);
+        // first delivery of every frame into the tile histogram; small key spaces are
+        // aggregated with a wave multi-split first (all 64 lanes may share one lane)
+        const uint32_t key = first & a.lane_mask;
+        if (a.key_bits <= 4u) {
+            unsigned long long peers = __ballot(delivered);
+            for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
+                const bool kb = (key >> bit) & 1u;
+                const unsigned long long bal = __ballot(kb);
+                peers &= kb ? bal : ~bal;
             }
-        } else {
-            // first delivery of every frame into the tile histogram; small key spaces are
-            // aggregated with a wave multi-split first (all 64 lanes may share one lane)
-            const uint32_t key = first & a.lane_mask;
-            if (a.key_bits <= 4u) {
-                unsigned long long peers = __ballot(delivered);
-                for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
-                    const bool kb = (key >> bit) & 1u;
-                    const unsigned long long bal = __ballot(kb);
-                    peers &= kb ? bal : ~bal;
-                }
-                if (delivered && lane == (uint32_t)__ffsll((long long)peers) - 1u)
-                    atomicAdd(&hist[key], (uint32_t)__popcll(peers));
-            } else if (delivered) {
-                atomicAdd(&hist[key], 1u);
-            }
+            if (delivered && lane == (uint32_t)__ffsll((long long)peers) - 1u)
+                atomicAdd(&hist[key], (uint32_t)__popcll(peers));
+        } else if (delivered) {
+            atomicAdd(&hist[key], 1u);
         }
         STAMP(6);
-#ifdef UDPDK_STAMPS
-        st_acc[11] += 1;
-#endif
         W = NW;
         c_off = n_off;
         c_len = n_len;
@@ -574,139 +543,85 @@ rx_classify(RxArgs a)
         return v;
     };
 #ifdef UDPDK_STAMPS
-    if (!FUSED) STAMP_END();
-    if (!FUSED && a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
-#endif
-
-    if (!FUSED) {
-        for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK)
-            a.hist[(size_t)s * a.n_tiles + tile] = hist[s];
-        if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = tile_counter(tid);
-        return;
-    }
-
-    // ---- FUSED: decoupled look-back over tiles, counters, lane writes ----
-    // The tile's delivery count is published at once (8-byte {tag, value} granules written and
-    // read at agent scope; the data is the flag); then all four waves look back together, wave w
-    // over predecessors [tile - 64 (w + 1), tile - 64 w) of the current round, each until its
-    // window is ready up to its nearest inclusive granule. A wave stops early once a nearer wave
-    // has found an inclusive granule (its window is then beyond the prefix).
-    unsigned long long *state = a.lb_state;
-    const unsigned long long agg = tile_counter(UDPDK_C_DELIVERIES);
-    const unsigned long long tagA = (unsigned long long)((a.epoch << 2) | LB_AGG) << LB_VALUE_BITS;
-    const unsigned long long tagI = (unsigned long long)((a.epoch << 2) | LB_INCL) << LB_VALUE_BITS;
-    if (tid == 0)
-        __hip_atomic_store(&state[tile], tagA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (w == 0) {
-        // exclusive prefix of per-step delivered counts (steps <= 256: 4 per lane)
-        uint32_t v[4], s4 = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t si = lane * 4 + i;
-            v[i] = si < steps ? scnt[si] : 0u;
-            s4 += v[i];
-        }
-        uint32_t run = scan_dpp(s4) - s4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t si = lane * 4 + i;
-            if (si < steps) scnt[si] = run;
-            run += v[i];
-        }
-    }
-    unsigned long long excl = 0;
-    bool timeout = false;
-    for (int32_t base = (int32_t)tile - 1, round = 0;; base -= RX_BLOCK, ++round) {
-        const int32_t pt = base - (int32_t)tid;
-        unsigned long long x = 0;
-        uint32_t first_incl = 64;
-        bool counted = true;
-        for (uint32_t spins = 0;; ++spins) {
-            uint32_t kind = LB_INCL;                       // before tile 0: an inclusive zero
-            x = 0;
-            if (pt >= 0) {
-                x = __hip_atomic_load(&state[pt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t tg = (uint32_t)(x >> LB_VALUE_BITS);
-                kind = (tg >> 2) == a.epoch ? (tg & 3u) : 0u;
-            }
-            const unsigned long long incl = __ballot(kind == LB_INCL);
-            const unsigned long long ready = __ballot(kind != 0u);
-            first_incl = incl ? (uint32_t)__ffsll((long long)incl) - 1u : 64u;
-            const unsigned long long need = first_incl >= 63u ? ~0ull : ((2ull << first_incl) - 1ull);
-            if ((ready & need) == need) break;
-            if (__hip_atomic_load(&misc[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < w) {
-                counted = false;                            // beyond the prefix: not needed
-                break;
-            }
-            if (spins > (1u << 22)) { timeout = true; break; }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (counted && first_incl < 64u && lane == 0)
-            __hip_atomic_fetch_min(&misc[3], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        unsigned long long val = counted && lane <= first_incl ? (x & LB_VALUE_MASK) : 0ull;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
-        if (lane == 0) lbv[(round & 1) * RX_WAVES + w] = val;
-        __syncthreads();
-        const uint32_t f = misc[3];
-#pragma unroll
-        for (int i = 0; i < RX_WAVES; ++i)
-            if ((uint32_t)i <= f) excl += lbv[(round & 1) * RX_WAVES + i];
-        if (f < RX_WAVES) break;
-    }
-    if (timeout) atomicExch(a.err, a.epoch);
-    if (tid == 0)
-        __hip_atomic_store(&state[tile], tagI | ((excl + agg) & LB_VALUE_MASK), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    STAMP(8);
-    // counters: write-through (sc1) row, drained, then one agent-scope ticket add whose return
-    // is awaited only after the lane writes; the last-arriving tile reads every row with sc1
-    // loads (no fences: MI355X_MICROARCH.md "Hand-offs measured with sc1 loads", first row)
-    uint32_t arrival = 0;
-    if (w == 0) {
-        if (lane < UDPDK_N_COUNTERS)
-            __hip_atomic_store(&a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + lane], tile_counter(lane),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-            arrival = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    STAMP(9);
-    const uint32_t lbase = (uint32_t)excl;
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    for (uint32_t s = w; s < steps; s += RX_WAVES) {
-        const unsigned long long m = smask[s];
-        if ((m >> lane) & 1ull) {
-            const uint32_t pos = lbase + scnt[s] + (uint32_t)__popcll(m & lt);
-            if (pos < a.lane_cap) a.lane_pkt[pos] = t0 + s * 64 + lane;
-        }
-    }
-    if (tid == 0) misc[2] = arrival;
-    STAMP(10);
-#ifdef UDPDK_STAMPS
     STAMP_END();
     if (a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
 #endif
+    for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK)
+        a.hist[(size_t)s * a.n_tiles + tile] = hist[s];
+    if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = tile_counter(tid);
+}
+
+// ------------------------------------------------------------------------------------------
+// rx_compact1: the single-lane batch's lane (no fan-out: every delivery is a whole frame).
+// Workgroup = tile. Each wave ballots its quarter of the tile's verdict words (delivered =
+// verdict 0) into LDS masks, the tile's base is the sum of the predecessors' delivery counts
+// (<= n_tiles words, read straight from the classify kernel's per-tile histogram: no scan
+// kernel and no cross-workgroup waits), then every delivered frame writes its index.
+// The last tile's workgroup writes lane_off[1] = total.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(RX_BLOCK)
+rx_compact1(Compact1Args a)
+{
+    constexpr uint32_t MAXS = RX_TILE_MAX / RX_BLOCK;      // steps per wave, <= 64
+    __shared__ unsigned long long msk[RX_WAVES][MAXS];
+    __shared__ uint32_t red[2 * RX_WAVES];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t steps = a.tile_frames / RX_BLOCK;
+    const uint32_t t1 = min(a.n, (tile + 1) * a.tile_frames);
+    const uint32_t wb = tile * a.tile_frames + w * steps * 64;
+    const uint32_t plast = a.n - 1u;
+    uint32_t wcount = 0;
+    for (uint32_t s0 = 0; s0 < steps; s0 += 8) {
+        uint32_t mv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) mv[u] = a.meta[min(wb + (s0 + u) * 64 + lane, plast)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t p = wb + (s0 + u) * 64 + lane;
+            const unsigned long long m = __ballot(s0 + u < steps && p < t1 && (mv[u] & 0xFu) == UDPDK_V_DELIVERED);
+            if (lane == 0 && s0 + u < steps) msk[w][s0 + u] = m;
+            wcount += (uint32_t)__popcll(m);
+        }
+    }
+    // predecessors' counts: the first two per thread unconditionally (clamped), so these loads
+    // are in flight together with the verdict words above
+    const uint32_t tl = a.n_tiles - 1u;
+    const uint32_t c0 = a.tile_count[min(tid, tl)], c1 = a.tile_count[min(tid + RX_BLOCK, tl)];
+    uint32_t pre = (tid < tile ? c0 : 0u) + (tid + RX_BLOCK < tile ? c1 : 0u);
+    for (uint32_t t = tid + 2 * RX_BLOCK; t < tile; t += RX_BLOCK) pre += a.tile_count[t];
+    pre = wave_sum(pre);
+    if (lane == 0) { red[w] = pre; red[RX_WAVES + w] = wcount; }
     __syncthreads();
-    if (misc[2] != a.n_tiles - 1u) return;
-#ifdef UDPDK_STAMPS
-    if (a.dbg && tid == 0) a.dbg[(size_t)a.n_tiles * 16 + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
-    reduce_counters<true>(a.tile_cnt, a.n_tiles, a.counters, reinterpret_cast<unsigned long long *>(smem));
-    if (tid == 0) {
-        const uint32_t tot = (uint32_t)a.counters[UDPDK_C_DELIVERIES];
+    uint32_t run = 0;
+#pragma unroll
+    for (int i = 0; i < RX_WAVES; ++i) run += red[i] + ((uint32_t)i < w ? red[RX_WAVES + i] : 0u);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (uint32_t s = 0; s < steps; ++s) {
+        const unsigned long long m = msk[w][s];
+        if ((m >> lane) & 1ull) {
+            const uint32_t pos = run + (uint32_t)__popcll(m & lt);
+            if (pos < a.lane_cap) a.lane_pkt[pos] = wb + s * 64 + lane;
+        }
+        run += (uint32_t)__popcll(m);
+    }
+    if (tile == a.n_tiles - 1u && tid == RX_BLOCK - 1u) {     // last wave: run = total
         a.lane_off[0] = 0u;
-        a.lane_off[1] = tot;
-        *a.total = tot;
-        *a.done = 0u;                                    // ready for the next launch
-#ifdef UDPDK_STAMPS
-        if (a.dbg) a.dbg[(size_t)a.n_tiles * 16] = __builtin_amdgcn_s_memrealtime();
-#endif
+        a.lane_off[1] = run;
+        *a.total = run;
     }
 }
 
-template __global__ void rx_classify<false>(RxArgs);
-template __global__ void rx_classify<true>(RxArgs);
+// ------------------------------------------------------------------------------------------
+// rx_counters: counters[c] = sum over the last call's tiles of tile_cnt[t][c] (one workgroup,
+// launched by udpdk_gpu_rx_stats only, so a batch that nobody asks statistics for pays nothing)
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+rx_counters(const uint32_t *tile_cnt, uint32_t n_tiles, unsigned long long *counters)
+{
+    __shared__ unsigned long long lcnt[16 * 4];
+    reduce_counters(tile_cnt, n_tiles, counters, lcnt);
+}
 
 // ------------------------------------------------------------------------------------------
 // rx_scan: exclusive scan of hist[E] (lane-major) in place; lane_off; counter reduction
@@ -733,7 +648,6 @@ __global__ void __launch_bounds__(SCAN_BLOCK)
 rx_scan_small(ScanArgs a)
 {
     __shared__ uint32_t lds16[SCAN_BLOCK / 64];
-    __shared__ unsigned long long lcnt[UDPDK_N_COUNTERS * 16];
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (a.n_elems + SCAN_BLOCK - 1) / SCAN_BLOCK;
     const uint32_t i0 = tid * per, i1 = min(a.n_elems, i0 + per);
@@ -748,7 +662,6 @@ rx_scan_small(ScanArgs a)
         run += v;
     }
     if (tid == 0) { a.lane_off[a.n_lanes] = total; *a.total = total; }
-    reduce_counters(a.tile_cnt, a.n_tiles, a.counters, lcnt);
 }
 
 // Large case, pass 1: partial[b] = sum of chunk b (SCAN_CHUNK elements).
@@ -777,7 +690,6 @@ __global__ void __launch_bounds__(SCAN_BLOCK)
 rx_scan_top(ScanArgs a, uint32_t n_part)
 {
     __shared__ uint32_t lds16[SCAN_BLOCK / 64];
-    __shared__ unsigned long long lcnt[UDPDK_N_COUNTERS * 16];
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (n_part + SCAN_BLOCK - 1) / SCAN_BLOCK;
     const uint32_t i0 = tid * per, i1 = min(n_part, i0 + per);
@@ -791,7 +703,6 @@ rx_scan_top(ScanArgs a, uint32_t n_part)
         run += v;
     }
     if (tid == 0) { a.lane_off[a.n_lanes] = total; *a.total = total; }
-    reduce_counters(a.tile_cnt, a.n_tiles, a.counters, lcnt);
 }
 
 // Large case, pass 3: rescan each chunk from its partial offset; write lane_off entries.

@@ -4,6 +4,7 @@
 // the RX and TX kernels. No hidden synchronisation on the RX/TX enqueue path: everything stays
 // on the context stream, so a caller may capture udpdk_gpu_rx into a hipGraph.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <errno.h>
 #include <stdint.h>
@@ -22,16 +23,19 @@ using namespace udpdk;
 namespace {
 
 constexpr int EVENT_SETS = 256;   // timed calls buffered between two timing reads
-constexpr uint32_t EPOCH_MAX = 1u << 24;   // look-back tag width (rx_kernels.hip)
 
 struct DevResult {
     unsigned long long counters[UDPDK_N_COUNTERS];
     uint32_t total;
-    uint32_t err;
+    uint32_t pad;
 };
 
+// Per-call kernel timing: start/stop events carried by the kernel dispatches themselves
+// (hipExtLaunchKernelGGL), so timing adds no marker packets between back-to-back kernels.
+constexpr int TIMED_KERNELS = 3;  // classify, scan, scatter (single-lane path: compact)
 struct TimingSet {
-    hipEvent_t ev[4];             // classify start, classify end, scan end, scatter end
+    hipEvent_t ev[2 * TIMED_KERNELS];
+    bool used[TIMED_KERNELS];
 };
 
 } // namespace
@@ -49,7 +53,7 @@ struct udpdk_gpu_ctx {
     uint4 *slots = nullptr;
     uint32_t slots_cap = 0, n_slots = 0;
     uint32_t n_lanes = 1, lane_mask = 0xFFFFFFFFu, key_bits = 0, max_fanout = 0;
-    uint32_t fused_tile = 0;   // UDPDK_FUSED_TILE (diagnostic): fused-path tile size override
+    uint32_t one_lane_tile = 0;    // UDPDK_ONE_LANE_TILE (diagnostic): single-lane tile override
     bool have_snapshot = false;
 
     // RX workspace
@@ -61,11 +65,7 @@ struct udpdk_gpu_ctx {
     size_t tiles_cap = 0;
     DevResult *res = nullptr;                 // counters, total, err (device)
     DevResult *h_res = nullptr;               // pinned mirror, filled by udpdk_gpu_rx_stats
-    unsigned long long *lb_state = nullptr;   // fused path look-back granules [tiles][16]
-    uint32_t *ticket = nullptr;
-    uint32_t epoch = 0;
-    uint32_t last_epoch = 0;
-    hipEvent_t done = nullptr;
+    uint32_t last_tiles = 0;                  // tiles of the last udpdk_gpu_rx (counter rows)
     uint32_t last_lane_cap = 0;
     bool pending = false;
 
@@ -112,20 +112,34 @@ int fold_timing(udpdk_gpu_ctx *c)
 {
     if (!c->n_sets_used) return 0;
     HIPC(c, hipStreamSynchronize(c->stream));
+    static const int kid[TIMED_KERNELS] = {UDPDK_K_RX_CLASSIFY, UDPDK_K_RX_SCAN, UDPDK_K_RX_SCATTER};
     for (int i = 0; i < c->n_sets_used; ++i) {
-        float a = 0, b = 0, d = 0;
-        HIPC(c, hipEventElapsedTime(&a, c->sets[i].ev[0], c->sets[i].ev[1]));
-        HIPC(c, hipEventElapsedTime(&b, c->sets[i].ev[1], c->sets[i].ev[2]));
-        HIPC(c, hipEventElapsedTime(&d, c->sets[i].ev[2], c->sets[i].ev[3]));
-        c->ms[UDPDK_K_RX_CLASSIFY] += a;
-        c->ms[UDPDK_K_RX_SCAN] += b;
-        c->ms[UDPDK_K_RX_SCATTER] += d;
-        c->launches[UDPDK_K_RX_CLASSIFY]++;
-        c->launches[UDPDK_K_RX_SCAN]++;
-        c->launches[UDPDK_K_RX_SCATTER]++;
+        for (int k = 0; k < TIMED_KERNELS; ++k) {
+            if (!c->sets[i].used[k]) continue;
+            float ms = 0;
+            HIPC(c, hipEventElapsedTime(&ms, c->sets[i].ev[2 * k], c->sets[i].ev[2 * k + 1]));
+            c->ms[kid[k]] += ms;
+            c->launches[kid[k]]++;
+        }
     }
     c->n_sets_used = 0;
     return 0;
+}
+
+// Launch on the context stream; with a timing set, kernel k's dispatch carries the set's start
+// event (first=true) and/or stop event (last=true).
+template <typename K, typename... A>
+hipError_t launch(udpdk_gpu_ctx *c, TimingSet *ts, int k, bool first, bool last, K kern, dim3 grid,
+                  dim3 block, uint32_t lds, A... args)
+{
+    if (ts) {
+        ts->used[k] = true;
+        hipExtLaunchKernelGGL(kern, grid, block, lds, c->stream, first ? ts->ev[2 * k] : nullptr,
+                              last ? ts->ev[2 * k + 1] : nullptr, 0u, args...);
+    } else {
+        hipLaunchKernelGGL(kern, grid, block, lds, c->stream, args...);
+    }
+    return hipGetLastError();
 }
 
 int ensure_dev(udpdk_gpu_ctx *c, void **p, size_t *cap, size_t need)
@@ -183,9 +197,9 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
     c->device = device;
     c->max_frames = max_frames;
     c->max_lanes = max_lanes;
-    if (const char *e = getenv("UDPDK_FUSED_TILE")) {
+    if (const char *e = getenv("UDPDK_ONE_LANE_TILE")) {
         const uint32_t t = (uint32_t)atoi(e);
-        if (t >= RX_TILE_MIN && t <= RX_TILE_MAX && (t & (t - 1)) == 0) c->fused_tile = t;
+        if (t >= RX_TILE_MIN && t <= RX_TILE_MAX && (t & (t - 1)) == 0) c->one_lane_tile = t;
     }
     int rc = -EIO;
     do {
@@ -204,15 +218,8 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
         if (hipMalloc((void **)&c->res, sizeof(DevResult)) != hipSuccess) break;
         if (hipMemset(c->res, 0, sizeof(DevResult)) != hipSuccess) break;
         if (hipHostMalloc((void **)&c->h_res, sizeof(DevResult), hipHostMallocDefault) != hipSuccess) break;
-        if (hipMalloc((void **)&c->lb_state, c->tiles_cap * UDPDK_N_COUNTERS * 8) != hipSuccess) break;
-        if (hipMemset(c->lb_state, 0, c->tiles_cap * UDPDK_N_COUNTERS * 8) != hipSuccess) break;
-        if (hipMalloc((void **)&c->ticket, 64) != hipSuccess) break;
-        if (hipMemset(c->ticket, 0, 64) != hipSuccess) break;
-        if (hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) break;
         // rx_classify needs up to 90 KiB of dynamic LDS at 16384 lanes
-        if (hipFuncSetAttribute((const void *)rx_classify<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024) != hipSuccess) break;
-        if (hipFuncSetAttribute((const void *)rx_classify<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void *)rx_classify, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) break;
@@ -233,16 +240,15 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *dev[] = {c->port_tab, c->binds, c->slots, c->hist, c->partial, c->tile_cnt,
-                   c->res, c->lb_state, c->ticket, c->st_frames_d, c->st_desc_d, c->st_out_d};
+                   c->res, c->st_frames_d, c->st_desc_d, c->st_out_d};
     for (void *p : dev) if (p) (void)hipFree(p);
     void *host[] = {c->h_res, c->st_frames_h, c->st_desc_h};
     for (void *p : host) if (p) (void)hipHostFree(p);
     if (c->sets) {
         for (int i = 0; i < EVENT_SETS; ++i)
-            for (int k = 0; k < 4; ++k) (void)hipEventDestroy(c->sets[i].ev[k]);
+            for (int k = 0; k < 2 * TIMED_KERNELS; ++k) (void)hipEventDestroy(c->sets[i].ev[k]);
         delete[] c->sets;
     }
-    if (c->done) (void)hipEventDestroy(c->done);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -384,7 +390,7 @@ int udpdk_gpu_timing_enable(udpdk_gpu_ctx *c, int enable)
         c->sets = new (std::nothrow) TimingSet[EVENT_SETS];
         if (!c->sets) return -ENOMEM;
         for (int i = 0; i < EVENT_SETS; ++i)
-            for (int k = 0; k < 4; ++k) HIPC(c, hipEventCreate(&c->sets[i].ev[k]));
+            for (int k = 0; k < 2 * TIMED_KERNELS; ++k) HIPC(c, hipEventCreate(&c->sets[i].ev[k]));
     }
     c->timing_every = enable > 0 ? (uint32_t)enable : 0u;
     c->timing_calls = 0;
@@ -426,28 +432,21 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     if (bt->n == 0) {
         HIPC(c, hipMemsetAsync(o->lane_off_dev, 0, (size_t)(S + 1) * 4, c->stream));
         HIPC(c, hipMemsetAsync(c->res, 0, sizeof(DevResult), c->stream));
-        c->last_epoch = 0;
-        if (ts) for (int k = 0; k < 4; ++k) HIPC(c, hipEventRecord(ts->ev[k], c->stream));
-        HIPC(c, hipEventRecord(c->done, c->stream));
+        c->last_tiles = 0;
+        if (ts) c->n_sets_used--;                         // nothing was launched
         return 0;
     }
     uint32_t T, tiles;
     geometry(bt->n, S, &T, &tiles);
-    if (S == 1 && c->max_fanout <= 1 && c->fused_tile > T) {   // diagnostic override
-        T = c->fused_tile;
+    if (S == 1 && c->max_fanout <= 1 && c->one_lane_tile) {   // diagnostic override
+        T = c->one_lane_tile;
         tiles = std::max<uint32_t>(1u, ceil_div(bt->n, T));
     }
     const uint64_t E = (uint64_t)S * tiles;
     if (E > c->hist_cap || tiles > c->tiles_cap) return -EINVAL;
-    const bool fused = S == 1 && c->max_fanout <= 1;
-
-    if (fused) {
-        if (++c->epoch >= EPOCH_MAX) {      // tag space exhausted: clear stale granules
-            HIPC(c, hipMemsetAsync(c->lb_state, 0, c->tiles_cap * UDPDK_N_COUNTERS * 8, c->stream));
-            c->epoch = 1;
-        }
-    }
-    c->last_epoch = fused ? c->epoch : 0;
+    // single lane, no fan-out: classify + rx_compact1; otherwise classify + scan + scatter
+    const bool one_lane = S == 1 && c->max_fanout <= 1;
+    c->last_tiles = tiles;
 
     RxArgs ra;
     memset(&ra, 0, sizeof(ra));
@@ -460,17 +459,7 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     ra.meta = o->meta_dev;
     ra.hist = c->hist;
     ra.tile_cnt = c->tile_cnt;
-    ra.lb_state = c->lb_state;
-    ra.ticket = c->ticket;
-    ra.done = c->ticket + 1;
-    ra.err = &c->res->err;
-    ra.lane_pkt = o->lane_pkt_dev;
-    ra.lane_off = o->lane_off_dev;
-    ra.counters = c->res->counters;
-    ra.total = &c->res->total;
-    ra.lane_cap = o->lane_cap;
     ra.dbg = c->dbg;
-    ra.epoch = c->epoch;
     ra.key_bits = c->key_bits;
     ra.frames_bytes = (uint32_t)bt->frames_bytes;
     ra.rsrc_bytes = (uint32_t)std::min<uint64_t>((bt->frames_bytes + 15) & ~15ull, 0xFFFFFFFFull);
@@ -480,43 +469,40 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     ra.lane_mask = c->lane_mask;
     ra.n_lanes = S;
 
-    if (ts) HIPC(c, hipEventRecord(ts->ev[0], c->stream));
-    if (fused) {
-        hipLaunchKernelGGL(rx_classify<true>, dim3(tiles), dim3(RX_BLOCK),
-                           classify_lds_bytes(true, S, T / 64), c->stream, ra);
-        HIPC(c, hipGetLastError());
-        if (ts) for (int k = 1; k < 4; ++k) HIPC(c, hipEventRecord(ts->ev[k], c->stream));
-        HIPC(c, hipEventRecord(c->done, c->stream));
+    if (ts) for (int k = 0; k < TIMED_KERNELS; ++k) ts->used[k] = false;
+    HIPC(c, launch(c, ts, 0, true, true, rx_classify, dim3(tiles), dim3(RX_BLOCK),
+                   classify_lds_bytes(S), ra));
+    if (one_lane) {
+        Compact1Args ca;
+        ca.meta = o->meta_dev;
+        ca.tile_count = c->hist;
+        ca.lane_pkt = o->lane_pkt_dev;
+        ca.lane_off = o->lane_off_dev;
+        ca.total = &c->res->total;
+        ca.n = bt->n;
+        ca.tile_frames = T;
+        ca.n_tiles = tiles;
+        ca.lane_cap = o->lane_cap;
+        HIPC(c, launch(c, ts, 2, true, true, rx_compact1, dim3(tiles), dim3(RX_BLOCK), 0u, ca));
         return 0;
     }
-    hipLaunchKernelGGL(rx_classify<false>, dim3(tiles), dim3(RX_BLOCK),
-                       classify_lds_bytes(false, S, T / 64), c->stream, ra);
-    HIPC(c, hipGetLastError());
-    if (ts) HIPC(c, hipEventRecord(ts->ev[1], c->stream));
 
     ScanArgs sa;
     sa.hist = c->hist;
     sa.partial = c->partial;
     sa.lane_off = o->lane_off_dev;
-    sa.tile_cnt = c->tile_cnt;
-    sa.counters = c->res->counters;
     sa.total = &c->res->total;
     sa.n_elems = (uint32_t)E;
     sa.n_tiles = tiles;
     sa.n_lanes = S;
     if (E <= SCAN_SMALL_MAX) {
-        hipLaunchKernelGGL(rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 0, c->stream, sa);
-        HIPC(c, hipGetLastError());
+        HIPC(c, launch(c, ts, 1, true, true, rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 0u, sa));
     } else {
         const uint32_t nb = ceil_div(E, SCAN_CHUNK);
-        hipLaunchKernelGGL(rx_scan_reduce, dim3(nb), dim3(SCAN_BLOCK), 0, c->stream, sa);
-        HIPC(c, hipGetLastError());
-        hipLaunchKernelGGL(rx_scan_top, dim3(1), dim3(SCAN_BLOCK), 0, c->stream, sa, nb);
-        HIPC(c, hipGetLastError());
-        hipLaunchKernelGGL(rx_scan_down, dim3(nb), dim3(SCAN_BLOCK), 0, c->stream, sa);
-        HIPC(c, hipGetLastError());
+        HIPC(c, launch(c, ts, 1, true, false, rx_scan_reduce, dim3(nb), dim3(SCAN_BLOCK), 0u, sa));
+        HIPC(c, launch(c, ts, 1, false, false, rx_scan_top, dim3(1), dim3(SCAN_BLOCK), 0u, sa, nb));
+        HIPC(c, launch(c, ts, 1, false, true, rx_scan_down, dim3(nb), dim3(SCAN_BLOCK), 0u, sa));
     }
-    if (ts) HIPC(c, hipEventRecord(ts->ev[2], c->stream));
 
     ScatterArgs xa;
     xa.meta = o->meta_dev;
@@ -533,10 +519,7 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     xa.lane_mask = c->lane_mask;
     xa.key_bits = c->key_bits;
     xa.lane_cap = o->lane_cap;
-    hipLaunchKernelGGL(rx_scatter, dim3(tiles), dim3(64), 4u * S, c->stream, xa);
-    HIPC(c, hipGetLastError());
-    if (ts) HIPC(c, hipEventRecord(ts->ev[3], c->stream));
-    HIPC(c, hipEventRecord(c->done, c->stream));
+    HIPC(c, launch(c, ts, 2, true, true, rx_scatter, dim3(tiles), dim3(64), 4u * S, xa));
     return 0;
 }
 
@@ -545,13 +528,16 @@ int udpdk_gpu_rx_stats(udpdk_gpu_ctx *c, udpdk_rx_stats_t *st)
     if (!c || !st) return -EINVAL;
     if (!c->pending) return -EINVAL;
     HIPC(c, hipSetDevice(c->device));
-    HIPC(c, hipEventSynchronize(c->done));
+    if (c->last_tiles) {
+        hipLaunchKernelGGL(rx_counters, dim3(1), dim3(256), 0, c->stream, (const uint32_t *)c->tile_cnt,
+                           c->last_tiles, c->res->counters);
+        HIPC(c, hipGetLastError());
+    }
     HIPC(c, hipMemcpyAsync(c->h_res, c->res, sizeof(DevResult), hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     for (int k = 0; k < UDPDK_N_COUNTERS; ++k) st->counters[k] = c->h_res->counters[k];
     st->deliveries = c->h_res->total;
     st->overflow = st->deliveries > c->last_lane_cap ? 1u : 0u;
-    if (c->last_epoch && c->h_res->err == c->last_epoch) return -EIO;   // look-back timed out
     return st->overflow ? -ENOSPC : 0;
 }
 
