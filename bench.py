@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1500 B / IMIX side lines")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU time per baseline leg")
-    p.add_argument("--timing-every", type=int, default=1,
+    p.add_argument("--timing-every", type=int, default=16,
                    help="per-kernel timing on every Nth call (dispatch-carried events)")
     return p.parse_args()
 

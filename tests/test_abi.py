@@ -32,12 +32,11 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_geometry():
     assert abi.lib().udpdk_gpu_abi_version() == 1
     # tile geometry policy: lanes x tiles bounded, tiles >= 1
-    assert abi.geometry(1 << 20, 1) == (2048, 512)     # single lane: longer tiles
+    assert abi.geometry(1 << 20, 1) == (1024, 1024)
     assert abi.geometry(1 << 20, 1024) == (1024, 1024)
     t, k = abi.geometry(1 << 22, 4096)
     assert t * k >= 1 << 22 and k * 4096 <= 1 << 21
-    assert abi.geometry(0, 1) == (2048, 1)
-    assert abi.geometry(0, 2) == (1024, 1)
+    assert abi.geometry(0, 1) == (1024, 1)
 
 
 def test_reference_api_surface_present():

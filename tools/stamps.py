@@ -10,8 +10,8 @@ sys.path.insert(0, ROOT)
 import numpy as np
 from udpdk_amd import abi, frames as F
 
-PH = ["prologue", "funnel+fields", "issue next", "wait demux", "tail sweep", "verdict/csum/demux",
-      "meta/ctr/hist", "tile ctr"]
+PH = ["prologue", "funnel+fields", "header sums+sweep", "issue next+wait demux", "udp state",
+      "demux+verdict", "meta/ctr/hist", "tile ctr"]
 L = abi.lib()
 L.udpdk_gpu_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 ctx = abi.GpuContext(0, max_frames=1 << 22, max_lanes=4096)

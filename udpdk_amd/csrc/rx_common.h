@@ -10,8 +10,6 @@ constexpr int RX_BLOCK  = 256;              // rx_classify workgroup (4 waves)
 constexpr int RX_WAVES  = RX_BLOCK / 64;
 constexpr int RX_UNROLL = 4;                // 16-byte chunk loads in flight per lane
 constexpr uint32_t RX_TILE_MIN = 1024;      // frames per tile (histogram granularity)
-constexpr uint32_t RX_TILE_ONE_LANE = 2048; // single-lane batches: fewer, longer tiles (the fused
-                                            // path's per-tile look-back and publish amortise better)
 constexpr uint32_t RX_TILE_MAX = 16384;
 constexpr uint32_t RX_HIST_CAP = 1u << 21;  // target bound on lanes x tiles
 

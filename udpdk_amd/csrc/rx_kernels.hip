@@ -327,90 +327,27 @@ rx_classify(RxArgs a)
         const uint32_t frag = ((g[2] & 0xFFu) << 8) | ((g[2] >> 8) & 0xFFu);
         const bool is_udp = good && (pt & 0x10u) && len >= 42u && !(frag & 0x3FFFu) && (g[2] >> 24) == 17u;
         const uint32_t dport = g[6] & 0xFFFFu;                   // poller.c:372
-        // The demux load goes out before the next step's loads, and is waited for only where it
-        // is used, so the next step's window loads stay in flight across this step.
+        // The demux load goes out first and is waited for only where it is used.
         STAMP(1);
         v4u32 ev = asm_load16(a.port_tab + dport);
 
-        // ---- next step of this wave: window loads stay in flight across this step ----
-        const uint32_t nst = st + RX_WAVES;
-        const Win NW = load_win(nst, n_off, n_len);
-        uint32_t nn_off, nn_len, nn_pt;
-        load_desc(nst + RX_WAVES, nn_off, nn_len, nn_pt);
-        STAMP(2);
-        // issued after the demux load: 5 window loads + 2 descriptor loads (+1 with ptype)
-        wait_vm<7>(ev);
-        STAMP(3);
-        const uint4 e = is_udp ? make_uint4(ev[0], ev[1], ev[2], ev[3]) : make_uint4(0, 0, 0, 0);
-
-        // ---- tail sweep: UDP bytes at frame offsets >= 64, as chunks swept across lanes ----
-        const uint32_t my_nt = (good && len > 64u) ? ((((off + 64u) & 15u) + (len - 64u) + 15u) >> 4) : 0u;
-        uint32_t tsum = 0;                                  // absolute-address word parity
-        if (__ballot(my_nt != 0u)) {
-            const uint32_t inc = scan_dpp(my_nt);
-            const uint32_t my_cs = inc - my_nt;
-            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-            l_cs[lane] = my_cs;
-            l_off[lane] = off;
-            l_len[lane] = len;
-            wave_sync();
-            for (uint32_t k0 = 0; k0 < total; k0 += 64 * RX_UNROLL) {
-                uint4 R[RX_UNROLL];
-                uint32_t Rq[RX_UNROLL];
-                // binary searches of the RX_UNROLL sub-iterations in lockstep (one LDS wait per level)
-#pragma unroll
-                for (int u = 0; u < RX_UNROLL; ++u) Rq[u] = 0;
-#pragma unroll
-                for (int sft = 32; sft >= 1; sft >>= 1) {
-                    uint32_t c[RX_UNROLL];
-#pragma unroll
-                    for (int u = 0; u < RX_UNROLL; ++u) c[u] = l_cs[Rq[u] + sft];
-#pragma unroll
-                    for (int u = 0; u < RX_UNROLL; ++u)
-                        if (c[u] <= k0 + u * 64 + lane) Rq[u] += sft;
-                }
-#pragma unroll
-                for (int u = 0; u < RX_UNROLL; ++u) {
-                    const uint32_t k = k0 + u * 64 + lane, q = Rq[u];
-                    R[u] = load16(fr, k < total ? ((l_off[q] + 64u) & ~15u) + 16u * (k - l_cs[q]) : 0u);
-                }
-#pragma unroll
-                for (int u = 0; u < RX_UNROLL; ++u) {
-                    const uint32_t base = k0 + u * 64;
-                    const uint32_t k = base + lane;
-                    uint32_t part = 0;
-                    if (k < total) {
-                        const uint32_t q = Rq[u], fo = l_off[q];
-                        const int rel = (int)((((fo + 64u) & ~15u) + 16u * (k - l_cs[q])) - fo);
-                        part = chunk_sum(R[u], 64 - rel, (int)l_len[q] - rel);
-                    }
-                    const uint32_t P = scan_dpp(part);
-                    const uint32_t lo = max(my_cs, base), hi = min(my_cs + my_nt, base + 64u);
-                    const uint32_t ph = __shfl(P, (int)((hi > base ? hi - 1u - base : 0u) & 63u), 64);
-                    const uint32_t pl = __shfl(P, (int)((lo > base ? lo - 1u - base : 0u) & 63u), 64);
-                    if (lo < hi) tsum += ph - (lo > base ? pl : 0u);
-                }
-            }
-            wave_sync();
-        }
-
-        STAMP(4);
-        // ---- verdict, checksums, demux (select-based; rare cases behind wave-uniform tests) ----
+        // ---- everything the header window gives (the window registers die here) ----
         const bool ipv4 = good && (pt & 0x10u);                   // udpdk_poller.c:334, :362-366
         const bool l3 = ipv4 && len >= 42u;
         const bool fragd = (frag & 0x3FFFu) != 0u;                // udpdk_poller.c:338
+        const bool not_udp = (g[2] >> 24) != 17u;                 // udpdk_poller.c:368-371
         // IPv4 header checksum over the fixed 20 bytes at offset 14 (RFC 1071)
         const uint32_t ipraw = (g[0] >> 16) + sum16(g[1]) + sum16(g[2]) + sum16(g[3]) +
                                sum16(g[4]) + (g[5] & 0xFFFFu);
         const bool ip_ok = fold32(ipraw) == 0xFFFFu;
         const bool ihl_ne5 = ((g[0] >> 16) & 0x0Fu) != 5u;
-        const uint32_t src = (g[3] >> 16) | (g[4] << 16);
         const uint32_t dip = (g[4] >> 16) | (g[5] << 16);         // poller.c:373
         const uint32_t ulen_raw = g[6] >> 16;
         const uint32_t ulen = ((ulen_raw & 0xFFu) << 8) | (ulen_raw >> 8);
         const uint32_t ucks = g[7] & 0xFFFFu;
         const bool len_bad = ulen < 8u || 34u + ulen > len;
-        // frame bytes [34, min(len, 64)) from the window (frame-relative words)
+        // UDP sum so far: pseudo-header {src, dst, proto 17, udp length} + frame bytes
+        // [34, min(len, 64)) from the window (frame-relative words)
         uint32_t ws = g[5] >> 16;
 #pragma unroll
         for (int i = 6; i < 13; ++i) ws += sum16(g[i]);
@@ -420,11 +357,79 @@ rx_classify(RxArgs a)
             for (int i = 5; i < 13; ++i) wm += sum16(g[i] & byte_mask(34, (int)len, 12 + 4 * i));
             ws = len < 64u ? wm : ws;
         }
-        // tail bytes [64, len): absolute-address words, byte-swapped at odd starts
-        uint32_t tf = fold32(tsum);
+        uint32_t us = ws + (g[3] >> 16) + (g[4] & 0xFFFFu) + (dip & 0xFFFFu) + (dip >> 16) + 0x1100u +
+                      ulen_raw;
+
+        // ---- tail sweep: frame bytes >= 64 as 64-byte super-chunks swept across the lanes ----
+        // Super-chunk j of a frame = 4 aligned 16-byte chunks from ((off + 64) & ~15) + 64 j; lane
+        // i of a group handles super-chunk k0 + i of the wave's 64 frames (found by binary search
+        // over the per-frame starts in LDS). Two groups in flight (loads of the next group are
+        // issued before the current one is summed). Sums are absolute-address word sums.
+        const uint32_t a64 = (off + 64u) & ~15u;
+        const uint32_t my_nt = (good && len > 64u) ? (off + len - a64 + 63u) >> 6 : 0u;
+        uint32_t tsum = 0;
+        if (__ballot(my_nt != 0u)) {
+            const uint32_t inc = scan_dpp(my_nt);
+            const uint32_t my_cs = inc - my_nt;
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            l_cs[lane] = my_cs;
+            l_off[lane] = off;
+            l_len[lane] = len;
+            wave_sync();
+            auto issue = [&](uint32_t k0, uint32_t &q, uint4 (&R)[4]) {
+                const uint32_t k = k0 + lane;
+                q = 0;
+#pragma unroll
+                for (int sft = 32; sft >= 1; sft >>= 1)
+                    if (l_cs[q + sft] <= k) q += sft;
+                const uint32_t base = k < total ? ((l_off[q] + 64u) & ~15u) + 64u * (k - l_cs[q]) : 0u;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) R[c] = load16(fr, base + 16u * c);
+            };
+            auto consume = [&](uint32_t k0, uint32_t q, const uint4 (&R)[4]) {
+                const uint32_t k = k0 + lane;
+                uint32_t part = 0;
+                if (k < total) {
+                    const uint32_t fo = l_off[q];
+                    const int rel = (int)((((fo + 64u) & ~15u) + 64u * (k - l_cs[q])) - fo);
+                    const int fl = (int)l_len[q];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) part += chunk_sum(R[c], 64 - rel - 16 * c, fl - rel - 16 * c);
+                }
+                const uint32_t P = scan_dpp(part);
+                const uint32_t lo = max(my_cs, k0), hi = min(my_cs + my_nt, k0 + 64u);
+                const uint32_t ph = __shfl(P, (int)((hi > k0 ? hi - 1u - k0 : 0u) & 63u), 64);
+                const uint32_t pl = __shfl(P, (int)((lo > k0 ? lo - 1u - k0 : 0u) & 63u), 64);
+                if (lo < hi) tsum += ph - (lo > k0 ? pl : 0u);
+            };
+            uint32_t qa, qb;
+            uint4 Ra[4], Rb[4];
+            issue(0, qa, Ra);
+            for (uint32_t k0 = 0; k0 < total; k0 += 128) {
+                issue(k0 + 64, qb, Rb);
+                consume(k0, qa, Ra);
+                if (k0 + 64 >= total) break;
+                issue(k0 + 128, qa, Ra);
+                consume(k0 + 64, qb, Rb);
+            }
+            wave_sync();
+        }
+        STAMP(2);
+
+        // ---- next step of this wave: window loads stay in flight across the rest of this step
+        const uint32_t nst = st + RX_WAVES;
+        const Win NW = load_win(nst, n_off, n_len);
+        uint32_t nn_off, nn_len, nn_pt;
+        load_desc(nst + RX_WAVES, nn_off, nn_len, nn_pt);
+        // issued after the demux load: 5 window loads + 2 descriptor loads (+1 with ptype)
+        wait_vm<7>(ev);
+        STAMP(3);
+        const uint4 e = is_udp ? make_uint4(ev[0], ev[1], ev[2], ev[3]) : make_uint4(0, 0, 0, 0);
+
+        // ---- UDP checksum state ----
+        uint32_t tf = fold32(tsum);                               // tail: byte-swapped at odd starts
         tf = (off & 1u) ? (((tf & 0xFFu) << 8) | (tf >> 8)) : tf;
-        uint32_t us = ws + tf + (src & 0xFFFFu) + (src >> 16) + (dip & 0xFFFFu) + (dip >> 16) +
-                      0x1100u + ulen_raw;                         // + pseudo-header
+        us += tf;
         const bool need_pad = is_udp && ucks != 0u && !len_bad && 34u + ulen < len;
         if (__ballot(need_pad)) {                                 // Ethernet padding after the datagram
             if (need_pad) {
@@ -437,6 +442,7 @@ rx_classify(RxArgs a)
         const uint32_t state = ucks == 0u ? UDPDK_UDP_CSUM_NONE
                              : (len_bad || fold32(us) != 0xFFFFu) ? UDPDK_UDP_CSUM_BAD
                                                                    : UDPDK_UDP_CSUM_OK;
+        STAMP(4);
 
         // ---- demux: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
         // the port entry carries the first binding; later ones only for ports with several
@@ -463,7 +469,7 @@ rx_classify(RxArgs a)
                                : !ipv4 ? UDPDK_V_NOT_IPV4
                                : !l3 ? UDPDK_V_TRUNC
                                : fragd ? UDPDK_V_FRAG
-                               : (g[2] >> 24) != 17u ? UDPDK_V_NOT_UDP   // udpdk_poller.c:368-371
+                               : not_udp ? UDPDK_V_NOT_UDP
                                : e.x == 0u ? UDPDK_V_NO_BIND
                                : fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
         STAMP(5);

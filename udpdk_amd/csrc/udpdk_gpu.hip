@@ -102,7 +102,7 @@ uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); 
 
 void geometry(uint32_t n, uint32_t lanes, uint32_t *T, uint32_t *tiles)
 {
-    uint32_t t = lanes == 1 ? RX_TILE_ONE_LANE : RX_TILE_MIN;
+    uint32_t t = RX_TILE_MIN;
     while (t < RX_TILE_MAX && (uint64_t)ceil_div(n, t) * lanes > RX_HIST_CAP) t *= 2;
     *T = t;
     *tiles = std::max<uint32_t>(1u, ceil_div(n, t));
