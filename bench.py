@@ -272,7 +272,7 @@ def main():
     if os.path.exists(tf):
         try:
             with open(tf) as f:
-                traffic = json.load(f).get(w.name, {}).get("rx_classify_hbm_bytes_per_launch")
+                traffic = json.load(f)["workloads"].get(w.name, {}).get("rx_classify_hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -298,6 +298,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": "rx_classify",
+                     "traffic_source": "profiles/traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                       "passes of this workload (tools/pmc_traffic.sh)",
                      "algorithmic_bytes_per_launch": cls_bytes},
         "cpu_baseline": None,
     }
