@@ -192,9 +192,13 @@ typedef struct {
     uint32_t overflow;       /* deliveries > lane_cap: lane_pkt holds only the first lane_cap  */
 } udpdk_rx_stats_t;
 
-/* Enqueue the RX pipeline for one batch on the context stream (async). */
+/* Enqueue the RX pipeline for one batch on the context stream (async): rx_classify, then either
+ * rx_compact1 (one lane and no fan-out in the snapshot) or rx_scan + rx_scatter. meta, lane_off
+ * and lane_pkt are complete when the stream reaches the end of the sequence. */
 int udpdk_gpu_rx(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch, const udpdk_rx_out_t *out);
-/* Wait for the last udpdk_gpu_rx and read its counters. Returns -ENOSPC on lane overflow. */
+/* Counters of the last udpdk_gpu_rx (reduced from its per-tile counter rows by one small kernel
+ * launched here, so batches nobody asks statistics for pay nothing), then wait for the stream.
+ * Returns -ENOSPC on lane overflow. */
 int udpdk_gpu_rx_stats(udpdk_gpu_ctx *ctx, udpdk_rx_stats_t *stats);
 
 /* End-to-end variant for host-resident batches (the real poller's situation: frames arrive in
@@ -238,15 +242,16 @@ int udpdk_gpu_tx_build(udpdk_gpu_ctx *ctx, const udpdk_tx_config_t *cfg,
                        const udpdk_tx_batch_t *batch, const udpdk_tx_out_t *out);
 
 /* ---------------------------------------------------------------------------------------------
- * Timing (for bench.py / the roofline): udpdk_gpu_rx records HIP events around each of its
- * kernels on the context stream on every `enable`-th call (0 = off, 1 = every call; sampling
- * keeps the ~10 us host cost of an event record off most calls); read back the accumulated
- * device milliseconds and the number of timed calls.
+ * Timing (for bench.py / the roofline): on every `enable`-th udpdk_gpu_rx call (0 = off, 1 =
+ * every call) each kernel is launched with start/stop events carried by its own dispatch
+ * (hipExtLaunchKernelGGL), so no marker packet separates back-to-back kernels; sampling keeps the
+ * host cost of the events (~10 us per timed call) off most calls. Read back the accumulated
+ * device milliseconds and the number of timed launches per kernel id.
  * ------------------------------------------------------------------------------------------- */
 enum udpdk_gpu_kernel_id {
     UDPDK_K_RX_CLASSIFY = 0,   /* parse + checksums + demux + tile histograms (dominant)      */
     UDPDK_K_RX_SCAN     = 1,   /* lane offsets (one or three launches)                         */
-    UDPDK_K_RX_SCATTER  = 2,   /* stable per-lane compaction                                   */
+    UDPDK_K_RX_SCATTER  = 2,   /* stable per-lane compaction (rx_scatter, or rx_compact1)      */
     UDPDK_K_TX_BUILD    = 3,
     UDPDK_N_KERNEL_IDS  = 4
 };
