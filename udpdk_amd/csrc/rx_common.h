@@ -14,8 +14,10 @@ constexpr uint32_t RX_TILE_MAX = 16384;
 constexpr uint32_t RX_HIST_CAP = 1u << 21;  // target bound on lanes x tiles
 
 constexpr int SCAN_BLOCK = 256;
-constexpr uint32_t SCAN_CHUNK = 4096;       // elements per workgroup in the 3-pass scan
+constexpr int SCAN_TOP_BLOCK = 1024;
+constexpr uint32_t SCAN_COL_CHUNK = 32;     // tiles per chunk of the 3-pass column scan
 constexpr uint32_t SCAN_SMALL_MAX = 16384;  // single-workgroup scan up to this many elements
+constexpr uint32_t SCAN_SMALL_TILES = 32;   // ... and this many tiles (serial per lane)
 
 constexpr int TX_BLOCK = 256;
 
@@ -43,7 +45,7 @@ struct RxArgs {
     const uint4    *port_tab;
     const uint2    *binds;
     uint32_t *meta;
-    uint32_t *hist;       // [n_lanes][n_tiles] per-tile per-lane delivery counts
+    uint32_t *hist;       // [n_tiles][n_lanes] per-tile per-lane delivery counts (tile-major)
     uint32_t *tile_cnt;   // [n_tiles][16] per-tile counters
     unsigned long long *dbg;        // diagnostic stamps (UDPDK_STAMPS builds), may be null
     uint32_t key_bits;

@@ -14,12 +14,12 @@
 //       reduced per frame by a DPP prefix scan.
 //       Demux: one 16-byte port-table entry per frame (first binding inline), the binding list
 //       only for ports with several. Writes the verdict word, the tile's per-lane delivery
-//       histogram (lane-major hist[lane][tile]) and the tile's counter row.
+//       histogram (tile-major row hist[tile][lane]) and the tile's counter row.
 //   rx_compact1  single lane without fan-out (the one bound socket of apps/pktgen): per tile,
 //       base = sum of the predecessors' counts, ballots over the verdict words, lane writes.
-//   rx_scan + rx_scatter  general case: exclusive scan of the lane-major histogram (one launch
-//       when small, reduce/top/down otherwise), then one wave per tile writes each delivery at
-//       its stable position.
+//   rx_scan + rx_scatter  general case: per-lane column scan of the tile-major histogram (one
+//       launch when small, reduce/top/down otherwise), then one wave per tile writes each
+//       delivery at its stable position.
 //   rx_counters  on demand (udpdk_gpu_rx_stats): sum of the per-tile counter rows.
 //
 // Algorithmic bytes per frame in rx_classify: frame_len + 6 (u32 offset + u16 length) + 4
@@ -553,7 +553,7 @@ rx_classify(RxArgs a)
     if (a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
 #endif
     for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK)
-        a.hist[(size_t)s * a.n_tiles + tile] = hist[s];
+        a.hist[(size_t)tile * a.n_lanes + s] = hist[s];
     if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = tile_counter(tid);
 }
 
@@ -630,8 +630,14 @@ rx_counters(const uint32_t *tile_cnt, uint32_t n_tiles, unsigned long long *coun
 }
 
 // ------------------------------------------------------------------------------------------
-// rx_scan: exclusive scan of hist[E] (lane-major) in place; lane_off; counter reduction
+// rx_scan: the tile-major histogram hist[tile][lane] becomes each (tile, lane)'s start position
+// in the lane array: pos(t, l) = lane_off[l] + sum_{t' < t} hist[t'][l], with lane_off the
+// exclusive scan of the lane totals. Every access is row-contiguous (threads = lanes).
+//   small (one launch):  lanes x tiles <= SCAN_SMALL_MAX and tiles <= SCAN_SMALL_TILES
+//   reduce / top / down: per-chunk column sums (chunks of SCAN_COL_CHUNK tiles), one workgroup
+//                        scanning chunks and lanes, then the in-place rescan of every chunk.
 // ------------------------------------------------------------------------------------------
+// exclusive scan over a block of any wave count; lds16 >= waves words
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds16, uint32_t *total)
 {
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -649,92 +655,98 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds16,
     return pre + inc - v;
 }
 
-// Small case: one workgroup of SCAN_BLOCK threads, E <= SCAN_SMALL_MAX.
+// Lane totals tot[] (LDS, n_lanes words) -> lane_off[] exclusive scan + total. Thread j takes the
+// contiguous lanes [j * L, (j + 1) * L).
+__device__ void scan_lane_totals(const uint32_t *tot, uint32_t n_lanes, uint32_t *lane_off,
+                                 uint32_t *total_out, uint32_t *lds16)
+{
+    const uint32_t tid = threadIdx.x, L = (n_lanes + blockDim.x - 1) / blockDim.x;
+    const uint32_t l0 = min(n_lanes, tid * L), l1 = min(n_lanes, l0 + L);
+    uint32_t s = 0;
+    for (uint32_t l = l0; l < l1; ++l) s += tot[l];
+    uint32_t total;
+    uint32_t run = block_excl_scan(s, lds16, &total);
+    for (uint32_t l = l0; l < l1; ++l) {
+        lane_off[l] = run;
+        run += tot[l];
+    }
+    if (tid == 0) { lane_off[n_lanes] = total; *total_out = total; }
+}
+
 __global__ void __launch_bounds__(SCAN_BLOCK)
 rx_scan_small(ScanArgs a)
 {
+    extern __shared__ uint32_t tot[];                       // [n_lanes]
     __shared__ uint32_t lds16[SCAN_BLOCK / 64];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t per = (a.n_elems + SCAN_BLOCK - 1) / SCAN_BLOCK;
-    const uint32_t i0 = tid * per, i1 = min(a.n_elems, i0 + per);
-    uint32_t s = 0;
-    for (uint32_t i = i0; i < i1; ++i) s += a.hist[i];
-    uint32_t total;
-    uint32_t run = block_excl_scan(s, lds16, &total);
-    for (uint32_t i = i0; i < i1; ++i) {
-        const uint32_t v = a.hist[i];
-        a.hist[i] = run;
-        if (i % a.n_tiles == 0) a.lane_off[i / a.n_tiles] = run;
-        run += v;
+    const uint32_t S = a.n_lanes;
+    for (uint32_t l = threadIdx.x; l < S; l += SCAN_BLOCK) {
+        uint32_t run = 0;
+        for (uint32_t t = 0; t < a.n_tiles; ++t) {
+            const uint32_t v = a.hist[(size_t)t * S + l];
+            a.hist[(size_t)t * S + l] = run;
+            run += v;
+        }
+        tot[l] = run;
     }
-    if (tid == 0) { a.lane_off[a.n_lanes] = total; *a.total = total; }
+    __syncthreads();
+    scan_lane_totals(tot, S, a.lane_off, a.total, lds16);
+    __syncthreads();
+    for (uint32_t l = threadIdx.x; l < S; l += SCAN_BLOCK) {
+        const uint32_t base = a.lane_off[l];
+        for (uint32_t t = 0; t < a.n_tiles; ++t) a.hist[(size_t)t * S + l] += base;
+    }
 }
 
-// Large case, pass 1: partial[b] = sum of chunk b (SCAN_CHUNK elements).
+// Pass 1, grid (chunks, ceil(lanes / SCAN_BLOCK)): partial[c][l] = column sum of chunk c.
 __global__ void __launch_bounds__(SCAN_BLOCK)
 rx_scan_reduce(ScanArgs a)
 {
-    __shared__ uint32_t lds16[SCAN_BLOCK / 64];
-    const uint32_t b = blockIdx.x, tid = threadIdx.x;
-    const uint32_t base = b * SCAN_CHUNK;
+    const uint32_t S = a.n_lanes, l = blockIdx.y * SCAN_BLOCK + threadIdx.x;
+    if (l >= S) return;
+    const uint32_t t0 = blockIdx.x * SCAN_COL_CHUNK, t1 = min(a.n_tiles, t0 + SCAN_COL_CHUNK);
     uint32_t s = 0;
-#pragma unroll 4
-    for (uint32_t i = tid; i < SCAN_CHUNK; i += SCAN_BLOCK)
-        if (base + i < a.n_elems) s += a.hist[base + i];
-    s = wave_sum(s);
-    if (lane_id() == 0) lds16[tid >> 6] = s;
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t t = 0;
-        for (uint32_t i = 0; i < SCAN_BLOCK / 64; ++i) t += lds16[i];
-        a.partial[b] = t;
-    }
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; ++t) s += a.hist[(size_t)t * S + l];
+    a.partial[(size_t)blockIdx.x * S + l] = s;
 }
 
-// Large case, pass 2: exclusive scan of partial[] (one workgroup) + counters.
-__global__ void __launch_bounds__(SCAN_BLOCK)
-rx_scan_top(ScanArgs a, uint32_t n_part)
+// Pass 2, one workgroup: per lane, exclusive scan of its chunk sums (in place) and its total;
+// then lane_off = exclusive scan of the totals.
+__global__ void __launch_bounds__(SCAN_TOP_BLOCK)
+rx_scan_top(ScanArgs a, uint32_t n_chunks)
 {
-    __shared__ uint32_t lds16[SCAN_BLOCK / 64];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t per = (n_part + SCAN_BLOCK - 1) / SCAN_BLOCK;
-    const uint32_t i0 = tid * per, i1 = min(n_part, i0 + per);
-    uint32_t s = 0;
-    for (uint32_t i = i0; i < i1; ++i) s += a.partial[i];
-    uint32_t total;
-    uint32_t run = block_excl_scan(s, lds16, &total);
-    for (uint32_t i = i0; i < i1; ++i) {
-        const uint32_t v = a.partial[i];
-        a.partial[i] = run;
-        run += v;
+    extern __shared__ uint32_t tot[];                       // [n_lanes]
+    __shared__ uint32_t lds16[SCAN_TOP_BLOCK / 64];
+    const uint32_t S = a.n_lanes;
+    for (uint32_t l = threadIdx.x; l < S; l += SCAN_TOP_BLOCK) {
+        uint32_t run = 0;
+#pragma unroll 8
+        for (uint32_t c = 0; c < n_chunks; ++c) {
+            const uint32_t v = a.partial[(size_t)c * S + l];
+            a.partial[(size_t)c * S + l] = run;
+            run += v;
+        }
+        tot[l] = run;
     }
-    if (tid == 0) { a.lane_off[a.n_lanes] = total; *a.total = total; }
+    __syncthreads();
+    scan_lane_totals(tot, S, a.lane_off, a.total, lds16);
 }
 
-// Large case, pass 3: rescan each chunk from its partial offset; write lane_off entries.
+// Pass 3, grid (chunks, ceil(lanes / SCAN_BLOCK)): rescan chunk c from lane_off + its prefix.
 __global__ void __launch_bounds__(SCAN_BLOCK)
 rx_scan_down(ScanArgs a)
 {
-    __shared__ uint32_t lds16[SCAN_BLOCK / 64];
-    constexpr uint32_t PER = SCAN_CHUNK / SCAN_BLOCK;
-    const uint32_t b = blockIdx.x, tid = threadIdx.x;
-    const uint32_t i0 = b * SCAN_CHUNK + tid * PER;
-    uint32_t v[PER];
-    uint32_t s = 0;
+    const uint32_t S = a.n_lanes, l = blockIdx.y * SCAN_BLOCK + threadIdx.x;
+    if (l >= S) return;
+    const uint32_t t0 = blockIdx.x * SCAN_COL_CHUNK, t1 = min(a.n_tiles, t0 + SCAN_COL_CHUNK);
+    uint32_t v[SCAN_COL_CHUNK];
 #pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) {
-        v[k] = (i0 + k < a.n_elems) ? a.hist[i0 + k] : 0u;
-        s += v[k];
-    }
-    uint32_t total;
-    uint32_t run = block_excl_scan(s, lds16, &total) + a.partial[b];
+    for (uint32_t k = 0; k < SCAN_COL_CHUNK; ++k)
+        v[k] = t0 + k < t1 ? a.hist[(size_t)(t0 + k) * S + l] : 0u;
+    uint32_t run = a.lane_off[l] + a.partial[(size_t)blockIdx.x * S + l];
 #pragma unroll
-    for (uint32_t k = 0; k < PER; ++k) {
-        const uint32_t i = i0 + k;
-        if (i < a.n_elems) {
-            a.hist[i] = run;
-            if (i % a.n_tiles == 0) a.lane_off[i / a.n_tiles] = run;
-        }
+    for (uint32_t k = 0; k < SCAN_COL_CHUNK; ++k) {
+        if (t0 + k < t1) a.hist[(size_t)(t0 + k) * S + l] = run;
         run += v[k];
     }
 }
@@ -751,7 +763,7 @@ rx_scatter(ScatterArgs a)
     const uint32_t tile = blockIdx.x;
     // cursor of every lane for this tile (independent loads, one latency)
 #pragma unroll 8
-    for (uint32_t s = lane; s < a.n_lanes; s += 64) cur[s] = a.base[(size_t)s * a.n_tiles + tile];
+    for (uint32_t s = lane; s < a.n_lanes; s += 64) cur[s] = a.base[(size_t)tile * a.n_lanes + s];
     wave_sync();
     const uint32_t t0 = tile * a.tile_frames;
     const uint32_t t1 = min(a.n, t0 + a.tile_frames);

@@ -211,7 +211,7 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
                                                   (uint64_t)ceil_div(max_frames, RX_TILE_MAX) * max_lanes);
         c->hist_cap = e_cap;
         if (hipMalloc((void **)&c->hist, e_cap * 4) != hipSuccess) break;
-        c->partial_cap = ceil_div(e_cap, SCAN_CHUNK) + 1;
+        c->partial_cap = e_cap / SCAN_COL_CHUNK + max_lanes + 1;   // chunks x lanes
         if (hipMalloc((void **)&c->partial, c->partial_cap * 4) != hipSuccess) break;
         c->tiles_cap = ceil_div(max_frames, RX_TILE_MIN) + 1;
         if (hipMalloc((void **)&c->tile_cnt, c->tiles_cap * UDPDK_N_COUNTERS * 4) != hipSuccess) break;
@@ -223,6 +223,11 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
                                 160 * 1024) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) break;
+        // lane totals: 4 B per lane, up to UDPDK_GPU_MAX_LANES (64 KiB) beside a few static words
+        if (hipFuncSetAttribute((const void *)rx_scan_small, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                4 * UDPDK_GPU_MAX_LANES) != hipSuccess) break;
+        if (hipFuncSetAttribute((const void *)rx_scan_top, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                4 * UDPDK_GPU_MAX_LANES) != hipSuccess) break;
         rc = 0;
     } while (0);
     if (rc) {
@@ -495,13 +500,15 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     sa.n_elems = (uint32_t)E;
     sa.n_tiles = tiles;
     sa.n_lanes = S;
-    if (E <= SCAN_SMALL_MAX) {
-        HIPC(c, launch(c, ts, 1, true, true, rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 0u, sa));
+    if (E <= SCAN_SMALL_MAX && tiles <= SCAN_SMALL_TILES) {
+        HIPC(c, launch(c, ts, 1, true, true, rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 4u * S, sa));
     } else {
-        const uint32_t nb = ceil_div(E, SCAN_CHUNK);
-        HIPC(c, launch(c, ts, 1, true, false, rx_scan_reduce, dim3(nb), dim3(SCAN_BLOCK), 0u, sa));
-        HIPC(c, launch(c, ts, 1, false, false, rx_scan_top, dim3(1), dim3(SCAN_BLOCK), 0u, sa, nb));
-        HIPC(c, launch(c, ts, 1, false, true, rx_scan_down, dim3(nb), dim3(SCAN_BLOCK), 0u, sa));
+        const uint32_t nc = ceil_div(tiles, SCAN_COL_CHUNK);
+        if ((uint64_t)nc * S > c->partial_cap) return -EINVAL;
+        const dim3 grid(nc, ceil_div(S, (uint32_t)SCAN_BLOCK));
+        HIPC(c, launch(c, ts, 1, true, false, rx_scan_reduce, grid, dim3(SCAN_BLOCK), 0u, sa));
+        HIPC(c, launch(c, ts, 1, false, false, rx_scan_top, dim3(1), dim3(SCAN_TOP_BLOCK), 4u * S, sa, nc));
+        HIPC(c, launch(c, ts, 1, false, true, rx_scan_down, grid, dim3(SCAN_BLOCK), 0u, sa));
     }
 
     ScatterArgs xa;
