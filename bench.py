@@ -181,7 +181,7 @@ def cpu_baseline(w: F.Workload, target_s: float):
 def side_config(ctx, cfg: int, steps: int, rotate: int):
     w = F.config_batch(cfg)
     rx = Rx(ctx, w, rotate)
-    wall, gpu_step, kt, st = time_loop(rx, steps, 5, lambda: None, 1)
+    wall, gpu_step, kt, st = time_loop(rx, steps, 5, lambda: None, 4)
     cls_gbps = rx.classify_bytes() / (kt.get("rx_classify", 1e3 * gpu_step) / 1e6) / 1e9
     out = {"workload": w.name, "mpkt_s": round(rx.n * steps / wall / 1e6, 1),
            "gbps_pipeline": round(rx.pipeline_bytes() * steps / wall / 1e9, 1),
@@ -193,6 +193,49 @@ def side_config(ctx, cfg: int, steps: int, rotate: int):
         a[4].frames.free(); a[4].offset.free(); a[4].length.free()
         a[5].meta.free(); a[5].lane_off.free(); a[5].lane_pkt.free()
     return out
+
+
+def tx_line(ctx, payload_len: int, n: int, steps: int):
+    """udpdk_gpu_tx_build over n datagrams of payload_len bytes (one bound socket, ANY:10000 ->
+    172.31.100.1:10001, frames back to back): device-resident TX header build + rte_ipv4_cksum +
+    payload copy, GPU time from events around `steps` back-to-back launches."""
+    slots = [(0, abi.raw_port(10000), 1)]
+    hs = abi.snapshot_from_lists({}, 1, slots=slots)
+    ctx.upload_snapshot(hs)
+    rng = np.random.default_rng(7)
+    pay = rng.integers(0, 256, n * payload_len + 64, dtype=np.uint8)
+    pay_off = (np.arange(n, dtype=np.uint64) * payload_len).astype(np.uint32)
+    lens = np.full(n, payload_len, np.uint16)
+    frame_off = (np.arange(n, dtype=np.uint64) * (payload_len + 42)).astype(np.uint32)
+    bufs = [ctx.upload(pay), ctx.upload(pay_off), ctx.upload(lens), ctx.upload(np.zeros(n, np.int32)),
+            ctx.upload(np.full(n, abi.raw_ip("172.31.100.1"), np.uint32)),
+            ctx.upload(np.full(n, abi.raw_port(10001), np.uint16)), ctx.upload(frame_off)]
+    cap = n * (payload_len + 42) + 64
+    out = ctx.alloc(cap)
+    cfg = abi.TxConfig((C.c_uint8 * 6)(*bytes.fromhex("6805ca95f8ec")),
+                       (C.c_uint8 * 6)(*bytes.fromhex("6805ca95fa64")), abi.raw_ip("172.31.100.2"))
+    bt = abi.TxBatch(bufs[0].ptr, pay.nbytes, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, bufs[4].ptr,
+                     bufs[5].ptr, n)
+    ot = abi.TxOut(out.ptr, cap, bufs[6].ptr)
+    f = abi.lib().udpdk_gpu_tx_build
+    args = (ctx.handle, C.byref(cfg), C.byref(bt), C.byref(ot))
+    for _ in range(5):
+        abi._check(f(*args), "udpdk_gpu_tx_build")
+    ev = HipEvents(ctx)
+    ctx.sync()
+    ev.record(0)
+    for _ in range(steps):
+        f(*args)
+    ev.record(1)
+    ctx.sync()
+    us = 1e3 * ev.elapsed_ms() / steps
+    ev.close()
+    nbytes = n * payload_len + n * (payload_len + 42) + 12 * n   # payload in, frames out, metadata
+    for b in bufs + [out]:
+        b.free()
+    return {"workload": f"TX {n} x {payload_len + 42} B frames", "mpkt_s": round(n / us, 1),
+            "us_per_launch": round(us, 2), "gbps": round(nbytes / us / 1e3, 1),
+            "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4)}
 
 
 def end_to_end(ctx, cfg: int, reps: int):
@@ -316,7 +359,7 @@ def main():
         }
     if rank == 0 and world == 1 and not args.no_extra:
         extra = []
-        for cfg in (3, 4):
+        for cfg in (3, 4, 5):
             if cfg != args.config:
                 try:
                     extra.append(side_config(ctx, cfg, max(10, args.steps // 4), args.rotate_mib << 20))
@@ -330,6 +373,13 @@ def main():
             except Exception as e:
                 e2e.append({"config": cfg, "error": repr(e)})
         line["end_to_end"] = e2e
+        tx = []
+        for plen in (22, 1458):                  # 64 B and 1500 B frames
+            try:
+                tx.append(tx_line(ctx, plen, 1 << 20, 50))
+            except Exception as e:
+                tx.append({"payload": plen, "error": repr(e)})
+        line["tx"] = tx
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()

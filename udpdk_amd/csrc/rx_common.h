@@ -124,6 +124,8 @@ __global__ void rx_scan_reduce(ScanArgs a);
 __global__ void rx_scan_top(ScanArgs a, uint32_t n_part);
 __global__ void rx_scan_down(ScanArgs a);
 __global__ void rx_scatter(ScatterArgs a);
+__global__ void rx_scatter4(ScatterArgs a);
+constexpr uint32_t SCATTER4_MAX_LANES = 4096;   // rx_scatter4 LDS: 5 x lanes words
 __global__ void rx_compact1(Compact1Args a);
 __global__ void rx_counters(const uint32_t *tile_cnt, uint32_t n_tiles, unsigned long long *counters);
 __global__ void tx_build(TxArgs a);

@@ -752,6 +752,83 @@ rx_scan_down(ScanArgs a)
 }
 
 // ------------------------------------------------------------------------------------------
+// rx_scatter4: stable per-lane compaction without fan-out, four waves per tile. Wave w owns the
+// w-th quarter of the tile. Pass 1 counts each wave's deliveries per lane key (wave multi-split:
+// one LDS update per distinct key per 64 frames); the wave bases of every key are the tile cursor
+// plus the counts of the earlier quarters; pass 2 re-reads the verdict words and writes each
+// delivery at base + rank. LDS: (1 + 4) x n_lanes words.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+rx_scatter4(ScatterArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm4[];
+    const uint32_t S = a.n_lanes;
+    uint32_t *cur = sm4;                                   // [S] tile cursor per lane
+    uint32_t *wc = sm4 + S;                                // [4][S] per-wave count, then base
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const uint32_t tile = blockIdx.x;
+    for (uint32_t k = tid; k < S; k += 256) {
+        cur[k] = a.base[(size_t)tile * S + k];
+        wc[k] = 0u; wc[S + k] = 0u; wc[2 * S + k] = 0u; wc[3 * S + k] = 0u;
+    }
+    __syncthreads();
+    const uint32_t t1 = min(a.n, (tile + 1) * a.tile_frames);
+    const uint32_t q = a.tile_frames / 4;
+    const uint32_t wb = tile * a.tile_frames + w * q, we = min(t1, wb + q);
+    const uint32_t plast = a.n - 1u;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    uint32_t *mine = wc + w * S;
+    constexpr int PF = 4;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (uint32_t g0 = wb; g0 < we; g0 += 64 * PF) {
+            uint32_t mv[PF];
+#pragma unroll
+            for (int i = 0; i < PF; ++i) mv[i] = a.meta[min(g0 + i * 64 + lane, plast)];
+#pragma unroll
+            for (int i = 0; i < PF; ++i) {
+                const uint32_t p = g0 + i * 64 + lane;
+                const bool deliver = p < we && UDPDK_META_VERDICT(mv[i]) == UDPDK_V_DELIVERED;
+                const uint32_t key = UDPDK_META_SOCKFD(mv[i]) & a.lane_mask;
+                unsigned long long peers = __ballot(deliver);
+                if (!peers) continue;                      // wave-uniform
+                for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
+                    const bool kb = (key >> bit) & 1u;
+                    const unsigned long long bal = __ballot(kb);
+                    peers &= kb ? bal : ~bal;
+                }
+                const uint32_t leader = deliver ? (uint32_t)__ffsll((long long)peers) - 1u : 64u;
+                const uint32_t cnt = (uint32_t)__popcll(peers);
+                if (pass == 0) {
+                    if (deliver && lane == leader) mine[key] += cnt;
+                } else {
+                    uint32_t c = 0;
+                    if (deliver && lane == leader) {
+                        c = mine[key];
+                        mine[key] = c + cnt;
+                    }
+                    c = __shfl(c, deliver ? (int)leader : 0, 64);
+                    const uint32_t pos = c + (uint32_t)__popcll(peers & lt_mask);
+                    if (deliver && pos < a.lane_cap) a.lane_pkt[pos] = p;
+                }
+            }
+        }
+        if (pass == 0) {
+            __syncthreads();
+            for (uint32_t k = tid; k < S; k += 256) {      // wave bases: cursor + earlier quarters
+                uint32_t c = cur[k];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t v = wc[i * S + k];
+                    wc[i * S + k] = c;
+                    c += v;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // rx_scatter: stable per-lane compaction, one wave per tile
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(64)

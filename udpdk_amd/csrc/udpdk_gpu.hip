@@ -223,6 +223,8 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
                                 160 * 1024) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) break;
+        if (hipFuncSetAttribute((const void *)rx_scatter4, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                20 * SCATTER4_MAX_LANES) != hipSuccess) break;
         // lane totals: 4 B per lane, up to UDPDK_GPU_MAX_LANES (64 KiB) beside a few static words
         if (hipFuncSetAttribute((const void *)rx_scan_small, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 4 * UDPDK_GPU_MAX_LANES) != hipSuccess) break;
@@ -526,7 +528,10 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     xa.lane_mask = c->lane_mask;
     xa.key_bits = c->key_bits;
     xa.lane_cap = o->lane_cap;
-    HIPC(c, launch(c, ts, 2, true, true, rx_scatter, dim3(tiles), dim3(64), 4u * S, xa));
+    if (c->max_fanout <= 1 && S <= SCATTER4_MAX_LANES)
+        HIPC(c, launch(c, ts, 2, true, true, rx_scatter4, dim3(tiles), dim3(256), 20u * S, xa));
+    else
+        HIPC(c, launch(c, ts, 2, true, true, rx_scatter, dim3(tiles), dim3(64), 4u * S, xa));
     return 0;
 }
 
