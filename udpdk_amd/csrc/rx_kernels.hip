@@ -226,7 +226,7 @@ __device__ __forceinline__ void wait_vm(v4u32 &r)
     asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r) : "n"(N) : "memory");
 }
 
-__global__ void __launch_bounds__(RX_BLOCK, 4)
+__global__ void __launch_bounds__(RX_BLOCK)
 rx_classify(RxArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -287,14 +287,17 @@ rx_classify(RxArgs a)
         return r;
     };
 
-    // Steps are software-pipelined two deep: a step's window registers are refilled with the
-    // window two steps ahead as soon as they are parsed, so every window has about two steps of
-    // work to arrive in; descriptors run three steps ahead.
-    struct Desc { uint32_t off, len, pt; };
-    auto body = [&](const uint32_t st, Win &X, const Desc &dc, const Desc &dp, Desc &dq) {
+    uint32_t st = w;
+    uint32_t c_off = 0, c_len = 0, c_pt = 0, n_off = 0, n_len = 0, n_pt = 0;
+    load_desc(st, c_off, c_len, c_pt);
+    Win W = load_win(st, c_off, c_len);
+    load_desc(st + RX_WAVES, n_off, n_len, n_pt);
+    STAMP(0);
+
+    while (st < steps) {
         const uint32_t p = t0 + st * 64 + lane;
         const bool valid = p < t1;
-        const uint32_t off = dc.off, len = dc.len;
+        const uint32_t off = c_off, len = c_len;
         const bool bad_desc = valid && ((uint64_t)off + len > (uint64_t)a.frames_bytes);
         const bool good = valid && !bad_desc;
 
@@ -303,12 +306,12 @@ rx_classify(RxArgs a)
         {
             const uint32_t sh = (off + 12u) & 15u, s3 = sh & 3u;
             uint32_t wd[17], w1[16], w2[14];
-            const uint4 wc[4] = {X.c0, X.c1, X.c2, X.c3};
+            const uint4 wc[4] = {W.c0, W.c1, W.c2, W.c3};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 wd[4 * i] = wc[i].x; wd[4 * i + 1] = wc[i].y; wd[4 * i + 2] = wc[i].z; wd[4 * i + 3] = wc[i].w;
             }
-            wd[16] = X.c4;
+            wd[16] = W.c4;
             // shift by (sh >> 2) dwords with lane-mask selects (a plain ?: here is turned into a
             // scratch-indexed array by the compiler)
             const unsigned long long m4 = __ballot((sh & 4u) != 0u), m8 = __ballot((sh & 8u) != 0u);
@@ -319,17 +322,14 @@ rx_classify(RxArgs a)
 #pragma unroll
             for (int i = 0; i < 13; ++i) g[i] = __builtin_amdgcn_alignbyte(w2[i + 1], w2[i], s3);
         }
-        const uint32_t pt = !good ? 0u : a.ptype ? dc.pt
+        const uint32_t pt = !good ? 0u : a.ptype ? c_pt
                           : (len >= 14 ? (((g[0] & 0xFFFFu) == 0x0008u) ? 0x211u : 0x1u) : 0u);
         const uint32_t frag = ((g[2] & 0xFFu) << 8) | ((g[2] >> 8) & 0xFFu);
         const bool is_udp = good && (pt & 0x10u) && len >= 42u && !(frag & 0x3FFFu) && (g[2] >> 24) == 17u;
         const uint32_t dport = g[6] & 0xFFFFu;                   // poller.c:372
-        // The demux load goes out first and is waited for only where it is used; then this
-        // window's registers take the window two steps ahead (and the descriptors three ahead).
+        // The demux load goes out first and is waited for only where it is used.
         STAMP(1);
         v4u32 ev = asm_load16(a.port_tab + dport);
-        X = load_win(st + 2 * RX_WAVES, dp.off, dp.len);
-        load_desc(st + 3 * RX_WAVES, dq.off, dq.len, dq.pt);
 
         // ---- everything the header window gives (the window registers die here) ----
         const bool ipv4 = good && (pt & 0x10u);                   // udpdk_poller.c:334, :362-366
@@ -359,41 +359,6 @@ rx_classify(RxArgs a)
         }
         uint32_t us = ws + (g[3] >> 16) + (g[4] & 0xFFFFu) + (dip & 0xFFFFu) + (dip >> 16) + 0x1100u +
                       ulen_raw;
-
-        // issued after the demux load: 5 window loads + 2 descriptor loads (+1 with ptype)
-        wait_vm<7>(ev);
-        STAMP(2);
-
-        const uint4 e = is_udp ? make_uint4(ev[0], ev[1], ev[2], ev[3]) : make_uint4(0, 0, 0, 0);
-
-        // ---- demux: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
-        // the port entry carries the first binding; later ones only for ports with several
-        const bool match0 = e.x != 0u && (dip == e.z || e.z == 0u);     // poller.c:391
-        uint32_t fan = match0 ? 1u : 0u;
-        uint32_t first = match0 ? (e.w & 0x7FFFFFFFu) : 0u;
-        const bool walk = e.x > 1u && !(match0 && !(e.w >> 31));        // poller.c:396-403
-        if (__ballot(walk)) {
-            if (walk) {
-                for (uint32_t i = 1; i < e.x; ++i) {
-                    const uint2 b = a.binds[e.y + i];
-                    if (dip == b.x || b.x == 0u) {
-                        const uint32_t sock = b.y & 0x7FFFFFFFu;
-                        if (fan > 0 && a.n_lanes > 1u)
-                            atomicAdd(&hist[sock & a.lane_mask], 1u);   // clones (rare)
-                        if (fan == 0) first = sock;
-                        ++fan;
-                        if (!(b.y >> 31)) break;
-                    }
-                }
-            }
-        }
-        const uint32_t verdict = !good ? UDPDK_V_BAD_DESC
-                               : !ipv4 ? UDPDK_V_NOT_IPV4
-                               : !l3 ? UDPDK_V_TRUNC
-                               : fragd ? UDPDK_V_FRAG
-                               : not_udp ? UDPDK_V_NOT_UDP
-                               : e.x == 0u ? UDPDK_V_NO_BIND
-                               : fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
 
         // ---- tail sweep: frame bytes >= 64 as 64-byte super-chunks swept across the lanes ----
         // Super-chunk j of a frame = 4 aligned 16-byte chunks from ((off + 64) & ~15) + 64 j; lane
@@ -437,15 +402,29 @@ rx_classify(RxArgs a)
                 const uint32_t pl = __shfl(P, (int)((lo > k0 ? lo - 1u - k0 : 0u) & 63u), 64);
                 if (lo < hi) tsum += ph - (lo > k0 ? pl : 0u);
             };
-            uint32_t qa;
-            uint4 Ra[4];
-            for (uint32_t k0 = 0; k0 < total; k0 += 64) {
-                issue(k0, qa, Ra);
+            uint32_t qa, qb;
+            uint4 Ra[4], Rb[4];
+            issue(0, qa, Ra);
+            for (uint32_t k0 = 0; k0 < total; k0 += 128) {
+                issue(k0 + 64, qb, Rb);
                 consume(k0, qa, Ra);
+                if (k0 + 64 >= total) break;
+                issue(k0 + 128, qa, Ra);
+                consume(k0 + 64, qb, Rb);
             }
             wave_sync();
         }
+        STAMP(2);
+
+        // ---- next step of this wave: window loads stay in flight across the rest of this step
+        const uint32_t nst = st + RX_WAVES;
+        const Win NW = load_win(nst, n_off, n_len);
+        uint32_t nn_off, nn_len, nn_pt;
+        load_desc(nst + RX_WAVES, nn_off, nn_len, nn_pt);
+        // issued after the demux load: 5 window loads + 2 descriptor loads (+1 with ptype)
+        wait_vm<7>(ev);
         STAMP(3);
+        const uint4 e = is_udp ? make_uint4(ev[0], ev[1], ev[2], ev[3]) : make_uint4(0, 0, 0, 0);
 
         // ---- UDP checksum state ----
         uint32_t tf = fold32(tsum);                               // tail: byte-swapped at odd starts
@@ -465,6 +444,34 @@ rx_classify(RxArgs a)
                                                                    : UDPDK_UDP_CSUM_OK;
         STAMP(4);
 
+        // ---- demux: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
+        // the port entry carries the first binding; later ones only for ports with several
+        const bool match0 = e.x != 0u && (dip == e.z || e.z == 0u);     // poller.c:391
+        uint32_t fan = match0 ? 1u : 0u;
+        uint32_t first = match0 ? (e.w & 0x7FFFFFFFu) : 0u;
+        const bool walk = e.x > 1u && !(match0 && !(e.w >> 31));        // poller.c:396-403
+        if (__ballot(walk)) {
+            if (walk) {
+                for (uint32_t i = 1; i < e.x; ++i) {
+                    const uint2 b = a.binds[e.y + i];
+                    if (dip == b.x || b.x == 0u) {
+                        const uint32_t sock = b.y & 0x7FFFFFFFu;
+                        if (fan > 0 && a.n_lanes > 1u)
+                            atomicAdd(&hist[sock & a.lane_mask], 1u);   // clones (rare)
+                        if (fan == 0) first = sock;
+                        ++fan;
+                        if (!(b.y >> 31)) break;
+                    }
+                }
+            }
+        }
+        const uint32_t verdict = !good ? UDPDK_V_BAD_DESC
+                               : !ipv4 ? UDPDK_V_NOT_IPV4
+                               : !l3 ? UDPDK_V_TRUNC
+                               : fragd ? UDPDK_V_FRAG
+                               : not_udp ? UDPDK_V_NOT_UDP
+                               : e.x == 0u ? UDPDK_V_NO_BIND
+                               : fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
         STAMP(5);
         const uint32_t l3f = l3 ? ((ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8) : 0u;
         const uint32_t udpf = is_udp ? (state << 5 | (len_bad ? 1u : 0u) << 7) : 0u;
@@ -499,20 +506,14 @@ rx_classify(RxArgs a)
             atomicAdd(&hist[key], 1u);
         }
         STAMP(6);
-    };
-    Desc D0, D1, D2, D3, D4;
-    load_desc(w, D0.off, D0.len, D0.pt);
-    load_desc(w + RX_WAVES, D1.off, D1.len, D1.pt);
-    load_desc(w + 2 * RX_WAVES, D2.off, D2.len, D2.pt);
-    Win A = load_win(w, D0.off, D0.len), B = load_win(w + RX_WAVES, D1.off, D1.len);
-    STAMP(0);
-    for (uint32_t st = w; st < steps; st += 2 * RX_WAVES) {
-        body(st, A, D0, D2, D3);
-        if (st + RX_WAVES >= steps) break;
-        body(st + RX_WAVES, B, D1, D3, D4);
-        D0 = D2;
-        D1 = D3;
-        D2 = D4;
+        W = NW;
+        c_off = n_off;
+        c_len = n_len;
+        c_pt = n_pt;
+        n_off = nn_off;
+        n_len = nn_len;
+        n_pt = nn_pt;
+        st = nst;
     }
 
     // ---- tile counters: one row per wave (lanes 0-15), summed by the readers ----
