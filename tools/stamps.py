@@ -5,7 +5,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["UDPDK_LIB_OVERRIDE"] = os.path.join(ROOT, "tools", "diag", "libudpdk_amd.so")
+os.environ["UDPDK_LIB_OVERRIDE"] = os.path.join(ROOT, "tools", "diag", os.environ.get("STAMPS_LIB", "libudpdk_amd.so"))
 sys.path.insert(0, ROOT)
 import numpy as np
 from udpdk_amd import abi, frames as F
@@ -20,13 +20,19 @@ L.udpdk_gpu_debug_buffer(ctx.handle, C.c_void_p(dbg.ptr))
 for cfg, n in [(2, 4096), (2, None), (4, 65536), (3, 65536)]:
     w = F.config_batch(cfg, n=n)
     ctx.upload_snapshot(abi.snapshot_from_lists(w.port_lists(), w.n_sockets))
-    db = abi.rx_upload(ctx, w.batch.frames, w.batch.offset, w.batch.length)
-    db.frames_bytes = w.batch.frames_bytes
+    # enough device copies that the 256 MiB Infinity Cache cannot hold them (as bench.py), so
+    # the stamps show HBM-cold behaviour
+    copies = max(1, -(-640 * 2**20 // (w.batch.frames.nbytes + 10 * w.batch.n)))
+    dbs = []
+    for _ in range(copies):
+        db = abi.rx_upload(ctx, w.batch.frames, w.batch.offset, w.batch.length)
+        db.frames_bytes = w.batch.frames_bytes
+        dbs.append(db)
     L.udpdk_gpu_memset(ctx.handle, C.c_void_p(dbg.ptr), 0, 16 * 8 * 8192 + 64)
     out = abi.rx_alloc_out(ctx, w.batch.n, w.n_sockets, w.batch.n)
-    abi.rx_run(ctx, db, out)
-    for _ in range(30):                 # back-to-back (warm GPU), the last launch's stamps stay
-        abi._check(abi.rx_enqueue(ctx, db, out), "udpdk_gpu_rx")
+    abi.rx_run(ctx, dbs[0], out)
+    for i in range(31):                 # back-to-back (warm GPU), the last launch's stamps stay
+        abi._check(abi.rx_enqueue(ctx, dbs[i % copies], out), "udpdk_gpu_rx")
     abi.rx_stats(ctx)
     _, tiles = abi.geometry(w.batch.n, w.n_sockets)
     d = ctx.download(dbg, np.uint64, 16 * tiles).reshape(tiles, 16).astype(np.float64)
@@ -59,6 +65,9 @@ for cfg, n in [(2, 4096), (2, None), (4, 65536), (3, 65536)]:
     order = np.argsort(tl)
     print(f"   tile order: start of tile k vs k: corr {np.corrcoef(tl, st0)[0, 1]:.3f}; "
           f"end(last tile) {en0[order[-1]] / 100:.2f} us")
-    for b in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt):
+    for db in dbs:
+        for b in (db.frames, db.offset, db.length):
+            b.free()
+    for b in (out.meta, out.lane_off, out.lane_pkt):
         b.free()
 ctx.close()

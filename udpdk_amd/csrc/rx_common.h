@@ -27,11 +27,12 @@ constexpr int TX_BLOCK = 256;
 constexpr int WAVE_ARRAYS = 3;                    // chunk start, offset, length
 constexpr int ARR_BYTES   = RX_WAVES * WAVE_ARRAYS * 64 * 4;
 constexpr int CNT_OFF     = ARR_BYTES;            // [RX_WAVES][16] per-wave counter rows
-constexpr int HIST_OFF    = CNT_OFF + RX_WAVES * 16 * 4;
+constexpr int HIST_OFF    = CNT_OFF + RX_WAVES * 16 * 4;   // [n_lanes], then the tile's
+                                                         // verdict words [tile_frames]
 
-__host__ __device__ constexpr uint32_t classify_lds_bytes(uint32_t n_lanes)
+__host__ __device__ constexpr uint32_t classify_lds_bytes(uint32_t n_lanes, uint32_t tile_frames)
 {
-    return (uint32_t)HIST_OFF + 4u * n_lanes;
+    return (uint32_t)HIST_OFF + 4u * ((n_lanes + 3u) & ~3u) + 4u * tile_frames;
 }
 
 // Port table entry (16 B per raw port): x = bindings on the port, y = index of the first in the

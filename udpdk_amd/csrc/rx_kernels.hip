@@ -241,6 +241,10 @@ rx_classify(RxArgs a)
     uint32_t *l_cs = arr, *l_off = arr + 64, *l_len = arr + 128;
     uint32_t *cntw = reinterpret_cast<uint32_t *>(smem + CNT_OFF);    // [wave][counter]
     uint32_t *hist = reinterpret_cast<uint32_t *>(smem + HIST_OFF);   // [n_lanes] this tile
+    // The tile's verdict words are staged in LDS and stored once per tile (16 B per lane): no
+    // global store inside the step loop, so no s_waitcnt there ever waits for a store (on gfx9
+    // stores count in vmcnt, in order with the loads).
+    uint32_t *mstage = hist + ((a.n_lanes + 3u) & ~3u);              // [tile_frames]
 
     for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK) hist[s] = 0;
     __syncthreads();
@@ -283,7 +287,10 @@ rx_classify(RxArgs a)
         r.c1 = load16(fr, ab + 16u);
         r.c2 = load16(fr, ab + 32u);
         r.c3 = load16(fr, ab + 48u);
-        r.c4 = __builtin_amdgcn_raw_buffer_load_b32(fr, (int)(ab + 64u), 0, 0);
+        // the 5th dword only when the chunks end before frame byte 64 (start misalignment > 12);
+        // other lanes read at the buffer's end, out of range: zero, no memory access
+        const uint32_t o4 = ok && ((o + 12u) & 15u) > 12u ? ab + 64u : a.rsrc_bytes;
+        r.c4 = __builtin_amdgcn_raw_buffer_load_b32(fr, (int)o4, 0, 0);
         return r;
     };
 
@@ -329,7 +336,11 @@ rx_classify(RxArgs a)
         const uint32_t dport = g[6] & 0xFFFFu;                   // poller.c:372
         // The demux load goes out first and is waited for only where it is used.
         STAMP(1);
+#ifdef UDPDK_EXP_NO_DEMUX_LOAD      // diagnostic experiment only: constant port entry
+        v4u32 ev = {1u, 0u, 0u, dport};
+#else
         v4u32 ev = asm_load16(a.port_tab + dport);
+#endif
 
         // ---- everything the header window gives (the window registers die here) ----
         const bool ipv4 = good && (pt & 0x10u);                   // udpdk_poller.c:334, :362-366
@@ -422,7 +433,9 @@ rx_classify(RxArgs a)
         uint32_t nn_off, nn_len, nn_pt;
         load_desc(nst + RX_WAVES, nn_off, nn_len, nn_pt);
         // issued after the demux load: 5 window loads + 2 descriptor loads (+1 with ptype)
+#ifndef UDPDK_EXP_NO_DEMUX_LOAD
         wait_vm<7>(ev);
+#endif
         STAMP(3);
         const uint4 e = is_udp ? make_uint4(ev[0], ev[1], ev[2], ev[3]) : make_uint4(0, 0, 0, 0);
 
@@ -475,8 +488,7 @@ rx_classify(RxArgs a)
         STAMP(5);
         const uint32_t l3f = l3 ? ((ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8) : 0u;
         const uint32_t udpf = is_udp ? (state << 5 | (len_bad ? 1u : 0u) << 7) : 0u;
-        if (valid)
-            a.meta[p] = verdict | l3f | udpf | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
+        mstage[st * 64 + lane] = verdict | l3f | udpf | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
         // per-lane packed counters (8-bit fields; a lane sees <= 64 frames per tile)
         const uint32_t vinc = valid ? 1u << (8u * (verdict & 3u)) : 0u;
         acc_v0 += verdict < 4u ? vinc : 0u;
@@ -550,6 +562,17 @@ rx_classify(RxArgs a)
         for (int i = 0; i < RX_WAVES; ++i) v += cntw[i * 16 + c];
         return v;
     };
+    {
+        const uint32_t nv = t1 - t0;
+        uint32_t *dst = a.meta + t0;
+        if (nv == a.tile_frames && ((uintptr_t)dst & 15u) == 0) {
+            uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+            const uint4 *s4 = reinterpret_cast<const uint4 *>(mstage);
+            for (uint32_t i = tid; i < nv / 4; i += RX_BLOCK) d4[i] = s4[i];
+        } else {
+            for (uint32_t i = tid; i < nv; i += RX_BLOCK) dst[i] = mstage[i];
+        }
+    }
 #ifdef UDPDK_STAMPS
     STAMP_END();
     if (a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];

@@ -478,7 +478,7 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
 
     if (ts) for (int k = 0; k < TIMED_KERNELS; ++k) ts->used[k] = false;
     HIPC(c, launch(c, ts, 0, true, true, rx_classify, dim3(tiles), dim3(RX_BLOCK),
-                   classify_lds_bytes(S), ra));
+                   classify_lds_bytes(S, T), ra));
     if (one_lane) {
         Compact1Args ca;
         ca.meta = o->meta_dev;
