@@ -606,31 +606,42 @@ rx_compact1(Compact1Args a)
     const uint32_t t1 = min(a.n, (tile + 1) * a.tile_frames);
     const uint32_t wb = tile * a.tile_frames + w * steps * 64;
     const uint32_t plast = a.n - 1u;
+    // predecessors' counts first (the first two per thread unconditionally, clamped), so they
+    // are in flight together with the verdict words: one memory round trip for both
+    const uint32_t tl = a.n_tiles - 1u;
+    const uint32_t c0 = a.tile_count[min(tid, tl)], c1 = a.tile_count[min(tid + RX_BLOCK, tl)];
     uint32_t wcount = 0;
-    for (uint32_t s0 = 0; s0 < steps; s0 += 8) {
-        uint32_t mv[8];
+    for (uint32_t s0 = 0; s0 < steps; s0 += 4) {
+        uint32_t mv[4];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) mv[u] = a.meta[min(wb + (s0 + u) * 64 + lane, plast)];
+        for (int u = 0; u < 4; ++u) mv[u] = a.meta[min(wb + (s0 + u) * 64 + lane, plast)];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 4; ++u) {
             const uint32_t p = wb + (s0 + u) * 64 + lane;
-            const unsigned long long m = __ballot(s0 + u < steps && p < t1 && (mv[u] & 0xFu) == UDPDK_V_DELIVERED);
-            if (lane == 0 && s0 + u < steps) msk[w][s0 + u] = m;
+            const unsigned long long m = __ballot(p < t1 && (mv[u] & 0xFu) == UDPDK_V_DELIVERED);
+            if (lane == 0) msk[w][s0 + u] = m;
             wcount += (uint32_t)__popcll(m);
         }
     }
-    // predecessors' counts: the first two per thread unconditionally (clamped), so these loads
-    // are in flight together with the verdict words above
-    const uint32_t tl = a.n_tiles - 1u;
-    const uint32_t c0 = a.tile_count[min(tid, tl)], c1 = a.tile_count[min(tid + RX_BLOCK, tl)];
     uint32_t pre = (tid < tile ? c0 : 0u) + (tid + RX_BLOCK < tile ? c1 : 0u);
     for (uint32_t t = tid + 2 * RX_BLOCK; t < tile; t += RX_BLOCK) pre += a.tile_count[t];
     pre = wave_sum(pre);
     if (lane == 0) { red[w] = pre; red[RX_WAVES + w] = wcount; }
     __syncthreads();
-    uint32_t run = 0;
+    uint32_t base = 0, tcount = 0, before = 0;
 #pragma unroll
-    for (int i = 0; i < RX_WAVES; ++i) run += red[i] + ((uint32_t)i < w ? red[RX_WAVES + i] : 0u);
+    for (int i = 0; i < RX_WAVES; ++i) {
+        base += red[i];
+        tcount += red[RX_WAVES + i];
+        before += (uint32_t)i < w ? red[RX_WAVES + i] : 0u;
+    }
+    uint32_t run = base + before;
+    const uint32_t total = base + tcount;
+    if (tile == a.n_tiles - 1u && tid == 0) {
+        a.lane_off[0] = 0u;
+        a.lane_off[1] = total;
+        *a.total = total;
+    }
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (uint32_t s = 0; s < steps; ++s) {
         const unsigned long long m = msk[w][s];
@@ -639,11 +650,6 @@ rx_compact1(Compact1Args a)
             if (pos < a.lane_cap) a.lane_pkt[pos] = wb + s * 64 + lane;
         }
         run += (uint32_t)__popcll(m);
-    }
-    if (tile == a.n_tiles - 1u && tid == RX_BLOCK - 1u) {     // last wave: run = total
-        a.lane_off[0] = 0u;
-        a.lane_off[1] = run;
-        *a.total = run;
     }
 }
 
