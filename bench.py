@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1500 B / IMIX side lines")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU time per baseline leg")
+    p.add_argument("--pipeline", type=int, default=2, choices=(1, 2),
+                   help="udpdk_gpu_pipeline_depth: 2 overlaps consecutive batches on two streams")
     p.add_argument("--timing-every", type=int, default=16,
                    help="per-kernel timing on every Nth call (dispatch-carried events)")
     return p.parse_args()
@@ -145,6 +147,7 @@ def time_loop(rx: Rx, steps: int, warmup: int, barrier, timing_every: int):
     ev.record(0)
     for i in range(steps):
         rx.step(warmup + i)
+    ctx.join()                           # the second pipe's calls before the closing event
     ev.record(1)
     ctx.sync()
     t1 = time.perf_counter()
@@ -181,11 +184,15 @@ def cpu_baseline(w: F.Workload, target_s: float):
 def side_config(ctx, cfg: int, steps: int, rotate: int):
     w = F.config_batch(cfg)
     rx = Rx(ctx, w, rotate)
-    wall, gpu_step, kt, st = time_loop(rx, steps, 5, lambda: None, 4)
-    cls_gbps = rx.classify_bytes() / (kt.get("rx_classify", 1e3 * gpu_step) / 1e6) / 1e9
+    ctx.pipeline(2)
+    wall, gpu_step, _, st = time_loop(rx, steps, 5, lambda: None, 0)
+    ctx.pipeline(1)
+    wall1, gpu_step1, kt, _ = time_loop(rx, steps, 5, lambda: None, 4)
+    cls_gbps = rx.classify_bytes() / (kt.get("rx_classify", 1e3 * gpu_step1) / 1e6) / 1e9
     out = {"workload": w.name, "mpkt_s": round(rx.n * steps / wall / 1e6, 1),
            "gbps_pipeline": round(rx.pipeline_bytes() * steps / wall / 1e9, 1),
            "gpu_us_per_step": round(1e3 * gpu_step, 2),
+           "depth1_mpkt_s": round(rx.n * steps / wall1 / 1e6, 1),
            "kernel_us": {k: round(v, 2) for k, v in kt.items()},
            "classify_gbps": round(cls_gbps, 1),
            "frac_hbm_classify": round(cls_gbps / HBM_PEAK_GBS, 4)}
@@ -298,7 +305,14 @@ def main():
     w = F.config_batch(args.config, n=args.frames, shard=rank)
     ctx = abi.GpuContext(device, max_frames=max(w.batch.n, 1 << 22), max_lanes=4096)
     rx = Rx(ctx, w, args.rotate_mib << 20)
-    wall, gpu_step, kt, st = time_loop(rx, args.steps, args.warmup, barrier, args.timing_every)
+    # the timed region (value): consecutive batches pipelined over two streams, no events inside
+    ctx.pipeline(args.pipeline)
+    wall, gpu_step, _, st = time_loop(rx, args.steps, args.warmup, barrier, 0)
+    # kernel durations for the roofline: the same calls one at a time (depth 1), every
+    # --timing-every-th call carrying dispatch events, so each kernel runs without a neighbour
+    ctx.pipeline(1)
+    k_steps = max(16, args.steps // 2)
+    wall1, gpu_step1, kt, _ = time_loop(rx, k_steps, 5, barrier, args.timing_every)
     if dist is not None:
         t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -307,7 +321,7 @@ def main():
     mpkt_s = total_pkts / wall / 1e6
     ms_step = 1e3 * wall / args.steps
     cls_bytes = rx.classify_bytes()
-    cls_us = kt.get("rx_classify", 1e3 * gpu_step)     # timing off: the whole step, an upper bound
+    cls_us = kt.get("rx_classify", 1e3 * gpu_step1)    # timing off: the whole step, an upper bound
     achieved = cls_bytes / (cls_us / 1e6) / 1e9
 
     traffic = None
@@ -337,6 +351,9 @@ def main():
                    "parallelism": f"shard{world}", "device_copies_rotated": rx.copies},
         "gbps_pipeline": round(rx.pipeline_bytes() * args.steps * world / wall / 1e9, 1),
         "gpu_us_per_step": round(1e3 * gpu_step, 3),
+        "pipeline_depth": args.pipeline,
+        "depth1": {"mpkt_s": round(rx.n * k_steps / wall1 / 1e6, 2), "gpu_us_per_step": round(1e3 * gpu_step1, 3),
+                   "note": "the same calls one at a time on one stream (kernel timing loop)"},
         "kernel_us": {k: round(v, 3) for k, v in kt.items()},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -187,3 +187,33 @@ def test_rx_host_end_to_end(gpu_ctx):
     assert np.array_equal(meta, wm) and np.array_equal(loff, wl)
     assert np.array_equal(pkt[:st.deliveries], wp)
     assert np.array_equal(np.array(st.counters[:], np.uint64), wc)
+
+
+def test_pipeline_depth2(gpu_ctx):
+    """Two pipes: consecutive calls on independent batches overlap; every call's outputs and the
+    last call's counters still equal the oracle's."""
+    ws = [F.config_batch(4, n=30000 + 1000 * i) for i in range(4)]     # same 1024-port lists
+    lists = ws[0].port_lists()
+    gpu_ctx.upload_snapshot(abi.snapshot_from_lists(lists, ws[0].n_sockets))
+    bt = O.bindtable_from_lists(lists)
+    runs = []
+    for w in ws:
+        db = abi.rx_upload(gpu_ctx, w.batch.frames, w.batch.offset, w.batch.length)
+        db.frames_bytes = w.batch.frames_bytes
+        runs.append((w, db, abi.rx_alloc_out(gpu_ctx, w.batch.n, w.n_sockets, w.batch.n)))
+    gpu_ctx.pipeline(2)
+    try:
+        for w, db, out in runs:
+            assert abi.rx_enqueue(gpu_ctx, db, out) == 0
+        rc, st = abi.rx_stats(gpu_ctx)
+        assert rc == 0
+        gpu_ctx.sync()
+        for w, db, out in runs:
+            b = w.batch
+            wm, wl, wp, wc = O.rx(bt, b.frames, b.frames_bytes, b.offset, b.length, None, w.n_sockets)
+            assert np.array_equal(gpu_ctx.download(out.meta, np.uint32, b.n), wm)
+            assert np.array_equal(gpu_ctx.download(out.lane_off, np.uint32, w.n_sockets + 1), wl)
+            assert np.array_equal(gpu_ctx.download(out.lane_pkt, np.uint32, len(wp)), wp)
+        assert np.array_equal(np.array(st.counters[:], np.uint64), wc)   # the last call's
+    finally:
+        gpu_ctx.pipeline(1)

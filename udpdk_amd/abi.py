@@ -113,6 +113,8 @@ _PROTOS = {
     "udpdk_gpu_bind_snapshot_upload": (C.c_int, [_P, C.POINTER(BindSnapshot)]),
     "udpdk_gpu_rx": (C.c_int, [_P, C.POINTER(RxBatch), C.POINTER(RxOut)]),
     "udpdk_gpu_rx_stats": (C.c_int, [_P, C.POINTER(RxStats)]),
+    "udpdk_gpu_pipeline_depth": (C.c_int, [_P, C.c_int]),
+    "udpdk_gpu_join": (C.c_int, [_P]),
     "udpdk_gpu_rx_host": (C.c_int, [_P, _P, C.c_uint64, _P, _P, _P, C.c_uint32, _P, _P, _P,
                                     C.c_uint32, C.POINTER(RxStats)]),
     "udpdk_gpu_tx_build": (C.c_int, [_P, C.POINTER(TxConfig), C.POINTER(TxBatch), C.POINTER(TxOut)]),
@@ -287,6 +289,14 @@ class GpuContext:
 
     def sync(self):
         _check(lib().udpdk_gpu_sync(self.handle), "udpdk_gpu_sync")
+
+    def pipeline(self, depth: int):
+        """1: every udpdk_gpu_rx in order on one stream; 2: consecutive calls alternate between
+        two streams (independent batches with distinct outputs overlap)."""
+        _check(lib().udpdk_gpu_pipeline_depth(self.handle, int(depth)), "udpdk_gpu_pipeline_depth")
+
+    def join(self):
+        _check(lib().udpdk_gpu_join(self.handle), "udpdk_gpu_join")
 
     def upload_snapshot(self, hs: HostSnapshot):
         _check(lib().udpdk_gpu_bind_snapshot_upload(self.handle, C.byref(hs.snap)),

@@ -329,6 +329,26 @@ rx_classify(RxArgs a)
 #pragma unroll
             for (int i = 0; i < 13; ++i) g[i] = __builtin_amdgcn_alignbyte(w2[i + 1], w2[i], s3);
         }
+#ifdef UDPDK_EXP_SKELETON   // diagnostic experiment only: the loads and stores without the work
+        {
+            const uint32_t nst = st + RX_WAVES;
+            const Win NW = load_win(nst, n_off, n_len);
+            uint32_t nn_off, nn_len, nn_pt;
+            load_desc(nst + RX_WAVES, nn_off, nn_len, nn_pt);
+            uint32_t x = 0;
+#pragma unroll
+            for (int i = 0; i < 13; ++i) x ^= g[i];
+            mstage[st * 64 + lane] = x & 0xFFFF0000u;
+            acc_fan += valid ? 1u : 0u;
+            acc_v0 += valid ? 1u : 0u;
+            lane_bytes += good ? len : 0u;
+            W = NW;
+            c_off = n_off; c_len = n_len; c_pt = n_pt;
+            n_off = nn_off; n_len = nn_len; n_pt = nn_pt;
+            st = nst;
+            continue;
+        }
+#endif
         const uint32_t pt = !good ? 0u : a.ptype ? c_pt
                           : (len >= 14 ? (((g[0] & 0xFFFFu) == 0x0008u) ? 0x211u : 0x1u) : 0u);
         const uint32_t frag = ((g[2] & 0xFFu) << 8) | ((g[2] >> 8) & 0xFFu);

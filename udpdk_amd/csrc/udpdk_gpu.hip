@@ -38,11 +38,28 @@ struct TimingSet {
     bool used[TIMED_KERNELS];
 };
 
+// One RX pipe = a stream and the per-call workspace. With pipelining depth 2, consecutive
+// udpdk_gpu_rx calls alternate between two pipes, so one batch's prologue, tail and compaction
+// overlap the next batch's streaming phase (the calls are independent: distinct batches and
+// output buffers).
+struct Pipe {
+    hipStream_t stream = nullptr;
+    uint32_t *hist = nullptr;
+    uint32_t *partial = nullptr;
+    uint32_t *tile_cnt = nullptr;
+    DevResult *res = nullptr;                 // counters, total (device)
+    DevResult *h_res = nullptr;               // pinned mirror, filled by udpdk_gpu_rx_stats
+    hipEvent_t tail = nullptr;                // join point for udpdk_gpu_join
+    uint32_t last_tiles = 0;                  // tiles of this pipe's last call (counter rows)
+    uint32_t last_lane_cap = 0;
+};
+constexpr int MAX_PIPES = 2;
+
 } // namespace
 
 struct udpdk_gpu_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;             // = pipes[0].stream: the context stream
     int last_err = 0;
     uint32_t max_frames = 0, max_lanes = 0;
 
@@ -56,18 +73,14 @@ struct udpdk_gpu_ctx {
     uint32_t one_lane_tile = 0;    // UDPDK_ONE_LANE_TILE (diagnostic): single-lane tile override
     bool have_snapshot = false;
 
-    // RX workspace
-    uint32_t *hist = nullptr;
+    // RX workspace, one set per pipe
+    Pipe pipes[MAX_PIPES];
+    int depth = 1;                            // udpdk_gpu_pipeline_depth
+    uint64_t rx_calls = 0;
+    int last_pipe = -1;                       // pipe of the last udpdk_gpu_rx (-1: none yet)
     size_t hist_cap = 0;
-    uint32_t *partial = nullptr;
     size_t partial_cap = 0;
-    uint32_t *tile_cnt = nullptr;
     size_t tiles_cap = 0;
-    DevResult *res = nullptr;                 // counters, total, err (device)
-    DevResult *h_res = nullptr;               // pinned mirror, filled by udpdk_gpu_rx_stats
-    uint32_t last_tiles = 0;                  // tiles of the last udpdk_gpu_rx (counter rows)
-    uint32_t last_lane_cap = 0;
-    bool pending = false;
 
     // end-to-end staging (lazy)
     uint8_t *st_frames_d = nullptr; size_t st_frames_dcap = 0;
@@ -111,7 +124,7 @@ void geometry(uint32_t n, uint32_t lanes, uint32_t *T, uint32_t *tiles)
 int fold_timing(udpdk_gpu_ctx *c)
 {
     if (!c->n_sets_used) return 0;
-    HIPC(c, hipStreamSynchronize(c->stream));
+    for (Pipe &P : c->pipes) HIPC(c, hipStreamSynchronize(P.stream));
     static const int kid[TIMED_KERNELS] = {UDPDK_K_RX_CLASSIFY, UDPDK_K_RX_SCAN, UDPDK_K_RX_SCATTER};
     for (int i = 0; i < c->n_sets_used; ++i) {
         for (int k = 0; k < TIMED_KERNELS; ++k) {
@@ -129,17 +142,36 @@ int fold_timing(udpdk_gpu_ctx *c)
 // Launch on the context stream; with a timing set, kernel k's dispatch carries the set's start
 // event (first=true) and/or stop event (last=true).
 template <typename K, typename... A>
-hipError_t launch(udpdk_gpu_ctx *c, TimingSet *ts, int k, bool first, bool last, K kern, dim3 grid,
+hipError_t launch(hipStream_t st, TimingSet *ts, int k, bool first, bool last, K kern, dim3 grid,
                   dim3 block, uint32_t lds, A... args)
 {
     if (ts) {
         ts->used[k] = true;
-        hipExtLaunchKernelGGL(kern, grid, block, lds, c->stream, first ? ts->ev[2 * k] : nullptr,
+        hipExtLaunchKernelGGL(kern, grid, block, lds, st, first ? ts->ev[2 * k] : nullptr,
                               last ? ts->ev[2 * k + 1] : nullptr, 0u, args...);
     } else {
-        hipLaunchKernelGGL(kern, grid, block, lds, c->stream, args...);
+        hipLaunchKernelGGL(kern, grid, block, lds, st, args...);
     }
     return hipGetLastError();
+}
+
+// Order everything enqueued on the other pipes before what comes next on the context stream.
+int join_pipes(udpdk_gpu_ctx *c)
+{
+    for (int i = 1; i < MAX_PIPES; ++i) {
+        Pipe &P = c->pipes[i];
+        if (!P.stream) continue;
+        HIPC(c, hipEventRecord(P.tail, P.stream));
+        HIPC(c, hipStreamWaitEvent(c->stream, P.tail, 0));
+    }
+    return 0;
+}
+
+int sync_all(udpdk_gpu_ctx *c)
+{
+    for (Pipe &P : c->pipes)
+        if (P.stream) HIPC(c, hipStreamSynchronize(P.stream));
+    return 0;
 }
 
 int ensure_dev(udpdk_gpu_ctx *c, void **p, size_t *cap, size_t need)
@@ -204,20 +236,29 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
     int rc = -EIO;
     do {
         if (hipSetDevice(device) != hipSuccess) break;
-        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) break;
+        bool ok = true;
+        for (Pipe &P : c->pipes) {
+            ok = ok && hipStreamCreateWithFlags(&P.stream, hipStreamNonBlocking) == hipSuccess;
+            ok = ok && hipEventCreateWithFlags(&P.tail, hipEventDisableTiming) == hipSuccess;
+        }
+        if (!ok) break;
+        c->stream = c->pipes[0].stream;
         if (hipMalloc((void **)&c->port_tab, UDPDK_UDP_PORTS * sizeof(uint4)) != hipSuccess) break;
         if (hipMemset(c->port_tab, 0, UDPDK_UDP_PORTS * sizeof(uint4)) != hipSuccess) break;
         const uint64_t e_cap = std::max<uint64_t>((uint64_t)RX_HIST_CAP + max_lanes,
                                                   (uint64_t)ceil_div(max_frames, RX_TILE_MAX) * max_lanes);
         c->hist_cap = e_cap;
-        if (hipMalloc((void **)&c->hist, e_cap * 4) != hipSuccess) break;
         c->partial_cap = e_cap / SCAN_COL_CHUNK + max_lanes + 1;   // chunks x lanes
-        if (hipMalloc((void **)&c->partial, c->partial_cap * 4) != hipSuccess) break;
         c->tiles_cap = ceil_div(max_frames, RX_TILE_MIN) + 1;
-        if (hipMalloc((void **)&c->tile_cnt, c->tiles_cap * UDPDK_N_COUNTERS * 4) != hipSuccess) break;
-        if (hipMalloc((void **)&c->res, sizeof(DevResult)) != hipSuccess) break;
-        if (hipMemset(c->res, 0, sizeof(DevResult)) != hipSuccess) break;
-        if (hipHostMalloc((void **)&c->h_res, sizeof(DevResult), hipHostMallocDefault) != hipSuccess) break;
+        for (Pipe &P : c->pipes) {
+            ok = ok && hipMalloc((void **)&P.hist, e_cap * 4) == hipSuccess;
+            ok = ok && hipMalloc((void **)&P.partial, c->partial_cap * 4) == hipSuccess;
+            ok = ok && hipMalloc((void **)&P.tile_cnt, c->tiles_cap * UDPDK_N_COUNTERS * 4) == hipSuccess;
+            ok = ok && hipMalloc((void **)&P.res, sizeof(DevResult)) == hipSuccess;
+            ok = ok && hipMemset(P.res, 0, sizeof(DevResult)) == hipSuccess;
+            ok = ok && hipHostMalloc((void **)&P.h_res, sizeof(DevResult), hipHostMallocDefault) == hipSuccess;
+        }
+        if (!ok) break;
         // rx_classify needs up to 90 KiB of dynamic LDS at 16384 lanes
         if (hipFuncSetAttribute((const void *)rx_classify, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) break;
@@ -245,18 +286,25 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
 {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *dev[] = {c->port_tab, c->binds, c->slots, c->hist, c->partial, c->tile_cnt,
-                   c->res, c->st_frames_d, c->st_desc_d, c->st_out_d};
+    for (Pipe &P : c->pipes)
+        if (P.stream) (void)hipStreamSynchronize(P.stream);
+    void *dev[] = {c->port_tab, c->binds, c->slots, c->st_frames_d, c->st_desc_d, c->st_out_d};
     for (void *p : dev) if (p) (void)hipFree(p);
-    void *host[] = {c->h_res, c->st_frames_h, c->st_desc_h};
+    void *host[] = {c->st_frames_h, c->st_desc_h};
     for (void *p : host) if (p) (void)hipHostFree(p);
+    for (Pipe &P : c->pipes) {
+        void *pd[] = {P.hist, P.partial, P.tile_cnt, P.res};
+        for (void *p : pd) if (p) (void)hipFree(p);
+        if (P.h_res) (void)hipHostFree(P.h_res);
+        if (P.tail) (void)hipEventDestroy(P.tail);
+    }
     if (c->sets) {
         for (int i = 0; i < EVENT_SETS; ++i)
             for (int k = 0; k < 2 * TIMED_KERNELS; ++k) (void)hipEventDestroy(c->sets[i].ev[k]);
         delete[] c->sets;
     }
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    for (Pipe &P : c->pipes)
+        if (P.stream) (void)hipStreamDestroy(P.stream);
     delete c;
     return 0;
 }
@@ -264,7 +312,22 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
 int udpdk_gpu_sync(udpdk_gpu_ctx *c)
 {
     if (!c) return -EINVAL;
-    HIPC(c, hipStreamSynchronize(c->stream));
+    return sync_all(c);
+}
+
+int udpdk_gpu_join(udpdk_gpu_ctx *c)
+{
+    if (!c) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    return join_pipes(c);
+}
+
+int udpdk_gpu_pipeline_depth(udpdk_gpu_ctx *c, int depth)
+{
+    if (!c || depth < 1 || depth > MAX_PIPES) return -EINVAL;
+    int rc = sync_all(c);
+    if (rc) return rc;
+    c->depth = depth;
     return 0;
 }
 
@@ -310,6 +373,7 @@ int udpdk_gpu_host_free(udpdk_gpu_ctx *c, void *host)
 int udpdk_gpu_memset(udpdk_gpu_ctx *c, void *dev, int value, size_t bytes)
 {
     if (!c || (!dev && bytes)) return -EINVAL;
+    if (c->depth > 1) { int rc = join_pipes(c); if (rc) return rc; }
     if (bytes) HIPC(c, hipMemsetAsync(dev, value, bytes, c->stream));
     return 0;
 }
@@ -317,6 +381,7 @@ int udpdk_gpu_memset(udpdk_gpu_ctx *c, void *dev, int value, size_t bytes)
 int udpdk_gpu_h2d(udpdk_gpu_ctx *c, void *dev, const void *host, size_t bytes)
 {
     if (!c || ((!dev || !host) && bytes)) return -EINVAL;
+    if (c->depth > 1) { int rc = join_pipes(c); if (rc) return rc; }
     if (bytes) HIPC(c, hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, c->stream));
     return 0;
 }
@@ -324,6 +389,7 @@ int udpdk_gpu_h2d(udpdk_gpu_ctx *c, void *dev, const void *host, size_t bytes)
 int udpdk_gpu_d2h(udpdk_gpu_ctx *c, void *host, const void *dev, size_t bytes)
 {
     if (!c || ((!dev || !host) && bytes)) return -EINVAL;
+    if (c->depth > 1) { int rc = join_pipes(c); if (rc) return rc; }
     if (bytes) HIPC(c, hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, c->stream));
     return 0;
 }
@@ -352,7 +418,7 @@ int udpdk_gpu_bind_snapshot_upload(udpdk_gpu_ctx *c, const udpdk_bind_snapshot_t
         b[i] = make_uint2(x.ip, (uint32_t)x.sockfd | (x.reuse ? 0x80000000u : 0u));
     }
     HIPC(c, hipSetDevice(c->device));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    { int rc = sync_all(c); if (rc) return rc; }
     if (s->n_binds > c->binds_cap) {
         if (c->binds) HIPC(c, hipFree(c->binds));
         c->binds = nullptr;
@@ -419,7 +485,9 @@ int udpdk_gpu_timing_read(udpdk_gpu_ctx *c, double ms[UDPDK_N_KERNEL_IDS],
     return 0;
 }
 
-int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_out_t *o)
+namespace {
+
+int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udpdk_rx_out_t *o)
 {
     if (!c || !bt || !o || !c->have_snapshot) return -EINVAL;
     if (bt->n > c->max_frames || bt->frames_bytes >= (1ull << 32)) return -EINVAL;
@@ -428,18 +496,20 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     if (!o->meta_dev && bt->n) return -EINVAL;
     if (!o->lane_off_dev || (!o->lane_pkt_dev && o->lane_cap)) return -EINVAL;
     HIPC(c, hipSetDevice(c->device));
+    Pipe &P = c->pipes[pipe];
+    const hipStream_t st = P.stream;
+    c->last_pipe = pipe;
     const uint32_t S = c->n_lanes;
     TimingSet *ts = nullptr;
     if (c->timing_every && (c->timing_calls++ % c->timing_every) == 0) {
         if (c->n_sets_used == EVENT_SETS) { int rc = fold_timing(c); if (rc) return rc; }
         ts = &c->sets[c->n_sets_used++];
     }
-    c->last_lane_cap = o->lane_cap;
-    c->pending = true;
+    P.last_lane_cap = o->lane_cap;
     if (bt->n == 0) {
-        HIPC(c, hipMemsetAsync(o->lane_off_dev, 0, (size_t)(S + 1) * 4, c->stream));
-        HIPC(c, hipMemsetAsync(c->res, 0, sizeof(DevResult), c->stream));
-        c->last_tiles = 0;
+        HIPC(c, hipMemsetAsync(o->lane_off_dev, 0, (size_t)(S + 1) * 4, st));
+        HIPC(c, hipMemsetAsync(P.res, 0, sizeof(DevResult), st));
+        P.last_tiles = 0;
         if (ts) c->n_sets_used--;                         // nothing was launched
         return 0;
     }
@@ -453,7 +523,7 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     if (E > c->hist_cap || tiles > c->tiles_cap) return -EINVAL;
     // single lane, no fan-out: classify + rx_compact1; otherwise classify + scan + scatter
     const bool one_lane = S == 1 && c->max_fanout <= 1;
-    c->last_tiles = tiles;
+    P.last_tiles = tiles;
 
     RxArgs ra;
     memset(&ra, 0, sizeof(ra));
@@ -464,8 +534,8 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     ra.port_tab = c->port_tab;
     ra.binds = c->binds;
     ra.meta = o->meta_dev;
-    ra.hist = c->hist;
-    ra.tile_cnt = c->tile_cnt;
+    ra.hist = P.hist;
+    ra.tile_cnt = P.tile_cnt;
     ra.dbg = c->dbg;
     ra.key_bits = c->key_bits;
     ra.frames_bytes = (uint32_t)bt->frames_bytes;
@@ -477,45 +547,45 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     ra.n_lanes = S;
 
     if (ts) for (int k = 0; k < TIMED_KERNELS; ++k) ts->used[k] = false;
-    HIPC(c, launch(c, ts, 0, true, true, rx_classify, dim3(tiles), dim3(RX_BLOCK),
+    HIPC(c, launch(st, ts, 0, true, true, rx_classify, dim3(tiles), dim3(RX_BLOCK),
                    classify_lds_bytes(S, T), ra));
     if (one_lane) {
         Compact1Args ca;
         ca.meta = o->meta_dev;
-        ca.tile_count = c->hist;
+        ca.tile_count = P.hist;
         ca.lane_pkt = o->lane_pkt_dev;
         ca.lane_off = o->lane_off_dev;
-        ca.total = &c->res->total;
+        ca.total = &P.res->total;
         ca.n = bt->n;
         ca.tile_frames = T;
         ca.n_tiles = tiles;
         ca.lane_cap = o->lane_cap;
-        HIPC(c, launch(c, ts, 2, true, true, rx_compact1, dim3(tiles), dim3(RX_BLOCK), 0u, ca));
+        HIPC(c, launch(st, ts, 2, true, true, rx_compact1, dim3(tiles), dim3(RX_BLOCK), 0u, ca));
         return 0;
     }
 
     ScanArgs sa;
-    sa.hist = c->hist;
-    sa.partial = c->partial;
+    sa.hist = P.hist;
+    sa.partial = P.partial;
     sa.lane_off = o->lane_off_dev;
-    sa.total = &c->res->total;
+    sa.total = &P.res->total;
     sa.n_elems = (uint32_t)E;
     sa.n_tiles = tiles;
     sa.n_lanes = S;
     if (E <= SCAN_SMALL_MAX && tiles <= SCAN_SMALL_TILES) {
-        HIPC(c, launch(c, ts, 1, true, true, rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 4u * S, sa));
+        HIPC(c, launch(st, ts, 1, true, true, rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 4u * S, sa));
     } else {
         const uint32_t nc = ceil_div(tiles, SCAN_COL_CHUNK);
         if ((uint64_t)nc * S > c->partial_cap) return -EINVAL;
         const dim3 grid(nc, ceil_div(S, (uint32_t)SCAN_BLOCK));
-        HIPC(c, launch(c, ts, 1, true, false, rx_scan_reduce, grid, dim3(SCAN_BLOCK), 0u, sa));
-        HIPC(c, launch(c, ts, 1, false, false, rx_scan_top, dim3(1), dim3(SCAN_TOP_BLOCK), 4u * S, sa, nc));
-        HIPC(c, launch(c, ts, 1, false, true, rx_scan_down, grid, dim3(SCAN_BLOCK), 0u, sa));
+        HIPC(c, launch(st, ts, 1, true, false, rx_scan_reduce, grid, dim3(SCAN_BLOCK), 0u, sa));
+        HIPC(c, launch(st, ts, 1, false, false, rx_scan_top, dim3(1), dim3(SCAN_TOP_BLOCK), 4u * S, sa, nc));
+        HIPC(c, launch(st, ts, 1, false, true, rx_scan_down, grid, dim3(SCAN_BLOCK), 0u, sa));
     }
 
     ScatterArgs xa;
     xa.meta = o->meta_dev;
-    xa.base = c->hist;
+    xa.base = P.hist;
     xa.frames = bt->frames_dev;
     xa.offset = bt->offset_dev;
     xa.port_tab = c->port_tab;
@@ -529,27 +599,39 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     xa.key_bits = c->key_bits;
     xa.lane_cap = o->lane_cap;
     if (c->max_fanout <= 1 && S <= SCATTER4_MAX_LANES)
-        HIPC(c, launch(c, ts, 2, true, true, rx_scatter4, dim3(tiles), dim3(256), 20u * S, xa));
+        HIPC(c, launch(st, ts, 2, true, true, rx_scatter4, dim3(tiles), dim3(256), 20u * S, xa));
     else
-        HIPC(c, launch(c, ts, 2, true, true, rx_scatter, dim3(tiles), dim3(64), 4u * S, xa));
+        HIPC(c, launch(st, ts, 2, true, true, rx_scatter, dim3(tiles), dim3(64), 4u * S, xa));
     return 0;
+}
+
+} // namespace
+
+int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_out_t *o)
+{
+    if (!c) return -EINVAL;
+    const int pipe = c->depth > 1 ? (int)(c->rx_calls % (uint64_t)c->depth) : 0;
+    const int rc = rx_on_pipe(c, pipe, bt, o);
+    if (rc == 0) ++c->rx_calls;
+    return rc;
 }
 
 int udpdk_gpu_rx_stats(udpdk_gpu_ctx *c, udpdk_rx_stats_t *st)
 {
     if (!c || !st) return -EINVAL;
-    if (!c->pending) return -EINVAL;
+    if (c->last_pipe < 0) return -EINVAL;
     HIPC(c, hipSetDevice(c->device));
-    if (c->last_tiles) {
-        hipLaunchKernelGGL(rx_counters, dim3(1), dim3(256), 0, c->stream, (const uint32_t *)c->tile_cnt,
-                           c->last_tiles, c->res->counters);
+    Pipe &P = c->pipes[c->last_pipe];
+    if (P.last_tiles) {
+        hipLaunchKernelGGL(rx_counters, dim3(1), dim3(256), 0, P.stream, (const uint32_t *)P.tile_cnt,
+                           P.last_tiles, P.res->counters);
         HIPC(c, hipGetLastError());
     }
-    HIPC(c, hipMemcpyAsync(c->h_res, c->res, sizeof(DevResult), hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
-    for (int k = 0; k < UDPDK_N_COUNTERS; ++k) st->counters[k] = c->h_res->counters[k];
-    st->deliveries = c->h_res->total;
-    st->overflow = st->deliveries > c->last_lane_cap ? 1u : 0u;
+    HIPC(c, hipMemcpyAsync(P.h_res, P.res, sizeof(DevResult), hipMemcpyDeviceToHost, P.stream));
+    HIPC(c, hipStreamSynchronize(P.stream));
+    for (int k = 0; k < UDPDK_N_COUNTERS; ++k) st->counters[k] = P.h_res->counters[k];
+    st->deliveries = P.h_res->total;
+    st->overflow = st->deliveries > P.last_lane_cap ? 1u : 0u;
     return st->overflow ? -ENOSPC : 0;
 }
 
@@ -563,6 +645,7 @@ int udpdk_gpu_rx_host(udpdk_gpu_ctx *c, const uint8_t *frames_host, uint64_t fra
     if (n && (!frames_host || !offset_host || !length_host || !meta_host)) return -EINVAL;
     if (lane_cap && !lane_pkt_host) return -EINVAL;
     HIPC(c, hipSetDevice(c->device));
+    if (c->depth > 1) { int r = join_pipes(c); if (r) return r; }
     const size_t fb = ((size_t)frames_bytes + 255) & ~(size_t)255;
     const size_t desc = (size_t)n * 10 + 64;
     const size_t outb = (size_t)n * 4 + (size_t)(c->n_lanes + 1) * 4 + (size_t)lane_cap * 4 + 64;
@@ -600,7 +683,7 @@ int udpdk_gpu_rx_host(udpdk_gpu_ctx *c, const uint8_t *frames_host, uint64_t fra
                           (const uint16_t *)(c->st_desc_d + (size_t)n * 4),
                           ptype_host ? (const uint32_t *)(c->st_desc_d + pt_off) : nullptr, n};
     udpdk_rx_out_t o = {meta_d, off_d, pkt_d, lane_cap};
-    if ((rc = udpdk_gpu_rx(c, &b, &o))) return rc;
+    if ((rc = rx_on_pipe(c, 0, &b, &o))) return rc;
     if (n) HIPC(c, hipMemcpyAsync(meta_host, meta_d, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(lane_off_host, off_d, (size_t)(c->n_lanes + 1) * 4, hipMemcpyDeviceToHost, c->stream));
     rc = udpdk_gpu_rx_stats(c, stats);
@@ -621,6 +704,7 @@ int udpdk_gpu_tx_build(udpdk_gpu_ctx *c, const udpdk_tx_config_t *cfg, const udp
     if (bt->payload_bytes >= (1ull << 32) || o->frames_bytes >= (1ull << 32)) return -EINVAL;
     if (((uintptr_t)o->frames_dev & 15u) || ((uintptr_t)bt->payload_dev & 15u)) return -EINVAL;
     HIPC(c, hipSetDevice(c->device));
+    if (c->depth > 1) { int r = join_pipes(c); if (r) return r; }
     TxArgs ta;
     ta.payload = bt->payload_dev;
     ta.payload_off = bt->payload_off_dev;
