@@ -226,7 +226,9 @@ __device__ __forceinline__ void wait_vm(v4u32 &r)
     asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r) : "n"(N) : "memory");
 }
 
-__global__ void __launch_bounds__(RX_BLOCK)
+// 5 waves per SIMD (<= 96 VGPRs, no spill): a fifth workgroup per CU lets the next pipelined
+// launch start while this one drains
+__global__ void __launch_bounds__(RX_BLOCK, 5)
 rx_classify(RxArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
