@@ -125,8 +125,13 @@ __global__ void rx_scan_reduce(ScanArgs a);
 __global__ void rx_scan_top(ScanArgs a, uint32_t n_part);
 __global__ void rx_scan_down(ScanArgs a);
 __global__ void rx_scatter(ScatterArgs a);
-__global__ void rx_scatter4(ScatterArgs a);
-constexpr uint32_t SCATTER4_MAX_LANES = 4096;   // rx_scatter4 LDS: 5 x lanes words
+__global__ void rx_scatterw(ScatterArgs a);
+constexpr uint32_t SCATTER_WAVES = 8;           // rx_scatterw workgroup: 8 waves per tile
+constexpr uint32_t SCATTERW_MAX_LANES = 4096;   // rx_scatterw LDS: (4 + 2 x 8) x lanes bytes
+__host__ __device__ constexpr uint32_t scatterw_lds_bytes(uint32_t n_lanes)
+{
+    return 4u * n_lanes + 2u * SCATTER_WAVES * n_lanes;
+}
 __global__ void rx_compact1(Compact1Args a);
 __global__ void rx_counters(const uint32_t *tile_cnt, uint32_t n_tiles, unsigned long long *counters);
 __global__ void tx_build(TxArgs a);

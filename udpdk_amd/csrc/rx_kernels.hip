@@ -761,9 +761,13 @@ rx_scan_reduce(ScanArgs a)
     const uint32_t S = a.n_lanes, l = blockIdx.y * SCAN_BLOCK + threadIdx.x;
     if (l >= S) return;
     const uint32_t t0 = blockIdx.x * SCAN_COL_CHUNK, t1 = min(a.n_tiles, t0 + SCAN_COL_CHUNK);
+    uint32_t v[SCAN_COL_CHUNK];                            // all loads in flight at once
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_COL_CHUNK; ++k)
+        v[k] = t0 + k < t1 ? a.hist[(size_t)(t0 + k) * S + l] : 0u;
     uint32_t s = 0;
-#pragma unroll 8
-    for (uint32_t t = t0; t < t1; ++t) s += a.hist[(size_t)t * S + l];
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_COL_CHUNK; ++k) s += v[k];
     a.partial[(size_t)blockIdx.x * S + l] = s;
 }
 
@@ -777,11 +781,16 @@ rx_scan_top(ScanArgs a, uint32_t n_chunks)
     const uint32_t S = a.n_lanes;
     for (uint32_t l = threadIdx.x; l < S; l += SCAN_TOP_BLOCK) {
         uint32_t run = 0;
-#pragma unroll 8
-        for (uint32_t c = 0; c < n_chunks; ++c) {
-            const uint32_t v = a.partial[(size_t)c * S + l];
-            a.partial[(size_t)c * S + l] = run;
-            run += v;
+        for (uint32_t c0 = 0; c0 < n_chunks; c0 += 32) {   // 32 loads in flight per batch
+            uint32_t v[32];
+#pragma unroll
+            for (uint32_t k = 0; k < 32; ++k)
+                v[k] = c0 + k < n_chunks ? a.partial[(size_t)(c0 + k) * S + l] : 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < 32; ++k) {
+                if (c0 + k < n_chunks) a.partial[(size_t)(c0 + k) * S + l] = run;
+                run += v[k];
+            }
         }
         tot[l] = run;
     }
@@ -809,32 +818,35 @@ rx_scan_down(ScanArgs a)
 }
 
 // ------------------------------------------------------------------------------------------
-// rx_scatter4: stable per-lane compaction without fan-out, four waves per tile. Wave w owns the
-// w-th quarter of the tile. Pass 1 counts each wave's deliveries per lane key (wave multi-split:
-// one LDS update per distinct key per 64 frames); the wave bases of every key are the tile cursor
-// plus the counts of the earlier quarters; pass 2 re-reads the verdict words and writes each
-// delivery at base + rank. LDS: (1 + 4) x n_lanes words.
+// rx_scatterw: stable per-lane compaction without fan-out, SCATTER_WAVES waves per tile. Wave w
+// owns the w-th slice of the tile. Pass 1 counts each wave's deliveries per lane key (wave
+// multi-split: one LDS update per distinct key per 64 frames); each key's wave offsets become
+// the exclusive prefix over the earlier slices (16-bit: a tile has <= 16384 frames); pass 2
+// re-reads the verdict words and writes each delivery at cursor + wave offset + rank.
+// LDS: 4 x n_lanes (cursors) + 2 x SCATTER_WAVES x n_lanes bytes.
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256)
-rx_scatter4(ScatterArgs a)
+__global__ void __launch_bounds__(64 * SCATTER_WAVES)
+rx_scatterw(ScatterArgs a)
 {
-    extern __shared__ __attribute__((aligned(16))) uint32_t sm4[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t smw[];
     const uint32_t S = a.n_lanes;
-    uint32_t *cur = sm4;                                   // [S] tile cursor per lane
-    uint32_t *wc = sm4 + S;                                // [4][S] per-wave count, then base
+    uint32_t *cur = smw;                                               // [S]
+    uint16_t *woff = reinterpret_cast<uint16_t *>(smw + S);            // [W][S]
+    constexpr uint32_t W = SCATTER_WAVES;
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t tile = blockIdx.x;
-    for (uint32_t k = tid; k < S; k += 256) {
+    for (uint32_t k = tid; k < S; k += 64 * W) {
         cur[k] = a.base[(size_t)tile * S + k];
-        wc[k] = 0u; wc[S + k] = 0u; wc[2 * S + k] = 0u; wc[3 * S + k] = 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < W; ++i) woff[i * S + k] = 0;
     }
     __syncthreads();
     const uint32_t t1 = min(a.n, (tile + 1) * a.tile_frames);
-    const uint32_t q = a.tile_frames / 4;
+    const uint32_t q = a.tile_frames / W;
     const uint32_t wb = tile * a.tile_frames + w * q, we = min(t1, wb + q);
     const uint32_t plast = a.n - 1u;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    uint32_t *mine = wc + w * S;
+    uint16_t *mine = woff + w * S;
     constexpr int PF = 4;
     for (int pass = 0; pass < 2; ++pass) {
         for (uint32_t g0 = wb; g0 < we; g0 += 64 * PF) {
@@ -856,12 +868,13 @@ rx_scatter4(ScatterArgs a)
                 const uint32_t leader = deliver ? (uint32_t)__ffsll((long long)peers) - 1u : 64u;
                 const uint32_t cnt = (uint32_t)__popcll(peers);
                 if (pass == 0) {
-                    if (deliver && lane == leader) mine[key] += cnt;
+                    if (deliver && lane == leader) mine[key] = (uint16_t)(mine[key] + cnt);
                 } else {
                     uint32_t c = 0;
                     if (deliver && lane == leader) {
-                        c = mine[key];
-                        mine[key] = c + cnt;
+                        const uint32_t o = mine[key];
+                        mine[key] = (uint16_t)(o + cnt);
+                        c = cur[key] + o;
                     }
                     c = __shfl(c, deliver ? (int)leader : 0, 64);
                     const uint32_t pos = c + (uint32_t)__popcll(peers & lt_mask);
@@ -871,12 +884,12 @@ rx_scatter4(ScatterArgs a)
         }
         if (pass == 0) {
             __syncthreads();
-            for (uint32_t k = tid; k < S; k += 256) {      // wave bases: cursor + earlier quarters
-                uint32_t c = cur[k];
+            for (uint32_t k = tid; k < S; k += 64 * W) {   // slice offsets: earlier slices' counts
+                uint32_t c = 0;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint32_t v = wc[i * S + k];
-                    wc[i * S + k] = c;
+                for (uint32_t i = 0; i < W; ++i) {
+                    const uint32_t v = woff[i * S + k];
+                    woff[i * S + k] = (uint16_t)c;
                     c += v;
                 }
             }

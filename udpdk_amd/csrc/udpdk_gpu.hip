@@ -264,8 +264,8 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
                                 160 * 1024) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) break;
-        if (hipFuncSetAttribute((const void *)rx_scatter4, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                20 * SCATTER4_MAX_LANES) != hipSuccess) break;
+        if (hipFuncSetAttribute((const void *)rx_scatterw, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                scatterw_lds_bytes(SCATTERW_MAX_LANES)) != hipSuccess) break;
         // lane totals: 4 B per lane, up to UDPDK_GPU_MAX_LANES (64 KiB) beside a few static words
         if (hipFuncSetAttribute((const void *)rx_scan_small, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 4 * UDPDK_GPU_MAX_LANES) != hipSuccess) break;
@@ -598,8 +598,9 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     xa.lane_mask = c->lane_mask;
     xa.key_bits = c->key_bits;
     xa.lane_cap = o->lane_cap;
-    if (c->max_fanout <= 1 && S <= SCATTER4_MAX_LANES)
-        HIPC(c, launch(st, ts, 2, true, true, rx_scatter4, dim3(tiles), dim3(256), 20u * S, xa));
+    if (c->max_fanout <= 1 && S <= SCATTERW_MAX_LANES)
+        HIPC(c, launch(st, ts, 2, true, true, rx_scatterw, dim3(tiles), dim3(64 * SCATTER_WAVES),
+                       scatterw_lds_bytes(S), xa));
     else
         HIPC(c, launch(st, ts, 2, true, true, rx_scatter, dim3(tiles), dim3(64), 4u * S, xa));
     return 0;
