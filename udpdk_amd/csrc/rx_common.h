@@ -12,6 +12,11 @@ constexpr int RX_UNROLL = 4;                // 16-byte chunk loads in flight per
 constexpr uint32_t RX_TILE_MIN = 1024;      // frames per tile (histogram granularity)
 constexpr uint32_t RX_TILE_MAX = 16384;
 constexpr uint32_t RX_HIST_CAP = 1u << 21;  // target bound on lanes x tiles
+#ifndef UDPDK_CLS_BLOCK
+#define UDPDK_CLS_BLOCK 256
+#endif
+constexpr int CLS_BLOCK = UDPDK_CLS_BLOCK;  // rx_classify workgroup
+constexpr int CLS_WAVES = CLS_BLOCK / 64;
 
 constexpr int SCAN_BLOCK = 256;
 constexpr int SCAN_TOP_BLOCK = 1024;
@@ -23,16 +28,24 @@ constexpr int TX_BLOCK = 256;
 
 // rx_classify LDS carve (one dynamic array, 16-byte aligned offsets: cdna_hip_programming.md
 // Guideline 17): per wave three 64-entry chunk-map arrays for the tail sweep; per-wave counter
-// rows; the tile's per-lane delivery histogram.
+// rows; the descriptors of one or two rounds of RX_ROUND frames (offset, length | ptype bit);
+// the tile's per-lane delivery histogram; the tile's verdict words.
 constexpr int WAVE_ARRAYS = 3;                    // chunk start, offset, length
-constexpr int ARR_BYTES   = RX_WAVES * WAVE_ARRAYS * 64 * 4;
-constexpr int CNT_OFF     = ARR_BYTES;            // [RX_WAVES][16] per-wave counter rows
-constexpr int HIST_OFF    = CNT_OFF + RX_WAVES * 16 * 4;   // [n_lanes], then the tile's
-                                                         // verdict words [tile_frames]
+constexpr int ARR_BYTES   = CLS_WAVES * WAVE_ARRAYS * 64 * 4;
+constexpr int CNT_OFF     = ARR_BYTES;            // [CLS_WAVES][16] per-wave counter rows
+constexpr int DSC_OFF     = CNT_OFF + CLS_WAVES * 16 * 4;
+constexpr uint32_t RX_ROUND = 1024;               // frames per descriptor-staging round
+
+// descriptor buffers: one round for a single-round tile, two (double-buffered) otherwise
+__host__ __device__ constexpr uint32_t classify_dsc_bufs(uint32_t tile_frames)
+{
+    return tile_frames > RX_ROUND ? 2u : 1u;
+}
 
 __host__ __device__ constexpr uint32_t classify_lds_bytes(uint32_t n_lanes, uint32_t tile_frames)
 {
-    return (uint32_t)HIST_OFF + 4u * ((n_lanes + 3u) & ~3u) + 4u * tile_frames;
+    return (uint32_t)DSC_OFF + 8u * RX_ROUND * classify_dsc_bufs(tile_frames) +
+           4u * ((n_lanes + 3u) & ~3u) + 4u * tile_frames;
 }
 
 // Port table entry (16 B per raw port): x = bindings on the port, y = index of the first in the

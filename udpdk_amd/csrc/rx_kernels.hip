@@ -94,15 +94,6 @@ __device__ __forceinline__ uint32_t chunk_sum(const uint4 d, int a, int e)
            sum16(d.z & dword_window(a, e, 2)) + sum16(d.w & dword_window(a, e, 3));
 }
 
-// XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
-// consecutive tiles land on one XCD so their lane-major histogram stores share L2 lines.
-__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb)
-{
-    if (nb < 16) return b;
-    const uint32_t q = nb / 8, r = nb % 8, x = b % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes)
 {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes,
@@ -117,7 +108,8 @@ __device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
 
 // Diagnostic build (-DUDPDK_STAMPS): wave 0 of every workgroup accumulates s_memtime cycles per
 // phase into a.dbg[block][16]. Stamps never feed an output (cdna_hip_programming.md §7).
-#ifdef UDPDK_STAMPS
+// -DUDPDK_STAMPS_LIGHT keeps only the entry/exit realtime stamps (dispatch timeline).
+#if defined(UDPDK_STAMPS) && !defined(UDPDK_STAMPS_LIGHT)
 #define STAMP(k)                                                                 \
     do {                                                                         \
         if (w == 0) {                                                            \
@@ -127,6 +119,10 @@ __device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
         }                                                                        \
     } while (0)
 // slots 12-15: realtime (100 MHz, chip-synchronous) at entry and exit, HW_ID | XCC_ID << 32, tile
+#else
+#define STAMP(k) do {} while (0)
+#endif
+#ifdef UDPDK_STAMPS
 #define STAMP_END()                                                                   \
     do {                                                                              \
         st_acc[13] = __builtin_amdgcn_s_memrealtime();                                \
@@ -134,8 +130,6 @@ __device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
                      ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32); \
         st_acc[15] = tile;                                                            \
     } while (0)
-#else
-#define STAMP(k) do {} while (0)
 #endif
 
 
@@ -228,12 +222,14 @@ __device__ __forceinline__ void wait_vm(v4u32 &r)
 
 // 5 waves per SIMD (<= 96 VGPRs, no spill): a fifth workgroup per CU lets the next pipelined
 // launch start while this one drains
-__global__ void __launch_bounds__(RX_BLOCK, 5)
+__global__ void __launch_bounds__(CLS_BLOCK) __attribute__((amdgpu_waves_per_eu(5, 8)))
 rx_classify(RxArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t steps = a.tile_frames / 64;
+    constexpr uint32_t SPR = (RX_ROUND / 64) / CLS_WAVES;   // steps per wave per staging round
+    static_assert(SPR >= 2, "round staging needs two steps per wave per round");
 #ifdef UDPDK_STAMPS
     unsigned long long st_acc[16] = {0}, st_last = __builtin_amdgcn_s_memtime();
     st_acc[12] = __builtin_amdgcn_s_memrealtime();
@@ -242,15 +238,25 @@ rx_classify(RxArgs a)
     uint32_t *arr = reinterpret_cast<uint32_t *>(smem) + w * WAVE_ARRAYS * 64;
     uint32_t *l_cs = arr, *l_off = arr + 64, *l_len = arr + 128;
     uint32_t *cntw = reinterpret_cast<uint32_t *>(smem + CNT_OFF);    // [wave][counter]
-    uint32_t *hist = reinterpret_cast<uint32_t *>(smem + HIST_OFF);   // [n_lanes] this tile
+    // descriptors of the current (and, double-buffered, the next) round of RX_ROUND frames:
+    // staged with coalesced loads by the whole workgroup, so the per-step reads are LDS reads
+    // (lgkmcnt) and never make a step wait on vector-memory loads it issued for a later step
+    const uint32_t nbuf = classify_dsc_bufs(a.tile_frames);
+    uint32_t *d_off = reinterpret_cast<uint32_t *>(smem + DSC_OFF);  // [nbuf][RX_ROUND]
+    uint32_t *d_lp = d_off + nbuf * RX_ROUND;                        // length | ptype-IPv4 << 16
+    uint32_t *hist = d_lp + nbuf * RX_ROUND;                         // [n_lanes] this tile
     // The tile's verdict words are staged in LDS and stored once per tile (16 B per lane): no
     // global store inside the step loop, so no s_waitcnt there ever waits for a store (on gfx9
     // stores count in vmcnt, in order with the loads).
     uint32_t *mstage = hist + ((a.n_lanes + 3u) & ~3u);              // [tile_frames]
 
-    for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK) hist[s] = 0;
-    __syncthreads();
-    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+    // (hist is only used with several lanes; its zeroing is ordered by the staging barrier)
+    if (a.n_lanes > 1u)
+        for (uint32_t s = tid; s < a.n_lanes; s += CLS_BLOCK) hist[s] = 0;
+    // Tiles in dispatch order (consecutive tiles on different XCDs). An XCD-contiguous remap
+    // (each XCD's L2 streaming one contiguous eighth of the batch) measured 1.7 us slower per
+    // 1 M x 64 B launch (tools/probe/stream_probe.hip, feat4).
+    const uint32_t tile = blockIdx.x;
 
     const __amdgpu_buffer_rsrc_t fr = make_rsrc(a.frames, a.rsrc_bytes);
     const uint32_t t0 = tile * a.tile_frames;
@@ -264,16 +270,30 @@ rx_classify(RxArgs a)
     // lane condition makes the compiler wait for it at the end of the branch, which would drain
     // the prefetch pipeline every step.
     const uint32_t plast = a.n - 1u;
-    auto load_desc = [&](uint32_t s, uint32_t &o, uint32_t &l, uint32_t &t) {
-        const uint32_t p = t0 + s * 64 + lane;
-        const bool v = s < steps && p < t1;
-        const uint32_t pc = min(p, plast);
-        const uint32_t o_ = a.offset[pc];
-        const uint32_t l_ = a.length[pc];
-        const uint32_t t_ = a.ptype ? a.ptype[pc] : 0u;
-        o = v ? o_ : 0u;
-        l = v ? l_ : 0u;
-        t = v ? t_ : 0u;
+    // round r's descriptors (frames t0 + RX_ROUND r + [0, RX_ROUND)) into buffer r & 1; the
+    // ptype array, when given, only contributes its L3_IPV4 bit (udpdk_poller.c:334)
+    auto stage = [&](uint32_t r) {
+        uint32_t o[RX_ROUND / CLS_BLOCK], l[RX_ROUND / CLS_BLOCK], t[RX_ROUND / CLS_BLOCK];
+#pragma unroll
+        for (uint32_t i = 0; i < RX_ROUND / CLS_BLOCK; ++i) {
+            const uint32_t pc = min(t0 + r * RX_ROUND + i * CLS_BLOCK + tid, plast);
+            o[i] = a.offset[pc];
+            l[i] = a.length[pc];
+            t[i] = a.ptype ? a.ptype[pc] : 0u;
+        }
+        const uint32_t b = (r & (nbuf - 1u)) * RX_ROUND;
+#pragma unroll
+        for (uint32_t i = 0; i < RX_ROUND / CLS_BLOCK; ++i) {
+            d_off[b + i * CLS_BLOCK + tid] = o[i];
+            d_lp[b + i * CLS_BLOCK + tid] = l[i] | ((t[i] & 0x10u) << 12);
+        }
+    };
+    // step s's descriptor for this lane (the index wraps inside the buffers for s >= steps)
+    auto read_desc = [&](uint32_t s, uint32_t &o, uint32_t &lp) {
+        const uint32_t i = s * 64 + lane;
+        const uint32_t b = (((i / RX_ROUND) & (nbuf - 1u)) * RX_ROUND) + (i % RX_ROUND);
+        o = d_off[b];
+        lp = d_lp[b];
     };
     // The frame's header window: 5 aligned 16-byte chunks from ((off + 12) & ~15) hold frame
     // bytes [12, 64] whatever the alignment (bytes 0-11, the MAC addresses, are never read).
@@ -289,24 +309,26 @@ rx_classify(RxArgs a)
         r.c1 = load16(fr, ab + 16u);
         r.c2 = load16(fr, ab + 32u);
         r.c3 = load16(fr, ab + 48u);
-        // the 5th dword only when the chunks end before frame byte 64 (start misalignment > 12);
-        // other lanes read at the buffer's end, out of range: zero, no memory access
-        const uint32_t o4 = ok && ((o + 12u) & 15u) > 12u ? ab + 64u : a.rsrc_bytes;
-        r.c4 = __builtin_amdgcn_raw_buffer_load_b32(fr, (int)o4, 0, 0);
+        // the 5th dword only when the chunks end before frame byte 64 (start misalignment > 12)
+        // (an out-of-range load for the other lanes costs 0.75 us per 1 M x 64 B launch, so the
+        // load is skipped when no lane of the wave needs it)
+        r.c4 = 0;
+        if (ok && ((o + 12u) & 15u) > 12u) r.c4 = __builtin_amdgcn_raw_buffer_load_b32(fr, (int)(ab + 64u), 0, 0);
         return r;
     };
 
+    stage(0);
+    __syncthreads();
     uint32_t st = w;
-    uint32_t c_off = 0, c_len = 0, c_pt = 0, n_off = 0, n_len = 0, n_pt = 0;
-    load_desc(st, c_off, c_len, c_pt);
-    Win W = load_win(st, c_off, c_len);
-    load_desc(st + RX_WAVES, n_off, n_len, n_pt);
+    uint32_t c_off, c_lp;
+    read_desc(st, c_off, c_lp);
+    Win W = load_win(st, c_off, c_lp & 0xFFFFu);
     STAMP(0);
 
     while (st < steps) {
         const uint32_t p = t0 + st * 64 + lane;
         const bool valid = p < t1;
-        const uint32_t off = c_off, len = c_len;
+        const uint32_t off = c_off, len = c_lp & 0xFFFFu;
         const bool bad_desc = valid && ((uint64_t)off + len > (uint64_t)a.frames_bytes);
         const bool good = valid && !bad_desc;
 
@@ -333,10 +355,10 @@ rx_classify(RxArgs a)
         }
 #ifdef UDPDK_EXP_SKELETON   // diagnostic experiment only: the loads and stores without the work
         {
-            const uint32_t nst = st + RX_WAVES;
-            const Win NW = load_win(nst, n_off, n_len);
-            uint32_t nn_off, nn_len, nn_pt;
-            load_desc(nst + RX_WAVES, nn_off, nn_len, nn_pt);
+            const uint32_t nst = st + CLS_WAVES;
+            uint32_t n_off, n_lp;
+            read_desc(nst, n_off, n_lp);
+            const Win NW = load_win(nst, n_off, n_lp & 0xFFFFu);
             uint32_t x = 0;
 #pragma unroll
             for (int i = 0; i < 13; ++i) x ^= g[i];
@@ -344,14 +366,17 @@ rx_classify(RxArgs a)
             acc_fan += valid ? 1u : 0u;
             acc_v0 += valid ? 1u : 0u;
             lane_bytes += good ? len : 0u;
+            if ((st / CLS_WAVES) % SPR == SPR - 2u && (st >> 4) + 1u < steps / 16u) {
+                stage((st >> 4) + 1u);
+                __syncthreads();
+            }
             W = NW;
-            c_off = n_off; c_len = n_len; c_pt = n_pt;
-            n_off = nn_off; n_len = nn_len; n_pt = nn_pt;
+            c_off = n_off; c_lp = n_lp;
             st = nst;
             continue;
         }
 #endif
-        const uint32_t pt = !good ? 0u : a.ptype ? c_pt
+        const uint32_t pt = !good ? 0u : a.ptype ? (c_lp >> 12) & 0x10u
                           : (len >= 14 ? (((g[0] & 0xFFFFu) == 0x0008u) ? 0x211u : 0x1u) : 0u);
         const uint32_t frag = ((g[2] & 0xFFu) << 8) | ((g[2] >> 8) & 0xFFu);
         const bool is_udp = good && (pt & 0x10u) && len >= 42u && !(frag & 0x3FFFu) && (g[2] >> 24) == 17u;
@@ -450,13 +475,14 @@ rx_classify(RxArgs a)
         STAMP(2);
 
         // ---- next step of this wave: window loads stay in flight across the rest of this step
-        const uint32_t nst = st + RX_WAVES;
-        const Win NW = load_win(nst, n_off, n_len);
-        uint32_t nn_off, nn_len, nn_pt;
-        load_desc(nst + RX_WAVES, nn_off, nn_len, nn_pt);
-        // issued after the demux load: 5 window loads + 2 descriptor loads (+1 with ptype)
+        const uint32_t nst = st + CLS_WAVES;
+        uint32_t n_off, n_lp;
+        read_desc(nst, n_off, n_lp);      // in range of the buffers for any s (unused past the tile)
+        const Win NW = load_win(nst, n_off, n_lp & 0xFFFFu);
+        // issued after the demux load (the sweep's loads have all been consumed): 4 window loads
+        // and, for some waves, the fifth dword; vmcnt(4) covers both cases
 #ifndef UDPDK_EXP_NO_DEMUX_LOAD
-        wait_vm<7>(ev);
+        wait_vm<4>(ev);
 #endif
         STAMP(3);
         const uint4 e = is_udp ? make_uint4(ev[0], ev[1], ev[2], ev[3]) : make_uint4(0, 0, 0, 0);
@@ -540,13 +566,18 @@ rx_classify(RxArgs a)
             atomicAdd(&hist[key], 1u);
         }
         STAMP(6);
+        // next round's descriptors into the other buffer at the wave's next-to-last step of a
+        // round (its steps of round r are 16 r + w + CLS_WAVES j, j < SPR): the last reads of that
+        // buffer were before the previous round's barrier, and the next round is first read at
+        // j = SPR - 1.
+        // Uniform across the workgroup (every wave has steps / 4 steps).
+        if ((st / CLS_WAVES) % SPR == SPR - 2u && (st >> 4) + 1u < steps / 16u) {
+            stage((st >> 4) + 1u);
+            __syncthreads();
+        }
         W = NW;
         c_off = n_off;
-        c_len = n_len;
-        c_pt = n_pt;
-        n_off = nn_off;
-        n_len = nn_len;
-        n_pt = nn_pt;
+        c_lp = n_lp;
         st = nst;
     }
 
@@ -581,7 +612,7 @@ rx_classify(RxArgs a)
     auto tile_counter = [&](uint32_t c) -> uint32_t {
         uint32_t v = 0;
 #pragma unroll
-        for (int i = 0; i < RX_WAVES; ++i) v += cntw[i * 16 + c];
+        for (int i = 0; i < CLS_WAVES; ++i) v += cntw[i * 16 + c];
         return v;
     };
     {
@@ -590,9 +621,9 @@ rx_classify(RxArgs a)
         if (nv == a.tile_frames && ((uintptr_t)dst & 15u) == 0) {
             uint4 *d4 = reinterpret_cast<uint4 *>(dst);
             const uint4 *s4 = reinterpret_cast<const uint4 *>(mstage);
-            for (uint32_t i = tid; i < nv / 4; i += RX_BLOCK) d4[i] = s4[i];
+            for (uint32_t i = tid; i < nv / 4; i += CLS_BLOCK) d4[i] = s4[i];
         } else {
-            for (uint32_t i = tid; i < nv; i += RX_BLOCK) dst[i] = mstage[i];
+            for (uint32_t i = tid; i < nv; i += CLS_BLOCK) dst[i] = mstage[i];
         }
     }
 #ifdef UDPDK_STAMPS
@@ -602,7 +633,7 @@ rx_classify(RxArgs a)
     if (a.n_lanes == 1u) {
         if (tid == 0) a.hist[tile] = tile_counter(UDPDK_C_DELIVERIES);
     } else {
-        for (uint32_t s = tid; s < a.n_lanes; s += RX_BLOCK)
+        for (uint32_t s = tid; s < a.n_lanes; s += CLS_BLOCK)
             a.hist[(size_t)tile * a.n_lanes + s] = hist[s];
     }
     if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = tile_counter(tid);
