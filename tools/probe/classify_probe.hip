@@ -1,0 +1,79 @@
+// The real rx_classify in the streaming-probe harness (back-to-back launches over 10 rotated
+// device copies of 1 M x 64 B valid UDP frames, one bound port, ptype derived), timed with the
+// same events as tools/probe/stream_probe.hip, to separate kernel cost from harness cost.
+// Build: hipcc -O3 --offload-arch=gfx950 -Iinclude -Iudpdk_amd/csrc [-DUDPDK_EXP_...]
+//        -o tools/probe/classify_probe tools/probe/classify_probe.hip
+#include "../../udpdk_amd/csrc/rx_kernels.hip"
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+using namespace udpdk;
+
+int main()
+{
+    const uint32_t N = 1u << 20, COPIES = 10, FL = 64;
+    // one valid Eth/IPv4/UDP frame, dst port 10001, 30-byte datagram (frame ends at the datagram)
+    uint8_t t[64] = {0};
+    const uint8_t hdr[42] = {0x68, 0x05, 0xca, 0x95, 0xf8, 0xec, 0x68, 0x05, 0xca, 0x95, 0xfa, 0x64, 0x08, 0x00,
+                             0x45, 0x00, 0x00, 0x32, 0x12, 0x34, 0x00, 0x00, 0x40, 0x11, 0x00, 0x00,
+                             0xac, 0x1f, 0x64, 0x02, 0xac, 0x1f, 0x64, 0x01,
+                             0x27, 0x10, 0x27, 0x11, 0x00, 0x1e, 0xab, 0xcd};
+    memcpy(t, hdr, 42);
+    for (int i = 42; i < 64; ++i) t[i] = (uint8_t)(i * 7);
+    std::vector<uint8_t> hf((size_t)N * FL);
+    for (uint32_t i = 0; i < N; ++i) memcpy(&hf[(size_t)i * FL], t, FL);
+    std::vector<uint32_t> ho(N);
+    std::vector<uint16_t> hl(N, FL);
+    for (uint32_t i = 0; i < N; ++i) ho[i] = i * FL;
+
+    uint8_t *fr; uint32_t *off; uint16_t *len;
+    (void)hipMalloc(&fr, (size_t)N * FL * COPIES);
+    (void)hipMalloc(&off, (size_t)N * 4 * COPIES);
+    (void)hipMalloc(&len, (size_t)N * 2 * COPIES);
+    for (uint32_t c = 0; c < COPIES; ++c) {
+        (void)hipMemcpy(fr + (size_t)c * N * FL, hf.data(), (size_t)N * FL, hipMemcpyHostToDevice);
+        (void)hipMemcpy(off + (size_t)c * N, ho.data(), (size_t)N * 4, hipMemcpyHostToDevice);
+        (void)hipMemcpy(len + (size_t)c * N, hl.data(), (size_t)N * 2, hipMemcpyHostToDevice);
+    }
+    std::vector<uint4> pt(65536, make_uint4(0, 0, 0, 0));
+    const uint32_t rp = (10001 >> 8) | ((10001 & 0xFF) << 8);
+    pt[rp] = make_uint4(1, 0, 0, 0);
+    uint4 *port_tab; uint2 *binds;
+    (void)hipMalloc(&port_tab, 65536 * 16);
+    (void)hipMemcpy(port_tab, pt.data(), 65536 * 16, hipMemcpyHostToDevice);
+    (void)hipMalloc(&binds, 8);
+    (void)hipMemset(binds, 0, 8);
+    const uint32_t T = 1024, tiles = N / T;
+    uint32_t *meta, *hist, *tcnt;
+    (void)hipMalloc(&meta, (size_t)N * 4);
+    (void)hipMalloc(&hist, tiles * 4);
+    (void)hipMalloc(&tcnt, tiles * 64);
+
+    RxArgs a;
+    memset(&a, 0, sizeof(a));
+    a.port_tab = port_tab; a.binds = binds; a.meta = meta; a.hist = hist; a.tile_cnt = tcnt;
+    a.frames_bytes = N * FL; a.rsrc_bytes = N * FL; a.n = N; a.tile_frames = T; a.n_tiles = tiles;
+    a.lane_mask = 0; a.n_lanes = 1; a.key_bits = 0;
+    const uint32_t lds = classify_lds_bytes(1, T);
+    auto launch = [&](int i) {
+        RxArgs b = a;
+        b.frames = fr + (size_t)(i % COPIES) * N * FL;
+        b.offset = off + (size_t)(i % COPIES) * N;
+        b.length = len + (size_t)(i % COPIES) * N;
+        hipLaunchKernelGGL(rx_classify, dim3(tiles), dim3(CLS_BLOCK), lds, 0, b);
+    };
+    hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+    for (int i = 0; i < 10; ++i) launch(i);
+    (void)hipEventRecord(e0, 0);
+    const int R = 200;
+    for (int i = 0; i < R; ++i) launch(i);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms; (void)hipEventElapsedTime(&ms, e0, e1);
+    std::vector<uint32_t> hm(16);
+    (void)hipMemcpy(hm.data(), meta, 64, hipMemcpyDeviceToHost);
+    printf("rx_classify %7.2f us per launch (meta[0] = %08x)\n", 1e3 * ms / R, hm[0]);
+    return 0;
+}

@@ -287,6 +287,38 @@ __global__ void __launch_bounds__(256) k_indp(const uint8_t *fr, const uint32_t 
     }
 }
 
+
+// window loaded straight from frame byte 12 (unaligned: 3 x 16 B + 4 B = bytes 12..63) with
+// buffer loads, U=1; aligned 4 x 16 B from (o + 12) & ~15, U=0
+template <int U>
+__global__ void __launch_bounds__(256) k_unal(const uint8_t *fr, const uint32_t *off, const uint16_t *len, uint32_t *out, uint32_t nbytes)
+{
+    constexpr int S = 4;
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t t0 = blockIdx.x * (256 * S);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(fr), (short)0, (int)nbytes, 0x00020000);
+    uint32_t o[S], l[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) { o[s] = off[t0 + s * 256 + w * 64 + lane]; l[s] = len[t0 + s * 256 + w * 64 + lane]; }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        uint32_t x = 0;
+        if (U) {
+            const uint32_t b = o[s] + 12u;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(b + 16 * c), 0, 0); x ^= v[0] + v[1] + v[2] + v[3]; }
+            x ^= __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(b + 48), 0, 0);
+        } else {
+            const uint32_t b = (o[s] + 12u) & ~15u;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) { const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(b + 16 * c), 0, 0); x ^= v[0] + v[1] + v[2] + v[3]; }
+        }
+        out[t0 + s * 256 + w * 64 + lane] = x + l[s];
+    }
+    (void)acc;
+}
+
 __global__ void __launch_bounds__(256) k_flat(const uint4 *fr, uint32_t *out, uint32_t n16)
 {
     const uint32_t stride = gridDim.x * 256;
@@ -362,6 +394,10 @@ int main()
     FEAT(121);
 
 #define INDP(S_, P_, C_) timei("indp" #S_ "_" #P_ "_c" #C_, [&](const uint8_t *f_, const uint32_t *o, const uint16_t *l) { hipLaunchKernelGGL((k_indp<S_, P_, C_>), dim3(N / (256 * S_)), dim3(256), 0, 0, f_, o, l, out); })
-    INDP(4, 1, 0); INDP(4, 2, 0); INDP(4, 1, 120); INDP(4, 2, 120); INDP(4, 1, 240); INDP(4, 2, 240); INDP(4, 3, 240); INDP(2, 1, 240); INDP(1, 1, 240); INDP(8, 2, 240); INDP(8, 3, 240); INDP(4, 1, 360); INDP(4, 2, 360);
+    INDP(4, 1, 0);
+    timei("unal0", [&](const uint8_t *f_, const uint32_t *o, const uint16_t *l) { hipLaunchKernelGGL((k_unal<0>), dim3(N / 1024), dim3(256), 0, 0, f_, o, l, out, (uint32_t)(N * 64)); });
+    timei("unal1", [&](const uint8_t *f_, const uint32_t *o, const uint16_t *l) { hipLaunchKernelGGL((k_unal<1>), dim3(N / 1024), dim3(256), 0, 0, f_, o, l, out, (uint32_t)(N * 64)); });
+    timei("unal0", [&](const uint8_t *f_, const uint32_t *o, const uint16_t *l) { hipLaunchKernelGGL((k_unal<0>), dim3(N / 1024), dim3(256), 0, 0, f_, o, l, out, (uint32_t)(N * 64)); });
+    timei("unal1", [&](const uint8_t *f_, const uint32_t *o, const uint16_t *l) { hipLaunchKernelGGL((k_unal<1>), dim3(N / 1024), dim3(256), 0, 0, f_, o, l, out, (uint32_t)(N * 64)); });
     return 0;
 }

@@ -10,10 +10,13 @@ constexpr int RX_BLOCK  = 256;              // rx_classify workgroup (4 waves)
 constexpr int RX_WAVES  = RX_BLOCK / 64;
 constexpr int RX_UNROLL = 4;                // 16-byte chunk loads in flight per lane
 constexpr uint32_t RX_TILE_MIN = 1024;      // frames per tile (histogram granularity)
-constexpr uint32_t RX_TILE_MAX = 16384;
+constexpr uint32_t RX_TILE_MAX = 8192;   // classify LDS: <= 143 KiB at 16384 lanes
 constexpr uint32_t RX_HIST_CAP = 1u << 21;  // target bound on lanes x tiles
 #ifndef UDPDK_CLS_BLOCK
 #define UDPDK_CLS_BLOCK 256
+#endif
+#ifndef UDPDK_CLS_WPE
+#define UDPDK_CLS_WPE 4                      // rx_classify minimum waves per SIMD (VGPR budget)
 #endif
 constexpr int CLS_BLOCK = UDPDK_CLS_BLOCK;  // rx_classify workgroup
 constexpr int CLS_WAVES = CLS_BLOCK / 64;
@@ -27,14 +30,15 @@ constexpr uint32_t SCAN_SMALL_TILES = 32;   // ... and this many tiles (serial p
 constexpr int TX_BLOCK = 256;
 
 // rx_classify LDS carve (one dynamic array, 16-byte aligned offsets: cdna_hip_programming.md
-// Guideline 17): per wave three 64-entry chunk-map arrays for the tail sweep; per-wave counter
-// rows; the descriptors of one or two rounds of RX_ROUND frames (offset, length | ptype bit);
-// the tile's per-lane delivery histogram; the tile's verdict words.
-constexpr int WAVE_ARRAYS = 3;                    // chunk start, offset, length
-constexpr int ARR_BYTES   = CLS_WAVES * WAVE_ARRAYS * 64 * 4;
-constexpr int CNT_OFF     = ARR_BYTES;            // [CLS_WAVES][16] per-wave counter rows
+// Guideline 17): the tail pass's per-wave arrays (chunk starts, frame offsets, datagram ends);
+// per-wave counter rows; the descriptors of one or two rounds of RX_ROUND frames (offset,
+// length | ptype bit); the tile's per-lane delivery histogram; the tile's verdict words; the
+// round's datagram ends + window sums (frames whose UDP checksum waits for the tail pass);
+// the round's port-table lookups (dst port, dst IPv4).
+constexpr uint32_t RX_ROUND = 1024;               // frames per descriptor-staging / tail round
+constexpr int TP_OFF      = 0;                    // [CLS_WAVES][3][64] chunk start, offset, dge
+constexpr int CNT_OFF     = TP_OFF + CLS_WAVES * 3 * 64 * 4;     // [CLS_WAVES][16] counter rows
 constexpr int DSC_OFF     = CNT_OFF + CLS_WAVES * 16 * 4;
-constexpr uint32_t RX_ROUND = 1024;               // frames per descriptor-staging round
 
 // descriptor buffers: one round for a single-round tile, two (double-buffered) otherwise
 __host__ __device__ constexpr uint32_t classify_dsc_bufs(uint32_t tile_frames)
@@ -45,7 +49,7 @@ __host__ __device__ constexpr uint32_t classify_dsc_bufs(uint32_t tile_frames)
 __host__ __device__ constexpr uint32_t classify_lds_bytes(uint32_t n_lanes, uint32_t tile_frames)
 {
     return (uint32_t)DSC_OFF + 8u * RX_ROUND * classify_dsc_bufs(tile_frames) +
-           4u * ((n_lanes + 3u) & ~3u) + 4u * tile_frames;
+           4u * ((n_lanes + 3u) & ~3u) + 4u * tile_frames + 4u * RX_ROUND + 8u * RX_ROUND;
 }
 
 // Port table entry (16 B per raw port): x = bindings on the port, y = index of the first in the

@@ -197,9 +197,12 @@ __device__ __forceinline__ uint32_t scan_dpp(uint32_t v)
     return v;
 }
 
+// Frame bytes [12, 64) of one frame, loaded straight from frame byte 12 (byte-aligned buffer
+// loads: 3 x 16 B + 4 B; unaligned dwordx4 buffer loads cost the same as aligned ones here,
+// tools/probe/stream_probe.hip k_unal): g[i] = frame bytes 12 + 4i .. 15 + 4i, no funnel shift.
 struct Win {
-    uint4 c0, c1, c2, c3;
-    uint32_t c4;                     // only the first dword of the fifth chunk is ever needed
+    uint4 a, b, c;
+    uint32_t d;
 };
 
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
@@ -222,7 +225,7 @@ __device__ __forceinline__ void wait_vm(v4u32 &r)
 
 // 5 waves per SIMD (<= 96 VGPRs, no spill): a fifth workgroup per CU lets the next pipelined
 // launch start while this one drains
-__global__ void __launch_bounds__(CLS_BLOCK) __attribute__((amdgpu_waves_per_eu(5, 8)))
+__global__ void __launch_bounds__(CLS_BLOCK) __attribute__((amdgpu_waves_per_eu(UDPDK_CLS_WPE, 8)))
 rx_classify(RxArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -235,8 +238,6 @@ rx_classify(RxArgs a)
     st_acc[12] = __builtin_amdgcn_s_memrealtime();
 #endif
 
-    uint32_t *arr = reinterpret_cast<uint32_t *>(smem) + w * WAVE_ARRAYS * 64;
-    uint32_t *l_cs = arr, *l_off = arr + 64, *l_len = arr + 128;
     uint32_t *cntw = reinterpret_cast<uint32_t *>(smem + CNT_OFF);    // [wave][counter]
     // descriptors of the current (and, double-buffered, the next) round of RX_ROUND frames:
     // staged with coalesced loads by the whole workgroup, so the per-step reads are LDS reads
@@ -249,6 +250,11 @@ rx_classify(RxArgs a)
     // global store inside the step loop, so no s_waitcnt there ever waits for a store (on gfx9
     // stores count in vmcnt, in order with the loads).
     uint32_t *mstage = hist + ((a.n_lanes + 3u) & ~3u);              // [tile_frames]
+    // datagram end (34 + UDP length) of the frames whose checksum the tail pass completes
+    // pending frames' datagram end | folded window part of the UDP sum << 16
+    uint32_t *dgl = mstage + a.tile_frames;                          // [RX_ROUND]
+    // the round's port-table lookups: raw dst port | is-UDP << 16, raw dst IPv4
+    uint2 *dstash = reinterpret_cast<uint2 *>(dgl + RX_ROUND);       // [RX_ROUND]
 
     // (hist is only used with several lanes; its zeroing is ordered by the staging barrier)
     if (a.n_lanes > 1u)
@@ -295,64 +301,44 @@ rx_classify(RxArgs a)
         o = d_off[b];
         lp = d_lp[b];
     };
-    // The frame's header window: 5 aligned 16-byte chunks from ((off + 12) & ~15) hold frame
-    // bytes [12, 64] whatever the alignment (bytes 0-11, the MAC addresses, are never read).
-    // One lane per frame.
+    // The frame's header window, frame bytes [12, 64) (bytes 0-11, the MAC addresses, are never
+    // read). One lane per frame. Bytes past the frame are never used (parse and sums mask by
+    // length); lanes without a frame read the buffer's first bytes (cached, never used).
     auto load_win = [&](uint32_t s, uint32_t o, uint32_t l) -> Win {
         const uint32_t p = t0 + s * 64 + lane;
-        const bool ok = s < steps && p < t1 && l != 0u && (uint64_t)o + l <= (uint64_t)a.frames_bytes;
-        // bytes past the frame are never used (parse and sums mask by length); out-of-range
-        // offsets of the range-checked buffer read zero
-        const uint32_t ab = ok ? ((o + 12u) & ~15u) : 0u;
+        const bool ok = s < steps && p < t1 && l >= 14u && l <= a.frames_bytes && o <= a.frames_bytes - l;
+        const uint32_t b = ok ? o + 12u : 0u;
         Win r;
-        r.c0 = load16(fr, ab);
-        r.c1 = load16(fr, ab + 16u);
-        r.c2 = load16(fr, ab + 32u);
-        r.c3 = load16(fr, ab + 48u);
-        // the 5th dword only when the chunks end before frame byte 64 (start misalignment > 12)
-        // (an out-of-range load for the other lanes costs 0.75 us per 1 M x 64 B launch, so the
-        // load is skipped when no lane of the wave needs it)
-        r.c4 = 0;
-        if (ok && ((o + 12u) & 15u) > 12u) r.c4 = __builtin_amdgcn_raw_buffer_load_b32(fr, (int)(ab + 64u), 0, 0);
+        r.a = load16(fr, b);
+        r.b = load16(fr, b + 16u);
+        r.c = load16(fr, b + 32u);
+        r.d = __builtin_amdgcn_raw_buffer_load_b32(fr, (int)(b + 48u), 0, 0);
         return r;
     };
 
     stage(0);
     __syncthreads();
-    uint32_t st = w;
+    uint32_t st = __builtin_amdgcn_readfirstlane(w);             // wave-uniform step (SGPR)
+    const bool has_ptype = a.ptype != nullptr;
     uint32_t c_off, c_lp;
     read_desc(st, c_off, c_lp);
     Win W = load_win(st, c_off, c_lp & 0xFFFFu);
     STAMP(0);
 
-    while (st < steps) {
+    // rounds of RX_ROUND frames: SPR steps per wave, then the wave's tail pass for them (the
+    // next round's first window is already in flight during the tail pass)
+    for (uint32_t rnd = 0; rnd < steps / 16u; ++rnd) {
+    bool tail_any = false;     // some frame of the wave's steps waits for the tail pass (SGPR)
+#pragma unroll 1
+    for (uint32_t jstep = 0; jstep < SPR; ++jstep) {
         const uint32_t p = t0 + st * 64 + lane;
         const bool valid = p < t1;
         const uint32_t off = c_off, len = c_lp & 0xFFFFu;
-        const bool bad_desc = valid && ((uint64_t)off + len > (uint64_t)a.frames_bytes);
-        const bool good = valid && !bad_desc;
+        const bool good = valid && len <= a.frames_bytes && off <= a.frames_bytes - len;
 
         // ---- header fields from the window registers (lane = frame) ----
-        uint32_t g[13];                                     // g[i] = frame bytes 12+4i .. 15+4i
-        {
-            const uint32_t sh = (off + 12u) & 15u, s3 = sh & 3u;
-            uint32_t wd[17], w1[16], w2[14];
-            const uint4 wc[4] = {W.c0, W.c1, W.c2, W.c3};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                wd[4 * i] = wc[i].x; wd[4 * i + 1] = wc[i].y; wd[4 * i + 2] = wc[i].z; wd[4 * i + 3] = wc[i].w;
-            }
-            wd[16] = W.c4;
-            // shift by (sh >> 2) dwords with lane-mask selects (a plain ?: here is turned into a
-            // scratch-indexed array by the compiler)
-            const unsigned long long m4 = __ballot((sh & 4u) != 0u), m8 = __ballot((sh & 8u) != 0u);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) w1[i] = lane_select(m4, wd[i], wd[i + 1]);
-#pragma unroll
-            for (int i = 0; i < 14; ++i) w2[i] = lane_select(m8, w1[i], w1[i + 2]);
-#pragma unroll
-            for (int i = 0; i < 13; ++i) g[i] = __builtin_amdgcn_alignbyte(w2[i + 1], w2[i], s3);
-        }
+        const uint32_t g[13] = {W.a.x, W.a.y, W.a.z, W.a.w, W.b.x, W.b.y, W.b.z, W.b.w,
+                                W.c.x, W.c.y, W.c.z, W.c.w, W.d};  // g[i] = frame bytes 12+4i ..
 #ifdef UDPDK_EXP_SKELETON   // diagnostic experiment only: the loads and stores without the work
         {
             const uint32_t nst = st + CLS_WAVES;
@@ -376,24 +362,19 @@ rx_classify(RxArgs a)
             continue;
         }
 #endif
-        const uint32_t pt = !good ? 0u : a.ptype ? (c_lp >> 12) & 0x10u
-                          : (len >= 14 ? (((g[0] & 0xFFFFu) == 0x0008u) ? 0x211u : 0x1u) : 0u);
+        // IPv4 gate (udpdk_poller.c:334): the ptype array's L3_IPV4 bit when given, else derived
+        // from ether_type (frames shorter than an Ethernet header are not IPv4)
+        const uint32_t eth_ip = (len >= 14u && (g[0] & 0xFFFFu) == 0x0008u) ? 0x10u : 0u;
+        const bool ipv4 = good && ((has_ptype ? (c_lp >> 12) : eth_ip) & 0x10u);
         const uint32_t frag = ((g[2] & 0xFFu) << 8) | ((g[2] >> 8) & 0xFFu);
-        const bool is_udp = good && (pt & 0x10u) && len >= 42u && !(frag & 0x3FFFu) && (g[2] >> 24) == 17u;
-        const uint32_t dport = g[6] & 0xFFFFu;                   // poller.c:372
-        // The demux load goes out first and is waited for only where it is used.
-        STAMP(1);
-#ifdef UDPDK_EXP_NO_DEMUX_LOAD      // diagnostic experiment only: constant port entry
-        v4u32 ev = {1u, 0u, 0u, dport};
-#else
-        v4u32 ev = asm_load16(a.port_tab + dport);
-#endif
-
-        // ---- everything the header window gives (the window registers die here) ----
-        const bool ipv4 = good && (pt & 0x10u);                   // udpdk_poller.c:334, :362-366
         const bool l3 = ipv4 && len >= 42u;
         const bool fragd = (frag & 0x3FFFu) != 0u;                // udpdk_poller.c:338
         const bool not_udp = (g[2] >> 24) != 17u;                 // udpdk_poller.c:368-371
+        const bool is_udp = l3 && !fragd && !not_udp;
+        const uint32_t dport = g[6] & 0xFFFFu;                   // poller.c:372
+        STAMP(1);
+
+        // ---- everything the header window gives ----
         // IPv4 header checksum over the fixed 20 bytes at offset 14 (RFC 1071)
         const uint32_t ipraw = (g[0] >> 16) + sum16(g[1]) + sum16(g[2]) + sum16(g[3]) +
                                sum16(g[4]) + (g[5] & 0xFFFFu);
@@ -404,74 +385,27 @@ rx_classify(RxArgs a)
         const uint32_t ulen = ((ulen_raw & 0xFFu) << 8) | (ulen_raw >> 8);
         const uint32_t ucks = g[7] & 0xFFFFu;
         const bool len_bad = ulen < 8u || 34u + ulen > len;
-        // UDP sum so far: pseudo-header {src, dst, proto 17, udp length} + frame bytes
-        // [34, min(len, 64)) from the window (frame-relative words)
-        uint32_t ws = g[5] >> 16;
+        // UDP checksum (RFC 768 over the datagram, frame bytes [34, 34 + ulen), plus the pseudo-
+        // header {src, dst, proto 17, udp length}), computed only where it decides the state:
+        // a frame whose datagram ends within the window is summed here; a longer one is left to
+        // the tile's tail pass (state 3 = pending until then). Ethernet padding after the
+        // datagram is never summed.
+        const bool need_cs = is_udp && ucks != 0u && !len_bad;
+        const uint32_t dge = 34u + ulen;                          // datagram end (<= len)
+        const bool pend = need_cs && dge > 64u;
+        uint32_t ws = 0;
 #pragma unroll
         for (int i = 6; i < 13; ++i) ws += sum16(g[i]);
-        if (__ballot(is_udp && len < 64u)) {
+        if (__ballot(need_cs && dge < 64u)) {                     // short or padded frames
             uint32_t wm = 0;
 #pragma unroll
-            for (int i = 5; i < 13; ++i) wm += sum16(g[i] & byte_mask(34, (int)len, 12 + 4 * i));
-            ws = len < 64u ? wm : ws;
+            for (int i = 6; i < 13; ++i) wm += sum16(g[i] & byte_mask(34, (int)dge, 12 + 4 * i));
+            ws = dge < 64u ? wm : ws;
         }
-        uint32_t us = ws + (g[3] >> 16) + (g[4] & 0xFFFFu) + (dip & 0xFFFFu) + (dip >> 16) + 0x1100u +
-                      ulen_raw;
-
-        // ---- tail sweep: frame bytes >= 64 as 64-byte super-chunks swept across the lanes ----
-        // Super-chunk j of a frame = 4 aligned 16-byte chunks from ((off + 64) & ~15) + 64 j; lane
-        // i of a group handles super-chunk k0 + i of the wave's 64 frames (found by binary search
-        // over the per-frame starts in LDS). Two groups in flight (loads of the next group are
-        // issued before the current one is summed). Sums are absolute-address word sums.
-        const uint32_t a64 = (off + 64u) & ~15u;
-        const uint32_t my_nt = (good && len > 64u) ? (off + len - a64 + 63u) >> 6 : 0u;
-        uint32_t tsum = 0;
-        if (__ballot(my_nt != 0u)) {
-            const uint32_t inc = scan_dpp(my_nt);
-            const uint32_t my_cs = inc - my_nt;
-            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-            l_cs[lane] = my_cs;
-            l_off[lane] = off;
-            l_len[lane] = len;
-            wave_sync();
-            auto issue = [&](uint32_t k0, uint32_t &q, uint4 (&R)[4]) {
-                const uint32_t k = k0 + lane;
-                q = 0;
-#pragma unroll
-                for (int sft = 32; sft >= 1; sft >>= 1)
-                    if (l_cs[q + sft] <= k) q += sft;
-                const uint32_t base = k < total ? ((l_off[q] + 64u) & ~15u) + 64u * (k - l_cs[q]) : 0u;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) R[c] = load16(fr, base + 16u * c);
-            };
-            auto consume = [&](uint32_t k0, uint32_t q, const uint4 (&R)[4]) {
-                const uint32_t k = k0 + lane;
-                uint32_t part = 0;
-                if (k < total) {
-                    const uint32_t fo = l_off[q];
-                    const int rel = (int)((((fo + 64u) & ~15u) + 64u * (k - l_cs[q])) - fo);
-                    const int fl = (int)l_len[q];
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) part += chunk_sum(R[c], 64 - rel - 16 * c, fl - rel - 16 * c);
-                }
-                const uint32_t P = scan_dpp(part);
-                const uint32_t lo = max(my_cs, k0), hi = min(my_cs + my_nt, k0 + 64u);
-                const uint32_t ph = __shfl(P, (int)((hi > k0 ? hi - 1u - k0 : 0u) & 63u), 64);
-                const uint32_t pl = __shfl(P, (int)((lo > k0 ? lo - 1u - k0 : 0u) & 63u), 64);
-                if (lo < hi) tsum += ph - (lo > k0 ? pl : 0u);
-            };
-            uint32_t qa, qb;
-            uint4 Ra[4], Rb[4];
-            issue(0, qa, Ra);
-            for (uint32_t k0 = 0; k0 < total; k0 += 128) {
-                issue(k0 + 64, qb, Rb);
-                consume(k0, qa, Ra);
-                if (k0 + 64 >= total) break;
-                issue(k0 + 128, qa, Ra);
-                consume(k0 + 64, qb, Rb);
-            }
-            wave_sync();
-        }
+        const uint32_t us = ws + (g[5] >> 16) + (g[3] >> 16) + (g[4] & 0xFFFFu) + (dip & 0xFFFFu) +
+                            (dip >> 16) + 0x1100u + ulen_raw;
+        tail_any = tail_any || __ballot(pend) != 0ull;
+        dgl[(st * 64 + lane) & (RX_ROUND - 1u)] = dge | fold32(us) << 16;
         STAMP(2);
 
         // ---- next step of this wave: window loads stay in flight across the rest of this step
@@ -479,92 +413,29 @@ rx_classify(RxArgs a)
         uint32_t n_off, n_lp;
         read_desc(nst, n_off, n_lp);      // in range of the buffers for any s (unused past the tile)
         const Win NW = load_win(nst, n_off, n_lp & 0xFFFFu);
-        // issued after the demux load (the sweep's loads have all been consumed): 4 window loads
-        // and, for some waves, the fifth dword; vmcnt(4) covers both cases
-#ifndef UDPDK_EXP_NO_DEMUX_LOAD
-        wait_vm<4>(ev);
-#endif
-        STAMP(3);
-        const uint4 e = is_udp ? make_uint4(ev[0], ev[1], ev[2], ev[3]) : make_uint4(0, 0, 0, 0);
 
-        // ---- UDP checksum state ----
-        uint32_t tf = fold32(tsum);                               // tail: byte-swapped at odd starts
-        tf = (off & 1u) ? (((tf & 0xFFu) << 8) | (tf >> 8)) : tf;
-        us += tf;
-        const bool need_pad = is_udp && ucks != 0u && !len_bad && 34u + ulen < len;
-        if (__ballot(need_pad)) {                                 // Ethernet padding after the datagram
-            if (need_pad) {
-                uint32_t pad = 0;
-                for (uint32_t r = 34u + ulen; r < len; ++r)
-                    pad += (uint32_t)a.frames[off + r] << (8u * (r & 1u));
-                us += 0xFFFFu - fold32(pad);                      // one's-complement subtraction
-            }
-        }
+        // ---- what does not need the port entry: UDP state, flags, flag counters ----
         const uint32_t state = ucks == 0u ? UDPDK_UDP_CSUM_NONE
+                             : pend ? 3u
                              : (len_bad || fold32(us) != 0xFFFFu) ? UDPDK_UDP_CSUM_BAD
                                                                    : UDPDK_UDP_CSUM_OK;
-        STAMP(4);
-
-        // ---- demux: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
-        // the port entry carries the first binding; later ones only for ports with several
-        const bool match0 = e.x != 0u && (dip == e.z || e.z == 0u);     // poller.c:391
-        uint32_t fan = match0 ? 1u : 0u;
-        uint32_t first = match0 ? (e.w & 0x7FFFFFFFu) : 0u;
-        const bool walk = e.x > 1u && !(match0 && !(e.w >> 31));        // poller.c:396-403
-        if (__ballot(walk)) {
-            if (walk) {
-                for (uint32_t i = 1; i < e.x; ++i) {
-                    const uint2 b = a.binds[e.y + i];
-                    if (dip == b.x || b.x == 0u) {
-                        const uint32_t sock = b.y & 0x7FFFFFFFu;
-                        if (fan > 0 && a.n_lanes > 1u)
-                            atomicAdd(&hist[sock & a.lane_mask], 1u);   // clones (rare)
-                        if (fan == 0) first = sock;
-                        ++fan;
-                        if (!(b.y >> 31)) break;
-                    }
-                }
-            }
-        }
-        const uint32_t verdict = !good ? UDPDK_V_BAD_DESC
-                               : !ipv4 ? UDPDK_V_NOT_IPV4
-                               : !l3 ? UDPDK_V_TRUNC
-                               : fragd ? UDPDK_V_FRAG
-                               : not_udp ? UDPDK_V_NOT_UDP
-                               : e.x == 0u ? UDPDK_V_NO_BIND
-                               : fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
-        STAMP(5);
+        const uint32_t pre = !good ? UDPDK_V_BAD_DESC
+                           : !ipv4 ? UDPDK_V_NOT_IPV4
+                           : !l3 ? UDPDK_V_TRUNC
+                           : fragd ? UDPDK_V_FRAG
+                           : not_udp ? UDPDK_V_NOT_UDP : 0xFFu;       // 0xFF: UDP, demux pending
         const uint32_t l3f = l3 ? ((ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8) : 0u;
         const uint32_t udpf = is_udp ? (state << 5 | (len_bad ? 1u : 0u) << 7) : 0u;
-        mstage[st * 64 + lane] = verdict | l3f | udpf | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
-        // per-lane packed counters (8-bit fields; a lane sees <= 64 frames per tile)
-        const uint32_t vinc = valid ? 1u << (8u * (verdict & 3u)) : 0u;
-        acc_v0 += verdict < 4u ? vinc : 0u;
-        acc_v1 += verdict < 4u ? 0u : vinc;
+        // (pending frames count their UDP state in the tail pass)
         acc_f0 += (l3 && !ip_ok ? 1u : 0u) | (l3 && ihl_ne5 ? 0x100u : 0u) |
                   (is_udp && state == UDPDK_UDP_CSUM_OK ? 0x10000u : 0u) |
                   (is_udp && state == UDPDK_UDP_CSUM_BAD ? 0x1000000u : 0u);
         acc_f1 += (is_udp && state == UDPDK_UDP_CSUM_NONE ? 1u : 0u) | (is_udp && len_bad ? 0x100u : 0u);
-        acc_fan += fan;
         if (good) lane_bytes += len;
-        const bool delivered = valid && fan > 0u;
-        // first delivery of every frame into the tile histogram; small key spaces are
-        // aggregated with a wave multi-split first (all 64 lanes may share one lane)
-        // (one lane: the tile's count is its delivery counter, written at the tile end)
-        const uint32_t key = first & a.lane_mask;
-        if (a.n_lanes == 1u) {
-        } else if (a.key_bits <= 4u) {
-            unsigned long long peers = __ballot(delivered);
-            for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
-                const bool kb = (key >> bit) & 1u;
-                const unsigned long long bal = __ballot(kb);
-                peers &= kb ? bal : ~bal;
-            }
-            if (delivered && lane == (uint32_t)__ffsll((long long)peers) - 1u)
-                atomicAdd(&hist[key], (uint32_t)__popcll(peers));
-        } else if (delivered) {
-            atomicAdd(&hist[key], 1u);
-        }
+
+        // the port-table lookup waits for the round's demux pass: verdict field 0xF until then
+        mstage[st * 64 + lane] = (pre == 0xFFu ? 0xFu : pre) | l3f | udpf;
+        dstash[(st * 64 + lane) & (RX_ROUND - 1u)] = make_uint2(dport | (is_udp ? 0x10000u : 0u), dip);
         STAMP(6);
         // next round's descriptors into the other buffer at the wave's next-to-last step of a
         // round (its steps of round r are 16 r + w + CLS_WAVES j, j < SPR): the last reads of that
@@ -579,6 +450,157 @@ rx_classify(RxArgs a)
         c_off = n_off;
         c_lp = n_lp;
         st = nst;
+    }
+    // ---- demux pass: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
+    // The round's port-table lookups of this wave, all SPR steps' 16-byte entries in flight at
+    // once (one round trip per round instead of one exposed per step). The entry carries the
+    // port's first binding; the binding list is walked only for ports with several.
+    {
+        uint4 E[SPR];
+        uint2 S[SPR];
+#pragma unroll
+        for (uint32_t j = 0; j < SPR; ++j) S[j] = dstash[((st - 16u + CLS_WAVES * j) * 64 + lane) & (RX_ROUND - 1u)];
+#pragma unroll
+        for (uint32_t j = 0; j < SPR; ++j) E[j] = a.port_tab[S[j].x & 0xFFFFu];
+#pragma unroll
+        for (uint32_t j = 0; j < SPR; ++j) {
+            const uint32_t i = (st - 16u + CLS_WAVES * j) * 64 + lane;
+            const uint32_t m = mstage[i];
+            const bool valid = t0 + i < t1;
+            const uint4 e = (S[j].x >> 16) ? E[j] : make_uint4(0, 0, 0, 0);
+            const uint32_t dip = S[j].y;
+            const bool match0 = e.x != 0u && (dip == e.z || e.z == 0u);     // poller.c:391
+            uint32_t fan = match0 ? 1u : 0u;
+            uint32_t first = match0 ? (e.w & 0x7FFFFFFFu) : 0u;
+            const bool walk = e.x > 1u && !(match0 && !(e.w >> 31));        // poller.c:396-403
+            if (__ballot(walk)) {
+                if (walk) {
+                    for (uint32_t b = 1; b < e.x; ++b) {
+                        const uint2 bd = a.binds[e.y + b];
+                        if (dip == bd.x || bd.x == 0u) {
+                            const uint32_t sock = bd.y & 0x7FFFFFFFu;
+                            if (fan > 0 && a.n_lanes > 1u)
+                                atomicAdd(&hist[sock & a.lane_mask], 1u);   // clones (rare)
+                            if (fan == 0) first = sock;
+                            ++fan;
+                            if (!(bd.y >> 31)) break;
+                        }
+                    }
+                }
+            }
+            const uint32_t pre = m & 0xFu;
+            const uint32_t verdict = pre != 0xFu ? pre
+                                   : e.x == 0u ? UDPDK_V_NO_BIND
+                                   : fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
+            mstage[i] = (m & ~0xFu) | verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
+            // per-lane packed counters (8-bit fields; a lane sees <= 64 frames per tile)
+            const uint32_t vinc = valid ? 1u << (8u * (verdict & 3u)) : 0u;
+            acc_v0 += verdict < 4u ? vinc : 0u;
+            acc_v1 += verdict < 4u ? 0u : vinc;
+            acc_fan += fan;
+            const bool delivered = valid && fan > 0u;
+            // first delivery of every frame into the tile histogram; small key spaces are
+            // aggregated with a wave multi-split first (all 64 lanes may share one lane)
+            // (one lane: the tile's count is its delivery counter, written at the tile end)
+            const uint32_t key = first & a.lane_mask;
+            if (a.n_lanes == 1u) {
+            } else if (a.key_bits <= 4u) {
+                unsigned long long peers = __ballot(delivered);
+                for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
+                    const bool kb = (key >> bit) & 1u;
+                    const unsigned long long bal = __ballot(kb);
+                    peers &= kb ? bal : ~bal;
+                }
+                if (delivered && lane == (uint32_t)__ffsll((long long)peers) - 1u)
+                    atomicAdd(&hist[key], (uint32_t)__popcll(peers));
+            } else if (delivered) {
+                atomicAdd(&hist[key], 1u);
+            }
+        }
+    }
+    // ---- tail pass: UDP checksums of the datagrams that extend past the header window ----
+    // The wave's pending frames of the round (state 3), one step (64 frames) at a time: frame
+    // bytes [64, dge) as 64-byte super-chunks, chunk j = frame bytes [64 + 64 j, 128 + 64 j)
+    // loaded as 4 byte-aligned 16-byte pieces (so the words are frame-relative whatever the
+    // frame's offset, and only a frame's last chunk needs byte masks), swept across the wave's
+    // lanes: lane i of a group takes chunk k0 + i of the step's chunk space (its frame found by
+    // binary search over the per-frame chunk starts in LDS), so a group is 4 KiB of dense frame
+    // bytes. Per-frame sums are segment sums of a DPP prefix scan; two groups in flight.
+    if (tail_any) {
+        uint32_t *l_cs = reinterpret_cast<uint32_t *>(smem + TP_OFF) + w * 192;  // [64] chunk starts
+        uint32_t *l_off = l_cs + 64, *l_dge = l_cs + 128;                       // [64] offset, dge
+        for (uint32_t s2 = st - 16u; s2 < st; s2 += CLS_WAVES) {      // this round's steps
+            const uint32_t i = s2 * 64 + lane;
+            const uint32_t m = mstage[i];
+            const bool pd = t0 + i < t1 && ((m >> 5) & 3u) == 3u;
+            if (!__ballot(pd)) continue;
+            // the frame's offset: the staged descriptor of a single-round tile, else global
+            const uint32_t fo = nbuf == 1u ? d_off[i] : a.offset[min(t0 + i, plast)];
+            const uint32_t dw = dgl[i & (RX_ROUND - 1u)];
+            const uint32_t de = pd ? dw & 0xFFFFu : 64u;
+            const uint32_t my_nt = (de - 64u + 63u) >> 6;
+            const uint32_t inc = scan_dpp(my_nt);
+            const uint32_t my_cs = inc - my_nt;
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            l_cs[lane] = my_cs;
+            l_off[lane] = fo;
+            l_dge[lane] = de;
+            wave_sync();
+            uint32_t tsum = 0;
+            auto issue = [&](uint32_t k0, uint32_t &q, uint4 (&R)[4]) {
+                const uint32_t k = k0 + lane;
+                q = 0;
+#pragma unroll
+                for (int sft = 32; sft >= 1; sft >>= 1)
+                    if (l_cs[q + sft] <= k) q += sft;
+                const uint32_t base = k < total ? l_off[q] + 64u + 64u * (k - l_cs[q]) : 0u;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) R[c] = load16(fr, base + 16u * c);
+            };
+            // The full-chunk sum reads every loaded register unconditionally, so the compiler's
+            // wait for this group is placed here on every path (a first use only inside a lane
+            // branch leaves the loads "pending" at the loop header, where it then waits for
+            // every load in flight, the next group's included).
+            auto consume = [&](uint32_t k0, uint32_t q, const uint4 (&R)[4]) {
+                const uint32_t k = k0 + lane;
+                uint32_t part = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) part += sum16(R[c].x) + sum16(R[c].y) + sum16(R[c].z) + sum16(R[c].w);
+                const int left = (int)l_dge[q] - 64 - 64 * (int)(k - l_cs[q]);   // chunk bytes in the datagram
+                if (left < 64) {                                       // the frame's last chunk
+                    part = 0;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) part += chunk_sum(R[c], 0, left - 16 * c);
+                }
+                part = k < total ? part : 0u;
+                const uint32_t P = scan_dpp(part);
+                const uint32_t lo = max(my_cs, k0), hi = min(my_cs + my_nt, k0 + 64u);
+                const uint32_t ph = __shfl(P, (int)((hi > k0 ? hi - 1u - k0 : 0u) & 63u), 64);
+                const uint32_t pl = __shfl(P, (int)((lo > k0 ? lo - 1u - k0 : 0u) & 63u), 64);
+                if (lo < hi) tsum += ph - (lo > k0 ? pl : 0u);
+            };
+            // Two groups in flight; one back edge, after the second group is consumed (a loop
+            // exit between the two halves leaves the second group's loads pending at the
+            // header, which then waits for everything). Groups past the end load from offset 0
+            // and contribute nothing.
+            uint32_t qa, qb;
+            uint4 Ra[4], Rb[4];
+            issue(0, qa, Ra);
+            for (uint32_t k0 = 0;; k0 += 128) {
+                issue(k0 + 64, qb, Rb);
+                consume(k0, qa, Ra);
+                issue(k0 + 128, qa, Ra);
+                consume(k0 + 64, qb, Rb);
+                if (k0 + 128 >= total) break;
+            }
+            wave_sync();
+            if (pd) {
+                const bool ok = fold32(fold32(tsum) + (dw >> 16)) == 0xFFFFu;
+                mstage[i] = (m & ~0x60u) | ((ok ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD) << 5);
+                acc_f0 += ok ? 0x10000u : 0x1000000u;
+            }
+        }
+    }
     }
 
     // ---- tile counters: one row per wave (lanes 0-15), summed by the readers ----

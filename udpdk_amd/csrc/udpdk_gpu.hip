@@ -259,9 +259,9 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
             ok = ok && hipHostMalloc((void **)&P.h_res, sizeof(DevResult), hipHostMallocDefault) == hipSuccess;
         }
         if (!ok) break;
-        // rx_classify needs up to 90 KiB of dynamic LDS at 16384 lanes
+        // rx_classify needs up to 141 KiB of dynamic LDS (16384 lanes, 8192-frame tiles)
         if (hipFuncSetAttribute((const void *)rx_classify, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024) != hipSuccess) break;
+                                (int)classify_lds_bytes(UDPDK_GPU_MAX_LANES, RX_TILE_MAX)) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatterw, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -539,7 +539,10 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     ra.dbg = c->dbg;
     ra.key_bits = c->key_bits;
     ra.frames_bytes = (uint32_t)bt->frames_bytes;
-    ra.rsrc_bytes = (uint32_t)std::min<uint64_t>((bt->frames_bytes + 15) & ~15ull, 0xFFFFFFFFull);
+    // Buffer loads are range-checked per dword (a dword is returned only if it ends within the
+    // range, tools/probe/range_probe.hip) and the kernels load at byte-aligned frame offsets:
+    // +3 keeps every dword holding a frame byte in range.
+    ra.rsrc_bytes = (uint32_t)std::min<uint64_t>((bt->frames_bytes + 3 + 15) & ~15ull, 0xFFFFFFFFull);
     ra.n = bt->n;
     ra.tile_frames = T;
     ra.n_tiles = tiles;
