@@ -155,7 +155,7 @@ def time_loop(rx: Rx, steps: int, warmup: int, barrier, timing_every: int):
     gpu_ms = ev.elapsed_ms()
     ev.close()
     st = rx.check()
-    ms, n = ctx.timing_read() if timing_every else ([0.0] * 4, [0] * 4)
+    ms, n = ctx.timing_read() if timing_every else ([0.0] * abi.N_KERNEL_IDS, [0] * abi.N_KERNEL_IDS)
     ctx.timing(0)
     kt = {name: 1e3 * ms[k] / n[k] for k, name in
           enumerate(("rx_classify", "rx_scan", "rx_scatter")) if n[k]}
@@ -243,6 +243,88 @@ def tx_line(ctx, payload_len: int, n: int, steps: int):
     return {"workload": f"TX {n} x {payload_len + 42} B frames", "mpkt_s": round(n / us, 1),
             "us_per_launch": round(us, 2), "gbps": round(nbytes / us / 1e3, 1),
             "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4)}
+
+
+def gather_line(ctx, cfg: int, steps: int, slot: int = 2048):
+    """udpdk_gpu_rx_gather (f1, the batch form of recvfrom) over every delivery of one RX batch
+    of config `cfg`: payload slots of `slot` bytes + length + source address per datagram, GPU
+    time from events around `steps` back-to-back launches. Bytes per datagram: payload read +
+    payload written + 16 header + 4 lane entry + 6 descriptor + 10 outputs."""
+    w = F.config_batch(cfg)
+    b = w.batch
+    ctx.upload_snapshot(abi.snapshot_from_lists(w.port_lists(), w.n_sockets))
+    db = abi.rx_upload(ctx, b.frames, b.offset, b.length)
+    db.frames_bytes = b.frames_bytes
+    out = abi.rx_alloc_out(ctx, b.n, w.n_sockets, b.n)
+    _, loff, pkt, _, rc = abi.rx_run(ctx, db, out)
+    d = int(loff[-1])
+    g = abi.rx_alloc_gather(ctx, d, slot)
+    for _ in range(3):
+        abi._check(abi.rx_gather_enqueue(ctx, db, out.lane_pkt, 0, g), "udpdk_gpu_rx_gather")
+    ev = HipEvents(ctx)
+    ctx.sync()
+    ev.record(0)
+    for _ in range(steps):
+        abi.rx_gather_enqueue(ctx, db, out.lane_pkt, 0, g)
+    ev.record(1)
+    ctx.sync()
+    us = 1e3 * ev.elapsed_ms() / steps
+    ev.close()
+    lens = ctx.download(g.length, np.uint32, d)
+    nbytes = 2 * int(lens.astype(np.int64).sum()) + 36 * d
+    for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt, g.payload,
+              g.length, g.src_ip, g.src_port):
+        x.free()
+    return {"workload": f"gather {w.name}, {slot} B slots", "mdgram_s": round(d / us, 1),
+            "us_per_launch": round(us, 2), "gbps": round(nbytes / us / 1e3, 1),
+            "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4)}
+
+
+def end_to_end_async(ctx, cfg: int, reps: int):
+    """The same host-resident batch stream through udpdk_gpu_rx_host_async with pipelining depth
+    2: batch k's H2D overlaps batch k-1's kernels and D2H (PCIe is full duplex); one
+    udpdk_gpu_rx_host_wait at the end. Frames in pinned memory; outputs alternate between two
+    pinned sets."""
+    w = F.config_batch(cfg)
+    b = w.batch
+    ctx.upload_snapshot(abi.snapshot_from_lists(w.port_lists(), w.n_sockets))
+    L = abi.lib()
+
+    def pinned(nbytes):
+        p = C.c_void_p()
+        abi._check(L.udpdk_gpu_host_alloc(ctx.handle, max(16, nbytes), C.byref(p)), "host_alloc")
+        return p
+    held = [pinned(b.frames_bytes)]
+    C.memmove(held[0].value, b.frames.ctypes.data, b.frames_bytes)
+    outs = []
+    for _ in range(2):
+        o = (pinned(4 * b.n), pinned(4 * (w.n_sockets + 1)), pinned(4 * b.n), abi.RxStats())
+        held += list(o[:3])
+        outs.append(o)
+    ctx.pipeline(2)
+
+    def run(k):
+        o = outs[k % 2]
+        abi._check(L.udpdk_gpu_rx_host_async(ctx.handle, held[0].value, b.frames_bytes,
+                                             b.offset.ctypes.data, b.length.ctypes.data, None, b.n,
+                                             o[0].value, o[1].value, o[2].value, b.n, C.byref(o[3])),
+                   "udpdk_gpu_rx_host_async")
+    for k in range(2):
+        run(k)
+    abi._check(L.udpdk_gpu_rx_host_wait(ctx.handle), "udpdk_gpu_rx_host_wait")
+    t0 = time.perf_counter()
+    for k in range(reps):
+        run(k)
+    abi._check(L.udpdk_gpu_rx_host_wait(ctx.handle), "udpdk_gpu_rx_host_wait")
+    dt = (time.perf_counter() - t0) / reps
+    ok = all(int(o[3].deliveries) == b.n for o in outs)
+    ctx.pipeline(1)
+    for p in held:
+        L.udpdk_gpu_host_free(ctx.handle, p)
+    return {"workload": w.name, "mpkt_s": round(b.n / dt / 1e6, 1),
+            "frame_gbps": round(int(b.length.sum()) / dt / 1e9, 2), "ms_per_batch": round(dt * 1e3, 3),
+            "all_delivered": ok,
+            "path": "pinned host frames -> H2D -> rx pipeline -> D2H meta+lanes, two pipes overlapped"}
 
 
 def end_to_end(ctx, cfg: int, reps: int):
@@ -389,6 +471,11 @@ def main():
                 e2e.append(end_to_end(ctx, cfg, 10))
             except Exception as e:
                 e2e.append({"config": cfg, "error": repr(e)})
+        for cfg in (2, 3):
+            try:
+                e2e.append(end_to_end_async(ctx, cfg, 20))
+            except Exception as e:
+                e2e.append({"config": cfg, "async": True, "error": repr(e)})
         line["end_to_end"] = e2e
         tx = []
         for plen in (22, 1458):                  # 64 B and 1500 B frames
@@ -397,6 +484,13 @@ def main():
             except Exception as e:
                 tx.append({"payload": plen, "error": repr(e)})
         line["tx"] = tx
+        ga = []
+        for cfg in (2, 3):
+            try:
+                ga.append(gather_line(ctx, cfg, 50))
+            except Exception as e:
+                ga.append({"config": cfg, "error": repr(e)})
+        line["gather"] = ga
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()

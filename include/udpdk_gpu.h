@@ -102,6 +102,9 @@ enum udpdk_rx_counter {
 #define UDPDK_GPU_MAX_BINDS        (1u << 20)
 #define UDPDK_GPU_MAX_PORT_BINDS   4095u
 #define UDPDK_UDP_PORTS            65536u     /* UDP_MAX_PORT, udpdk_constants.h:13 */
+/* Readable bytes the RX kernels need after frames_bytes (byte-aligned dword loads of a batch's
+ * last frame may end up to 3 bytes past it). */
+#define UDPDK_GPU_FRAMES_TAILROOM  16u
 
 /* ---------------------------------------------------------------------------------------------
  * Context
@@ -170,7 +173,10 @@ int udpdk_gpu_bind_snapshot_upload(udpdk_gpu_ctx *ctx, const udpdk_bind_snapshot
  * ------------------------------------------------------------------------------------------- */
 typedef struct {
     const uint8_t  *frames_dev;   /* frame bytes (rte_pktmbuf_mtod, Ethernet first, no FCS),
-                                     16-byte aligned base                                      */
+                                     16-byte aligned base, readable for frames_bytes +
+                                     UDPDK_GPU_FRAMES_TAILROOM bytes (tailroom, as every DPDK
+                                     mbuf data room has); bytes past frames_bytes never
+                                     affect a result                                          */
     uint64_t        frames_bytes; /* < 2^32                                                    */
     const uint32_t *offset_dev;   /* [n] byte offset of each frame in frames_dev               */
     const uint16_t *length_dev;   /* [n] data_len of each frame                                */
@@ -220,6 +226,46 @@ int udpdk_gpu_rx_host(udpdk_gpu_ctx *ctx,
                       uint32_t *lane_pkt_host, uint32_t lane_cap,
                       udpdk_rx_stats_t *stats);
 
+/* Asynchronous form of udpdk_gpu_rx_host for a stream of host-resident batches: the staging,
+ * H2D, RX pipeline, counter reduction and D2H of meta, lane_off and lane_pkt[0, lane_cap) are
+ * enqueued on the next pipe (udpdk_gpu_pipeline_depth) with its own staging buffers, and the
+ * call returns; with depth 2 one batch's PCIe copies overlap the other's kernels and copies in
+ * the opposite direction. At most `depth` calls are outstanding (a call first completes the one
+ * that used its pipe). Host inputs must stay untouched, and outputs and *stats are valid, only
+ * once udpdk_gpu_rx_host_wait returns (or a later call reuses the pipe). */
+int udpdk_gpu_rx_host_async(udpdk_gpu_ctx *ctx,
+                            const uint8_t *frames_host, uint64_t frames_bytes,
+                            const uint32_t *offset_host, const uint16_t *length_host,
+                            const uint32_t *ptype_host, uint32_t n,
+                            uint32_t *meta_host, uint32_t *lane_off_host,
+                            uint32_t *lane_pkt_host, uint32_t lane_cap,
+                            udpdk_rx_stats_t *stats);
+/* Complete every outstanding udpdk_gpu_rx_host_async call (oldest first). */
+int udpdk_gpu_rx_host_wait(udpdk_gpu_ctx *ctx);
+
+/* ---------------------------------------------------------------------------------------------
+ * RX payload delivery: the batch form of udpdk_recvfrom (udpdk_syscall.c:401-488) over the lane
+ * entries [first, first + count) of an RX output (e.g. one socket's lane, lane_off[s] ..
+ * lane_off[s + 1], or all of them). Entry k = frame lane_pkt[first + k]: its UDP payload, frame
+ * bytes [42, 42 + min(data_len - 42, dgram_len - 8)) (Ethernet padding trimmed, :459-466),
+ * truncated to slot_bytes (recvfrom's len), goes to payload_dev + k * slot_bytes; len_dev[k] =
+ * bytes copied (recvfrom's return value); src_ip_dev[k] / src_port_dev[k] = ip_hdr->src_addr /
+ * udp_hdr->src_port as raw network-order values (sin_addr / sin_port, :446-447). Slot bytes past
+ * len_dev[k] are scratch. Async on the context stream; the batch must be the one lane_pkt_dev
+ * was computed from.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+    uint8_t  *payload_dev;    /* [count * slot_bytes], 16-byte aligned                         */
+    uint32_t  slot_bytes;     /* per-datagram buffer (recvfrom len), multiple of 16, >= 16      */
+    uint32_t *len_dev;        /* [count]                                                       */
+    uint32_t *src_ip_dev;     /* [count]                                                       */
+    uint16_t *src_port_dev;   /* [count]                                                       */
+} udpdk_rx_gather_t;
+
+int udpdk_gpu_rx_gather(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch,
+                        const uint32_t *lane_pkt_dev, uint32_t first, uint32_t count,
+                        const udpdk_rx_gather_t *out);
+
 /* ---------------------------------------------------------------------------------------------
  * TX: Eth/IPv4/UDP header build + rte_ipv4_cksum + payload copy (udpdk_syscall.c:314-356)
  * ------------------------------------------------------------------------------------------- */
@@ -261,7 +307,8 @@ enum udpdk_gpu_kernel_id {
     UDPDK_K_RX_SCAN     = 1,   /* lane offsets (one or three launches)                         */
     UDPDK_K_RX_SCATTER  = 2,   /* stable per-lane compaction (rx_scatter, or rx_compact1)      */
     UDPDK_K_TX_BUILD    = 3,
-    UDPDK_N_KERNEL_IDS  = 4
+    UDPDK_K_RX_GATHER   = 4,   /* payload delivery (udpdk_gpu_rx_gather)                       */
+    UDPDK_N_KERNEL_IDS  = 5
 };
 int udpdk_gpu_timing_enable(udpdk_gpu_ctx *ctx, int enable);
 /* Synchronises; ms[k] = accumulated device ms, launches[k] = number of timed calls. Resets. */

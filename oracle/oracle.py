@@ -41,6 +41,7 @@ def lib() -> C.CDLL:
         L.oracle_rte_ipv4_cksum.argtypes = [P]
         L.oracle_tx_frame.argtypes = [P, P, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32,
                                       C.c_uint32, C.c_uint32, P, C.c_uint32, P]
+        L.oracle_recv_gather.argtypes = [P, P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, P, P, P, P]
         _lib = L
     return _lib
 
@@ -135,3 +136,21 @@ def bindtable_from_lists(port_lists: dict[int, list[tuple[int, int, int]]]) -> B
         for ip, s, reuse in specs:
             assert bt.add(s, ip, p, 15 if reuse else 0) == 0
     return bt
+
+
+def recv_gather(frames: np.ndarray, offset: np.ndarray, length: np.ndarray, lane_pkt: np.ndarray,
+                first: int, count: int, slot: int):
+    """recvfrom payload delivery (udpdk_syscall.c:401-488) for lane entries [first, first+count):
+    (payload [count, slot] u8, len u32, src_ip u32 raw, src_port u16 raw)."""
+    fr = np.ascontiguousarray(frames, np.uint8)
+    off = np.ascontiguousarray(offset, np.uint32)
+    ln = np.ascontiguousarray(length, np.uint16)
+    lp = np.ascontiguousarray(lane_pkt, np.uint32)
+    pay = np.zeros((max(1, count), slot), np.uint8)
+    olen = np.zeros(max(1, count), np.uint32)
+    sip = np.zeros(max(1, count), np.uint32)
+    spt = np.zeros(max(1, count), np.uint16)
+    P = lambda a: a.ctypes.data_as(C.c_void_p)
+    lib().oracle_recv_gather(P(fr), P(off), P(ln), P(lp), first, count, slot, P(pay), P(olen),
+                             P(sip), P(spt))
+    return pay[:count], olen[:count], sip[:count], spt[:count]

@@ -489,3 +489,28 @@ void oracle_tx_frame(const uint8_t src_mac[6], const uint8_t dst_mac[6], uint32_
     udp[6] = 0; udp[7] = 0;                                               /* :343 */
     if (len) memcpy(out + 42, payload, len);                              /* :355-356 */
 }
+
+/* ---------------------------------------------------------------------------------------------
+ * recvfrom payload delivery, udpdk_syscall.c:401-488 (single-segment mbufs), for lane entries
+ * [first, first + count): entry k's payload into out_payload + k * len (len = recvfrom's len),
+ * bytes copied into out_len[k], ip_hdr->src_addr / udp_hdr->src_port raw into out_src_*.
+ * ------------------------------------------------------------------------------------------- */
+void oracle_recv_gather(const uint8_t *frames, const uint32_t *offset, const uint16_t *length,
+                        const uint32_t *lane_pkt, uint32_t first, uint32_t count, uint32_t len,
+                        uint8_t *out_payload, uint32_t *out_len, uint32_t *out_src_ip,
+                        uint16_t *out_src_port)
+{
+    for (uint32_t k = 0; k < count; k++) {
+        const uint8_t *f = frames + offset[lane_pkt[first + k]];
+        const uint32_t data_len = length[lane_pkt[first + k]];
+        const uint16_t dgram_len = (uint16_t)(((uint32_t)f[38] << 8) | f[39]);
+        const uint16_t dgram_payl_len = (uint16_t)(dgram_len - 8u);                 /* :436 */
+        memcpy(&out_src_ip[k], f + 26, 4);                                          /* :447 */
+        out_src_port[k] = (uint16_t)((uint32_t)f[34] | ((uint32_t)f[35] << 8));      /* :446 */
+        uint32_t seg_len = data_len - 42u;                                          /* :458 */
+        if (seg_len > dgram_payl_len) seg_len = dgram_payl_len;                     /* :459-462 */
+        const uint32_t eff = seg_len < len ? seg_len : len;                         /* :464-468 */
+        memcpy(out_payload + (size_t)k * len, f + 42, eff);                         /* :470 */
+        out_len[k] = eff;                                                           /* :487 */
+    }
+}

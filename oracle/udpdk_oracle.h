@@ -67,6 +67,14 @@ void oracle_tx_frame(const uint8_t src_mac[6], const uint8_t dst_mac[6], uint32_
                      uint32_t dst_ip, uint32_t dst_port, const uint8_t *payload, uint32_t len,
                      uint8_t *out);
 
+/* recvfrom payload delivery (udpdk_syscall.c:401-488) for lane entries [first, first + count):
+ * payload k into out_payload + k * len (len = recvfrom's len), out_len[k] = bytes copied,
+ * out_src_ip / out_src_port = raw ip src_addr / udp src_port. */
+void oracle_recv_gather(const uint8_t *frames, const uint32_t *offset, const uint16_t *length,
+                        const uint32_t *lane_pkt, uint32_t first, uint32_t count, uint32_t len,
+                        uint8_t *out_payload, uint32_t *out_len, uint32_t *out_src_ip,
+                        uint16_t *out_src_port);
+
 #ifdef __cplusplus
 }
 #endif

@@ -217,3 +217,43 @@ def test_pipeline_depth2(gpu_ctx):
         assert np.array_equal(np.array(st.counters[:], np.uint64), wc)   # the last call's
     finally:
         gpu_ctx.pipeline(1)
+
+
+def test_rx_host_sync_and_async(gpu_ctx):
+    """Host-resident batches (udpdk_gpu_rx_host and the two-pipe udpdk_gpu_rx_host_async) give
+    the device path's results; the frames buffer is staged at exactly its size + tailroom."""
+    import ctypes as C
+    b = F.mixed_batch(21, 5000, [10001, 10002, 10004], [9, 20000], [IP1, IP9])
+    lists = {k: v for k, v in MIXED_LISTS.items()}
+    gpu_ctx.upload_snapshot(abi.snapshot_from_lists(lists, 8))
+    bt = O.bindtable_from_lists(lists)
+    want = O.rx(bt, b.frames, b.frames_bytes, b.offset, b.length, None, 8)
+    L = abi.lib()
+    fr = np.ascontiguousarray(b.frames[:b.frames_bytes])
+
+    def call(fn, depth):
+        gpu_ctx.pipeline(depth)
+        res = []
+        for k in range(3):
+            meta = np.zeros(b.n, np.uint32)
+            loff = np.zeros(9, np.uint32)
+            pkt = np.zeros(4 * b.n, np.uint32)
+            st = abi.RxStats()
+            rc = fn(gpu_ctx.handle, fr.ctypes.data, b.frames_bytes, b.offset.ctypes.data,
+                    b.length.ctypes.data, None, b.n, meta.ctypes.data, loff.ctypes.data,
+                    pkt.ctypes.data, 4 * b.n, C.byref(st))
+            assert rc == 0
+            res.append((meta, loff, pkt, st))
+        if fn is L.udpdk_gpu_rx_host_async:
+            assert L.udpdk_gpu_rx_host_wait(gpu_ctx.handle) == 0
+        gpu_ctx.pipeline(1)
+        return res
+
+    for fn, depth in ((L.udpdk_gpu_rx_host, 1), (L.udpdk_gpu_rx_host_async, 2)):
+        for meta, loff, pkt, st in call(fn, depth):
+            assert np.array_equal(meta, want[0])
+            assert np.array_equal(loff, want[1])
+            d = int(st.deliveries)
+            assert d == int(want[1][-1])
+            assert np.array_equal(pkt[:d], want[2])
+            assert np.array_equal(np.array(st.counters[:], np.uint64), want[3])

@@ -23,6 +23,7 @@ VERDICT_NAMES = ["DELIVERED", "NOT_IPV4", "FRAG", "NOT_UDP", "NO_BIND", "NO_MATC
                  "BAD_DESC"]
 UDP_NONE, UDP_OK, UDP_BAD = 0, 1, 2
 N_COUNTERS = 16
+N_KERNEL_IDS = 5          # udpdk_gpu_kernel_id: classify, scan, scatter, tx_build, rx_gather
 C_DELIVERIES, C_IP_BAD, C_UDP_OK, C_UDP_BAD, C_UDP_NONE, C_LEN_BAD, C_IHL_NE5, C_BYTES = range(8, 16)
 K_RX_CLASSIFY, K_RX_SCAN, K_RX_SCATTER, K_TX_BUILD = range(4)
 MAX_LANES = 16384
@@ -76,6 +77,11 @@ class RxStats(C.Structure):
                 ("overflow", C.c_uint32)]
 
 
+class RxGather(C.Structure):
+    _fields_ = [("payload_dev", C.c_void_p), ("slot_bytes", C.c_uint32), ("len_dev", C.c_void_p),
+                ("src_ip_dev", C.c_void_p), ("src_port_dev", C.c_void_p)]
+
+
 class TxConfig(C.Structure):
     _fields_ = [("src_mac", C.c_uint8 * 6), ("dst_mac", C.c_uint8 * 6), ("src_ip", C.c_uint32)]
 
@@ -117,6 +123,11 @@ _PROTOS = {
     "udpdk_gpu_join": (C.c_int, [_P]),
     "udpdk_gpu_rx_host": (C.c_int, [_P, _P, C.c_uint64, _P, _P, _P, C.c_uint32, _P, _P, _P,
                                     C.c_uint32, C.POINTER(RxStats)]),
+    "udpdk_gpu_rx_host_async": (C.c_int, [_P, _P, C.c_uint64, _P, _P, _P, C.c_uint32, _P, _P, _P,
+                                          C.c_uint32, C.POINTER(RxStats)]),
+    "udpdk_gpu_rx_host_wait": (C.c_int, [_P]),
+    "udpdk_gpu_rx_gather": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint32, C.c_uint32,
+                                      C.POINTER(RxGather)]),
     "udpdk_gpu_tx_build": (C.c_int, [_P, C.POINTER(TxConfig), C.POINTER(TxBatch), C.POINTER(TxOut)]),
     "udpdk_gpu_timing_enable": (C.c_int, [_P, C.c_int]),
     "udpdk_gpu_timing_read": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
@@ -307,8 +318,8 @@ class GpuContext:
         _check(lib().udpdk_gpu_timing_enable(self.handle, int(every)), "timing_enable")
 
     def timing_read(self):
-        ms = (C.c_double * 4)()
-        n = (C.c_uint32 * 4)()
+        ms = (C.c_double * N_KERNEL_IDS)()
+        n = (C.c_uint32 * N_KERNEL_IDS)()
         _check(lib().udpdk_gpu_timing_read(self.handle, ms, n), "timing_read")
         return list(ms), list(n)
 
@@ -333,9 +344,18 @@ class RxDeviceOut:
     n_lanes: int
 
 
+FRAMES_TAILROOM = 16    # UDPDK_GPU_FRAMES_TAILROOM
+
+
 def rx_upload(ctx: GpuContext, frames: np.ndarray, offset: np.ndarray, length: np.ndarray,
               ptype: np.ndarray | None = None) -> RxDeviceBatch:
-    return RxDeviceBatch(ctx.upload(frames), int(frames.nbytes), ctx.upload(offset.astype(np.uint32)),
+    """Device copies of a batch; the frames buffer gets UDPDK_GPU_FRAMES_TAILROOM readable bytes
+    past the frame data."""
+    fb = ctx.alloc(int(frames.nbytes) + FRAMES_TAILROOM)
+    _check(lib().udpdk_gpu_h2d(ctx.handle, C.c_void_p(fb.ptr), frames.ctypes.data_as(C.c_void_p),
+                               int(frames.nbytes)), "udpdk_gpu_h2d")
+    ctx.sync()
+    return RxDeviceBatch(fb, int(frames.nbytes), ctx.upload(offset.astype(np.uint32)),
                          ctx.upload(length.astype(np.uint16)),
                          ctx.upload(ptype.astype(np.uint32)) if ptype is not None else None,
                          int(len(offset)))
@@ -370,6 +390,42 @@ def rx_run(ctx: GpuContext, b: RxDeviceBatch, o: RxDeviceOut):
     d = min(int(st.deliveries), o.lane_cap)
     pkt = ctx.download(o.lane_pkt, np.uint32, d)
     return meta, loff, pkt, np.array(st.counters[:], np.uint64), rc
+
+
+@dataclass
+class RxDeviceGather:
+    payload: DeviceBuffer
+    slot_bytes: int
+    length: DeviceBuffer
+    src_ip: DeviceBuffer
+    src_port: DeviceBuffer
+    count: int
+
+
+def rx_alloc_gather(ctx: GpuContext, count: int, slot_bytes: int) -> RxDeviceGather:
+    c = max(1, count)
+    return RxDeviceGather(ctx.alloc(c * slot_bytes), slot_bytes, ctx.alloc(4 * c), ctx.alloc(4 * c),
+                          ctx.alloc(2 * c), count)
+
+
+def rx_gather_enqueue(ctx: GpuContext, b: RxDeviceBatch, lane_pkt: DeviceBuffer, first: int,
+                      g: RxDeviceGather) -> int:
+    bt = RxBatch(b.frames.ptr, b.frames_bytes, b.offset.ptr, b.length.ptr,
+                 b.ptype.ptr if b.ptype is not None else None, b.n)
+    gt = RxGather(g.payload.ptr, g.slot_bytes, g.length.ptr, g.src_ip.ptr, g.src_port.ptr)
+    return lib().udpdk_gpu_rx_gather(ctx.handle, C.byref(bt), C.c_void_p(lane_pkt.ptr), first,
+                                     g.count, C.byref(gt))
+
+
+def rx_gather_run(ctx: GpuContext, b: RxDeviceBatch, lane_pkt: DeviceBuffer, first: int,
+                  g: RxDeviceGather):
+    """Gather lane entries [first, first + count) and download (payload slots as a
+    [count, slot_bytes] u8 array, len, src_ip, src_port)."""
+    _check(rx_gather_enqueue(ctx, b, lane_pkt, first, g), "udpdk_gpu_rx_gather")
+    ctx.sync()
+    pay = ctx.download(g.payload, np.uint8, g.count * g.slot_bytes).reshape(g.count, g.slot_bytes)
+    return (pay, ctx.download(g.length, np.uint32, g.count), ctx.download(g.src_ip, np.uint32, g.count),
+            ctx.download(g.src_port, np.uint16, g.count))
 
 
 def geometry(n: int, n_lanes: int) -> tuple[int, int]:

@@ -136,7 +136,27 @@ struct TxArgs {
     uint32_t mac_lo[3];        // 12 MAC bytes: dst(6) src(6) as three LE dwords
 };
 
+// Payload delivery (rx_gather): lane entries [first, first + count) -> payload slots + source
+// addresses (the batch form of udpdk_recvfrom, udpdk_syscall.c:401-488).
+constexpr int GATHER_BLOCK = 256;
+struct GatherArgs {
+    const uint8_t  *frames;
+    const uint32_t *offset;
+    const uint16_t *length;
+    const uint32_t *lane_pkt;
+    uint8_t  *payload;
+    uint32_t *len_out;
+    uint32_t *src_ip;
+    uint16_t *src_port;
+    uint32_t first;
+    uint32_t count;
+    uint32_t slot_bytes;
+    uint32_t rsrc_bytes;
+    uint32_t n;
+};
+
 __global__ void rx_classify(RxArgs a);
+__global__ void rx_gather(GatherArgs a);
 __global__ void rx_scan_small(ScanArgs a);
 __global__ void rx_scan_reduce(ScanArgs a);
 __global__ void rx_scan_top(ScanArgs a, uint32_t n_part);

@@ -1,0 +1,58 @@
+// rx_gather.hip — gfx950 payload delivery: the batch form of udpdk_recvfrom
+// (udpdk_syscall.c:401-488) over a range of lane entries produced by the RX pipeline.
+//
+// Lane entry k (frame i = lane_pkt[first + k]): payload = frame bytes
+// [42, 42 + min(data_len - 42, dgram_len - 8)) (Ethernet padding trimmed, :459-466), truncated
+// to slot_bytes (recvfrom's len, :467-472), copied to payload + k * slot_bytes; len[k] = bytes
+// copied (recvfrom's return, :487); src_ip[k] / src_port[k] = ip_hdr->src_addr /
+// udp_hdr->src_port, raw (:446-447).
+//
+// One lane per entry: one byte-aligned 16-byte load of frame bytes [26, 42) gives the source
+// address, source port and dgram_len; the payload moves in 16-byte pieces, four loads in flight
+// per lane, stored as aligned 16-byte slot writes (the slot tail past len is scratch). HBM-bound:
+// bytes per entry = payload read + payload written + 16 (header) + 4 (lane entry) + 6
+// (descriptor) + 10 (len, src_ip, src_port).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "udpdk_gpu.h"
+#include "rx_common.h"
+
+namespace udpdk {
+
+__global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
+{
+    const __amdgpu_buffer_rsrc_t fr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.frames), (short)0, (int)a.rsrc_bytes, 0x00020000);
+    for (uint32_t k = blockIdx.x * GATHER_BLOCK + threadIdx.x; k - threadIdx.x < a.count;
+         k += gridDim.x * GATHER_BLOCK) {
+        const bool valid = k < a.count;
+        const uint32_t i = valid ? min(a.lane_pkt[a.first + k], a.n - 1u) : 0u;
+        const uint32_t o = a.offset[i];
+        const uint32_t len = a.length[i];
+        const auto h = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)(o + 26u), 0, 0);  // bytes 26..41
+        const uint32_t dlr = h[3] & 0xFFFFu;                                           // dgram_len, BE
+        const uint32_t dl = ((dlr & 0xFFu) << 8) | (dlr >> 8);
+        const uint32_t pl = (dl - 8u) & 0xFFFFu;                 // uint16_t dgram_payl_len (:436)
+        const uint32_t seg = len >= 42u ? len - 42u : 0u;        // data_len - offset_payload (:458)
+        const uint32_t n = valid ? min(min(seg, pl), a.slot_bytes) : 0u;
+        if (valid) {
+            a.len_out[k] = n;
+            a.src_ip[k] = h[0];
+            a.src_port[k] = (uint16_t)(h[2] & 0xFFFFu);
+        }
+        uint8_t *dst = a.payload + (size_t)k * a.slot_bytes;
+        for (uint32_t c = 0; c < n; c += 64u) {
+            uint4 v[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const auto x = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)(o + 42u + c + 16u * u), 0, 0);
+                v[u] = make_uint4(x[0], x[1], x[2], x[3]);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u)
+                if (c + 16u * u < n) *reinterpret_cast<uint4 *>(dst + c + 16u * u) = v[u];
+        }
+    }
+}
+
+} // namespace udpdk

@@ -52,6 +52,13 @@ struct Pipe {
     hipEvent_t tail = nullptr;                // join point for udpdk_gpu_join
     uint32_t last_tiles = 0;                  // tiles of this pipe's last call (counter rows)
     uint32_t last_lane_cap = 0;
+    // host-resident batches (udpdk_gpu_rx_host[_async]): staging, lazily sized
+    uint8_t *st_frames_d = nullptr; size_t st_frames_dcap = 0;
+    uint8_t *st_frames_h = nullptr; size_t st_frames_hcap = 0;
+    uint8_t *st_desc_d = nullptr; size_t st_desc_dcap = 0;
+    uint8_t *st_desc_h = nullptr; size_t st_desc_hcap = 0;
+    uint8_t *st_out_d = nullptr; size_t st_out_cap = 0;
+    udpdk_rx_stats_t *host_stats = nullptr;   // outstanding async host call: where its stats go
 };
 constexpr int MAX_PIPES = 2;
 
@@ -82,12 +89,7 @@ struct udpdk_gpu_ctx {
     size_t partial_cap = 0;
     size_t tiles_cap = 0;
 
-    // end-to-end staging (lazy)
-    uint8_t *st_frames_d = nullptr; size_t st_frames_dcap = 0;
-    uint8_t *st_frames_h = nullptr; size_t st_frames_hcap = 0;
-    uint8_t *st_desc_d = nullptr; size_t st_desc_dcap = 0;
-    uint8_t *st_desc_h = nullptr; size_t st_desc_hcap = 0;
-    uint8_t *st_out_d = nullptr; size_t st_out_cap = 0;
+    uint64_t host_calls = 0;                  // udpdk_gpu_rx_host_async calls (pipe choice)
 
     unsigned long long *dbg = nullptr;        // diagnostic stamp buffer (UDPDK_STAMPS builds)
 
@@ -96,8 +98,8 @@ struct udpdk_gpu_ctx {
     uint64_t timing_calls = 0;
     TimingSet *sets = nullptr;
     int n_sets_used = 0;
-    double ms[UDPDK_N_KERNEL_IDS] = {0, 0, 0, 0};
-    uint32_t launches[UDPDK_N_KERNEL_IDS] = {0, 0, 0, 0};
+    double ms[UDPDK_N_KERNEL_IDS] = {};
+    uint32_t launches[UDPDK_N_KERNEL_IDS] = {};
 };
 
 #define HIPC(ctx, expr)                                                      \
@@ -112,6 +114,17 @@ struct udpdk_gpu_ctx {
 namespace {
 
 uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+// Range of the frames buffer resource. Buffer loads are range-checked per dword (a dword is
+// returned only if it ends within the range, zero otherwise, with no memory access:
+// tools/probe/range_probe.hip) and the RX kernels load at byte-aligned frame offsets, so a
+// dword holding the last frame bytes may end up to 3 bytes past frames_bytes: the range is
+// frames_bytes + 3 rounded up to a dword, inside the UDPDK_GPU_FRAMES_TAILROOM bytes the frames
+// buffer must keep readable after frames_bytes (udpdk_gpu.h).
+uint32_t frames_rsrc_bytes(uint64_t frames_bytes)
+{
+    return (uint32_t)std::min<uint64_t>((frames_bytes + 3 + 3) & ~3ull, 0xFFFFFFFCull);
+}
 
 void geometry(uint32_t n, uint32_t lanes, uint32_t *T, uint32_t *tiles)
 {
@@ -288,12 +301,12 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
     (void)hipSetDevice(c->device);
     for (Pipe &P : c->pipes)
         if (P.stream) (void)hipStreamSynchronize(P.stream);
-    void *dev[] = {c->port_tab, c->binds, c->slots, c->st_frames_d, c->st_desc_d, c->st_out_d};
+    void *dev[] = {c->port_tab, c->binds, c->slots};
     for (void *p : dev) if (p) (void)hipFree(p);
-    void *host[] = {c->st_frames_h, c->st_desc_h};
-    for (void *p : host) if (p) (void)hipHostFree(p);
     for (Pipe &P : c->pipes) {
-        void *pd[] = {P.hist, P.partial, P.tile_cnt, P.res};
+        void *ph[] = {P.st_frames_h, P.st_desc_h};
+        for (void *p : ph) if (p) (void)hipHostFree(p);
+        void *pd[] = {P.hist, P.partial, P.tile_cnt, P.res, P.st_frames_d, P.st_desc_d, P.st_out_d};
         for (void *p : pd) if (p) (void)hipFree(p);
         if (P.h_res) (void)hipHostFree(P.h_res);
         if (P.tail) (void)hipEventDestroy(P.tail);
@@ -539,10 +552,7 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     ra.dbg = c->dbg;
     ra.key_bits = c->key_bits;
     ra.frames_bytes = (uint32_t)bt->frames_bytes;
-    // Buffer loads are range-checked per dword (a dword is returned only if it ends within the
-    // range, tools/probe/range_probe.hip) and the kernels load at byte-aligned frame offsets:
-    // +3 keeps every dword holding a frame byte in range.
-    ra.rsrc_bytes = (uint32_t)std::min<uint64_t>((bt->frames_bytes + 3 + 15) & ~15ull, 0xFFFFFFFFull);
+    ra.rsrc_bytes = frames_rsrc_bytes(bt->frames_bytes);
     ra.n = bt->n;
     ra.tile_frames = T;
     ra.n_tiles = tiles;
@@ -620,37 +630,73 @@ int udpdk_gpu_rx(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rx_ou
     return rc;
 }
 
+namespace {
+int enqueue_result(udpdk_gpu_ctx *c, Pipe &P);
+int read_result(Pipe &P, udpdk_rx_stats_t *st);
+} // namespace
+
 int udpdk_gpu_rx_stats(udpdk_gpu_ctx *c, udpdk_rx_stats_t *st)
 {
     if (!c || !st) return -EINVAL;
     if (c->last_pipe < 0) return -EINVAL;
     HIPC(c, hipSetDevice(c->device));
     Pipe &P = c->pipes[c->last_pipe];
+    int rc = enqueue_result(c, P);
+    if (rc) return rc;
+    HIPC(c, hipStreamSynchronize(P.stream));
+    return read_result(P, st);
+}
+
+namespace {
+
+// The counter reduction and the result row (counters, delivery total) of pipe p's last call
+// into its pinned mirror, on the pipe's stream.
+int enqueue_result(udpdk_gpu_ctx *c, Pipe &P)
+{
     if (P.last_tiles) {
         hipLaunchKernelGGL(rx_counters, dim3(1), dim3(256), 0, P.stream, (const uint32_t *)P.tile_cnt,
                            P.last_tiles, P.res->counters);
         HIPC(c, hipGetLastError());
     }
     HIPC(c, hipMemcpyAsync(P.h_res, P.res, sizeof(DevResult), hipMemcpyDeviceToHost, P.stream));
-    HIPC(c, hipStreamSynchronize(P.stream));
+    return 0;
+}
+
+int read_result(Pipe &P, udpdk_rx_stats_t *st)
+{
     for (int k = 0; k < UDPDK_N_COUNTERS; ++k) st->counters[k] = P.h_res->counters[k];
     st->deliveries = P.h_res->total;
     st->overflow = st->deliveries > P.last_lane_cap ? 1u : 0u;
     return st->overflow ? -ENOSPC : 0;
 }
 
-int udpdk_gpu_rx_host(udpdk_gpu_ctx *c, const uint8_t *frames_host, uint64_t frames_bytes,
-                      const uint32_t *offset_host, const uint16_t *length_host,
-                      const uint32_t *ptype_host, uint32_t n, uint32_t *meta_host,
-                      uint32_t *lane_off_host, uint32_t *lane_pkt_host, uint32_t lane_cap,
-                      udpdk_rx_stats_t *stats)
+// Wait for pipe p's outstanding host call, if any, and fill its stats.
+int finish_host(udpdk_gpu_ctx *c, Pipe &P)
 {
-    if (!c || !stats || !lane_off_host || n > c->max_frames) return -EINVAL;
+    if (!P.host_stats) return 0;
+    udpdk_rx_stats_t *st = P.host_stats;
+    P.host_stats = nullptr;
+    HIPC(c, hipStreamSynchronize(P.stream));
+    return read_result(P, st);
+}
+
+// One host-resident batch on pipe p, all on the pipe's stream: (pageable input: a host copy
+// into pinned staging first) H2D of frames + descriptors, the RX pipeline, the counter
+// reduction, D2H of the result row, meta, lane_off and lane_pkt[0, lane_cap).
+int enqueue_host(udpdk_gpu_ctx *c, int pipe, const uint8_t *frames_host, uint64_t frames_bytes,
+                 const uint32_t *offset_host, const uint16_t *length_host,
+                 const uint32_t *ptype_host, uint32_t n, uint32_t *meta_host,
+                 uint32_t *lane_off_host, uint32_t *lane_pkt_host, uint32_t lane_cap,
+                 udpdk_rx_stats_t *stats)
+{
+    if (!stats || !lane_off_host || n > c->max_frames) return -EINVAL;
     if (n && (!frames_host || !offset_host || !length_host || !meta_host)) return -EINVAL;
     if (lane_cap && !lane_pkt_host) return -EINVAL;
-    HIPC(c, hipSetDevice(c->device));
-    if (c->depth > 1) { int r = join_pipes(c); if (r) return r; }
-    const size_t fb = ((size_t)frames_bytes + 255) & ~(size_t)255;
+    if (frames_bytes >= (1ull << 32)) return -EINVAL;
+    Pipe &P = c->pipes[pipe];
+    const hipStream_t s = P.stream;
+    // frames + the tailroom the kernels may read past them (UDPDK_GPU_FRAMES_TAILROOM)
+    const size_t fb = (((size_t)frames_bytes + 255) & ~(size_t)255) + UDPDK_GPU_FRAMES_TAILROOM;
     const size_t desc = (size_t)n * 10 + 64;
     const size_t outb = (size_t)n * 4 + (size_t)(c->n_lanes + 1) * 4 + (size_t)lane_cap * 4 + 64;
     int rc;
@@ -660,41 +706,141 @@ int udpdk_gpu_rx_host(udpdk_gpu_ctx *c, const uint8_t *frames_host, uint64_t fra
     const bool pinned = n && hipPointerGetAttributes(&attr, frames_host) == hipSuccess &&
                         attr.type == hipMemoryTypeHost;
     (void)hipGetLastError();
-    if ((rc = ensure_dev(c, (void **)&c->st_frames_d, &c->st_frames_dcap, fb ? fb : 256))) return rc;
+    if ((rc = ensure_dev(c, (void **)&P.st_frames_d, &P.st_frames_dcap, fb))) return rc;
     if (n && !pinned &&
-        (rc = ensure_host(c, (void **)&c->st_frames_h, &c->st_frames_hcap, fb ? fb : 256))) return rc;
-    if ((rc = ensure_dev(c, (void **)&c->st_desc_d, &c->st_desc_dcap, desc))) return rc;
-    if ((rc = ensure_host(c, (void **)&c->st_desc_h, &c->st_desc_hcap, desc))) return rc;
-    if ((rc = ensure_dev(c, (void **)&c->st_out_d, &c->st_out_cap, outb))) return rc;
+        (rc = ensure_host(c, (void **)&P.st_frames_h, &P.st_frames_hcap, fb))) return rc;
+    if ((rc = ensure_dev(c, (void **)&P.st_desc_d, &P.st_desc_dcap, desc))) return rc;
+    if ((rc = ensure_host(c, (void **)&P.st_desc_h, &P.st_desc_hcap, desc))) return rc;
+    if ((rc = ensure_dev(c, (void **)&P.st_out_d, &P.st_out_cap, outb))) return rc;
     const uint8_t *src = frames_host;
     if (n && !pinned) {
-        memcpy(c->st_frames_h, frames_host, frames_bytes);
-        src = c->st_frames_h;
+        memcpy(P.st_frames_h, frames_host, frames_bytes);
+        src = P.st_frames_h;
     }
-    uint8_t *dh = c->st_desc_h;
+    uint8_t *dh = P.st_desc_h;
     memcpy(dh, offset_host, (size_t)n * 4);
     memcpy(dh + (size_t)n * 4, length_host, (size_t)n * 2);
     const size_t pt_off = ((size_t)n * 6 + 15) & ~(size_t)15;
     if (ptype_host) memcpy(dh + pt_off, ptype_host, (size_t)n * 4);
-    if (n) HIPC(c, hipMemcpyAsync(c->st_frames_d, src, frames_bytes, hipMemcpyHostToDevice, c->stream));
-    HIPC(c, hipMemcpyAsync(c->st_desc_d, dh, pt_off + (ptype_host ? (size_t)n * 4 : 0),
-                           hipMemcpyHostToDevice, c->stream));
-
-    uint32_t *meta_d = (uint32_t *)c->st_out_d;
+    if (n) HIPC(c, hipMemcpyAsync(P.st_frames_d, src, frames_bytes, hipMemcpyHostToDevice, s));
+    HIPC(c, hipMemcpyAsync(P.st_desc_d, dh, pt_off + (ptype_host ? (size_t)n * 4 : 0),
+                           hipMemcpyHostToDevice, s));
+    uint32_t *meta_d = (uint32_t *)P.st_out_d;
     uint32_t *off_d = meta_d + n;
     uint32_t *pkt_d = off_d + c->n_lanes + 1;
-    udpdk_rx_batch_t b = {c->st_frames_d, frames_bytes, (const uint32_t *)c->st_desc_d,
-                          (const uint16_t *)(c->st_desc_d + (size_t)n * 4),
-                          ptype_host ? (const uint32_t *)(c->st_desc_d + pt_off) : nullptr, n};
+    udpdk_rx_batch_t b = {P.st_frames_d, frames_bytes, (const uint32_t *)P.st_desc_d,
+                          (const uint16_t *)(P.st_desc_d + (size_t)n * 4),
+                          ptype_host ? (const uint32_t *)(P.st_desc_d + pt_off) : nullptr, n};
     udpdk_rx_out_t o = {meta_d, off_d, pkt_d, lane_cap};
-    if ((rc = rx_on_pipe(c, 0, &b, &o))) return rc;
-    if (n) HIPC(c, hipMemcpyAsync(meta_host, meta_d, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipMemcpyAsync(lane_off_host, off_d, (size_t)(c->n_lanes + 1) * 4, hipMemcpyDeviceToHost, c->stream));
-    rc = udpdk_gpu_rx_stats(c, stats);
-    const uint32_t d = std::min(stats->deliveries, lane_cap);
-    if (d) HIPC(c, hipMemcpyAsync(lane_pkt_host, pkt_d, (size_t)d * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if ((rc = rx_on_pipe(c, pipe, &b, &o))) return rc;
+    if ((rc = enqueue_result(c, P))) return rc;
+    if (n) HIPC(c, hipMemcpyAsync(meta_host, meta_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIPC(c, hipMemcpyAsync(lane_off_host, off_d, (size_t)(c->n_lanes + 1) * 4, hipMemcpyDeviceToHost, s));
+    if (lane_cap) HIPC(c, hipMemcpyAsync(lane_pkt_host, pkt_d, (size_t)lane_cap * 4, hipMemcpyDeviceToHost, s));
+    P.host_stats = stats;
+    return 0;
+}
+
+int finish_all_host(udpdk_gpu_ctx *c)
+{
+    int rc = 0;
+    const int d = std::max(1, c->depth);
+    for (int k = 0; k < d; ++k) {          // oldest first
+        Pipe &P = c->pipes[(c->host_calls + (uint64_t)k) % (uint64_t)d];
+        const int r = finish_host(c, P);
+        if (r && !rc) rc = r;
+    }
     return rc;
+}
+
+} // namespace
+
+int udpdk_gpu_rx_host(udpdk_gpu_ctx *c, const uint8_t *frames_host, uint64_t frames_bytes,
+                      const uint32_t *offset_host, const uint16_t *length_host,
+                      const uint32_t *ptype_host, uint32_t n, uint32_t *meta_host,
+                      uint32_t *lane_off_host, uint32_t *lane_pkt_host, uint32_t lane_cap,
+                      udpdk_rx_stats_t *stats)
+{
+    if (!c) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    int rc = finish_all_host(c);
+    if (rc && rc != -ENOSPC) return rc;
+    if (c->depth > 1) { int r = join_pipes(c); if (r) return r; }
+    if ((rc = enqueue_host(c, 0, frames_host, frames_bytes, offset_host, length_host, ptype_host, n,
+                           meta_host, lane_off_host, lane_pkt_host, lane_cap, stats))) return rc;
+    return finish_host(c, c->pipes[0]);
+}
+
+int udpdk_gpu_rx_host_async(udpdk_gpu_ctx *c, const uint8_t *frames_host, uint64_t frames_bytes,
+                            const uint32_t *offset_host, const uint16_t *length_host,
+                            const uint32_t *ptype_host, uint32_t n, uint32_t *meta_host,
+                            uint32_t *lane_off_host, uint32_t *lane_pkt_host, uint32_t lane_cap,
+                            udpdk_rx_stats_t *stats)
+{
+    if (!c) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    const int pipe = (int)(c->host_calls % (uint64_t)std::max(1, c->depth));
+    Pipe &P = c->pipes[pipe];
+    int rc = finish_host(c, P);                 // at most `depth` calls outstanding
+    if (rc && rc != -ENOSPC) return rc;
+    if ((rc = enqueue_host(c, pipe, frames_host, frames_bytes, offset_host, length_host, ptype_host,
+                           n, meta_host, lane_off_host, lane_pkt_host, lane_cap, stats))) return rc;
+    ++c->host_calls;
+    return 0;
+}
+
+int udpdk_gpu_rx_host_wait(udpdk_gpu_ctx *c)
+{
+    if (!c) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    return finish_all_host(c);
+}
+
+int udpdk_gpu_rx_gather(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint32_t *lane_pkt_dev,
+                        uint32_t first, uint32_t count, const udpdk_rx_gather_t *o)
+{
+    if (!c || !bt || !o) return -EINVAL;
+    if (!count) return 0;
+    if (!bt->n || !bt->frames_dev || !bt->offset_dev || !bt->length_dev || !lane_pkt_dev ||
+        !o->payload_dev || !o->len_dev || !o->src_ip_dev || !o->src_port_dev) return -EINVAL;
+    if (o->slot_bytes < 16u || (o->slot_bytes & 15u) || ((uintptr_t)o->payload_dev & 15u)) return -EINVAL;
+    if (bt->frames_bytes >= (1ull << 32) || (uint64_t)first + count > 0xFFFFFFFFull) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    if (c->depth > 1) { int r = join_pipes(c); if (r) return r; }
+    GatherArgs ga;
+    ga.frames = bt->frames_dev;
+    ga.offset = bt->offset_dev;
+    ga.length = bt->length_dev;
+    ga.lane_pkt = lane_pkt_dev;
+    ga.payload = o->payload_dev;
+    ga.len_out = o->len_dev;
+    ga.src_ip = o->src_ip_dev;
+    ga.src_port = o->src_port_dev;
+    ga.first = first;
+    ga.count = count;
+    ga.slot_bytes = o->slot_bytes;
+    ga.rsrc_bytes = frames_rsrc_bytes(bt->frames_bytes);
+    ga.n = bt->n;
+    const uint32_t grid = std::min<uint32_t>(ceil_div(count, GATHER_BLOCK), 16384);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->timing_every) {
+        HIPC(c, hipEventCreate(&e0));
+        HIPC(c, hipEventCreate(&e1));
+        HIPC(c, hipEventRecord(e0, c->stream));
+    }
+    hipLaunchKernelGGL(rx_gather, dim3(grid), dim3(GATHER_BLOCK), 0, c->stream, ga);
+    HIPC(c, hipGetLastError());
+    if (c->timing_every) {
+        HIPC(c, hipEventRecord(e1, c->stream));
+        HIPC(c, hipEventSynchronize(e1));
+        float ms = 0;
+        HIPC(c, hipEventElapsedTime(&ms, e0, e1));
+        c->ms[UDPDK_K_RX_GATHER] += ms;
+        c->launches[UDPDK_K_RX_GATHER]++;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    return 0;
 }
 
 int udpdk_gpu_tx_build(udpdk_gpu_ctx *c, const udpdk_tx_config_t *cfg, const udpdk_tx_batch_t *bt,
