@@ -8,8 +8,10 @@
 // udp_hdr->src_port, raw (:446-447).
 //
 // One lane per entry: one byte-aligned 16-byte load of frame bytes [26, 42) gives the source
-// address, source port and dgram_len; the payload moves in 16-byte pieces, four loads in flight
-// per lane, stored as aligned 16-byte slot writes (the slot tail past len is scratch). HBM-bound:
+// address, source port and dgram_len. Payloads move in 16-byte pieces stored as aligned 16-byte
+// slot writes (the slot tail past len is scratch): a wave whose payloads are all short copies
+// one per lane; otherwise the wave copies its entries two at a time with every wave-load a
+// contiguous KiB of one payload (coalesced reads and writes). HBM-bound:
 // bytes per entry = payload read + payload written + 16 (header) + 4 (lane entry) + 6
 // (descriptor) + 10 (len, src_ip, src_port).
 #include <hip/hip_runtime.h>
@@ -23,6 +25,7 @@ __global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
 {
     const __amdgpu_buffer_rsrc_t fr =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.frames), (short)0, (int)a.rsrc_bytes, 0x00020000);
+    const uint32_t lane = __lane_id();
     for (uint32_t k = blockIdx.x * GATHER_BLOCK + threadIdx.x; k - threadIdx.x < a.count;
          k += gridDim.x * GATHER_BLOCK) {
         const bool valid = k < a.count;
@@ -40,17 +43,53 @@ __global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
             a.src_ip[k] = h[0];
             a.src_port[k] = (uint16_t)(h[2] & 0xFFFFu);
         }
-        uint8_t *dst = a.payload + (size_t)k * a.slot_bytes;
-        for (uint32_t c = 0; c < n; c += 64u) {
-            uint4 v[4];
+        const uint32_t kw = k - lane;                            // the wave's first entry
+        if (!__ballot(n > 128u)) {
+            // short payloads: each lane copies its own, 16-byte pieces, four loads in flight
+            uint8_t *dst = a.payload + (size_t)k * a.slot_bytes;
+            for (uint32_t c = 0; c < n; c += 64u) {
+                uint4 v[4];
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
-                const auto x = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)(o + 42u + c + 16u * u), 0, 0);
-                v[u] = make_uint4(x[0], x[1], x[2], x[3]);
+                for (uint32_t u = 0; u < 4; ++u) {
+                    const auto x = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)(o + 42u + c + 16u * u), 0, 0);
+                    v[u] = make_uint4(x[0], x[1], x[2], x[3]);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 4; ++u)
+                    if (c + 16u * u < n) *reinterpret_cast<uint4 *>(dst + c + 16u * u) = v[u];
             }
+        } else {
+            // long payloads: the wave copies its entries one pair at a time, every wave-load a
+            // contiguous KiB of one payload (lane i: bytes 16 i .. 16 i + 15 of each KiB)
+            for (uint32_t j = 0; j < 64u; j += 2u) {
+                uint32_t nj[2], oj[2];
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u)
-                if (c + 16u * u < n) *reinterpret_cast<uint4 *>(dst + c + 16u * u) = v[u];
+                for (uint32_t u = 0; u < 2; ++u) {
+                    nj[u] = (uint32_t)__builtin_amdgcn_readlane((int)n, (int)(j + u));
+                    oj[u] = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)(j + u));
+                }
+                const uint32_t m = max(nj[0], nj[1]);
+                for (uint32_t c = 0; c < m; c += 2048u) {
+                    uint4 v[2][2];
+#pragma unroll
+                    for (uint32_t u = 0; u < 2; ++u)
+#pragma unroll
+                        for (uint32_t h2 = 0; h2 < 2; ++h2) {
+                            const uint32_t b = c + 1024u * h2 + 16u * lane;
+                            const auto x = __builtin_amdgcn_raw_buffer_load_b128(
+                                fr, (int)(b < nj[u] ? oj[u] + 42u + b : 0u), 0, 0);
+                            v[u][h2] = make_uint4(x[0], x[1], x[2], x[3]);
+                        }
+#pragma unroll
+                    for (uint32_t u = 0; u < 2; ++u)
+#pragma unroll
+                        for (uint32_t h2 = 0; h2 < 2; ++h2) {
+                            const uint32_t b = c + 1024u * h2 + 16u * lane;
+                            if (b < nj[u])
+                                *reinterpret_cast<uint4 *>(a.payload + (size_t)(kw + j + u) * a.slot_bytes + b) = v[u][h2];
+                        }
+                }
+            }
         }
     }
 }
