@@ -340,7 +340,7 @@ int main()
     auto time = [&](const char *name, auto launch) {
         for (int i = 0; i < 10; ++i) launch(fr + (i % COPIES) * N * 4);
         (void)hipEventRecord(e0, 0);
-        const int R = 200;
+        const int R = getenv("PROBE_REPS") ? atoi(getenv("PROBE_REPS")) : 200;
         for (int i = 0; i < R; ++i) launch(fr + (i % COPIES) * N * 4);
         (void)hipEventRecord(e1, 0);
         (void)hipEventSynchronize(e1);
@@ -372,7 +372,7 @@ int main()
     auto timei = [&](const char *name, auto launch) {
         for (int i = 0; i < 10; ++i) launch((const uint8_t *)(fr + (i % COPIES) * N * 4), offs + (i % COPIES) * N, lens + (i % COPIES) * N);
         (void)hipEventRecord(e0, 0);
-        const int R = 200;
+        const int R = getenv("PROBE_REPS") ? atoi(getenv("PROBE_REPS")) : 200;
         for (int i = 0; i < R; ++i) launch((const uint8_t *)(fr + (i % COPIES) * N * 4), offs + (i % COPIES) * N, lens + (i % COPIES) * N);
         (void)hipEventRecord(e1, 0);
         (void)hipEventSynchronize(e1);
