@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <chrono>
 
 using namespace udpdk;
 
@@ -57,23 +58,50 @@ int main()
     a.frames_bytes = N * FL; a.rsrc_bytes = N * FL; a.n = N; a.tile_frames = T; a.n_tiles = tiles;
     a.lane_mask = 0; a.n_lanes = 1; a.key_bits = 0;
     const uint32_t lds = classify_lds_bytes(1, T);
+    // STREAMS=2: consecutive launches alternate between two streams with their own outputs,
+    // so two launches may run concurrently
+    const int NS = getenv("STREAMS") ? atoi(getenv("STREAMS")) : 1;
+    hipStream_t ss[2];
+    uint32_t *meta2, *hist2, *tcnt2;
+    (void)hipMalloc(&meta2, (size_t)N * 4);
+    (void)hipMalloc(&hist2, tiles * 4);
+    (void)hipMalloc(&tcnt2, tiles * 64);
+    for (int k = 0; k < 2; ++k) (void)hipStreamCreateWithFlags(&ss[k], hipStreamNonBlocking);
+    uint32_t *lp1, *lp2, *lo1, *lo2, *tot1, *tot2;
+    (void)hipMalloc(&lp1, (size_t)N * 4); (void)hipMalloc(&lp2, (size_t)N * 4);
+    (void)hipMalloc(&lo1, 64); (void)hipMalloc(&lo2, 64); (void)hipMalloc(&tot1, 64); (void)hipMalloc(&tot2, 64);
     auto launch = [&](int i) {
         RxArgs b = a;
         b.frames = fr + (size_t)(i % COPIES) * N * FL;
         b.offset = off + (size_t)(i % COPIES) * N;
         b.length = len + (size_t)(i % COPIES) * N;
-        hipLaunchKernelGGL(rx_classify, dim3(tiles), dim3(CLS_BLOCK), lds, 0, b);
+        const int k = NS > 1 ? (i & 1) : 0;
+        if (k) { b.meta = meta2; b.hist = hist2; b.tile_cnt = tcnt2; }
+        hipLaunchKernelGGL(rx_classify, dim3(tiles), dim3(CLS_BLOCK), lds, ss[k], b);
+        if (getenv("COMPACT")) {              // the single-lane compaction after it, same stream
+            Compact1Args ca;
+            ca.meta = b.meta; ca.tile_count = b.hist; ca.lane_pkt = k ? lp2 : lp1;
+            ca.lane_off = k ? lo2 : lo1; ca.total = k ? tot2 : tot1; ca.n = N; ca.tile_frames = T;
+            ca.n_tiles = tiles; ca.lane_cap = N;
+            hipLaunchKernelGGL(rx_compact1, dim3(tiles), dim3(RX_BLOCK), 0, ss[k], ca);
+        }
     };
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
     for (int i = 0; i < 10; ++i) launch(i);
-    (void)hipEventRecord(e0, 0);
+    (void)hipDeviceSynchronize();
     const int R = 200;
+    const auto t0 = std::chrono::steady_clock::now();
     for (int i = 0; i < R; ++i) launch(i);
+    (void)hipDeviceSynchronize();
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    (void)hipEventRecord(e0, 0);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms; (void)hipEventElapsedTime(&ms, e0, e1);
     std::vector<uint32_t> hm(16);
     (void)hipMemcpy(hm.data(), meta, 64, hipMemcpyDeviceToHost);
-    printf("rx_classify %7.2f us per launch (meta[0] = %08x)\n", 1e3 * ms / R, hm[0]);
+    (void)ms;
+    printf("rx_classify%s %7.2f us per launch, %d stream(s) (meta[0] = %08x)\n",
+           getenv("COMPACT") ? "+compact1" : "", us / R, NS, hm[0]);
     return 0;
 }

@@ -5,16 +5,16 @@
 // (udpdk_poller.c:274-298). All integer/byte work, bound by HBM:
 //
 //   rx_classify  one workgroup (4 waves) per tile of T frames, lane = frame, each wave walking
-//       64-frame steps, software-pipelined one step ahead (the next step's descriptors and
-//       header windows are in flight while the current step is parsed).
-//       Header window: 4 x 16 B + 4 B aligned loads covering frame bytes [12, 64], funnel-
-//       shifted into 13 frame-relative dwords with lane-mask selects + alignbyte.
-//       Bytes >= 64 (the rest of the UDP datagram): 16-byte chunks swept across the wave's
-//       lanes (a wave-instruction reads consecutive bytes whatever the frame sizes), chunk sums
-//       reduced per frame by a DPP prefix scan.
-//       Demux: one 16-byte port-table entry per frame (first binding inline), the binding list
-//       only for ports with several. Writes the verdict word, the tile's per-lane delivery
-//       histogram (tile-major row hist[tile][lane]) and the tile's counter row.
+//       64-frame steps in rounds of 1024 frames. The round's descriptors are staged in LDS;
+//       the header window (frame bytes [12, 64), byte-aligned 3 x 16 B + 4 B loads, so the 13
+//       dwords are frame-relative) of the next step is in flight while the current one is
+//       parsed. Per step: IPv4 gate, fragment / protocol tests, IPv4 header checksum, the UDP
+//       checksum of datagrams that end within the window. Per round: the demux pass (all the
+//       round's 16-byte port-table entries in flight at once, first binding inline, the list
+//       walked only for ports with several) and, for longer datagrams, the tail pass (frame
+//       bytes >= 64 as 64-byte super-chunks swept across the wave's lanes, per-frame sums from
+//       a DPP prefix scan). Writes the verdict words, the tile's per-lane delivery histogram
+//       (tile-major row hist[tile][lane]) and the tile's counter row.
 //   rx_compact1  single lane without fan-out (the one bound socket of apps/pktgen): per tile,
 //       base = sum of the predecessors' counts, ballots over the verdict words, lane writes.
 //   rx_scan + rx_scatter  general case: per-lane column scan of the tile-major histogram (one
@@ -177,14 +177,6 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi, int base)
     return hm & ~lm;
 }
 
-// m[lane] ? b : a, as one v_cndmask_b32 with an SGPR-pair lane mask.
-__device__ __forceinline__ uint32_t lane_select(unsigned long long m, uint32_t a, uint32_t b)
-{
-    uint32_t r;
-    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
-    return r;
-}
-
 // Inclusive wave64 prefix sum on the DPP network (row shifts + row broadcasts; no LDS traffic).
 __device__ __forceinline__ uint32_t scan_dpp(uint32_t v)
 {
@@ -205,26 +197,9 @@ struct Win {
     uint32_t d;
 };
 
-typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
-
-// 16-byte global load the compiler does not see as a load: it cannot sink it into the branch
-// that uses it (and wait there). The destination is only valid after wait_vm<N>(), N = number
-// of vector-memory operations issued after it (cdna_hip_programming.md §5.7 item 1).
-__device__ __forceinline__ v4u32 asm_load16(const void *p)
-{
-    v4u32 r;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
-    return r;
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm(v4u32 &r)
-{
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r) : "n"(N) : "memory");
-}
-
-// 5 waves per SIMD (<= 96 VGPRs, no spill): a fifth workgroup per CU lets the next pipelined
-// launch start while this one drains
+// 4 waves per SIMD (<= 128 VGPRs, the tail pass's two groups in flight): one tile of 1024 frames
+// per workgroup puts 4 workgroups on each CU at 1 M frames. (A 96-VGPR budget spills and runs
+// 19 % slower at 64 B.)
 __global__ void __launch_bounds__(CLS_BLOCK) __attribute__((amdgpu_waves_per_eu(UDPDK_CLS_WPE, 8)))
 rx_classify(RxArgs a)
 {
@@ -328,279 +303,256 @@ rx_classify(RxArgs a)
     // rounds of RX_ROUND frames: SPR steps per wave, then the wave's tail pass for them (the
     // next round's first window is already in flight during the tail pass)
     for (uint32_t rnd = 0; rnd < steps / 16u; ++rnd) {
-    bool tail_any = false;     // some frame of the wave's steps waits for the tail pass (SGPR)
+        bool tail_any = false;     // some frame of the wave's steps waits for the tail pass (SGPR)
 #pragma unroll 1
-    for (uint32_t jstep = 0; jstep < SPR; ++jstep) {
-        const uint32_t p = t0 + st * 64 + lane;
-        const bool valid = p < t1;
-        const uint32_t off = c_off, len = c_lp & 0xFFFFu;
-        const bool good = valid && len <= a.frames_bytes && off <= a.frames_bytes - len;
+        for (uint32_t jstep = 0; jstep < SPR; ++jstep) {
+            const uint32_t p = t0 + st * 64 + lane;
+            const bool valid = p < t1;
+            const uint32_t off = c_off, len = c_lp & 0xFFFFu;
+            const bool good = valid && len <= a.frames_bytes && off <= a.frames_bytes - len;
 
-        // ---- header fields from the window registers (lane = frame) ----
-        const uint32_t g[13] = {W.a.x, W.a.y, W.a.z, W.a.w, W.b.x, W.b.y, W.b.z, W.b.w,
-                                W.c.x, W.c.y, W.c.z, W.c.w, W.d};  // g[i] = frame bytes 12+4i ..
-#ifdef UDPDK_EXP_SKELETON   // diagnostic experiment only: the loads and stores without the work
-        {
+            // ---- header fields from the window registers (lane = frame) ----
+            const uint32_t g[13] = {W.a.x, W.a.y, W.a.z, W.a.w, W.b.x, W.b.y, W.b.z, W.b.w,
+                                    W.c.x, W.c.y, W.c.z, W.c.w, W.d};  // g[i] = frame bytes 12+4i ..
+            // IPv4 gate (udpdk_poller.c:334): the ptype array's L3_IPV4 bit when given, else derived
+            // from ether_type (frames shorter than an Ethernet header are not IPv4)
+            const uint32_t eth_ip = (len >= 14u && (g[0] & 0xFFFFu) == 0x0008u) ? 0x10u : 0u;
+            const bool ipv4 = good && ((has_ptype ? (c_lp >> 12) : eth_ip) & 0x10u);
+            const uint32_t frag = ((g[2] & 0xFFu) << 8) | ((g[2] >> 8) & 0xFFu);
+            const bool l3 = ipv4 && len >= 42u;
+            const bool fragd = (frag & 0x3FFFu) != 0u;                // udpdk_poller.c:338
+            const bool not_udp = (g[2] >> 24) != 17u;                 // udpdk_poller.c:368-371
+            const bool is_udp = l3 && !fragd && !not_udp;
+            const uint32_t dport = g[6] & 0xFFFFu;                   // poller.c:372
+            STAMP(1);
+
+            // ---- everything the header window gives ----
+            // IPv4 header checksum over the fixed 20 bytes at offset 14 (RFC 1071)
+            const uint32_t ipraw = (g[0] >> 16) + sum16(g[1]) + sum16(g[2]) + sum16(g[3]) +
+                                   sum16(g[4]) + (g[5] & 0xFFFFu);
+            const bool ip_ok = fold32(ipraw) == 0xFFFFu;
+            const bool ihl_ne5 = ((g[0] >> 16) & 0x0Fu) != 5u;
+            const uint32_t dip = (g[4] >> 16) | (g[5] << 16);         // poller.c:373
+            const uint32_t ulen_raw = g[6] >> 16;
+            const uint32_t ulen = ((ulen_raw & 0xFFu) << 8) | (ulen_raw >> 8);
+            const uint32_t ucks = g[7] & 0xFFFFu;
+            const bool len_bad = ulen < 8u || 34u + ulen > len;
+            // UDP checksum (RFC 768 over the datagram, frame bytes [34, 34 + ulen), plus the pseudo-
+            // header {src, dst, proto 17, udp length}), computed only where it decides the state:
+            // a frame whose datagram ends within the window is summed here; a longer one is left to
+            // the tile's tail pass (state 3 = pending until then). Ethernet padding after the
+            // datagram is never summed.
+            const bool need_cs = is_udp && ucks != 0u && !len_bad;
+            const uint32_t dge = 34u + ulen;                          // datagram end (<= len)
+            const bool pend = need_cs && dge > 64u;
+            uint32_t ws = 0;
+#pragma unroll
+            for (int i = 6; i < 13; ++i) ws += sum16(g[i]);
+            if (__ballot(need_cs && dge < 64u)) {                     // short or padded frames
+                uint32_t wm = 0;
+#pragma unroll
+                for (int i = 6; i < 13; ++i) wm += sum16(g[i] & byte_mask(34, (int)dge, 12 + 4 * i));
+                ws = dge < 64u ? wm : ws;
+            }
+            const uint32_t us = ws + (g[5] >> 16) + (g[3] >> 16) + (g[4] & 0xFFFFu) + (dip & 0xFFFFu) +
+                                (dip >> 16) + 0x1100u + ulen_raw;
+            tail_any = tail_any || __ballot(pend) != 0ull;
+            dgl[(st * 64 + lane) & (RX_ROUND - 1u)] = dge | fold32(us) << 16;
+            STAMP(2);
+
+            // ---- next step of this wave: window loads stay in flight across the rest of this step
             const uint32_t nst = st + CLS_WAVES;
             uint32_t n_off, n_lp;
-            read_desc(nst, n_off, n_lp);
+            read_desc(nst, n_off, n_lp);      // in range of the buffers for any s (unused past the tile)
             const Win NW = load_win(nst, n_off, n_lp & 0xFFFFu);
-            uint32_t x = 0;
-#pragma unroll
-            for (int i = 0; i < 13; ++i) x ^= g[i];
-            mstage[st * 64 + lane] = x & 0xFFFF0000u;
-            acc_fan += valid ? 1u : 0u;
-            acc_v0 += valid ? 1u : 0u;
-            lane_bytes += good ? len : 0u;
+
+            // ---- what does not need the port entry: UDP state, flags, flag counters ----
+            const uint32_t state = ucks == 0u ? UDPDK_UDP_CSUM_NONE
+                                 : pend ? 3u
+                                 : (len_bad || fold32(us) != 0xFFFFu) ? UDPDK_UDP_CSUM_BAD
+                                                                       : UDPDK_UDP_CSUM_OK;
+            const uint32_t pre = !good ? UDPDK_V_BAD_DESC
+                               : !ipv4 ? UDPDK_V_NOT_IPV4
+                               : !l3 ? UDPDK_V_TRUNC
+                               : fragd ? UDPDK_V_FRAG
+                               : not_udp ? UDPDK_V_NOT_UDP : 0xFFu;       // 0xFF: UDP, demux pending
+            const uint32_t l3f = l3 ? ((ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8) : 0u;
+            const uint32_t udpf = is_udp ? (state << 5 | (len_bad ? 1u : 0u) << 7) : 0u;
+            // (pending frames count their UDP state in the tail pass)
+            acc_f0 += (l3 && !ip_ok ? 1u : 0u) | (l3 && ihl_ne5 ? 0x100u : 0u) |
+                      (is_udp && state == UDPDK_UDP_CSUM_OK ? 0x10000u : 0u) |
+                      (is_udp && state == UDPDK_UDP_CSUM_BAD ? 0x1000000u : 0u);
+            acc_f1 += (is_udp && state == UDPDK_UDP_CSUM_NONE ? 1u : 0u) | (is_udp && len_bad ? 0x100u : 0u);
+            if (good) lane_bytes += len;
+
+            // the port-table lookup waits for the round's demux pass: verdict field 0xF until then
+            mstage[st * 64 + lane] = (pre == 0xFFu ? 0xFu : pre) | l3f | udpf;
+            dstash[(st * 64 + lane) & (RX_ROUND - 1u)] = make_uint2(dport | (is_udp ? 0x10000u : 0u), dip);
+            STAMP(6);
+            // next round's descriptors into the other buffer at the wave's next-to-last step of a
+            // round (its steps of round r are 16 r + w + CLS_WAVES j, j < SPR): the last reads of that
+            // buffer were before the previous round's barrier, and the next round is first read at
+            // j = SPR - 1.
+            // Uniform across the workgroup (every wave has steps / 4 steps).
             if ((st / CLS_WAVES) % SPR == SPR - 2u && (st >> 4) + 1u < steps / 16u) {
                 stage((st >> 4) + 1u);
                 __syncthreads();
             }
             W = NW;
-            c_off = n_off; c_lp = n_lp;
+            c_off = n_off;
+            c_lp = n_lp;
             st = nst;
-            continue;
         }
-#endif
-        // IPv4 gate (udpdk_poller.c:334): the ptype array's L3_IPV4 bit when given, else derived
-        // from ether_type (frames shorter than an Ethernet header are not IPv4)
-        const uint32_t eth_ip = (len >= 14u && (g[0] & 0xFFFFu) == 0x0008u) ? 0x10u : 0u;
-        const bool ipv4 = good && ((has_ptype ? (c_lp >> 12) : eth_ip) & 0x10u);
-        const uint32_t frag = ((g[2] & 0xFFu) << 8) | ((g[2] >> 8) & 0xFFu);
-        const bool l3 = ipv4 && len >= 42u;
-        const bool fragd = (frag & 0x3FFFu) != 0u;                // udpdk_poller.c:338
-        const bool not_udp = (g[2] >> 24) != 17u;                 // udpdk_poller.c:368-371
-        const bool is_udp = l3 && !fragd && !not_udp;
-        const uint32_t dport = g[6] & 0xFFFFu;                   // poller.c:372
-        STAMP(1);
-
-        // ---- everything the header window gives ----
-        // IPv4 header checksum over the fixed 20 bytes at offset 14 (RFC 1071)
-        const uint32_t ipraw = (g[0] >> 16) + sum16(g[1]) + sum16(g[2]) + sum16(g[3]) +
-                               sum16(g[4]) + (g[5] & 0xFFFFu);
-        const bool ip_ok = fold32(ipraw) == 0xFFFFu;
-        const bool ihl_ne5 = ((g[0] >> 16) & 0x0Fu) != 5u;
-        const uint32_t dip = (g[4] >> 16) | (g[5] << 16);         // poller.c:373
-        const uint32_t ulen_raw = g[6] >> 16;
-        const uint32_t ulen = ((ulen_raw & 0xFFu) << 8) | (ulen_raw >> 8);
-        const uint32_t ucks = g[7] & 0xFFFFu;
-        const bool len_bad = ulen < 8u || 34u + ulen > len;
-        // UDP checksum (RFC 768 over the datagram, frame bytes [34, 34 + ulen), plus the pseudo-
-        // header {src, dst, proto 17, udp length}), computed only where it decides the state:
-        // a frame whose datagram ends within the window is summed here; a longer one is left to
-        // the tile's tail pass (state 3 = pending until then). Ethernet padding after the
-        // datagram is never summed.
-        const bool need_cs = is_udp && ucks != 0u && !len_bad;
-        const uint32_t dge = 34u + ulen;                          // datagram end (<= len)
-        const bool pend = need_cs && dge > 64u;
-        uint32_t ws = 0;
+        // ---- demux pass: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
+        // The round's port-table lookups of this wave, all SPR steps' 16-byte entries in flight at
+        // once (one round trip per round instead of one exposed per step). The entry carries the
+        // port's first binding; the binding list is walked only for ports with several.
+        {
+            uint4 E[SPR];
+            uint2 S[SPR];
 #pragma unroll
-        for (int i = 6; i < 13; ++i) ws += sum16(g[i]);
-        if (__ballot(need_cs && dge < 64u)) {                     // short or padded frames
-            uint32_t wm = 0;
+            for (uint32_t j = 0; j < SPR; ++j) S[j] = dstash[((st - 16u + CLS_WAVES * j) * 64 + lane) & (RX_ROUND - 1u)];
 #pragma unroll
-            for (int i = 6; i < 13; ++i) wm += sum16(g[i] & byte_mask(34, (int)dge, 12 + 4 * i));
-            ws = dge < 64u ? wm : ws;
-        }
-        const uint32_t us = ws + (g[5] >> 16) + (g[3] >> 16) + (g[4] & 0xFFFFu) + (dip & 0xFFFFu) +
-                            (dip >> 16) + 0x1100u + ulen_raw;
-        tail_any = tail_any || __ballot(pend) != 0ull;
-        dgl[(st * 64 + lane) & (RX_ROUND - 1u)] = dge | fold32(us) << 16;
-        STAMP(2);
-
-        // ---- next step of this wave: window loads stay in flight across the rest of this step
-        const uint32_t nst = st + CLS_WAVES;
-        uint32_t n_off, n_lp;
-        read_desc(nst, n_off, n_lp);      // in range of the buffers for any s (unused past the tile)
-        const Win NW = load_win(nst, n_off, n_lp & 0xFFFFu);
-
-        // ---- what does not need the port entry: UDP state, flags, flag counters ----
-        const uint32_t state = ucks == 0u ? UDPDK_UDP_CSUM_NONE
-                             : pend ? 3u
-                             : (len_bad || fold32(us) != 0xFFFFu) ? UDPDK_UDP_CSUM_BAD
-                                                                   : UDPDK_UDP_CSUM_OK;
-        const uint32_t pre = !good ? UDPDK_V_BAD_DESC
-                           : !ipv4 ? UDPDK_V_NOT_IPV4
-                           : !l3 ? UDPDK_V_TRUNC
-                           : fragd ? UDPDK_V_FRAG
-                           : not_udp ? UDPDK_V_NOT_UDP : 0xFFu;       // 0xFF: UDP, demux pending
-        const uint32_t l3f = l3 ? ((ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8) : 0u;
-        const uint32_t udpf = is_udp ? (state << 5 | (len_bad ? 1u : 0u) << 7) : 0u;
-        // (pending frames count their UDP state in the tail pass)
-        acc_f0 += (l3 && !ip_ok ? 1u : 0u) | (l3 && ihl_ne5 ? 0x100u : 0u) |
-                  (is_udp && state == UDPDK_UDP_CSUM_OK ? 0x10000u : 0u) |
-                  (is_udp && state == UDPDK_UDP_CSUM_BAD ? 0x1000000u : 0u);
-        acc_f1 += (is_udp && state == UDPDK_UDP_CSUM_NONE ? 1u : 0u) | (is_udp && len_bad ? 0x100u : 0u);
-        if (good) lane_bytes += len;
-
-        // the port-table lookup waits for the round's demux pass: verdict field 0xF until then
-        mstage[st * 64 + lane] = (pre == 0xFFu ? 0xFu : pre) | l3f | udpf;
-        dstash[(st * 64 + lane) & (RX_ROUND - 1u)] = make_uint2(dport | (is_udp ? 0x10000u : 0u), dip);
-        STAMP(6);
-        // next round's descriptors into the other buffer at the wave's next-to-last step of a
-        // round (its steps of round r are 16 r + w + CLS_WAVES j, j < SPR): the last reads of that
-        // buffer were before the previous round's barrier, and the next round is first read at
-        // j = SPR - 1.
-        // Uniform across the workgroup (every wave has steps / 4 steps).
-        if ((st / CLS_WAVES) % SPR == SPR - 2u && (st >> 4) + 1u < steps / 16u) {
-            stage((st >> 4) + 1u);
-            __syncthreads();
-        }
-        W = NW;
-        c_off = n_off;
-        c_lp = n_lp;
-        st = nst;
-    }
-    // ---- demux pass: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
-    // The round's port-table lookups of this wave, all SPR steps' 16-byte entries in flight at
-    // once (one round trip per round instead of one exposed per step). The entry carries the
-    // port's first binding; the binding list is walked only for ports with several.
-    {
-        uint4 E[SPR];
-        uint2 S[SPR];
+            for (uint32_t j = 0; j < SPR; ++j) E[j] = a.port_tab[S[j].x & 0xFFFFu];
 #pragma unroll
-        for (uint32_t j = 0; j < SPR; ++j) S[j] = dstash[((st - 16u + CLS_WAVES * j) * 64 + lane) & (RX_ROUND - 1u)];
-#pragma unroll
-        for (uint32_t j = 0; j < SPR; ++j) E[j] = a.port_tab[S[j].x & 0xFFFFu];
-#pragma unroll
-        for (uint32_t j = 0; j < SPR; ++j) {
-            const uint32_t i = (st - 16u + CLS_WAVES * j) * 64 + lane;
-            const uint32_t m = mstage[i];
-            const bool valid = t0 + i < t1;
-            const uint4 e = (S[j].x >> 16) ? E[j] : make_uint4(0, 0, 0, 0);
-            const uint32_t dip = S[j].y;
-            const bool match0 = e.x != 0u && (dip == e.z || e.z == 0u);     // poller.c:391
-            uint32_t fan = match0 ? 1u : 0u;
-            uint32_t first = match0 ? (e.w & 0x7FFFFFFFu) : 0u;
-            const bool walk = e.x > 1u && !(match0 && !(e.w >> 31));        // poller.c:396-403
-            if (__ballot(walk)) {
-                if (walk) {
-                    for (uint32_t b = 1; b < e.x; ++b) {
-                        const uint2 bd = a.binds[e.y + b];
-                        if (dip == bd.x || bd.x == 0u) {
-                            const uint32_t sock = bd.y & 0x7FFFFFFFu;
-                            if (fan > 0 && a.n_lanes > 1u)
-                                atomicAdd(&hist[sock & a.lane_mask], 1u);   // clones (rare)
-                            if (fan == 0) first = sock;
-                            ++fan;
-                            if (!(bd.y >> 31)) break;
+            for (uint32_t j = 0; j < SPR; ++j) {
+                const uint32_t i = (st - 16u + CLS_WAVES * j) * 64 + lane;
+                const uint32_t m = mstage[i];
+                const bool valid = t0 + i < t1;
+                const uint4 e = (S[j].x >> 16) ? E[j] : make_uint4(0, 0, 0, 0);
+                const uint32_t dip = S[j].y;
+                const bool match0 = e.x != 0u && (dip == e.z || e.z == 0u);     // poller.c:391
+                uint32_t fan = match0 ? 1u : 0u;
+                uint32_t first = match0 ? (e.w & 0x7FFFFFFFu) : 0u;
+                const bool walk = e.x > 1u && !(match0 && !(e.w >> 31));        // poller.c:396-403
+                if (__ballot(walk)) {
+                    if (walk) {
+                        for (uint32_t b = 1; b < e.x; ++b) {
+                            const uint2 bd = a.binds[e.y + b];
+                            if (dip == bd.x || bd.x == 0u) {
+                                const uint32_t sock = bd.y & 0x7FFFFFFFu;
+                                if (fan > 0 && a.n_lanes > 1u)
+                                    atomicAdd(&hist[sock & a.lane_mask], 1u);   // clones (rare)
+                                if (fan == 0) first = sock;
+                                ++fan;
+                                if (!(bd.y >> 31)) break;
+                            }
                         }
                     }
                 }
-            }
-            const uint32_t pre = m & 0xFu;
-            const uint32_t verdict = pre != 0xFu ? pre
-                                   : e.x == 0u ? UDPDK_V_NO_BIND
-                                   : fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
-            mstage[i] = (m & ~0xFu) | verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
-            // per-lane packed counters (8-bit fields; a lane sees <= 64 frames per tile)
-            const uint32_t vinc = valid ? 1u << (8u * (verdict & 3u)) : 0u;
-            acc_v0 += verdict < 4u ? vinc : 0u;
-            acc_v1 += verdict < 4u ? 0u : vinc;
-            acc_fan += fan;
-            const bool delivered = valid && fan > 0u;
-            // first delivery of every frame into the tile histogram; small key spaces are
-            // aggregated with a wave multi-split first (all 64 lanes may share one lane)
-            // (one lane: the tile's count is its delivery counter, written at the tile end)
-            const uint32_t key = first & a.lane_mask;
-            if (a.n_lanes == 1u) {
-            } else if (a.key_bits <= 4u) {
-                unsigned long long peers = __ballot(delivered);
-                for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
-                    const bool kb = (key >> bit) & 1u;
-                    const unsigned long long bal = __ballot(kb);
-                    peers &= kb ? bal : ~bal;
+                const uint32_t pre = m & 0xFu;
+                const uint32_t verdict = pre != 0xFu ? pre
+                                       : e.x == 0u ? UDPDK_V_NO_BIND
+                                       : fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
+                mstage[i] = (m & ~0xFu) | verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
+                // per-lane packed counters (8-bit fields; a lane sees <= 64 frames per tile)
+                const uint32_t vinc = valid ? 1u << (8u * (verdict & 3u)) : 0u;
+                acc_v0 += verdict < 4u ? vinc : 0u;
+                acc_v1 += verdict < 4u ? 0u : vinc;
+                acc_fan += fan;
+                const bool delivered = valid && fan > 0u;
+                // first delivery of every frame into the tile histogram; small key spaces are
+                // aggregated with a wave multi-split first (all 64 lanes may share one lane)
+                // (one lane: the tile's count is its delivery counter, written at the tile end)
+                const uint32_t key = first & a.lane_mask;
+                if (a.n_lanes == 1u) {
+                } else if (a.key_bits <= 4u) {
+                    unsigned long long peers = __ballot(delivered);
+                    for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
+                        const bool kb = (key >> bit) & 1u;
+                        const unsigned long long bal = __ballot(kb);
+                        peers &= kb ? bal : ~bal;
+                    }
+                    if (delivered && lane == (uint32_t)__ffsll((long long)peers) - 1u)
+                        atomicAdd(&hist[key], (uint32_t)__popcll(peers));
+                } else if (delivered) {
+                    atomicAdd(&hist[key], 1u);
                 }
-                if (delivered && lane == (uint32_t)__ffsll((long long)peers) - 1u)
-                    atomicAdd(&hist[key], (uint32_t)__popcll(peers));
-            } else if (delivered) {
-                atomicAdd(&hist[key], 1u);
             }
         }
-    }
-    // ---- tail pass: UDP checksums of the datagrams that extend past the header window ----
-    // The wave's pending frames of the round (state 3), one step (64 frames) at a time: frame
-    // bytes [64, dge) as 64-byte super-chunks, chunk j = frame bytes [64 + 64 j, 128 + 64 j)
-    // loaded as 4 byte-aligned 16-byte pieces (so the words are frame-relative whatever the
-    // frame's offset, and only a frame's last chunk needs byte masks), swept across the wave's
-    // lanes: lane i of a group takes chunk k0 + i of the step's chunk space (its frame found by
-    // binary search over the per-frame chunk starts in LDS), so a group is 4 KiB of dense frame
-    // bytes. Per-frame sums are segment sums of a DPP prefix scan; two groups in flight.
-    if (tail_any) {
-        uint32_t *l_cs = reinterpret_cast<uint32_t *>(smem + TP_OFF) + w * 192;  // [64] chunk starts
-        uint32_t *l_off = l_cs + 64, *l_dge = l_cs + 128;                       // [64] offset, dge
-        for (uint32_t s2 = st - 16u; s2 < st; s2 += CLS_WAVES) {      // this round's steps
-            const uint32_t i = s2 * 64 + lane;
-            const uint32_t m = mstage[i];
-            const bool pd = t0 + i < t1 && ((m >> 5) & 3u) == 3u;
-            if (!__ballot(pd)) continue;
-            // the frame's offset: the staged descriptor of a single-round tile, else global
-            const uint32_t fo = nbuf == 1u ? d_off[i] : a.offset[min(t0 + i, plast)];
-            const uint32_t dw = dgl[i & (RX_ROUND - 1u)];
-            const uint32_t de = pd ? dw & 0xFFFFu : 64u;
-            const uint32_t my_nt = (de - 64u + 63u) >> 6;
-            const uint32_t inc = scan_dpp(my_nt);
-            const uint32_t my_cs = inc - my_nt;
-            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-            l_cs[lane] = my_cs;
-            l_off[lane] = fo;
-            l_dge[lane] = de;
-            wave_sync();
-            uint32_t tsum = 0;
-            auto issue = [&](uint32_t k0, uint32_t &q, uint4 (&R)[4]) {
-                const uint32_t k = k0 + lane;
-                q = 0;
+        // ---- tail pass: UDP checksums of the datagrams that extend past the header window ----
+        // The wave's pending frames of the round (state 3), one step (64 frames) at a time: frame
+        // bytes [64, dge) as 64-byte super-chunks, chunk j = frame bytes [64 + 64 j, 128 + 64 j)
+        // loaded as 4 byte-aligned 16-byte pieces (so the words are frame-relative whatever the
+        // frame's offset, and only a frame's last chunk needs byte masks), swept across the wave's
+        // lanes: lane i of a group takes chunk k0 + i of the step's chunk space (its frame found by
+        // binary search over the per-frame chunk starts in LDS), so a group is 4 KiB of dense frame
+        // bytes. Per-frame sums are segment sums of a DPP prefix scan; two groups in flight.
+        if (tail_any) {
+            uint32_t *l_cs = reinterpret_cast<uint32_t *>(smem + TP_OFF) + w * 192;  // [64] chunk starts
+            uint32_t *l_off = l_cs + 64, *l_dge = l_cs + 128;                       // [64] offset, dge
+            for (uint32_t s2 = st - 16u; s2 < st; s2 += CLS_WAVES) {      // this round's steps
+                const uint32_t i = s2 * 64 + lane;
+                const uint32_t m = mstage[i];
+                const bool pd = t0 + i < t1 && ((m >> 5) & 3u) == 3u;
+                if (!__ballot(pd)) continue;
+                // the frame's offset: the staged descriptor of a single-round tile, else global
+                const uint32_t fo = nbuf == 1u ? d_off[i] : a.offset[min(t0 + i, plast)];
+                const uint32_t dw = dgl[i & (RX_ROUND - 1u)];
+                const uint32_t de = pd ? dw & 0xFFFFu : 64u;
+                const uint32_t my_nt = (de - 64u + 63u) >> 6;
+                const uint32_t inc = scan_dpp(my_nt);
+                const uint32_t my_cs = inc - my_nt;
+                const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+                l_cs[lane] = my_cs;
+                l_off[lane] = fo;
+                l_dge[lane] = de;
+                wave_sync();
+                uint32_t tsum = 0;
+                auto issue = [&](uint32_t k0, uint32_t &q, uint4 (&R)[4]) {
+                    const uint32_t k = k0 + lane;
+                    q = 0;
 #pragma unroll
-                for (int sft = 32; sft >= 1; sft >>= 1)
-                    if (l_cs[q + sft] <= k) q += sft;
-                const uint32_t base = k < total ? l_off[q] + 64u + 64u * (k - l_cs[q]) : 0u;
+                    for (int sft = 32; sft >= 1; sft >>= 1)
+                        if (l_cs[q + sft] <= k) q += sft;
+                    const uint32_t base = k < total ? l_off[q] + 64u + 64u * (k - l_cs[q]) : 0u;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) R[c] = load16(fr, base + 16u * c);
-            };
-            // The full-chunk sum reads every loaded register unconditionally, so the compiler's
-            // wait for this group is placed here on every path (a first use only inside a lane
-            // branch leaves the loads "pending" at the loop header, where it then waits for
-            // every load in flight, the next group's included).
-            auto consume = [&](uint32_t k0, uint32_t q, const uint4 (&R)[4]) {
-                const uint32_t k = k0 + lane;
-                uint32_t part = 0;
+                    for (int c = 0; c < 4; ++c) R[c] = load16(fr, base + 16u * c);
+                };
+                // The full-chunk sum reads every loaded register unconditionally, so the compiler's
+                // wait for this group is placed here on every path (a first use only inside a lane
+                // branch leaves the loads "pending" at the loop header, where it then waits for
+                // every load in flight, the next group's included).
+                auto consume = [&](uint32_t k0, uint32_t q, const uint4 (&R)[4]) {
+                    const uint32_t k = k0 + lane;
+                    uint32_t part = 0;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) part += sum16(R[c].x) + sum16(R[c].y) + sum16(R[c].z) + sum16(R[c].w);
-                const int left = (int)l_dge[q] - 64 - 64 * (int)(k - l_cs[q]);   // chunk bytes in the datagram
-                if (left < 64) {                                       // the frame's last chunk
-                    part = 0;
+                    for (int c = 0; c < 4; ++c) part += sum16(R[c].x) + sum16(R[c].y) + sum16(R[c].z) + sum16(R[c].w);
+                    const int left = (int)l_dge[q] - 64 - 64 * (int)(k - l_cs[q]);   // chunk bytes in the datagram
+                    if (left < 64) {                                       // the frame's last chunk
+                        part = 0;
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) part += chunk_sum(R[c], 0, left - 16 * c);
+                        for (int c = 0; c < 4; ++c) part += chunk_sum(R[c], 0, left - 16 * c);
+                    }
+                    part = k < total ? part : 0u;
+                    const uint32_t P = scan_dpp(part);
+                    const uint32_t lo = max(my_cs, k0), hi = min(my_cs + my_nt, k0 + 64u);
+                    const uint32_t ph = __shfl(P, (int)((hi > k0 ? hi - 1u - k0 : 0u) & 63u), 64);
+                    const uint32_t pl = __shfl(P, (int)((lo > k0 ? lo - 1u - k0 : 0u) & 63u), 64);
+                    if (lo < hi) tsum += ph - (lo > k0 ? pl : 0u);
+                };
+                // Two groups in flight; one back edge, after the second group is consumed (a loop
+                // exit between the two halves leaves the second group's loads pending at the
+                // header, which then waits for everything). Groups past the end load from offset 0
+                // and contribute nothing.
+                uint32_t qa, qb;
+                uint4 Ra[4], Rb[4];
+                issue(0, qa, Ra);
+                for (uint32_t k0 = 0;; k0 += 128) {
+                    issue(k0 + 64, qb, Rb);
+                    consume(k0, qa, Ra);
+                    issue(k0 + 128, qa, Ra);
+                    consume(k0 + 64, qb, Rb);
+                    if (k0 + 128 >= total) break;
                 }
-                part = k < total ? part : 0u;
-                const uint32_t P = scan_dpp(part);
-                const uint32_t lo = max(my_cs, k0), hi = min(my_cs + my_nt, k0 + 64u);
-                const uint32_t ph = __shfl(P, (int)((hi > k0 ? hi - 1u - k0 : 0u) & 63u), 64);
-                const uint32_t pl = __shfl(P, (int)((lo > k0 ? lo - 1u - k0 : 0u) & 63u), 64);
-                if (lo < hi) tsum += ph - (lo > k0 ? pl : 0u);
-            };
-            // Two groups in flight; one back edge, after the second group is consumed (a loop
-            // exit between the two halves leaves the second group's loads pending at the
-            // header, which then waits for everything). Groups past the end load from offset 0
-            // and contribute nothing.
-            uint32_t qa, qb;
-            uint4 Ra[4], Rb[4];
-            issue(0, qa, Ra);
-            for (uint32_t k0 = 0;; k0 += 128) {
-                issue(k0 + 64, qb, Rb);
-                consume(k0, qa, Ra);
-                issue(k0 + 128, qa, Ra);
-                consume(k0 + 64, qb, Rb);
-                if (k0 + 128 >= total) break;
-            }
-            wave_sync();
-            if (pd) {
-                const bool ok = fold32(fold32(tsum) + (dw >> 16)) == 0xFFFFu;
-                mstage[i] = (m & ~0x60u) | ((ok ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD) << 5);
-                acc_f0 += ok ? 0x10000u : 0x1000000u;
+                wave_sync();
+                if (pd) {
+                    const bool ok = fold32(fold32(tsum) + (dw >> 16)) == 0xFFFFu;
+                    mstage[i] = (m & ~0x60u) | ((ok ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD) << 5);
+                    acc_f0 += ok ? 0x10000u : 0x1000000u;
+                }
             }
         }
-    }
     }
 
     // ---- tile counters: one row per wave (lanes 0-15), summed by the readers ----
