@@ -289,11 +289,28 @@ typedef struct {
 typedef struct {
     uint8_t        *frames_dev;      /* output frames                                          */
     uint64_t        frames_bytes;    /* capacity                                               */
-    const uint32_t *frame_off_dev;   /* [n] where frame i starts (len_i + 42 bytes)            */
+    const uint32_t *frame_off_dev;   /* [n] where datagram i's frame(s) start (len_i + 42
+                                        bytes, or udpdk_gpu_tx_span() with fragmentation)    */
 } udpdk_tx_out_t;
 
 int udpdk_gpu_tx_build(udpdk_gpu_ctx *ctx, const udpdk_tx_config_t *cfg,
                        const udpdk_tx_batch_t *batch, const udpdk_tx_out_t *out);
+
+/* TX with the poller's IPv4 fragmentation (udpdk_poller.c:461-501: a frame of pkt_len =
+ * len + 42 > IPV4_MTU_DEFAULT goes through rte_ipv4_fragment_packet(pkt, ..., mtu) and gets its
+ * Ethernet header back per fragment). mtu = 1500 reproduces the reference (IPV4_MTU_DEFAULT =
+ * RTE_ETHER_MTU, udpdk_constants.h:37); mtu = 0 is udpdk_gpu_tx_build. (mtu - 20) must be a
+ * multiple of 8 and mtu >= 68. Every fragment carries mtu - 20 bytes of the IPv4 payload (the
+ * UDP header + data), the last the remainder; fragment k of datagram i starts at
+ * frame_off[i] + k * (mtu + 14), so datagram i occupies udpdk_gpu_tx_span(len_i, mtu) bytes.
+ * Fragment headers: total length 20 + fragment payload, fragment offset (8-byte units) + MF on
+ * all but the last, id 0 (as sent), and the IPv4 checksum a NIC fills for PKT_TX_IP_CKSUM
+ * (~RFC 1071 sum; DPDK leaves 0 in the mbuf). Unfragmented frames are exactly tx_build's. */
+int udpdk_gpu_tx_build_mtu(udpdk_gpu_ctx *ctx, const udpdk_tx_config_t *cfg,
+                           const udpdk_tx_batch_t *batch, const udpdk_tx_out_t *out,
+                           uint32_t mtu);
+/* Output bytes of one datagram of `len` payload bytes and its frame count (host helper). */
+uint64_t udpdk_gpu_tx_span(uint32_t len, uint32_t mtu, uint32_t *n_frames);
 
 /* ---------------------------------------------------------------------------------------------
  * Timing (for bench.py / the roofline): on every `enable`-th udpdk_gpu_rx call (0 = off, 1 =

@@ -41,6 +41,8 @@ def lib() -> C.CDLL:
         L.oracle_rte_ipv4_cksum.argtypes = [P]
         L.oracle_tx_frame.argtypes = [P, P, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32,
                                       C.c_uint32, C.c_uint32, P, C.c_uint32, P]
+        L.oracle_tx_fragment.restype = C.c_uint32
+        L.oracle_tx_fragment.argtypes = [P, C.c_uint32, C.c_uint32, P]
         L.oracle_recv_gather.argtypes = [P, P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, P, P, P, P]
         _lib = L
     return _lib
@@ -120,6 +122,19 @@ def tx_frame(src_mac: bytes, dst_mac: bytes, cfg_src_ip: int, slot_bound: int, s
                           cfg_src_ip, slot_bound, slot_ip, slot_port, dst_ip, dst_port, pb,
                           len(payload), out)
     return out.raw
+
+
+def tx_fragment(frame: bytes, mtu: int) -> list[bytes]:
+    """The poller's fragmentation of one sendto frame (udpdk_poller.c:461-501): the frames."""
+    n_max = max(1, (len(frame) + mtu) // max(1, mtu - 20) + 2) if mtu else 1
+    out = C.create_string_buffer(len(frame) + 34 * n_max + 16)
+    n = lib().oracle_tx_fragment(C.create_string_buffer(frame, len(frame)), len(frame), mtu, out)
+    raw, frames, pos = out.raw, [], 0
+    for _ in range(n):
+        flen = 14 + ((raw[pos + 16] << 8) | raw[pos + 17])     # IPv4 total length + Ethernet
+        frames.append(raw[pos:pos + flen])
+        pos += flen
+    return frames
 
 
 def bindtable_from_lists(port_lists: dict[int, list[tuple[int, int, int]]]) -> BindTable:

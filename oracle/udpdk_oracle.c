@@ -491,6 +491,62 @@ void oracle_tx_frame(const uint8_t src_mac[6], const uint8_t dst_mac[6], uint32_
 }
 
 /* ---------------------------------------------------------------------------------------------
+ * The poller's TX fragmentation, udpdk_poller.c:461-501: a frame of pkt_len > IPV4_MTU_DEFAULT
+ * (udpdk_constants.h:37, RTE_ETHER_MTU = 1500) loses its Ethernet header (rte_pktmbuf_adj), is
+ * cut by rte_ipv4_fragment_packet(pkt, out, n, IPV4_MTU_DEFAULT, ...) and every fragment gets the
+ * saved Ethernet header back (rte_pktmbuf_prepend + copies of ether_type, s_addr, d_addr).
+ *
+ * rte_ipv4_fragment_packet (DPDK 20.05 lib/librte_ip_frag/rte_ipv4_fragmentation.c, not in the
+ * container; restated from its published source): frag_size = mtu - 20 (a multiple of 8); the
+ * input's IP payload is cut into runs of frag_size bytes, the last the remainder; each fragment
+ * header is the input header (__fill_ipv4hdr_frag) with fragment_offset = input flags/offset +
+ * (data offset >> 3), MF set unless it is the last, total_length = 20 + its payload and
+ * hdr_checksum = 0 (the poller sets PKT_TX_IP_CKSUM: the NIC computes it). Here the checksum is
+ * written as the NIC would: ~(RFC 1071 sum), i.e. 0 when the sum folds to 0xffff.
+ *
+ * `frame` is one udpdk_sendto frame of len + 42 bytes (oracle_tx_frame); the fragments are
+ * written back to back into `out`; returns the number of frames. mtu = 0 or pkt_len <= mtu:
+ * the frame is copied unchanged.
+ * ------------------------------------------------------------------------------------------- */
+uint32_t oracle_tx_fragment(const uint8_t *frame, uint32_t pkt_len, uint32_t mtu, uint8_t *out)
+{
+    if (!mtu || pkt_len <= mtu) {                                         /* poller.c:466 */
+        memcpy(out, frame, pkt_len);
+        return 1;
+    }
+    const uint8_t *ip = frame + 14;                                       /* :471 adj */
+    const uint32_t ip_payload = pkt_len - 14 - 20;
+    const uint32_t frag_size = mtu - 20;
+    const uint16_t in_fo = (uint16_t)((ip[6] << 8) | ip[7]);
+    uint32_t n = 0, pos = 0;
+    uint8_t *o = out;
+    while (pos < ip_payload) {
+        const uint32_t len = ip_payload - pos < frag_size ? ip_payload - pos : frag_size;
+        const int more = pos + len < ip_payload;
+        memcpy(o, frame, 14);                                             /* :484-490 */
+        uint8_t *h = o + 14;
+        memcpy(h, ip, 20);                                                /* __fill_ipv4hdr_frag */
+        uint16_t fo = (uint16_t)(in_fo + (pos >> 3));
+        fo = (uint16_t)(fo | (more ? 0x2000u : 0u));
+        h[6] = (uint8_t)(fo >> 8); h[7] = (uint8_t)fo;
+        const uint32_t tl = 20 + len;
+        h[2] = (uint8_t)(tl >> 8); h[3] = (uint8_t)tl;
+        h[10] = 0; h[11] = 0;
+        uint32_t sum = 0;
+        for (int i = 0; i < 20; i += 2) sum += (uint32_t)h[i] | ((uint32_t)h[i + 1] << 8);
+        sum = (sum >> 16) + (sum & 0xFFFFu);
+        sum = (sum >> 16) + (sum & 0xFFFFu);
+        const uint16_t ck = (uint16_t)~sum;                               /* NIC IP checksum */
+        memcpy(h + 10, &ck, 2);
+        memcpy(o + 34, ip + 20 + pos, len);
+        o += 34 + len;
+        pos += len;
+        n++;
+    }
+    return n;
+}
+
+/* ---------------------------------------------------------------------------------------------
  * recvfrom payload delivery, udpdk_syscall.c:401-488 (single-segment mbufs), for lane entries
  * [first, first + count): entry k's payload into out_payload + k * len (len = recvfrom's len),
  * bytes copied into out_len[k], ip_hdr->src_addr / udp_hdr->src_port raw into out_src_*.

@@ -70,6 +70,10 @@ void oracle_tx_frame(const uint8_t src_mac[6], const uint8_t dst_mac[6], uint32_
 /* recvfrom payload delivery (udpdk_syscall.c:401-488) for lane entries [first, first + count):
  * payload k into out_payload + k * len (len = recvfrom's len), out_len[k] = bytes copied,
  * out_src_ip / out_src_port = raw ip src_addr / udp src_port. */
+/* The poller's TX fragmentation of one sendto frame (udpdk_poller.c:461-501 +
+ * rte_ipv4_fragment_packet): fragments back to back into out; returns the frame count. */
+uint32_t oracle_tx_fragment(const uint8_t *frame, uint32_t pkt_len, uint32_t mtu, uint8_t *out);
+
 void oracle_recv_gather(const uint8_t *frames, const uint32_t *offset, const uint16_t *length,
                         const uint32_t *lane_pkt, uint32_t first, uint32_t count, uint32_t len,
                         uint8_t *out_payload, uint32_t *out_len, uint32_t *out_src_ip,

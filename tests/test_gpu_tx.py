@@ -17,7 +17,7 @@ DST_MAC = bytes.fromhex("6805ca95fa64")
 SRC_IP = abi.raw_ip("172.31.100.2")
 
 
-def _tx_gpu(ctx, slots, sock, dst_ip, dst_port, payloads, frame_off, frames_cap):
+def _tx_gpu(ctx, slots, sock, dst_ip, dst_port, payloads, frame_off, frames_cap, mtu=None):
     n = len(payloads)
     pay_off = np.zeros(n, np.uint32)
     pos = 0
@@ -38,7 +38,10 @@ def _tx_gpu(ctx, slots, sock, dst_ip, dst_port, payloads, frame_off, frames_cap)
     cfg = abi.TxConfig((C.c_uint8 * 6)(*SRC_MAC), (C.c_uint8 * 6)(*DST_MAC), SRC_IP)
     bt = abi.TxBatch(bufs[0].ptr, pos, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, bufs[4].ptr, bufs[5].ptr, n)
     ot = abi.TxOut(out.ptr, frames_cap, bufs[6].ptr)
-    rc = abi.lib().udpdk_gpu_tx_build(ctx.handle, C.byref(cfg), C.byref(bt), C.byref(ot))
+    if mtu is None:
+        rc = abi.lib().udpdk_gpu_tx_build(ctx.handle, C.byref(cfg), C.byref(bt), C.byref(ot))
+    else:
+        rc = abi.lib().udpdk_gpu_tx_build_mtu(ctx.handle, C.byref(cfg), C.byref(bt), C.byref(ot), mtu)
     assert rc == 0
     res = ctx.download(out, np.uint8, frames_cap)
     for b in bufs + [out]:
@@ -97,3 +100,37 @@ def test_tx_golden_vectors(gpu_ctx):
         fr = res[fo[i]:fo[i] + v["pkt_len"]].tobytes()
         assert fr[:42].hex() == v["hdr"], v["id"]
         assert fr[42:] == payloads[i]
+
+
+@pytest.mark.parametrize("mtu", [1500, 1020])
+def test_tx_fragmentation(gpu_ctx, mtu):
+    """udpdk_gpu_tx_build_mtu against the poller's fragmentation restated (oracle_tx_fragment):
+    unfragmented, single-'fragment' (pkt_len in (mtu, mtu + 14]), 2-fragment and 45-fragment
+    datagrams mixed, frames back to back from an unaligned start."""
+    rng = np.random.default_rng(11)
+    slots = [(0, abi.raw_port(10000), 1), (abi.raw_ip("10.1.2.3"), abi.raw_port(5353), 1)]
+    n = 700
+    lens = rng.integers(0, 4000, n)
+    lens[:16] = [0, 1, mtu - 42, mtu - 41, mtu - 28, mtu - 27, 2006, 2952, 2953, 65507, 8, 9,
+                 mtu - 29, 2 * (mtu - 20) - 8, 2 * (mtu - 20) - 7, 1458]
+    lens[rng.integers(16, n, 5)] = rng.integers(20000, 65508, 5)
+    payloads = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
+    sock = rng.integers(0, 2, n)
+    dip = rng.integers(0, 2**32, n, dtype=np.uint64)
+    dport = rng.integers(0, 65536, n)
+    fo = np.zeros(n, np.uint32)
+    pos = 3
+    for i in range(n):
+        fo[i] = pos
+        pos += int(abi.lib().udpdk_gpu_tx_span(int(lens[i]), mtu, None))
+    cap = pos + 64
+    res = _tx_gpu(gpu_ctx, slots, sock, dip, dport, payloads, fo, cap, mtu=mtu)
+    assert np.all(res[:3] == 0xEE) and np.all(res[pos:pos + 32] == 0xEE)
+    for i in range(n):
+        ip, port, bound = slots[sock[i]]
+        frame = O.tx_frame(SRC_MAC, DST_MAC, SRC_IP, bound, ip, port, int(dip[i]), int(dport[i]),
+                           payloads[i])
+        want = b"".join(O.tx_fragment(frame, mtu))
+        got = res[fo[i]:fo[i] + len(want)].tobytes()
+        assert got == want, f"datagram {i} len {lens[i]}"
+

@@ -129,6 +129,9 @@ _PROTOS = {
     "udpdk_gpu_rx_gather": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint32, C.c_uint32,
                                       C.POINTER(RxGather)]),
     "udpdk_gpu_tx_build": (C.c_int, [_P, C.POINTER(TxConfig), C.POINTER(TxBatch), C.POINTER(TxOut)]),
+    "udpdk_gpu_tx_build_mtu": (C.c_int, [_P, C.POINTER(TxConfig), C.POINTER(TxBatch),
+                                         C.POINTER(TxOut), C.c_uint32]),
+    "udpdk_gpu_tx_span": (C.c_uint64, [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
     "udpdk_gpu_timing_enable": (C.c_int, [_P, C.c_int]),
     "udpdk_gpu_timing_read": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
     "udpdk_gpu_rx_geometry": (C.c_int, [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32),

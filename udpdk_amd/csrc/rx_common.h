@@ -133,6 +133,7 @@ struct TxArgs {
     uint32_t payload_rsrc;
     uint32_t frames_bytes;
     uint32_t src_ip;
+    uint32_t mtu;              // 0: no fragmentation; else IPv4 MTU ((mtu - 20) % 8 == 0)
     uint32_t mac_lo[3];        // 12 MAC bytes: dst(6) src(6) as three LE dwords
 };
 

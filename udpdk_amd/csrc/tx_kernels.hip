@@ -1,13 +1,26 @@
-// tx_kernels.hip — gfx950 TX header build (udpdk_syscall.c:314-356) for a batch of datagrams.
+// tx_kernels.hip — gfx950 TX header build (udpdk_syscall.c:314-356) for a batch of datagrams,
+// with the poller's IPv4 fragmentation (udpdk_poller.c:461-501) when an MTU is given.
 //
 // Per datagram: Ethernet (config MACs, type 0x0800), IPv4 (0x45, tos 0, total length, id 0,
 // frag 0, ttl 64, proto 17, rte_ipv4_cksum, src = bound slot IP unless ANY else config IP,
-// dst), UDP (raw src/dst ports, length, checksum 0), then the payload. The 42 header bytes of a
-// wave's 64 datagrams are built by one lane each into an LDS window laid out with the output
-// frame's 16-byte alignment; the output is then written as 16-byte chunks swept across lanes
-// (whole chunks as one 16 B store, frame-boundary chunks byte-masked), the payload read with two
-// aligned 16 B loads and a funnel shift. Bytes per datagram: len read + (len + 42) written +
-// 4 x 4 B + 2 x 2 B descriptors.
+// dst), UDP (raw src/dst ports, length, checksum 0), then the payload.
+//
+// Fragmentation (mtu != 0 and len + 42 > mtu, the poller's pkt_len > IPV4_MTU_DEFAULT test):
+// the IPv4 packet is cut the way DPDK 20.05 rte_ipv4_fragment_packet does (restated in
+// oracle/udpdk_oracle.c): every fragment carries mtu - 20 bytes of the IP payload (UDP header +
+// data), the last the remainder; each fragment repeats the Ethernet header and the IPv4 header
+// with total length = 20 + its payload, fragment offset in 8-byte units and MF on all but the
+// last. DPDK leaves the fragment header checksum 0 with PKT_TX_IP_CKSUM set, so the NIC fills
+// it: here it is filled as the NIC would (~fold of the RFC 1071 sum). A datagram's frames are
+// contiguous from frame_off[i]: fragment k at + k * (mtu + 14), so its span is
+// (len + 8) + 34 * n_frames (len + 42 unfragmented).
+//
+// A wave takes 64 datagrams, expands them into output frames (one per datagram unless it is
+// fragmented) and handles 64 frames per round: one lane builds a frame's 42 (or 34) header
+// bytes into an LDS window laid out with the output frame's 16-byte alignment; the frames are
+// then written as 16-byte chunks swept across lanes (whole chunks as one 16 B store,
+// frame-boundary chunks byte-masked), the payload read with two aligned 16 B loads and a funnel
+// shift. Bytes per datagram: len read + span written + 4 x 4 B + 2 x 2 B descriptors.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -54,145 +67,208 @@ __device__ __forceinline__ uint32_t sel4(uint32_t d, uint32_t a0, uint32_t a1, u
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
-// rte_raw_cksum + rte_ipv4_cksum of DPDK 20.05 over the 20-byte header built below
-// (cksum field zero): raw == 0xffff is returned unchanged.
-__device__ __forceinline__ uint32_t ipv4_cksum(uint32_t tl, uint32_t src, uint32_t dst)
+// Sum of the 20-byte IPv4 header built below (checksum field zero) as LE 16-bit words:
+// version/IHL 0x45, tos 0, total length tl, id 0, fragment field ff (host order), ttl 64,
+// proto 17, src, dst (raw).
+__device__ __forceinline__ uint32_t ipv4_raw(uint32_t tl, uint32_t ff, uint32_t src, uint32_t dst)
 {
-    uint32_t s = 0x0045u + bswap16(tl) + 0x1140u + (src & 0xFFFFu) + (src >> 16) +
+    uint32_t s = 0x0045u + bswap16(tl) + bswap16(ff) + 0x1140u + (src & 0xFFFFu) + (src >> 16) +
                  (dst & 0xFFFFu) + (dst >> 16);
     s = (s >> 16) + (s & 0xFFFFu);
     s = (s >> 16) + (s & 0xFFFFu);
-    s &= 0xFFFFu;
-    return s == 0xFFFFu ? s : (~s & 0xFFFFu);
+    return s & 0xFFFFu;
 }
 
-constexpr int TX_WIN = 64;  // bytes of header window per datagram (16 dwords)
+// rte_ipv4_cksum of DPDK 20.05: raw == 0xffff is returned unchanged.
+__device__ __forceinline__ uint32_t ipv4_cksum(uint32_t raw) { return raw == 0xFFFFu ? raw : (~raw & 0xFFFFu); }
+
+// The checksum a NIC computes for PKT_TX_IP_CKSUM (fragments, rte_ipv4_fragment_packet leaves 0).
+__device__ __forceinline__ uint32_t ipv4_cksum_nic(uint32_t raw) { return ~raw & 0xFFFFu; }
+
+constexpr int TX_WIN = 64;  // bytes of header window per frame (16 dwords)
+constexpr int TXW = TX_BLOCK / 64;
 
 } // namespace
 
 __global__ void __launch_bounds__(TX_BLOCK)
 tx_build(TxArgs a)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t win[TX_BLOCK / 64][64][TX_WIN / 4];
-    __shared__ uint32_t l_cs[TX_BLOCK / 64][64], l_fo[TX_BLOCK / 64][64],
-        l_len[TX_BLOCK / 64][64], l_po[TX_BLOCK / 64][64];
+    __shared__ __attribute__((aligned(16))) uint32_t win[TXW][64][TX_WIN / 4];
+    // per output frame of the current round
+    __shared__ uint32_t l_cs[TXW][64], l_fo[TXW][64], l_len[TXW][64], l_po[TXW][64], l_hl[TXW][64];
+    // per datagram of the wave: first frame, frame offset, length | n_frames << 16, payload
+    // offset, src ip, dst ip, src port | dst port << 16
+    __shared__ uint32_t d_fs[TXW][64], d_fo[TXW][64], d_ln[TXW][64], d_po[TXW][64],
+        d_src[TXW][64], d_dst[TXW][64], d_pt[TXW][64];
     const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
     const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.payload), (short)0, (int)a.payload_rsrc, 0x00020000);
-    const uint32_t waves_total = gridDim.x * (TX_BLOCK / 64);
+    const uint32_t waves_total = gridDim.x * TXW;
+    const uint32_t fpl = a.mtu ? a.mtu - 20u : 0u;      // IP payload bytes per full fragment
 
-    for (uint32_t g = blockIdx.x * (TX_BLOCK / 64) + w; g * 64 < a.n; g += waves_total) {
+    for (uint32_t g = blockIdx.x * TXW + w; g * 64 < a.n; g += waves_total) {
         const uint32_t i = g * 64 + lane;
-        const bool valid = i < a.n;
-        uint32_t fo = 0, L = 0, po = 0, nch = 0;
-        if (valid) {
+        uint32_t nf = 0, fo = 0, L = 0, po = 0, src = 0, dst = 0, pt = 0;
+        if (i < a.n) {
             fo = a.frame_off[i];
             L = a.payload_len[i];
             po = a.payload_off[i];
             const int32_t sock = a.sockfd[i];
-            const bool ok = (uint64_t)fo + L + 42u <= a.frames_bytes &&
+            const bool frag = a.mtu && L + 42u > a.mtu;                    // poller.c:466
+            const uint32_t n_fr = frag ? (L + 8u + fpl - 1u) / fpl : 1u;
+            const uint32_t span = frag ? L + 8u + 34u * n_fr : L + 42u;
+            const bool ok = (uint64_t)fo + span <= a.frames_bytes &&
                             (uint64_t)po + L <= a.payload_bytes && sock >= 0 &&
                             (uint32_t)sock < a.n_slots;
             if (ok) {
-                nch = ((fo & 15u) + L + 42u + 15u) >> 4;
+                nf = n_fr;
                 const uint4 sl = a.slots[sock];
-                const uint32_t src = (sl.z && sl.x != 0u) ? sl.x : a.src_ip;   // :329-334
-                const uint32_t dst = a.dst_ip[i];                               // :335
-                const uint32_t tl = L + 28u;                                    // :336
-                const uint32_t ul = L + 8u;                                     // :344
-                const uint32_t ck = ipv4_cksum(tl, src, dst);                   // :337
+                src = (sl.z && sl.x != 0u) ? sl.x : a.src_ip;                   // :329-334
+                dst = a.dst_ip[i];                                               // :335
+                pt = (sl.y & 0xFFFFu) | ((uint32_t)a.dst_port[i] << 16);          // :341-342
+            }
+        }
+        uint32_t n_frames;
+        const uint32_t fs = excl_scan64(nf, &n_frames);
+        d_fs[w][lane] = fs;
+        d_fo[w][lane] = fo;
+        d_ln[w][lane] = L | ((a.mtu && L + 42u > a.mtu) ? nf << 16 : 0u);
+        d_po[w][lane] = po;
+        d_src[w][lane] = src;
+        d_dst[w][lane] = dst;
+        d_pt[w][lane] = pt;
+        wave_sync_tx();
+
+        for (uint32_t r0 = 0; r0 < n_frames; r0 += 64) {
+            const uint32_t f = r0 + lane;
+            uint32_t nch = 0, ffo = 0, plen = 0, ppo = 0, hl = 0;
+            if (f < n_frames) {
+                // the datagram of frame f: the last q with d_fs[q] <= f (datagrams without
+                // frames share their successor's first index)
+                uint32_t q = 0;
+#pragma unroll
+                for (int sft = 32; sft >= 1; sft >>= 1)
+                    if (d_fs[w][q + sft] <= f) q += sft;
+                const uint32_t k = f - d_fs[w][q];
+                const uint32_t ln = d_ln[w][q], Lq = ln & 0xFFFFu, nfq = ln >> 16;
+                const uint32_t sq = d_src[w][q], dq = d_dst[w][q], ptq = d_pt[w][q];
+                uint32_t tl, ff, ck;
+                if (!nfq) {                       // unfragmented: udpdk_sendto's frame as built
+                    tl = Lq + 28u;                                               // :336
+                    ff = 0u;
+                    ck = ipv4_cksum(ipv4_raw(tl, 0u, sq, dq));                   // :337
+                    hl = 42u;
+                    ffo = d_fo[w][q];
+                    ppo = d_po[w][q];
+                    plen = Lq;
+                } else {                          // fragment k of nfq (rte_ipv4_fragment_packet)
+                    const uint32_t ofs = k * fpl;
+                    const bool last = k + 1u == nfq;
+                    const uint32_t ipp = last ? Lq + 8u - ofs : fpl;
+                    tl = 20u + ipp;
+                    ff = (ofs >> 3) | (last ? 0u : 0x2000u);
+                    ck = ipv4_cksum_nic(ipv4_raw(tl, ff, sq, dq));
+                    hl = k ? 34u : 42u;
+                    ffo = d_fo[w][q] + k * (a.mtu + 14u);
+                    ppo = d_po[w][q] + (k ? ofs - 8u : 0u);
+                    plen = k ? ipp : ipp - 8u;
+                }
+                const uint32_t ul = Lq + 8u;                                     // :344
                 uint32_t h[12];
                 h[0] = a.mac_lo[0]; h[1] = a.mac_lo[1]; h[2] = a.mac_lo[2];      // :315-317
                 h[3] = 0x00450008u;                                 // type 0x0800, 0x45, tos 0
                 h[4] = bswap16(tl);                                 // total length, id 0
-                h[5] = 0x11400000u;                                 // frag 0, ttl 64, proto 17
-                h[6] = ck | ((src & 0xFFFFu) << 16);
-                h[7] = (src >> 16) | ((dst & 0xFFFFu) << 16);
-                h[8] = (dst >> 16) | ((sl.y & 0xFFFFu) << 16);      // src port raw, :341
-                h[9] = ((uint32_t)a.dst_port[i] & 0xFFFFu) | (bswap16(ul) << 16); // :342, :344
+                h[5] = bswap16(ff) | 0x11400000u;                   // fragment field, ttl 64, 17
+                h[6] = ck | ((sq & 0xFFFFu) << 16);
+                h[7] = (sq >> 16) | ((dq & 0xFFFFu) << 16);
+                h[8] = (dq >> 16) | ((ptq & 0xFFFFu) << 16);        // src port raw, :341
+                h[9] = (ptq >> 16) | (bswap16(ul) << 16);           // dst port raw, :342, :344
                 h[10] = 0u;                                         // UDP checksum 0, :343
                 h[11] = 0u;
                 // shift into the frame's 16-byte alignment: byte r of the header lands at
-                // window byte (fo & 15) + r
-                const uint32_t sh = fo & 15u, s3 = sh & 3u, d0 = sh >> 2;
+                // window byte (ffo & 15) + r
+                const uint32_t sh = ffo & 15u, s3 = sh & 3u, d0 = sh >> 2;
                 uint32_t *wq = win[w][lane];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) wq[k] = 0u;
+                for (int t = 0; t < 16; ++t) wq[t] = 0u;
 #pragma unroll
-                for (int k = 0; k < 12; ++k) {
-                    const uint32_t prev = k ? h[k - 1] : 0u;
-                    const uint32_t gk = s3 ? ((h[k] << (8u * s3)) | (prev >> (32u - 8u * s3))) : h[k];
-                    wq[d0 + k] = gk;
+                for (int t = 0; t < 12; ++t) {
+                    const uint32_t prev = t ? h[t - 1] : 0u;
+                    const uint32_t gk = s3 ? ((h[t] << (8u * s3)) | (prev >> (32u - 8u * s3))) : h[t];
+                    wq[d0 + t] = gk;
                 }
                 if (s3) wq[d0 + 12] = h[11] >> (32u - 8u * s3);
+                nch = ((ffo & 15u) + hl + plen + 15u) >> 4;
             }
-        }
-        uint32_t total;
-        const uint32_t cs = excl_scan64(nch, &total);
-        l_cs[w][lane] = cs;
-        l_fo[w][lane] = fo;
-        l_len[w][lane] = L;
-        l_po[w][lane] = po;
-        wave_sync_tx();
+            uint32_t total;
+            const uint32_t cs = excl_scan64(nch, &total);
+            l_cs[w][lane] = cs;
+            l_fo[w][lane] = ffo;
+            l_len[w][lane] = plen;
+            l_po[w][lane] = ppo;
+            l_hl[w][lane] = hl;
+            wave_sync_tx();
 
-        for (uint32_t k = lane; k < total; k += 64) {
-            uint32_t q = 0;
+            for (uint32_t k = lane; k < total; k += 64) {
+                uint32_t q = 0;
 #pragma unroll
-            for (int sft = 32; sft >= 1; sft >>= 1)
-                if (l_cs[w][q + sft] <= k) q += sft;
-            const uint32_t j = k - l_cs[w][q];
-            const uint32_t fq = l_fo[w][q], Lq = l_len[w][q], pq = l_po[w][q];
-            const uint32_t abase = (fq & ~15u) + 16u * j;
-            const int r0 = (int)(abase - fq);
-            // header part
-            uint32_t H[4] = {0u, 0u, 0u, 0u};
-            if (j < 4) {
-                const uint4 hv = *reinterpret_cast<const uint4 *>(&win[w][q][4 * j]);
-                H[0] = hv.x; H[1] = hv.y; H[2] = hv.z; H[3] = hv.w;
-            }
-            // payload part: bytes at payload offset pq + r0 - 42 + b
-            uint32_t P[4] = {0u, 0u, 0u, 0u};
-            if (r0 + 16 > 42) {
-                const int64_t src0 = (int64_t)pq + r0 - 42;
-                const int64_t sa = src0 & ~(int64_t)15;
-                const uint32_t sft = (uint32_t)(src0 - sa);       // 0..15
-                const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)(uint32_t)sa, 0, 0);
-                const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)(uint32_t)(sa + 16), 0, 0);
-                const uint32_t wv[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-                const uint32_t d = sft >> 2, s = sft & 3u;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const uint32_t lo = sel4(d, wv[t], wv[t + 1], wv[t + 2], wv[t + 3]);
-                    const uint32_t hi = sel4(d, wv[t + 1], wv[t + 2], wv[t + 3], wv[t + 4]);
-                    P[t] = __builtin_amdgcn_alignbyte(hi, lo, s);
+                for (int sft = 32; sft >= 1; sft >>= 1)
+                    if (l_cs[w][q + sft] <= k) q += sft;
+                const uint32_t j = k - l_cs[w][q];
+                const uint32_t fq = l_fo[w][q], Lq = l_len[w][q], pq = l_po[w][q];
+                const int hq = (int)l_hl[w][q];
+                const uint32_t abase = (fq & ~15u) + 16u * j;
+                const int r0c = (int)(abase - fq);
+                // header part
+                uint32_t H[4] = {0u, 0u, 0u, 0u};
+                if (j < 4) {
+                    const uint4 hv = *reinterpret_cast<const uint4 *>(&win[w][q][4 * j]);
+                    H[0] = hv.x; H[1] = hv.y; H[2] = hv.z; H[3] = hv.w;
                 }
-            }
-            uint32_t o[4], own[4];
-            bool full = true;
+                // payload part: bytes at payload offset pq + r0c - hq + b
+                uint32_t P[4] = {0u, 0u, 0u, 0u};
+                if (r0c + 16 > hq) {
+                    const int64_t src0 = (int64_t)pq + r0c - hq;
+                    const int64_t sa = src0 & ~(int64_t)15;
+                    const uint32_t sft = (uint32_t)(src0 - sa);       // 0..15
+                    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)(uint32_t)sa, 0, 0);
+                    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)(uint32_t)(sa + 16), 0, 0);
+                    const uint32_t wv[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+                    const uint32_t d = sft >> 2, s = sft & 3u;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const uint32_t hm = win_mask(-r0, 42 - r0, t);
-                const uint32_t pm = win_mask(42 - r0, 42 + (int)Lq - r0, t);
-                o[t] = (H[t] & hm) | (P[t] & pm);
-                own[t] = hm | pm;
-                full = full && own[t] == 0xFFFFFFFFu;
-            }
-            uint8_t *dst = a.frames + abase;
-            if (full) {
-                *reinterpret_cast<uint4 *>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
-            } else {
+                    for (int t = 0; t < 4; ++t) {
+                        const uint32_t lo = sel4(d, wv[t], wv[t + 1], wv[t + 2], wv[t + 3]);
+                        const uint32_t hi = sel4(d, wv[t + 1], wv[t + 2], wv[t + 3], wv[t + 4]);
+                        P[t] = __builtin_amdgcn_alignbyte(hi, lo, s);
+                    }
+                }
+                uint32_t o[4], own[4];
+                bool full = true;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    if (own[t] == 0xFFFFFFFFu) {
-                        *reinterpret_cast<uint32_t *>(dst + 4 * t) = o[t];
-                    } else if (own[t]) {
-                        for (int b = 0; b < 4; ++b)
-                            if ((own[t] >> (8 * b)) & 0xFFu) dst[4 * t + b] = (uint8_t)(o[t] >> (8 * b));
+                    const uint32_t hm = win_mask(-r0c, hq - r0c, t);
+                    const uint32_t pm = win_mask(hq - r0c, hq + (int)Lq - r0c, t);
+                    o[t] = (H[t] & hm) | (P[t] & pm);
+                    own[t] = hm | pm;
+                    full = full && own[t] == 0xFFFFFFFFu;
+                }
+                uint8_t *dstp = a.frames + abase;
+                if (full) {
+                    *reinterpret_cast<uint4 *>(dstp) = make_uint4(o[0], o[1], o[2], o[3]);
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (own[t] == 0xFFFFFFFFu) {
+                            *reinterpret_cast<uint32_t *>(dstp + 4 * t) = o[t];
+                        } else if (own[t]) {
+                            for (int b = 0; b < 4; ++b)
+                                if ((own[t] >> (8 * b)) & 0xFFu) dstp[4 * t + b] = (uint8_t)(o[t] >> (8 * b));
+                        }
                     }
                 }
             }
+            wave_sync_tx();
         }
-        wave_sync_tx();
     }
 }
 

@@ -843,10 +843,29 @@ int udpdk_gpu_rx_gather(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint
     return 0;
 }
 
+uint64_t udpdk_gpu_tx_span(uint32_t len, uint32_t mtu, uint32_t *n_frames)
+{
+    uint32_t nf = 1;
+    uint64_t span = (uint64_t)len + 42u;
+    if (mtu >= 68u && (mtu - 20u) % 8u == 0 && (uint64_t)len + 42u > mtu) {
+        nf = (uint32_t)(((uint64_t)len + 8u + (mtu - 20u) - 1u) / (mtu - 20u));
+        span = (uint64_t)len + 8u + 34ull * nf;
+    }
+    if (n_frames) *n_frames = nf;
+    return span;
+}
+
 int udpdk_gpu_tx_build(udpdk_gpu_ctx *c, const udpdk_tx_config_t *cfg, const udpdk_tx_batch_t *bt,
                        const udpdk_tx_out_t *o)
 {
+    return udpdk_gpu_tx_build_mtu(c, cfg, bt, o, 0);
+}
+
+int udpdk_gpu_tx_build_mtu(udpdk_gpu_ctx *c, const udpdk_tx_config_t *cfg,
+                           const udpdk_tx_batch_t *bt, const udpdk_tx_out_t *o, uint32_t mtu)
+{
     if (!c || !cfg || !bt || !o) return -EINVAL;
+    if (mtu && (mtu < 68u || mtu > 65535u || (mtu - 20u) % 8u)) return -EINVAL;
     if (!bt->n) return 0;
     if (!bt->payload_dev || !bt->payload_off_dev || !bt->payload_len_dev || !bt->sockfd_dev ||
         !bt->dst_ip_dev || !bt->dst_port_dev || !o->frames_dev || !o->frame_off_dev) return -EINVAL;
@@ -871,6 +890,7 @@ int udpdk_gpu_tx_build(udpdk_gpu_ctx *c, const udpdk_tx_config_t *cfg, const udp
     ta.payload_rsrc = (uint32_t)std::min<uint64_t>((bt->payload_bytes + 15) & ~15ull, 0xFFFFFFFFull);
     ta.frames_bytes = (uint32_t)o->frames_bytes;
     ta.src_ip = cfg->src_ip;
+    ta.mtu = mtu;
     uint8_t mac[12];
     memcpy(mac, cfg->dst_mac, 6);   // Ethernet d_addr first (udpdk_syscall.c:317)
     memcpy(mac + 6, cfg->src_mac, 6);
