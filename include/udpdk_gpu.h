@@ -267,6 +267,52 @@ int udpdk_gpu_rx_gather(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch,
                         const udpdk_rx_gather_t *out);
 
 /* ---------------------------------------------------------------------------------------------
+ * RX reassembly of IPv4 fragments (udpdk_poller.c:338-361: FRAG frames go through
+ * rte_ipv4_frag_reassemble_packet on the table of udpdk_poller.c:130, and a completed datagram
+ * continues through the demux at the position of the fragment that completed it)
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+    uint32_t bucket_num;      /* NUM_FLOWS_DEF = 0x1000 (udpdk_constants.h:32)                  */
+    uint32_t bucket_entries;  /* IP_FRAG_TBL_BUCKET_ENTRIES = 16 (power of two, <= 32)          */
+    uint64_t max_cycles;      /* flow lifetime in the unit of the tms argument (frag_cycles =
+                                 MAX_FLOW_TTL = 1 s of TSC cycles in the reference)              */
+    uint32_t max_dgram;       /* IPv4 payload bytes one flow can hold, <= 65515; device memory is
+                                 about entries x (max_dgram + 34) bytes                           */
+} udpdk_frag_table_cfg_t;
+
+enum udpdk_rs_stat {
+    UDPDK_RS_FRAGS      = 0, /* FRAG-verdict frames of the batch                                */
+    UDPDK_RS_DROP_LEN   = 1, /* total_length <= 20 (rte_ipv4_frag_reassemble_packet drops it)    */
+    UDPDK_RS_DROP_SHORT = 2, /* IP data past the frame or past max_dgram (divergence) */
+    UDPDK_RS_NO_SPACE   = 3, /* no free or expired entry in the key's two buckets                */
+    UDPDK_RS_ERRORS     = 4, /* flows dropped: duplicate first/last, > 4 fragments, bad size     */
+    UDPDK_RS_HOLES      = 5, /* flows dropped: size complete but the fragments do not chain      */
+    UDPDK_RS_EXPIRED    = 6, /* flows freed on timeout                                           */
+    UDPDK_RS_DONE       = 7, /* datagrams reassembled                                             */
+    UDPDK_RS_STORED     = 8, /* fragments of this batch held by the table for later batches      */
+    UDPDK_RS_N          = 9
+};
+
+typedef struct {
+    udpdk_rx_batch_t batch;   /* reassembled frames (context-owned, valid until the next call):
+                                 first fragment's Ethernet/IPv4 header with total length, DF-only
+                                 fragment field and a valid checksum, then the IPv4 payload;
+                                 ptype 0x211. Feed it to udpdk_gpu_rx for the demux.           */
+    const uint32_t *origin_dev; /* [batch.n] index (in the input batch) of the fragment that
+                                 completed each datagram; the datagrams are in this order       */
+    uint64_t stats[UDPDK_RS_N];
+} udpdk_reasm_out_t;
+
+/* rte_ip_frag_table_create (udpdk_poller.c:130) on the device; replaces an existing table. */
+int udpdk_gpu_frag_table_create(udpdk_gpu_ctx *ctx, const udpdk_frag_table_cfg_t *cfg);
+/* Reassembly step for one batch whose udpdk_gpu_rx verdicts are in meta_dev (FRAG frames are
+ * consumed; state persists across calls). tms is the batch's timestamp (the poller's cur_tsc).
+ * Synchronous. Equals one-fragment-at-a-time processing in arrival order unless the batch's
+ * flows compete for the last free entries of a bucket pair. */
+int udpdk_gpu_rx_reassemble(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch,
+                            const uint32_t *meta_dev, uint64_t tms, udpdk_reasm_out_t *out);
+
+/* ---------------------------------------------------------------------------------------------
  * TX: Eth/IPv4/UDP header build + rte_ipv4_cksum + payload copy (udpdk_syscall.c:314-356)
  * ------------------------------------------------------------------------------------------- */
 typedef struct {

@@ -43,6 +43,14 @@ def lib() -> C.CDLL:
                                       C.c_uint32, C.c_uint32, P, C.c_uint32, P]
         L.oracle_tx_fragment.restype = C.c_uint32
         L.oracle_tx_fragment.argtypes = [P, C.c_uint32, C.c_uint32, P]
+        L.oracle_ftable_new.restype = P
+        L.oracle_ftable_new.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32]
+        L.oracle_ftable_free.argtypes = [P]
+        L.oracle_frag_hash.restype = C.c_uint32
+        L.oracle_frag_hash.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.oracle_reassemble.restype = C.c_int64
+        L.oracle_reassemble.argtypes = [P, P, C.c_uint64, P, P, P, C.c_uint32, C.c_uint64, P,
+                                        C.c_uint64, P, P, P, C.c_uint32, P]
         L.oracle_recv_gather.argtypes = [P, P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, P, P, P, P]
         _lib = L
     return _lib
@@ -169,3 +177,50 @@ def recv_gather(frames: np.ndarray, offset: np.ndarray, length: np.ndarray, lane
     lib().oracle_recv_gather(P(fr), P(off), P(ln), P(lp), first, count, slot, P(pay), P(olen),
                              P(sip), P(spt))
     return pay[:count], olen[:count], sip[:count], spt[:count]
+
+
+RS_STATS = ("frags", "drop_len", "drop_short", "no_space", "errors", "holes", "expired", "done",
+            "stored")
+
+
+class FragTable:
+    """The poller's reassembly table (udpdk_poller.c:130 rte_ip_frag_table_create) restated:
+    state persists across reassemble() calls like the reference's."""
+
+    def __init__(self, bucket_num=0x1000, bucket_entries=16, max_cycles=1000, max_dgram=65515):
+        self.h = C.c_void_p(lib().oracle_ftable_new(bucket_num, bucket_entries, max_cycles, max_dgram))
+        if not self.h:
+            raise ValueError("bad table geometry")
+        self.fed = 0          # bytes fed so far: bounds what held fragments can add to an output
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_ftable_free(self.h)
+            self.h = None
+
+    def reassemble(self, frames: np.ndarray, offset, length, meta, tms: int):
+        """FRAG frames of one batch -> (frames u8, offset u32, length u16, origin u32, stats)."""
+        fr = np.ascontiguousarray(frames, np.uint8)
+        off = np.ascontiguousarray(offset, np.uint32)
+        ln = np.ascontiguousarray(length, np.uint16)
+        mt = np.ascontiguousarray(meta, np.uint32)
+        n = len(off)
+        self.fed += int(ln.astype(np.int64).sum())
+        cap = self.fed + 64 * n + 64
+        out = np.zeros(cap, np.uint8)
+        oo = np.zeros(max(1, n), np.uint32)
+        ol = np.zeros(max(1, n), np.uint16)
+        og = np.zeros(max(1, n), np.uint32)
+        st = np.zeros(len(RS_STATS), np.uint64)
+        P = lambda a: a.ctypes.data_as(C.c_void_p)
+        k = lib().oracle_reassemble(self.h, P(fr), len(fr), P(off), P(ln), P(mt), n, tms, P(out),
+                                    cap, P(oo), P(ol), P(og), max(1, n), P(st))
+        if k < 0:
+            raise RuntimeError("oracle_reassemble: output capacity")
+        return out, oo[:k], ol[:k], og[:k], dict(zip(RS_STATS, st.tolist()))
+
+
+def frag_hash(src: int, dst: int, pid: int):
+    s2 = C.c_uint32()
+    s1 = lib().oracle_frag_hash(src, dst, pid, C.byref(s2))
+    return s1, s2.value

@@ -74,6 +74,33 @@ void oracle_tx_frame(const uint8_t src_mac[6], const uint8_t dst_mac[6], uint32_
  * rte_ipv4_fragment_packet): fragments back to back into out; returns the frame count. */
 uint32_t oracle_tx_fragment(const uint8_t *frame, uint32_t pkt_len, uint32_t mtu, uint8_t *out);
 
+/* RX reassembly (udpdk_oracle_frag.c): DPDK 20.05 rte_ipv4_frag_reassemble_packet restated. */
+typedef struct oracle_ftable oracle_ftable;
+enum oracle_rs_stat {
+    ORACLE_RS_FRAGS = 0,      /* FRAG-verdict frames seen                                      */
+    ORACLE_RS_DROP_LEN,       /* total_length <= 20 (rte_ipv4_frag_reassemble_packet)          */
+    ORACLE_RS_DROP_SHORT,     /* IP data past the frame or past the datagram capacity          */
+    ORACLE_RS_NO_SPACE,       /* ip_frag_find found no entry                                    */
+    ORACLE_RS_ERRORS,         /* flows dropped: duplicate first/last, > 4 fragments, size      */
+    ORACLE_RS_HOLES,          /* flows dropped: complete size but the chain walk found a hole  */
+    ORACLE_RS_EXPIRED,        /* flows freed on timeout (own reuse or stale slot)              */
+    ORACLE_RS_DONE,           /* datagrams reassembled                                          */
+    ORACLE_RS_STORED,         /* fragments of this call still held by the table at its end      */
+    ORACLE_RS_N
+};
+oracle_ftable *oracle_ftable_new(uint32_t bucket_num, uint32_t bucket_entries, uint64_t max_cycles,
+                                 uint32_t max_dgram);
+void           oracle_ftable_free(oracle_ftable *t);
+uint32_t       oracle_frag_hash(uint32_t src, uint32_t dst, uint32_t id, uint32_t *sig2);
+/* FRAG-verdict frames of one batch in arrival order; reassembled frames 16-byte aligned into
+ * out, with their offset/length and the index of the completing fragment. Returns the count or
+ * -1 if out/out_max is too small. stats accumulate. */
+int64_t oracle_reassemble(oracle_ftable *t, const uint8_t *frames, uint64_t frames_bytes,
+                          const uint32_t *offset, const uint16_t *length, const uint32_t *meta,
+                          uint32_t n, uint64_t tms, uint8_t *out, uint64_t out_cap,
+                          uint32_t *out_off, uint16_t *out_len, uint32_t *out_origin,
+                          uint32_t out_max, uint64_t stats[ORACLE_RS_N]);
+
 void oracle_recv_gather(const uint8_t *frames, const uint32_t *offset, const uint16_t *length,
                         const uint32_t *lane_pkt, uint32_t first, uint32_t count, uint32_t len,
                         uint8_t *out_payload, uint32_t *out_len, uint32_t *out_src_ip,

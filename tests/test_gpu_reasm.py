@@ -1,0 +1,156 @@
+"""RX reassembly parity (f2): udpdk_gpu_rx_reassemble against the oracle's restatement of the
+poller's rte_ipv4_frag_reassemble_packet step (oracle_reassemble), over multi-batch seeded
+scenarios with shuffled, lost, duplicated, overlapping and hole-making fragments, flow expiry and
+key reuse; the reassembled datagrams then go through udpdk_gpu_rx (the demux the reference runs
+on them) and are compared with the oracle's RX of the oracle's datagrams. Plus a GPU-only loop:
+udpdk_gpu_tx_build_mtu's fragments come back as the datagrams that were sent."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle as O
+from reasm_util import batch, scenario
+from udpdk_amd import abi
+
+pytestmark = pytest.mark.gpu
+
+PORTS = (10000, 10001, 10002, 10003)
+LISTS = {abi.raw_port(p): [(0, k, 0)] for k, p in enumerate(PORTS)}
+
+
+def _frames(ctx, rb):
+    off = abi.download_ptr(ctx, rb.offset.ptr, np.uint32, rb.n)
+    ln = abi.download_ptr(ctx, rb.length.ptr, np.uint16, rb.n)
+    buf = abi.download_ptr(ctx, rb.frames.ptr, np.uint8, rb.frames_bytes)
+    return buf, off, ln
+
+
+@pytest.mark.parametrize("seed", [5, 6, 7])
+def test_reassembly_matches_oracle(gpu_ctx, seed):
+    abi.frag_table_create(gpu_ctx, bucket_num=256, bucket_entries=16, max_cycles=25)
+    t = O.FragTable(bucket_num=256, bucket_entries=16, max_cycles=25)
+    gpu_ctx.upload_snapshot(abi.snapshot_from_lists(LISTS, 4))
+    bt = O.bindtable_from_lists(LISTS)
+    tot = {}
+    for b, (frames, tms) in enumerate(scenario(seed)):
+        buf, off, ln = batch(frames)
+        n = len(off)
+        db = abi.rx_upload(gpu_ctx, buf, off, ln)
+        db.frames_bytes = len(buf) - 64
+        out = abi.rx_alloc_out(gpu_ctx, n, 4, 4 * n)
+        gm, gl, gp, gc, rc = abi.rx_run(gpu_ctx, db, out)
+        wm, wl, wp, wc = O.rx(bt, buf, len(buf) - 64, off, ln, None, 4)
+        assert rc == 0 and np.array_equal(gm, wm)
+        rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, out.meta, tms)
+        wout, woo, wol, wog, wst = t.reassemble(buf, off, ln, wm, tms)
+        # every outcome count is exact except "expired": which flow reclaims a stale slot first
+        # (the reference: arrival order; here: wave timing) decides whether a newcomer frees a
+        # stale entry or takes an empty one. No datagram depends on it.
+        assert {k: v for k, v in gst.items() if k != "expired"} == \
+            {k: v for k, v in wst.items() if k != "expired"}, f"batch {b}: stats {gst} vs {wst}"
+        assert rb.n == len(woo)
+        for k, v in gst.items():
+            tot[k] = tot.get(k, 0) + v
+        tot["oracle_expired"] = tot.get("oracle_expired", 0) + wst["expired"]
+        if rb.n:
+            gbuf, goff, gln = _frames(gpu_ctx, rb)
+            gorg = abi.download_ptr(gpu_ctx, origin.ptr, np.uint32, rb.n)
+            assert np.array_equal(gorg, wog) and np.array_equal(gln, wol)
+            for k in range(rb.n):
+                g = gbuf[goff[k]:goff[k] + gln[k]].tobytes()
+                w = wout[woo[k]:woo[k] + wol[k]].tobytes()
+                assert g == w, f"batch {b} datagram {k}"
+            # the demux of the reassembled datagrams (poller.c:362-412 after reassembly)
+            out2 = abi.rx_alloc_out(gpu_ctx, rb.n, 4, 4 * rb.n)
+            g2 = abi.rx_run(gpu_ctx, rb, out2)
+            w2 = O.rx(bt, wout, len(wout), woo, wol, np.full(rb.n, 0x211, np.uint32), 4)
+            assert g2[4] == 0
+            for x, y in zip(w2[:3], g2[:3]):
+                assert np.array_equal(x, y)
+            assert np.all(abi.meta_verdict(g2[0]) == 0)          # every datagram delivered
+            assert np.all(abi.meta_udp(g2[0]) == 0)             # checksum 0: "absent"
+            for bb in (out2.meta, out2.lane_off, out2.lane_pkt):
+                bb.free()
+        for bb in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt):
+            bb.free()
+    for k in ("errors", "holes", "expired", "done", "stored"):
+        assert tot[k] > 0, (k, tot)
+    assert abs(tot["expired"] - tot["oracle_expired"]) <= max(2, tot["oracle_expired"] // 4), tot
+
+
+def test_no_space_and_table_reuse(gpu_ctx):
+    """Two-slot table: a third live flow finds no space; expired flows free their slots."""
+    from reasm_util import split, udp_datagram, raw_ip
+    abi.frag_table_create(gpu_ctx, bucket_num=1, bucket_entries=2, max_cycles=100, max_dgram=256)
+    t = O.FragTable(bucket_num=1, bucket_entries=2, max_cycles=100, max_dgram=256)
+    src, dst = raw_ip("10.0.0.1"), raw_ip("172.31.100.1")
+    d = udp_datagram(1, 2, b"c" * 24)
+    fa, fb, fc = (split(src, dst, pid, d, [16, 16]) for pid in (10, 11, 12))
+    big = split(src, dst, 13, udp_datagram(1, 2, b"d" * 300), [160, 148])   # past max_dgram
+    steps = [([fa[0], fb[0]], 0), ([fc[0]], 50), ([fa[1]], 101), ([fc[0], fc[1]], 102), (big, 103)]
+    for frames, tms in steps:
+        buf, off, ln = batch(frames)
+        db = abi.rx_upload(gpu_ctx, buf, off, ln)
+        db.frames_bytes = len(buf) - 64
+        meta = O.rx(O.BindTable(), buf, len(buf) - 64, off, ln, None, 1)[0]
+        mb = gpu_ctx.upload(meta)
+        rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, mb, tms)
+        _, woo, _, _, wst = t.reassemble(buf, off, ln, meta, tms)
+        assert gst == wst and rb.n == len(woo), (tms, gst, wst)
+        for bb in (db.frames, db.offset, db.length, mb):
+            bb.free()
+
+
+def test_tx_fragments_come_back(gpu_ctx):
+    """GPU loop: tx_build_mtu (udpdk_sendto + the poller's fragmentation) -> rx -> reassembly ->
+    rx on the datagrams: every datagram is delivered with the payload that was sent."""
+    rng = np.random.default_rng(9)
+    mtu, n = 1500, 300
+    lens = [L for L in rng.integers(1473, 5900, 3 * n).tolist()
+            if (L + 8) % (mtu - 20) == 0 or (L + 8) % (mtu - 20) >= 26][:n]
+    pays = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in lens]
+    port = abi.raw_port(10001)
+    gpu_ctx.upload_snapshot(abi.snapshot_from_lists({port: [(0, 0, 0)]}, 1,
+                                                    slots=[(0, abi.raw_port(10000), 1)]))
+    abi.frag_table_create(gpu_ctx, bucket_num=64, bucket_entries=16, max_cycles=1000)
+    po = np.cumsum([0] + lens[:-1]).astype(np.uint32)
+    pay = np.zeros(int(po[-1]) + lens[-1] + 64, np.uint8)
+    for o, p in zip(po, pays):
+        pay[o:o + len(p)] = np.frombuffer(p, np.uint8)
+    spans = [int(abi.lib().udpdk_gpu_tx_span(L, mtu, None)) for L in lens]
+    fo = np.cumsum([0] + spans[:-1]).astype(np.uint32)
+    cap = int(fo[-1]) + spans[-1] + 64
+    bufs = [gpu_ctx.upload(pay), gpu_ctx.upload(po), gpu_ctx.upload(np.array(lens, np.uint16)),
+            gpu_ctx.upload(np.zeros(n, np.int32)),
+            gpu_ctx.upload(np.full(n, abi.raw_ip("172.31.100.1"), np.uint32)),
+            gpu_ctx.upload(np.full(n, port, np.uint16)), gpu_ctx.upload(fo)]
+    frames = gpu_ctx.alloc(cap)
+    cfg = abi.TxConfig((C.c_uint8 * 6)(*bytes.fromhex("6805ca95f8ec")),
+                       (C.c_uint8 * 6)(*bytes.fromhex("6805ca95fa64")), abi.raw_ip("172.31.100.2"))
+    tb = abi.TxBatch(bufs[0].ptr, len(pay), bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, bufs[4].ptr,
+                     bufs[5].ptr, n)
+    assert abi.lib().udpdk_gpu_tx_build_mtu(gpu_ctx.handle, C.byref(cfg), C.byref(tb),
+                                            C.byref(abi.TxOut(frames.ptr, cap, bufs[6].ptr)), mtu) == 0
+    # the fragment frames as an RX batch, in send order (every datagram has id 0, as sent)
+    off, ln = [], []
+    for L, f0 in zip(lens, fo):
+        nf = -(-(L + 8) // (mtu - 20))
+        for k in range(nf):
+            off.append(int(f0) + k * (mtu + 14))
+            ln.append(mtu + 14 if k + 1 < nf else 34 + (L + 8) - (nf - 1) * (mtu - 20))
+    off, ln = np.array(off, np.uint32), np.array(ln, np.uint16)
+    db = abi.RxDeviceBatch(frames, cap - 64, gpu_ctx.upload(off), gpu_ctx.upload(ln), None, len(off))
+    out = abi.rx_alloc_out(gpu_ctx, len(off), 1, len(off))
+    m1 = abi.rx_run(gpu_ctx, db, out)[0]
+    assert np.all(abi.meta_verdict(m1) == abi.V_FRAG)
+    rb, origin, st = abi.rx_reassemble(gpu_ctx, db, out.meta, 0)
+    assert st["done"] == n and st["errors"] == st["holes"] == st["stored"] == 0
+    out2 = abi.rx_alloc_out(gpu_ctx, n, 1, n)
+    m2, loff, lp, cnt, rc = abi.rx_run(gpu_ctx, rb, out2)
+    assert rc == 0 and np.all(abi.meta_verdict(m2) == 0) and np.array_equal(lp, np.arange(n))
+    g = abi.rx_alloc_gather(gpu_ctx, n, 6016)
+    gp, glen, gip, gport = abi.rx_gather_run(gpu_ctx, rb, out2.lane_pkt, 0, g)
+    for k in range(n):
+        assert glen[k] == lens[k] and gp[k, :lens[k]].tobytes() == pays[k], k
+    assert np.all(gport == abi.raw_port(10000)) and np.all(gip == abi.raw_ip("172.31.100.2"))

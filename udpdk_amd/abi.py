@@ -82,6 +82,20 @@ class RxGather(C.Structure):
                 ("src_ip_dev", C.c_void_p), ("src_port_dev", C.c_void_p)]
 
 
+RS_N = 9                  # udpdk_rs_stat
+RS_STATS = ("frags", "drop_len", "drop_short", "no_space", "errors", "holes", "expired", "done",
+            "stored")
+
+
+class FragTableCfg(C.Structure):
+    _fields_ = [("bucket_num", C.c_uint32), ("bucket_entries", C.c_uint32),
+                ("max_cycles", C.c_uint64), ("max_dgram", C.c_uint32)]
+
+
+class ReasmOut(C.Structure):
+    _fields_ = [("batch", RxBatch), ("origin_dev", C.c_void_p), ("stats", C.c_uint64 * RS_N)]
+
+
 class TxConfig(C.Structure):
     _fields_ = [("src_mac", C.c_uint8 * 6), ("dst_mac", C.c_uint8 * 6), ("src_ip", C.c_uint32)]
 
@@ -128,6 +142,8 @@ _PROTOS = {
     "udpdk_gpu_rx_host_wait": (C.c_int, [_P]),
     "udpdk_gpu_rx_gather": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint32, C.c_uint32,
                                       C.POINTER(RxGather)]),
+    "udpdk_gpu_frag_table_create": (C.c_int, [_P, C.POINTER(FragTableCfg)]),
+    "udpdk_gpu_rx_reassemble": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint64, C.POINTER(ReasmOut)]),
     "udpdk_gpu_tx_build": (C.c_int, [_P, C.POINTER(TxConfig), C.POINTER(TxBatch), C.POINTER(TxOut)]),
     "udpdk_gpu_tx_build_mtu": (C.c_int, [_P, C.POINTER(TxConfig), C.POINTER(TxBatch),
                                          C.POINTER(TxOut), C.c_uint32]),
@@ -429,6 +445,41 @@ def rx_gather_run(ctx: GpuContext, b: RxDeviceBatch, lane_pkt: DeviceBuffer, fir
     pay = ctx.download(g.payload, np.uint8, g.count * g.slot_bytes).reshape(g.count, g.slot_bytes)
     return (pay, ctx.download(g.length, np.uint32, g.count), ctx.download(g.src_ip, np.uint32, g.count),
             ctx.download(g.src_port, np.uint16, g.count))
+
+
+@dataclass
+class DevRef:
+    """A device pointer the context owns (no free)."""
+    ptr: int
+
+
+def frag_table_create(ctx: GpuContext, bucket_num: int = 0x1000, bucket_entries: int = 16,
+                      max_cycles: int = 1000, max_dgram: int = 65515):
+    cfg = FragTableCfg(bucket_num, bucket_entries, max_cycles, max_dgram)
+    _check(lib().udpdk_gpu_frag_table_create(ctx.handle, C.byref(cfg)), "udpdk_gpu_frag_table_create")
+
+
+def rx_reassemble(ctx: GpuContext, b: RxDeviceBatch, meta: DeviceBuffer, tms: int):
+    """Reassembly step for a batch whose verdicts are in meta. Returns (RxDeviceBatch of the
+    reassembled frames (context-owned), origin DevRef, stats dict)."""
+    bt = RxBatch(b.frames.ptr, b.frames_bytes, b.offset.ptr, b.length.ptr,
+                 b.ptype.ptr if b.ptype is not None else None, b.n)
+    o = ReasmOut()
+    _check(lib().udpdk_gpu_rx_reassemble(ctx.handle, C.byref(bt), C.c_void_p(meta.ptr), tms,
+                                         C.byref(o)), "udpdk_gpu_rx_reassemble")
+    ob = o.batch
+    rb = RxDeviceBatch(DevRef(ob.frames_dev or 0), int(ob.frames_bytes), DevRef(ob.offset_dev or 0),
+                       DevRef(ob.length_dev or 0), DevRef(ob.ptype_dev or 0), int(ob.n))
+    return rb, DevRef(o.origin_dev or 0), dict(zip(RS_STATS, list(o.stats)))
+
+
+def download_ptr(ctx: GpuContext, ptr: int, dtype, count: int) -> np.ndarray:
+    out = np.zeros(max(1, count), dtype)
+    if count:
+        _check(lib().udpdk_gpu_d2h(ctx.handle, out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr),
+                                   count * np.dtype(dtype).itemsize), "udpdk_gpu_d2h")
+        ctx.sync()
+    return out[:count]
 
 
 def geometry(n: int, n_lanes: int) -> tuple[int, int]:

@@ -172,6 +172,14 @@ __host__ __device__ constexpr uint32_t scatterw_lds_bytes(uint32_t n_lanes)
 }
 __global__ void rx_compact1(Compact1Args a);
 __global__ void rx_counters(const uint32_t *tile_cnt, uint32_t n_tiles, unsigned long long *counters);
+// RX reassembly (rx_reasm.hip): host-side table object driven by udpdk_gpu_rx_reassemble.
+struct Reasm;
+int  reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_table_cfg_t *cfg,
+                  int *hip_err);
+void reasm_destroy(Reasm *r);
+int  reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32_t *meta_dev,
+               uint64_t tms, udpdk_reasm_out_t *o, int *hip_err);
+
 __global__ void tx_build(TxArgs a);
 
 } // namespace udpdk

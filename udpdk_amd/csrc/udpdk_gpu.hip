@@ -92,6 +92,7 @@ struct udpdk_gpu_ctx {
     uint64_t host_calls = 0;                  // udpdk_gpu_rx_host_async calls (pipe choice)
 
     unsigned long long *dbg = nullptr;        // diagnostic stamp buffer (UDPDK_STAMPS builds)
+    Reasm *reasm = nullptr;                   // udpdk_gpu_frag_table_create
 
     // timing
     uint32_t timing_every = 0;                // 0 off, N: events on every Nth call
@@ -301,6 +302,8 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
     (void)hipSetDevice(c->device);
     for (Pipe &P : c->pipes)
         if (P.stream) (void)hipStreamSynchronize(P.stream);
+    reasm_destroy(c->reasm);
+    c->reasm = nullptr;
     void *dev[] = {c->port_tab, c->binds, c->slots};
     for (void *p : dev) if (p) (void)hipFree(p);
     for (Pipe &P : c->pipes) {
@@ -841,6 +844,29 @@ int udpdk_gpu_rx_gather(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint
         (void)hipEventDestroy(e1);
     }
     return 0;
+}
+
+int udpdk_gpu_frag_table_create(udpdk_gpu_ctx *c, const udpdk_frag_table_cfg_t *cfg)
+{
+    if (!c || !cfg) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    { int r = join_pipes(c); if (r) return r; }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    reasm_destroy(c->reasm);
+    c->reasm = nullptr;
+    return reasm_create(&c->reasm, c->device, c->max_frames, cfg, &c->last_err);
+}
+
+int udpdk_gpu_rx_reassemble(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint32_t *meta_dev,
+                            uint64_t tms, udpdk_reasm_out_t *o)
+{
+    if (!c || !bt || !o) return -EINVAL;
+    if (!c->reasm) return -EINVAL;
+    if (bt->n && (!bt->frames_dev || !bt->offset_dev || !bt->length_dev || !meta_dev)) return -EINVAL;
+    if (bt->frames_bytes >= (1ull << 32) || bt->n > c->max_frames) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    { int r = join_pipes(c); if (r) return r; }
+    return reasm_run(c->reasm, c->stream, bt, meta_dev, tms, o, &c->last_err);
 }
 
 uint64_t udpdk_gpu_tx_span(uint32_t len, uint32_t mtu, uint32_t *n_frames)
