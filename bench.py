@@ -202,10 +202,11 @@ def side_config(ctx, cfg: int, steps: int, rotate: int):
     return out
 
 
-def tx_line(ctx, payload_len: int, n: int, steps: int):
+def tx_line(ctx, payload_len: int, n: int, steps: int, mtu: int = 0):
     """udpdk_gpu_tx_build over n datagrams of payload_len bytes (one bound socket, ANY:10000 ->
     172.31.100.1:10001, frames back to back): device-resident TX header build + rte_ipv4_cksum +
-    payload copy, GPU time from events around `steps` back-to-back launches."""
+    payload copy, GPU time from events around `steps` back-to-back launches. mtu != 0: the
+    poller's fragmentation too (udpdk_gpu_tx_build_mtu)."""
     slots = [(0, abi.raw_port(10000), 1)]
     hs = abi.snapshot_from_lists({}, 1, slots=slots)
     ctx.upload_snapshot(hs)
@@ -213,19 +214,20 @@ def tx_line(ctx, payload_len: int, n: int, steps: int):
     pay = rng.integers(0, 256, n * payload_len + 64, dtype=np.uint8)
     pay_off = (np.arange(n, dtype=np.uint64) * payload_len).astype(np.uint32)
     lens = np.full(n, payload_len, np.uint16)
-    frame_off = (np.arange(n, dtype=np.uint64) * (payload_len + 42)).astype(np.uint32)
+    span = int(abi.lib().udpdk_gpu_tx_span(payload_len, mtu, None))
+    frame_off = (np.arange(n, dtype=np.uint64) * span).astype(np.uint32)
     bufs = [ctx.upload(pay), ctx.upload(pay_off), ctx.upload(lens), ctx.upload(np.zeros(n, np.int32)),
             ctx.upload(np.full(n, abi.raw_ip("172.31.100.1"), np.uint32)),
             ctx.upload(np.full(n, abi.raw_port(10001), np.uint16)), ctx.upload(frame_off)]
-    cap = n * (payload_len + 42) + 64
+    cap = n * span + 64
     out = ctx.alloc(cap)
     cfg = abi.TxConfig((C.c_uint8 * 6)(*bytes.fromhex("6805ca95f8ec")),
                        (C.c_uint8 * 6)(*bytes.fromhex("6805ca95fa64")), abi.raw_ip("172.31.100.2"))
     bt = abi.TxBatch(bufs[0].ptr, pay.nbytes, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, bufs[4].ptr,
                      bufs[5].ptr, n)
     ot = abi.TxOut(out.ptr, cap, bufs[6].ptr)
-    f = abi.lib().udpdk_gpu_tx_build
-    args = (ctx.handle, C.byref(cfg), C.byref(bt), C.byref(ot))
+    f = abi.lib().udpdk_gpu_tx_build_mtu
+    args = (ctx.handle, C.byref(cfg), C.byref(bt), C.byref(ot), mtu)
     for _ in range(5):
         abi._check(f(*args), "udpdk_gpu_tx_build")
     ev = HipEvents(ctx)
@@ -237,12 +239,52 @@ def tx_line(ctx, payload_len: int, n: int, steps: int):
     ctx.sync()
     us = 1e3 * ev.elapsed_ms() / steps
     ev.close()
-    nbytes = n * payload_len + n * (payload_len + 42) + 12 * n   # payload in, frames out, metadata
+    nbytes = n * payload_len + n * span + 12 * n   # payload in, frames out, metadata
     for b in bufs + [out]:
         b.free()
-    return {"workload": f"TX {n} x {payload_len + 42} B frames", "mpkt_s": round(n / us, 1),
+    nf = C.c_uint32()
+    abi.lib().udpdk_gpu_tx_span(payload_len, mtu, C.byref(nf))
+    what = f"TX {n} x {payload_len + 42} B frames" if nf.value == 1 else \
+        f"TX {n} x {payload_len} B datagrams -> {nf.value} fragments at MTU {mtu}"
+    return {"workload": what, "mpkt_s": round(n / us, 1),
             "us_per_launch": round(us, 2), "gbps": round(nbytes / us / 1e3, 1),
             "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4)}
+
+
+def reasm_line(ctx, n_dgrams: int, payload_len: int, reps: int):
+    """udpdk_gpu_rx_reassemble (f2) over a batch of n_dgrams datagrams of payload_len bytes cut
+    at MTU 1500 (frames.frag_batch: every datagram its own flow, fragments in order), the table
+    at the reference geometry (0x1000 buckets x 16, udpdk_poller.c:130). The call is synchronous
+    (collect, two radix sorts, flow processing, completion sort + scan, emit), so the time is
+    host wall clock per call. Bytes: fragment frames read + datagram frames written."""
+    b = F.frag_batch(n_dgrams, payload_len)
+    ctx.upload_snapshot(abi.snapshot_from_lists({abi.raw_port(F.PORT_RECV): [(0, 0, 0)]}, 1))
+    abi.frag_table_create(ctx, 0x1000, 16, 1 << 40, 65515)
+    db = abi.rx_upload(ctx, b.frames, b.offset, b.length)
+    db.frames_bytes = b.frames_bytes
+    out = abi.rx_alloc_out(ctx, b.n, 1, b.n)
+    abi.rx_run(ctx, db, out)
+    rb, _, st = abi.rx_reassemble(ctx, db, out.meta, 0)
+    assert st["done"] == n_dgrams, st
+    out_bytes = int(rb.frames_bytes)
+    t0 = time.perf_counter()
+    for r in range(reps):
+        rb, _, st = abi.rx_reassemble(ctx, db, out.meta, r + 1)
+    us = 1e6 * (time.perf_counter() - t0) / reps
+    assert st["done"] == n_dgrams, st
+    # the demux of the reassembled datagrams (full UDP checksum over each datagram)
+    out2 = abi.rx_alloc_out(ctx, n_dgrams, 1, n_dgrams)
+    m2 = abi.rx_run(ctx, rb, out2)[0]
+    ok = bool(np.all(abi.meta_verdict(m2) == 0) and np.all(abi.meta_udp(m2) == 1))
+    for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt, out2.meta,
+              out2.lane_off, out2.lane_pkt):
+        x.free()
+    nbytes = b.frames_bytes + out_bytes
+    return {"workload": f"reassembly {n_dgrams} x {payload_len} B datagrams ({b.n // n_dgrams} fragments "
+                        f"each, MTU 1500), one batch", "mdgram_s": round(n_dgrams / us, 2),
+            "us_per_call": round(us, 1), "gbps": round(nbytes / us / 1e3, 1),
+            "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4), "all_delivered_udp_ok": ok,
+            "timing": "host wall clock per synchronous call"}
 
 
 def gather_line(ctx, cfg: int, steps: int, slot: int = 2048):
@@ -483,7 +525,15 @@ def main():
                 tx.append(tx_line(ctx, plen, 1 << 20, 50))
             except Exception as e:
                 tx.append({"payload": plen, "error": repr(e)})
+        try:
+            tx.append(tx_line(ctx, 2952, 1 << 18, 50, mtu=1500))     # 2 x 1514 B fragments each
+        except Exception as e:
+            tx.append({"payload": 2952, "mtu": 1500, "error": repr(e)})
         line["tx"] = tx
+        try:
+            line["reassembly"] = [reasm_line(ctx, 1 << 18, 2952, 10)]
+        except Exception as e:
+            line["reassembly"] = [{"error": repr(e)}]
         ga = []
         for cfg in (2, 3):
             try:

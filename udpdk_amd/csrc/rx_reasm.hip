@@ -45,17 +45,22 @@ constexpr uint32_t RS_BLOCK = 256;
 constexpr uint32_t RS_WAVES = RS_BLOCK / 64;
 constexpr uint32_t RS_HELD = 0xFFFFFFFFu;       // fragment data lives in the entry buffer
 constexpr uint32_t RS_NONE = 0xFFFFFFFFu;
+constexpr uint32_t RS_VIRTUAL = 0xFFFFFFFEu;    // flow state only in LDS (no table entry yet)
 constexpr uint32_t RS_MAX_FRAG = 4;             // RTE_LIBRTE_IP_FRAG_MAX_FRAG
 constexpr uint32_t RS_SPIN = 1u << 20;          // bound on lock spins / find retries
 
-struct FragEntry {            // one table entry (struct ip_frag_pkt)
-    uint32_t lock;            // 0 free, else holder tag
-    uint32_t valid;           // key_len != 0
-    uint32_t src, dst, id;
-    uint32_t frag_size, total_size, last_idx;
-    unsigned long long start;
-    uint32_t fr[RS_MAX_FRAG];     // ofs | len << 16, 0 = empty slot (len > 0 when present)
-    uint32_t where[RS_MAX_FRAG];  // frame index in the current call, or RS_HELD
+// One table entry (struct ip_frag_pkt) as 20 u32 words, every one accessed with agent-scope
+// relaxed atomics; a wave holding the entry's lock owns the words after E_ID.
+enum : uint32_t {
+    E_LOCK = 0,         // 0 free, else holder tag
+    E_VALID = 1,        // key_len != 0
+    E_SRC = 2, E_DST = 3, E_ID = 4,
+    E_FSIZE = 5, E_TOTAL = 6, E_LAST = 7,
+    E_START = 8,        // u64 start (lo, hi)
+    E_FR = 10,          // [4] ofs | len << 16, 0 = empty slot (len > 0 when present)
+    E_WHERE = 14,       // [4] frame index in the current call, or RS_HELD
+    E_USED = 18,
+    E_WORDS = 20
 };
 
 struct ReasmDone {            // one reassembled datagram
@@ -76,15 +81,20 @@ struct ReasmArgs {
     const uint32_t *v1s;               // [F] frame indices sorted by (id, index)
     unsigned long long *k2;            // [F] src | dst << 32 in v1s order
     const uint32_t *order;             // [F] frame indices sorted by (src, dst, id, index)
+    // per sorted position (reasm_prep): frame index, key, crc32c signature, and
+    // len | (fragment offset / 8) << 16 | MF << 29 | class << 30 (0 ok, 1 no data, 2 too long)
+    uint32_t *s_i, *s_src, *s_dst, *s_id, *s_sig, *s_meta;
     uint32_t *counts;                  // [0] F, [1] completions, [2] store jobs
     unsigned long long *stats;         // [UDPDK_RS_N]
     unsigned long long *out_bytes;
-    FragEntry *tab;
+    uint32_t *tab;                     // [entries][E_WORDS]
     uint8_t *ebuf;
     uint32_t mask, assoc, max_dgram, stride;
     unsigned long long max_cycles, tms;
-    ReasmDone *done;
-    ReasmJob *jobs;
+    ReasmDone *done;                   // [F] at the completing fragment's position
+    unsigned long long *dk;            // [F] origin of the completion there, or ~0
+    uint32_t *dv;                      // [F] 0..F-1
+    ReasmJob *jobs;                    // [F] at the stored fragment's position (frame ~0: none)
     uint32_t tag_base;
 };
 
@@ -153,27 +163,58 @@ __device__ void wave_copy(uint8_t *dst, __amdgpu_buffer_rsrc_t r, uint32_t src_o
     if (lane < tail) dst[head + 4u * body + lane] = (uint8_t)ld32(r, src_off + head + 4u * body + lane);
 }
 
+// As wave_copy, with 16-byte stores once the destination is 16-byte aligned (byte-aligned
+// 16-byte loads from the source).
+__device__ void wave_copy16(uint8_t *dst, __amdgpu_buffer_rsrc_t r, uint32_t src_off, uint32_t len)
+{
+    const uint32_t lane = __lane_id();
+    const uint32_t head = std::min<uint32_t>((16u - ((uint32_t)(uintptr_t)dst & 15u)) & 15u, len);
+    if (lane < head) dst[lane] = (uint8_t)ld32(r, src_off + lane);
+    const uint32_t body = (len - head) >> 4;
+    uint4 *d16 = reinterpret_cast<uint4 *>(dst + head);
+    for (uint32_t k = lane; k < body; k += 64) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(src_off + head + 16u * k), 0, 0);
+        d16[k] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    const uint32_t done = head + 16u * body, tail = len - done;
+    if (lane < tail) dst[done + lane] = (uint8_t)ld32(r, src_off + done + lane);
+}
+
 } // namespace
 
 // FRAG verdicts -> fragment list and sort keys (order within the list does not matter: the
-// keys carry the arrival index).
+// keys carry the arrival index). Each workgroup takes a contiguous range of frames, counts its
+// fragments, reserves their slots with one atomic, then writes them.
 __global__ void __launch_bounds__(RS_BLOCK) reasm_collect(ReasmArgs a)
 {
+    __shared__ uint32_t s_n, s_base, s_off;
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
     const uint32_t lane = __lane_id();
-    for (uint32_t i0 = (blockIdx.x * RS_BLOCK + threadIdx.x) & ~63u; i0 < a.n; i0 += gridDim.x * RS_BLOCK) {
+    const uint32_t per = ((a.n + gridDim.x - 1) / gridDim.x + RS_BLOCK - 1) / RS_BLOCK * RS_BLOCK;
+    const uint32_t b0 = blockIdx.x * per, b1 = min(a.n, b0 + per);
+    if (threadIdx.x == 0) { s_n = 0; s_off = 0; }
+    __syncthreads();
+    uint32_t c = 0;
+    for (uint32_t i = b0 + threadIdx.x; i < b1; i += RS_BLOCK) c += (a.meta[i] & 0xFu) == UDPDK_V_FRAG;
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+    if (lane == 0 && c) atomicAdd(&s_n, c);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_base = s_n ? atomicAdd(&a.counts[0], s_n) : 0u;
+        if (s_n) atomicAdd(&a.stats[UDPDK_RS_FRAGS], (unsigned long long)s_n);
+    }
+    __syncthreads();
+    if (!s_n) return;
+    for (uint32_t i0 = b0 + (threadIdx.x & ~63u); i0 < b1; i0 += RS_BLOCK) {
         const uint32_t i = i0 + lane;
-        const bool f = i < a.n && (a.meta[i] & 0xFu) == UDPDK_V_FRAG;
+        const bool f = i < b1 && (a.meta[i] & 0xFu) == UDPDK_V_FRAG;
         const unsigned long long m = __ballot(f);
         if (!m) continue;
-        uint32_t base = 0;
-        if (lane == 0) {
-            base = atomicAdd(&a.counts[0], (uint32_t)__popcll(m));
-            atomicAdd(&a.stats[UDPDK_RS_FRAGS], (unsigned long long)__popcll(m));
-        }
-        base = __shfl(base, 0, 64);
+        uint32_t off = 0;
+        if (lane == 0) off = atomicAdd(&s_off, (uint32_t)__popcll(m));
+        off = __shfl(off, 0, 64);
         if (f) {
-            const uint32_t j = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            const uint32_t j = s_base + off + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
             const uint32_t id = ld32(fr, a.offset[i] + 16) >> 16;
             a.frag_list[j] = i;
             a.k1[j] = ((unsigned long long)id << 32) | i;
@@ -191,135 +232,183 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_keys(ReasmArgs a, uint32_t F)
     }
 }
 
+// Per sorted position: the fragment's frame, key, signature and length class (all lanes in
+// parallel, so the flow walk below reads one coalesced record per fragment).
+__global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
+{
+    const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
+    for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
+        const uint32_t i = a.order[p];
+        const FragHdr h = frag_hdr(a, fr, i);
+        const int32_t ip_len = (int32_t)h.tl - 20;                    // l3_len = 20
+        const uint32_t ofs = (h.ff & 0x1FFFu) * 8u;
+        uint32_t cls = 0, len = 0;
+        if (ip_len <= 0) {
+            cls = 1;
+        } else {
+            len = (uint32_t)ip_len;
+            if (34u + len > h.flen || ofs + len > a.max_dgram) cls = 2;
+        }
+        uint32_t v = crc32c_u32(0xeaad8405u, h.src);
+        v = crc32c_u32(v, h.dst);
+        v = crc32c_u32(v, h.id);
+        a.s_i[p] = i;
+        a.s_src[p] = h.src;
+        a.s_dst[p] = h.dst;
+        a.s_id[p] = h.id;
+        a.s_sig[p] = v;
+        a.s_meta[p] = (cls ? 0u : len) | ((h.ff & 0x1FFFu) << 16) | ((h.ff & 0x2000u) << 16) | (cls << 30);
+        a.dv[p] = p;
+    }
+}
+
 namespace {
 
-struct WaveState {                // lane 0's copy of the held entry (LDS, one per wave)
-    uint32_t frag_size, total_size, last_idx;
-    uint32_t fr[RS_MAX_FRAG], where[RS_MAX_FRAG];
-};
+// Orders a wave's LDS accesses across lanes (DS instructions of one wave execute in order).
+__device__ __forceinline__ void wave_sync_rs()
+{
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
 
-// ip_frag_find: returns the locked entry for the key, or RS_NONE (no space). Wave-uniform.
+// Every store this wave issued has completed (CDNA counts stores in vmcnt).
+__device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Fresh flow state (ip_frag_reset) for lane 0.
+__device__ void state_reset(const ReasmArgs &a, uint32_t *st, uint32_t src, uint32_t dst, uint32_t id)
+{
+    st[E_VALID] = 1;
+    st[E_SRC] = src;
+    st[E_DST] = dst;
+    st[E_ID] = id;
+    st[E_FSIZE] = 0;
+    st[E_TOTAL] = 0xFFFFFFFFu;
+    st[E_LAST] = 2;
+    st[E_START] = (uint32_t)a.tms;
+    st[E_START + 1] = (uint32_t)(a.tms >> 32);
+    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) { st[E_FR + k] = 0; st[E_WHERE + k] = RS_HELD; }
+}
+
+// ip_frag_find: returns the entry for the key, locked by this wave with its words in st[], or
+// RS_NONE (no space). With allow_virtual, a key that is not in the table while its buckets
+// have a free slot (and no expired one to reclaim) gets RS_VIRTUAL: the flow starts in LDS and
+// only takes a table entry if it is still pending when the wave leaves it (a flow that
+// completes or fails inside one batch never touches the table). Wave-uniform.
 __device__ uint32_t table_find(const ReasmArgs &a, uint32_t src, uint32_t dst, uint32_t id,
-                               uint32_t tag, WaveState &ws)
+                               uint32_t sig, uint32_t tag, uint32_t *st, unsigned long long *cnt,
+                               bool allow_virtual)
 {
     const uint32_t lane = __lane_id();
-    uint32_t v = crc32c_u32(0xeaad8405u, src);
-    v = crc32c_u32(v, dst);
-    v = crc32c_u32(v, id);
-    const uint32_t p1 = v & a.mask, p2 = ((v << 7) + (v >> 14)) & a.mask;
+    const uint32_t p1 = sig & a.mask, p2 = ((sig << 7) + (sig >> 14)) & a.mask;
     for (uint32_t tries = 0; tries < RS_SPIN; ++tries) {
         // lanes scan p1[0], p2[0], p1[1], p2[1], ... (ip_frag_lookup's order)
-        const bool in = lane < 2u * a.assoc;
         const uint32_t slot = (lane & 1u ? p2 : p1) + (lane >> 1);
         bool match = false, empty = false, stale = false;
-        if (in) {
-            const FragEntry *e = a.tab + slot;
-            const uint32_t val = ld_a(&e->valid);
-            if (val) {
-                match = ld_a(&e->src) == src && ld_a(&e->dst) == dst && ld_a(&e->id) == id;
-                stale = !match && a.max_cycles + ld_a(&e->start) < a.tms;
-            } else {
-                empty = true;
-            }
+        if (lane < 2u * a.assoc) {
+            const uint32_t *e = a.tab + (size_t)slot * E_WORDS;
+            const uint32_t val = ld_a(e + E_VALID), es = ld_a(e + E_SRC), ed = ld_a(e + E_DST);
+            const uint32_t ei = ld_a(e + E_ID), lo = ld_a(e + E_START), hi = ld_a(e + E_START + 1);
+            const unsigned long long start = ((unsigned long long)hi << 32) | lo;
+            match = val && es == src && ed == dst && ei == id;
+            stale = val && !match && a.max_cycles + start < a.tms;
+            empty = !val;
         }
         const unsigned long long mm = __ballot(match), ms = __ballot(stale), me = __ballot(empty);
         uint32_t cand;
-        int kind;                                  // 0 match, 1 stale, 2 empty
+        uint32_t kind;                               // 0 match, 1 stale, 2 empty
         if (mm) { cand = __shfl(slot, __ffsll((long long)mm) - 1, 64); kind = 0; }
         else if (ms) { cand = __shfl(slot, __ffsll((long long)ms) - 1, 64); kind = 1; }
-        else if (me) { cand = __shfl(slot, __ffsll((long long)me) - 1, 64); kind = 2; }
-        else return RS_NONE;
-        uint32_t ok = 0;
+        else if (me) {
+            if (allow_virtual) {
+                if (lane == 0) state_reset(a, st, src, dst, id);
+                wave_sync_rs();
+                return RS_VIRTUAL;
+            }
+            cand = __shfl(slot, __ffsll((long long)me) - 1, 64);
+            kind = 2;
+        } else {
+            return RS_NONE;
+        }
+        uint32_t *e = a.tab + (size_t)cand * E_WORDS;
+        uint32_t got = 0;
         if (lane == 0) {
-            FragEntry *e = a.tab + cand;
             uint32_t exp = 0;
-            bool got = __hip_atomic_compare_exchange_strong(&e->lock, &exp, tag, __ATOMIC_ACQUIRE,
-                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // a matching entry can only be held briefly by a wave testing it as a candidate
-            for (uint32_t s = 0; !got && kind == 0 && s < RS_SPIN; ++s) {
+            got = __hip_atomic_compare_exchange_strong(e + E_LOCK, &exp, tag, __ATOMIC_RELAXED,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // a matching entry is only held briefly by a wave testing it as a candidate
+            for (uint32_t k = 0; !got && kind == 0 && k < RS_SPIN; ++k) {
                 __builtin_amdgcn_s_sleep(2);
                 exp = 0;
-                got = __hip_atomic_compare_exchange_strong(&e->lock, &exp, tag, __ATOMIC_ACQUIRE,
+                got = __hip_atomic_compare_exchange_strong(e + E_LOCK, &exp, tag, __ATOMIC_RELAXED,
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (got) {
-                const uint32_t val = ld_a(&e->valid);
-                const bool same = val && ld_a(&e->src) == src && ld_a(&e->dst) == dst && ld_a(&e->id) == id;
-                const bool expired = val && a.max_cycles + ld_a(&e->start) < a.tms;
-                bool fresh = false;
-                if (kind == 0 && same) {
-                    ok = 1;
-                    if (expired) {                                   // ip_frag_tbl_reuse
-                        atomicAdd(&a.stats[UDPDK_RS_EXPIRED], 1ull);
-                        fresh = true;
-                    }
-                } else if (kind == 1 && val && !same && expired) {   // ip_frag_tbl_del + add
-                    atomicAdd(&a.stats[UDPDK_RS_EXPIRED], 1ull);
-                    ok = 1;
-                    fresh = true;
-                } else if (kind == 2 && !val) {                      // ip_frag_tbl_add
-                    ok = 1;
-                    fresh = true;
-                }
-                if (ok && fresh) {
-                    st_a(&e->src, src);
-                    st_a(&e->dst, dst);
-                    st_a(&e->id, id);
-                    st_a(&e->start, a.tms);
-                    st_a(&e->valid, 1u);
-                    ws.frag_size = 0;
-                    ws.total_size = 0xFFFFFFFFu;
-                    ws.last_idx = 2;
-                    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) { ws.fr[k] = 0; ws.where[k] = RS_HELD; }
-                } else if (ok) {
-                    ws.frag_size = ld_a(&e->frag_size);
-                    ws.total_size = ld_a(&e->total_size);
-                    ws.last_idx = ld_a(&e->last_idx);
-                    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
-                        ws.fr[k] = ld_a(&e->fr[k]);
-                        ws.where[k] = ld_a(&e->where[k]);
-                    }
-                } else {
-                    __hip_atomic_store(&e->lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
         }
+        if (!__shfl(got, 0, 64)) continue;
+        // under the lock: the entry's words (the previous holder's stores completed before it
+        // released the lock)
+        if (lane < E_USED) st[lane] = lane == E_LOCK ? tag : ld_a(e + lane);
+        wave_sync_rs();
+        uint32_t ok = 0, fresh = 0;
+        if (lane == 0) {
+            const bool val = st[E_VALID] != 0;
+            const bool same = val && st[E_SRC] == src && st[E_DST] == dst && st[E_ID] == id;
+            const unsigned long long start =
+                ((unsigned long long)st[E_START + 1] << 32) | st[E_START];
+            const bool expired = val && a.max_cycles + start < a.tms;
+            if (kind == 0 && same) {
+                ok = 1;
+                if (expired) {                                   // ip_frag_tbl_reuse
+                    atomicAdd(&cnt[UDPDK_RS_EXPIRED], 1ull);
+                    fresh = 1;
+                }
+            } else if (kind == 1 && val && !same && expired) {   // ip_frag_tbl_del + add
+                atomicAdd(&cnt[UDPDK_RS_EXPIRED], 1ull);
+                ok = fresh = 1;
+            } else if (kind == 2 && !val) {                      // ip_frag_tbl_add
+                ok = fresh = 1;
+            }
+            if (fresh) state_reset(a, st, src, dst, id);
+        }
+        wave_sync_rs();
         ok = __shfl(ok, 0, 64);
-        if (ok) return cand;
+        if (!ok) {
+            if (lane == 0) st_a(e + E_LOCK, 0u);
+            continue;
+        }
+        if (__shfl(fresh, 0, 64) && lane >= E_VALID && lane < E_USED) st_a(e + lane, st[lane]);
+        return cand;
     }
     return RS_NONE;
 }
 
-// Write the held entry's state back and release it (lane 0).
-__device__ void table_release(const ReasmArgs &a, uint32_t cur, const WaveState &ws, bool invalidate)
+// Write the held entry back (or invalidate it) and release the lock. Wave-uniform.
+__device__ void table_release(const ReasmArgs &a, uint32_t cur, const uint32_t *st, bool invalidate)
 {
-    FragEntry *e = a.tab + cur;
+    const uint32_t lane = __lane_id();
+    uint32_t *e = a.tab + (size_t)cur * E_WORDS;
+    wave_sync_rs();
     if (invalidate) {
-        st_a(&e->valid, 0u);
-    } else {
-        st_a(&e->frag_size, ws.frag_size);
-        st_a(&e->total_size, ws.total_size);
-        st_a(&e->last_idx, ws.last_idx);
-        for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
-            st_a(&e->fr[k], ws.fr[k]);
-            st_a(&e->where[k], ws.where[k]);
-        }
+        if (lane == 0) st_a(e + E_VALID, 0u);
+    } else if (lane >= E_FSIZE && lane < E_USED) {
+        st_a(e + lane, st[lane]);
     }
-    __hip_atomic_store(&e->lock, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    stores_done();
+    if (lane == 0) st_a(e + E_LOCK, 0u);
 }
 
 // ipv4_frag_reassemble's backward chain walk over the held fragments.
-__device__ bool chain_ok(const WaveState &ws)
+__device__ bool chain_ok(const uint32_t *st)
 {
-    const uint32_t first_len = ws.fr[0] >> 16;
-    const uint32_t n = ws.last_idx - 1u;
-    uint32_t ofs = ws.fr[1] & 0xFFFFu, curr = 1;
+    const uint32_t *fr = st + E_FR;
+    const uint32_t first_len = fr[0] >> 16;
+    const uint32_t n = st[E_LAST] - 1u;
+    uint32_t ofs = fr[1] & 0xFFFFu, curr = 1;
     for (uint32_t guard = 0; ofs != first_len && guard < 8; ++guard) {
         const uint32_t prev = curr;
         for (uint32_t i = n; i != 0 && ofs != first_len; i--) {
-            if ((ws.fr[i] & 0xFFFFu) + (ws.fr[i] >> 16) == ofs) {
+            if ((fr[i] & 0xFFFFu) + (fr[i] >> 16) == ofs) {
                 curr = i;
-                ofs = ws.fr[i] & 0xFFFFu;
+                ofs = fr[i] & 0xFFFFu;
             }
         }
         if (curr == prev) return false;
@@ -329,128 +418,132 @@ __device__ bool chain_ok(const WaveState &ws)
 
 } // namespace
 
-// One wave per flow segment of the sorted fragment list.
+// One wave per flow segment of the sorted fragment list; lane 0 runs ip_frag_process on the
+// held entry's words in LDS, the other lanes scan buckets and move entry words.
 __global__ void __launch_bounds__(RS_BLOCK) reasm_process(ReasmArgs a, uint32_t F)
 {
-    __shared__ WaveState s_ws[RS_WAVES];
-    const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
+    __shared__ uint32_t s_st[RS_WAVES][E_WORDS];
+    __shared__ uint32_t s_tmp[RS_WAVES][E_WORDS];           // entry words while installing
+    __shared__ uint32_t s_pos[RS_WAVES][RS_MAX_FRAG];      // sorted position of each held slot
+    __shared__ unsigned long long s_cnt[UDPDK_RS_N + 1];    // block totals: stats, out bytes
     const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
-    WaveState &ws = s_ws[w];
+    uint32_t *st = s_st[w];
+    unsigned long long *cnt = s_cnt;
+    if (threadIdx.x <= UDPDK_RS_N) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
     const uint32_t gw = blockIdx.x * RS_WAVES + w, nw = gridDim.x * RS_WAVES;
     const uint32_t tag = a.tag_base + gw + 1u;
     for (uint32_t base = gw * 64u; base < F; base += nw * 64u) {
         const uint32_t p = base + lane;
         bool start = false;
         if (p < F) {
-            const FragHdr h = frag_hdr(a, fr, a.order[p]);
-            if (p == 0) {
-                start = true;
-            } else {
-                const FragHdr g = frag_hdr(a, fr, a.order[p - 1]);
-                start = g.src != h.src || g.dst != h.dst || g.id != h.id;
-            }
+            start = p == 0 || a.s_src[p] != a.s_src[p - 1] || a.s_dst[p] != a.s_dst[p - 1] ||
+                    a.s_id[p] != a.s_id[p - 1];
         }
         unsigned long long starts = __ballot(start);
         while (starts) {
             const uint32_t s = base + (uint32_t)(__ffsll((long long)starts) - 1);
             starts &= starts - 1ull;
-            const FragHdr k0 = frag_hdr(a, fr, a.order[s]);
+            const uint32_t ksrc = a.s_src[s], kdst = a.s_dst[s], kid = a.s_id[s], sig = a.s_sig[s];
             uint32_t cur = RS_NONE;
             for (uint32_t q = s; q < F; ++q) {
-                const uint32_t i = a.order[q];
-                const FragHdr h = frag_hdr(a, fr, i);
-                if (q != s && (h.src != k0.src || h.dst != k0.dst || h.id != k0.id)) break;
-                const int32_t ip_len = (int32_t)h.tl - 20;                // l3_len = 20
-                if (ip_len <= 0) {
-                    if (lane == 0) atomicAdd(&a.stats[UDPDK_RS_DROP_LEN], 1ull);
+                const uint32_t i = a.s_i[q], m = a.s_meta[q];
+                if (q != s && (a.s_src[q] != ksrc || a.s_dst[q] != kdst || a.s_id[q] != kid)) break;
+                const uint32_t cls = m >> 30;
+                if (cls) {
+                    if (lane == 0) atomicAdd(&cnt[cls == 1 ? UDPDK_RS_DROP_LEN : UDPDK_RS_DROP_SHORT], 1ull);
                     continue;
                 }
-                const uint32_t len = (uint32_t)ip_len;
-                const uint32_t ofs = (h.ff & 0x1FFFu) * 8u, mf = h.ff & 0x2000u;
-                if (34u + len > h.flen || ofs + len > a.max_dgram) {
-                    if (lane == 0) atomicAdd(&a.stats[UDPDK_RS_DROP_SHORT], 1ull);
-                    continue;
-                }
+                const uint32_t len = m & 0xFFFFu, ofs = ((m >> 16) & 0x1FFFu) * 8u, mf = (m >> 29) & 1u;
                 if (cur == RS_NONE) {
-                    cur = table_find(a, k0.src, k0.dst, k0.id, tag, ws);
+                    cur = table_find(a, ksrc, kdst, kid, sig, tag, st, cnt, true);
                     if (cur == RS_NONE) {
-                        if (lane == 0) atomicAdd(&a.stats[UDPDK_RS_NO_SPACE], 1ull);
+                        if (lane == 0) atomicAdd(&cnt[UDPDK_RS_NO_SPACE], 1ull);
                         continue;
                     }
                 }
                 // ip_frag_process (lane 0 owns the state; the outcome is broadcast)
-                uint32_t keep = 1;
+                uint32_t outcome = 0;                 // 0 keep, 1 invalidate
                 if (lane == 0) {
                     uint32_t idx;
-                    ws.frag_size += len;
+                    st[E_FSIZE] += len;
                     if (ofs == 0) {
-                        idx = ws.fr[0] == 0 ? 0u : RS_NONE;
+                        idx = st[E_FR + 0] == 0 ? 0u : RS_NONE;
                     } else if (!mf) {
-                        ws.total_size = ofs + len;
-                        idx = ws.fr[1] == 0 ? 1u : RS_NONE;
+                        st[E_TOTAL] = ofs + len;
+                        idx = st[E_FR + 1] == 0 ? 1u : RS_NONE;
                     } else {
-                        idx = ws.last_idx;
-                        if (idx < RS_MAX_FRAG) ws.last_idx++;
+                        idx = st[E_LAST];
+                        if (idx < RS_MAX_FRAG) st[E_LAST] = idx + 1u;
                     }
                     if (idx >= RS_MAX_FRAG) {
-                        atomicAdd(&a.stats[UDPDK_RS_ERRORS], 1ull);
-                        table_release(a, cur, ws, true);
-                        keep = 0;
+                        atomicAdd(&cnt[UDPDK_RS_ERRORS], 1ull);
+                        outcome = 1;
                     } else {
-                        ws.fr[idx] = ofs | (len << 16);
-                        ws.where[idx] = i;
-                        if (ws.frag_size >= ws.total_size) {
-                            const bool sized = ws.frag_size == ws.total_size && ws.fr[0] != 0;
-                            if (sized && chain_ok(ws)) {
-                                const uint32_t d = atomicAdd(&a.counts[1], 1u);
+                        st[E_FR + idx] = ofs | (len << 16);
+                        st[E_WHERE + idx] = i;
+                        s_pos[w][idx] = q;
+                        if (st[E_FSIZE] >= st[E_TOTAL]) {
+                            const bool sized = st[E_FSIZE] == st[E_TOTAL] && st[E_FR + 0] != 0;
+                            if (sized && chain_ok(st)) {
                                 ReasmDone r;
                                 r.origin = i;
-                                r.total = ws.total_size;
-                                r.n = ws.last_idx;
+                                r.total = st[E_TOTAL];
+                                r.n = st[E_LAST];
                                 r.entry = cur;
-                                for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) { r.fr[k] = ws.fr[k]; r.where[k] = ws.where[k]; }
-                                a.done[d] = r;
-                                atomicAdd(a.out_bytes, (unsigned long long)((34u + ws.total_size + 15u) & ~15u));
-                                atomicAdd(&a.stats[UDPDK_RS_DONE], 1ull);
+                                for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
+                                    r.fr[k] = st[E_FR + k];
+                                    r.where[k] = st[E_WHERE + k];
+                                }
+                                a.done[q] = r;
+                                a.dk[q] = i;
+                                atomicAdd(&cnt[UDPDK_RS_N], (unsigned long long)((34u + st[E_TOTAL] + 15u) & ~15u));
+                                atomicAdd(&cnt[UDPDK_RS_DONE], 1ull);
                             } else {
-                                atomicAdd(&a.stats[sized ? UDPDK_RS_HOLES : UDPDK_RS_ERRORS], 1ull);
+                                atomicAdd(&cnt[sized ? UDPDK_RS_HOLES : UDPDK_RS_ERRORS], 1ull);
                             }
-                            table_release(a, cur, ws, true);
-                            keep = 0;
+                            outcome = 1;
                         }
                     }
                 }
-                if (!__shfl(keep, 0, 64)) cur = RS_NONE;
+                if (__shfl(outcome, 0, 64)) {
+                    if (cur != RS_VIRTUAL) table_release(a, cur, st, true);
+                    cur = RS_NONE;
+                }
             }
-            if (cur != RS_NONE && lane == 0) {
-                // still pending: this call's fragments move into the entry buffer (reasm_store)
-                for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
-                    if (ws.fr[k] && ws.where[k] != RS_HELD) {
-                        const uint32_t j = atomicAdd(&a.counts[2], 1u);
-                        ReasmJob jb;
-                        jb.frame = ws.where[k];
-                        jb.entry = cur;
-                        jb.fr = ws.fr[k];
-                        jb.pad = 0;
-                        a.jobs[j] = jb;
-                        ws.where[k] = RS_HELD;
-                        atomicAdd(&a.stats[UDPDK_RS_STORED], 1ull);
+            if (cur == RS_VIRTUAL) {
+                // still pending: the flow takes a table entry now (its key is not in the table:
+                // no other wave handles it), or is dropped if its buckets have filled meanwhile
+                cur = table_find(a, ksrc, kdst, kid, sig, tag, s_tmp[w], cnt, false);
+                if (cur == RS_NONE) {
+                    if (lane == 0) atomicAdd(&cnt[UDPDK_RS_NO_SPACE], 1ull);
+                } else if (lane >= E_VALID && lane < E_USED) {
+                    st_a(a.tab + (size_t)cur * E_WORDS + lane, st[lane]);
+                }
+            }
+            if (cur != RS_NONE) {
+                if (lane == 0) {
+                    // still pending: this call's fragments move into the entry buffer (reasm_store)
+                    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
+                        if (st[E_FR + k] && st[E_WHERE + k] != RS_HELD) {
+                            ReasmJob jb;
+                            jb.frame = st[E_WHERE + k];
+                            jb.entry = cur;
+                            jb.fr = st[E_FR + k];
+                            jb.pad = 0;
+                            a.jobs[s_pos[w][k]] = jb;
+                            st[E_WHERE + k] = RS_HELD;
+                            atomicAdd(&cnt[UDPDK_RS_STORED], 1ull);
+                        }
                     }
                 }
-                table_release(a, cur, ws, false);
+                table_release(a, cur, st, false);
             }
         }
     }
-}
-
-// Sort keys of the completions: the arrival index of the completing fragment.
-__global__ void __launch_bounds__(RS_BLOCK) reasm_origin_keys(const ReasmDone *done, unsigned long long *k,
-                                                             uint32_t *v, uint32_t C)
-{
-    for (uint32_t j = blockIdx.x * RS_BLOCK + threadIdx.x; j < C; j += gridDim.x * RS_BLOCK) {
-        k[j] = done[j].origin;
-        v[j] = j;
-    }
+    __syncthreads();
+    if (threadIdx.x < UDPDK_RS_N && s_cnt[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], s_cnt[threadIdx.x]);
+    if (threadIdx.x == UDPDK_RS_N && s_cnt[UDPDK_RS_N]) atomicAdd(a.out_bytes, s_cnt[UDPDK_RS_N]);
 }
 
 // Frame sizes of the completions in origin order (for the offset scan).
@@ -522,8 +615,8 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
         for (uint32_t q = 0; q < r.n && q < RS_MAX_FRAG; ++q) {
             if (!r.fr[q]) continue;
             const uint32_t ofs = r.fr[q] & 0xFFFFu, len = r.fr[q] >> 16;
-            if (r.where[q] == RS_HELD) wave_copy(o + 34 + ofs, er, 34u + ofs, len);
-            else wave_copy(o + 34 + ofs, fr, a.offset[r.where[q]] + 34u, len);
+            if (r.where[q] == RS_HELD) wave_copy16(o + 34 + ofs, er, 34u + ofs, len);
+            else wave_copy16(o + 34 + ofs, fr, a.offset[r.where[q]] + 34u, len);
         }
         if (lane == 0) {
             a.out_off[k] = oo;
@@ -550,10 +643,11 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_store(StoreArgs a)
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
     for (uint32_t k = blockIdx.x * RS_WAVES + w; k < a.J; k += gridDim.x * RS_WAVES) {
         const ReasmJob jb = a.jobs[k];
+        if (jb.frame == RS_NONE) continue;
         uint8_t *eb = a.ebuf + (size_t)jb.entry * a.stride;
         const uint32_t ofs = jb.fr & 0xFFFFu, len = jb.fr >> 16, fo = a.offset[jb.frame];
         if (ofs == 0) wave_copy(eb, fr, fo, 34u);
-        wave_copy(eb + 34 + ofs, fr, fo + 34u, len);
+        wave_copy16(eb + 34 + ofs, fr, fo + 34u, len);
     }
 }
 
@@ -562,7 +656,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_store(StoreArgs a)
 // ------------------------------------------------------------------------------------------
 struct Reasm {
     int device = 0;
-    FragEntry *tab = nullptr;
+    uint32_t *tab = nullptr;                 // [entries][E_WORDS]
     uint8_t *ebuf = nullptr;
     uint32_t entries = 0, assoc = 0, mask = 0, max_dgram = 0, stride = 0;
     uint64_t max_cycles = 0;
@@ -638,8 +732,8 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
     auto fail = [&](hipError_t e) { *hip_err = (int)e; rc = e == hipErrorOutOfMemory ? -ENOMEM : -EIO; };
     hipError_t e = hipSuccess;
     const size_t C = r->cap;
-    if ((e = dalloc(&r->tab, r->entries)) != hipSuccess ||
-        (e = hipMemset(r->tab, 0, (size_t)r->entries * sizeof(FragEntry))) != hipSuccess ||
+    if ((e = dalloc(&r->tab, (size_t)r->entries * E_WORDS)) != hipSuccess ||
+        (e = hipMemset(r->tab, 0, (size_t)r->entries * E_WORDS * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void **)&r->ebuf, (size_t)r->entries * r->stride)) != hipSuccess ||
         (e = dalloc(&r->frag_list, C)) != hipSuccess || (e = dalloc(&r->v1s, C)) != hipSuccess ||
         (e = dalloc(&r->v2s, C)) != hipSuccess || (e = dalloc(&r->k1, C)) != hipSuccess ||
@@ -700,12 +794,14 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     a.max_cycles = r->max_cycles;
     a.tms = tms;
     a.done = r->done;
+    a.dk = r->dk;
+    a.dv = r->dv;
     a.jobs = r->jobs;
     a.tag_base = 0;
     RS_HIP(hipMemsetAsync(r->counts, 0, 4 * sizeof(uint32_t), st));
     RS_HIP(hipMemsetAsync(r->stats, 0, UDPDK_RS_N * sizeof(unsigned long long), st));
     RS_HIP(hipMemsetAsync(r->out_bytes, 0, sizeof(unsigned long long), st));
-    const uint32_t g1 = std::max<uint32_t>(1, std::min<uint32_t>((n + RS_BLOCK - 1) / RS_BLOCK, 4096));
+    const uint32_t g1 = std::max<uint32_t>(1, std::min<uint32_t>((n + 2047) / 2048, 1024));
     hipLaunchKernelGGL(reasm_collect, dim3(g1), dim3(RS_BLOCK), 0, st, a);
     RS_HIP(hipGetLastError());
     RS_HIP(hipMemcpyAsync(r->host, r->counts, 4, hipMemcpyDeviceToHost, st));
@@ -720,20 +816,30 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         RS_HIP(hipGetLastError());
         tb = r->tmp_bytes;
         RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k2, r->k2s, r->v1s, r->v2s, (size_t)F, 0, 64, st));
+        // the sort keys are dead now: their buffers hold the per-position records
+        a.s_i = reinterpret_cast<uint32_t *>(r->k1);
+        a.s_src = a.s_i + F;
+        a.s_dst = reinterpret_cast<uint32_t *>(r->k1s);
+        a.s_id = a.s_dst + F;
+        a.s_sig = reinterpret_cast<uint32_t *>(r->k2);
+        a.s_meta = a.s_sig + F;
+        hipLaunchKernelGGL(reasm_prep, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
+        RS_HIP(hipGetLastError());
+        RS_HIP(hipMemsetAsync(r->dk, 0xFF, (size_t)F * sizeof(unsigned long long), st));
+        RS_HIP(hipMemsetAsync(r->jobs, 0xFF, (size_t)F * sizeof(ReasmJob), st));
         a.tag_base = (r->calls++ & 0x3FFu) << 20;
         const uint32_t waves = (F + 63u) / 64u;
         const uint32_t gp = std::max<uint32_t>(1, std::min<uint32_t>((waves + RS_WAVES - 1) / RS_WAVES, 2048));
         hipLaunchKernelGGL(reasm_process, dim3(gp), dim3(RS_BLOCK), 0, st, a, F);
         RS_HIP(hipGetLastError());
     }
-    RS_HIP(hipMemcpyAsync(r->host, r->counts, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     RS_HIP(hipMemcpyAsync(r->host + 4, r->out_bytes, 8, hipMemcpyDeviceToHost, st));
     RS_HIP(hipMemcpyAsync(r->host + 8, r->stats, UDPDK_RS_N * 8, hipMemcpyDeviceToHost, st));
     RS_HIP(hipStreamSynchronize(st));
-    const uint32_t Cn = r->host[1], J = r->host[2];
     uint64_t ob;
     memcpy(&ob, r->host + 4, 8);
     memcpy(o->stats, r->host + 8, UDPDK_RS_N * 8);
+    const uint32_t Cn = (uint32_t)o->stats[UDPDK_RS_DONE], J = (uint32_t)o->stats[UDPDK_RS_STORED];
     if (Cn) {
         if (ob + UDPDK_GPU_FRAMES_TAILROOM > r->out_cap) {
             if (r->out) RS_HIP(hipFree(r->out));
@@ -743,13 +849,11 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
             RS_HIP(hipMalloc((void **)&r->out, nc));
             r->out_cap = nc;
         }
-        // completions in origin (arrival) order, then their frame offsets
+        // completions in origin (arrival) order (positions without one sort last), then their
+        // frame offsets
         const uint32_t gC = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_BLOCK - 1) / RS_BLOCK, 4096));
-        hipLaunchKernelGGL(reasm_origin_keys, dim3(gC), dim3(RS_BLOCK), 0, st,
-                           (const ReasmDone *)r->done, r->dk, r->dv, Cn);
-        RS_HIP(hipGetLastError());
         size_t tb = r->tmp_bytes;
-        RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->dk, r->dks, r->dv, r->perm, (size_t)Cn, 0, 32, st));
+        RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->dk, r->dks, r->dv, r->perm, (size_t)F, 0, 32, st));
         hipLaunchKernelGGL(reasm_sizes, dim3(gC), dim3(RS_BLOCK), 0, st, (const ReasmDone *)r->done,
                            (const uint32_t *)r->perm, r->sizes, Cn);
         RS_HIP(hipGetLastError());
@@ -783,8 +887,8 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         sa.ebuf = r->ebuf;
         sa.stride = r->stride;
         sa.jobs = r->jobs;
-        sa.J = J;
-        const uint32_t gs = std::max<uint32_t>(1, std::min<uint32_t>((J + RS_WAVES - 1) / RS_WAVES, 8192));
+        sa.J = F;                  // positional: waves skip positions without a job
+        const uint32_t gs = std::max<uint32_t>(1, std::min<uint32_t>((F + RS_WAVES - 1) / RS_WAVES, 8192));
         hipLaunchKernelGGL(reasm_store, dim3(gs), dim3(RS_BLOCK), 0, st, sa);
         RS_HIP(hipGetLastError());
     }

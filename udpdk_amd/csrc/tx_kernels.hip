@@ -90,16 +90,13 @@ constexpr int TXW = TX_BLOCK / 64;
 
 } // namespace
 
-__global__ void __launch_bounds__(TX_BLOCK)
+__global__ void __launch_bounds__(TX_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8)))
 tx_build(TxArgs a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t win[TXW][64][TX_WIN / 4];
     // per output frame of the current round
-    __shared__ uint32_t l_cs[TXW][64], l_fo[TXW][64], l_len[TXW][64], l_po[TXW][64], l_hl[TXW][64];
-    // per datagram of the wave: first frame, frame offset, length | n_frames << 16, payload
-    // offset, src ip, dst ip, src port | dst port << 16
-    __shared__ uint32_t d_fs[TXW][64], d_fo[TXW][64], d_ln[TXW][64], d_po[TXW][64],
-        d_src[TXW][64], d_dst[TXW][64], d_pt[TXW][64];
+    // (l_len bit 31: 34-byte header, a fragment after the first)
+    __shared__ uint32_t l_cs[TXW][64], l_fo[TXW][64], l_len[TXW][64], l_po[TXW][64];
     const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
     const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.payload), (short)0, (int)a.payload_rsrc, 0x00020000);
@@ -128,38 +125,49 @@ tx_build(TxArgs a)
                 pt = (sl.y & 0xFFFFu) | ((uint32_t)a.dst_port[i] << 16);          // :341-342
             }
         }
+        // per datagram, kept in its lane's registers and read across lanes with shuffles:
+        // first frame, frame offset, length | n_frames << 16 (fragmented), payload offset, src
+        // ip, dst ip, src port | dst port << 16
         uint32_t n_frames;
         const uint32_t fs = excl_scan64(nf, &n_frames);
-        d_fs[w][lane] = fs;
-        d_fo[w][lane] = fo;
-        d_ln[w][lane] = L | ((a.mtu && L + 42u > a.mtu) ? nf << 16 : 0u);
-        d_po[w][lane] = po;
-        d_src[w][lane] = src;
-        d_dst[w][lane] = dst;
-        d_pt[w][lane] = pt;
-        wave_sync_tx();
+        const uint32_t ln = L | ((a.mtu && L + 42u > a.mtu) ? nf << 16 : 0u);
 
-        for (uint32_t r0 = 0; r0 < n_frames; r0 += 64) {
+        // no fragmented datagram in the wave: frame = datagram = lane, no shuffles
+        const bool direct = !__ballot(nf && (ln >> 16));
+        for (uint32_t r0 = 0; r0 < (direct ? 1u : n_frames); r0 += 64) {
             const uint32_t f = r0 + lane;
             uint32_t nch = 0, ffo = 0, plen = 0, ppo = 0, hl = 0;
-            if (f < n_frames) {
-                // the datagram of frame f: the last q with d_fs[q] <= f (datagrams without
-                // frames share their successor's first index)
+            uint32_t k = 0, lnq = ln, sq = src, dq = dst, ptq = pt, foq = fo, poq = po;
+            bool act = nf != 0;
+            if (!direct) {
+                // the datagram of frame f: the last q with fs[q] <= f (datagrams without frames
+                // share their successor's first index); shuffles run with every lane active
+                const uint32_t fc = min(f, n_frames - 1u);
                 uint32_t q = 0;
 #pragma unroll
-                for (int sft = 32; sft >= 1; sft >>= 1)
-                    if (d_fs[w][q + sft] <= f) q += sft;
-                const uint32_t k = f - d_fs[w][q];
-                const uint32_t ln = d_ln[w][q], Lq = ln & 0xFFFFu, nfq = ln >> 16;
-                const uint32_t sq = d_src[w][q], dq = d_dst[w][q], ptq = d_pt[w][q];
+                for (int sft = 32; sft >= 1; sft >>= 1) {
+                    const uint32_t v = __shfl(fs, (int)(q + sft), 64);
+                    if (v <= fc) q += sft;
+                }
+                k = fc - __shfl(fs, (int)q, 64);
+                lnq = __shfl(ln, (int)q, 64);
+                sq = __shfl(src, (int)q, 64);
+                dq = __shfl(dst, (int)q, 64);
+                ptq = __shfl(pt, (int)q, 64);
+                foq = __shfl(fo, (int)q, 64);
+                poq = __shfl(po, (int)q, 64);
+                act = f < n_frames;
+            }
+            const uint32_t Lq = lnq & 0xFFFFu, nfq = lnq >> 16;
+            if (act) {
                 uint32_t tl, ff, ck;
                 if (!nfq) {                       // unfragmented: udpdk_sendto's frame as built
                     tl = Lq + 28u;                                               // :336
                     ff = 0u;
                     ck = ipv4_cksum(ipv4_raw(tl, 0u, sq, dq));                   // :337
                     hl = 42u;
-                    ffo = d_fo[w][q];
-                    ppo = d_po[w][q];
+                    ffo = foq;
+                    ppo = poq;
                     plen = Lq;
                 } else {                          // fragment k of nfq (rte_ipv4_fragment_packet)
                     const uint32_t ofs = k * fpl;
@@ -169,8 +177,8 @@ tx_build(TxArgs a)
                     ff = (ofs >> 3) | (last ? 0u : 0x2000u);
                     ck = ipv4_cksum_nic(ipv4_raw(tl, ff, sq, dq));
                     hl = k ? 34u : 42u;
-                    ffo = d_fo[w][q] + k * (a.mtu + 14u);
-                    ppo = d_po[w][q] + (k ? ofs - 8u : 0u);
+                    ffo = foq + k * (a.mtu + 14u);
+                    ppo = poq + (k ? ofs - 8u : 0u);
                     plen = k ? ipp : ipp - 8u;
                 }
                 const uint32_t ul = Lq + 8u;                                     // :344
@@ -204,9 +212,8 @@ tx_build(TxArgs a)
             const uint32_t cs = excl_scan64(nch, &total);
             l_cs[w][lane] = cs;
             l_fo[w][lane] = ffo;
-            l_len[w][lane] = plen;
+            l_len[w][lane] = plen | (hl == 34u ? 0x80000000u : 0u);
             l_po[w][lane] = ppo;
-            l_hl[w][lane] = hl;
             wave_sync_tx();
 
             for (uint32_t k = lane; k < total; k += 64) {
@@ -215,8 +222,9 @@ tx_build(TxArgs a)
                 for (int sft = 32; sft >= 1; sft >>= 1)
                     if (l_cs[w][q + sft] <= k) q += sft;
                 const uint32_t j = k - l_cs[w][q];
-                const uint32_t fq = l_fo[w][q], Lq = l_len[w][q], pq = l_po[w][q];
-                const int hq = (int)l_hl[w][q];
+                const uint32_t fq = l_fo[w][q], lw = l_len[w][q], pq = l_po[w][q];
+                const uint32_t Lq = lw & 0x7FFFFFFFu;
+                const int hq = (lw >> 31) ? 34 : 42;
                 const uint32_t abase = (fq & ~15u) + 16u * j;
                 const int r0c = (int)(abase - fq);
                 // header part

@@ -296,3 +296,57 @@ def mixed_batch(seed: int, n: int, bound_ports: list[int], unbound_ports: list[i
     flat[:total] = np.frombuffer(bytes(out), np.uint8)
     return Batch(flat, np.array(offs, np.uint32), np.array(lens, np.uint16), total,
                  np.array(pts, np.uint32) if with_ptype else None, {"kinds": kk})
+
+
+# ---- fragment workloads (f2) --------------------------------------------------------------------
+def frag_batch(n_dgrams: int, payload_len: int, mtu: int = 1500, seed: int = 0x5EED) -> Batch:
+    """n_dgrams UDP datagrams of payload_len bytes (valid UDP checksums), each cut the way the
+    poller's rte_ipv4_fragment_packet cuts it at `mtu` (mtu - 20 data bytes per fragment), the
+    fragments of a datagram back to back and in order. Datagram k has IPv4 id k & 0xffff and
+    source 172.31.(100 + (k >> 16)).2, so every datagram is its own flow."""
+    L = payload_len
+    fpl = mtu - 20
+    ipl = L + 8
+    nf = -(-ipl // fpl)
+    src = build_frames(np.full(n_dgrams, L + 42, np.uint32), np.full(n_dgrams, PORT_RECV, np.uint32), seed)
+    whole = src.frames[:src.frames_bytes].reshape(n_dgrams, L + 42)
+    k = np.arange(n_dgrams, dtype=np.uint32)
+    sizes = [34 + min(fpl, ipl - j * fpl) for j in range(nf)]
+    per = sum(sizes)
+    total = n_dgrams * per
+    flat = np.zeros((total + 255) // 256 * 256 + 256, np.uint8)
+    view = flat[:total].reshape(n_dgrams, per)
+    pos = 0
+    for j, fs in enumerate(sizes):
+        h = whole[:, :34].copy()
+        tl = fs - 14
+        h[:, 16] = tl >> 8
+        h[:, 17] = tl & 0xFF
+        h[:, 18] = k & 0xFF                                  # id raw LE = k & 0xffff
+        h[:, 19] = (k >> 8) & 0xFF
+        ff = (j * fpl) // 8 | (0x2000 if j + 1 < nf else 0)
+        h[:, 20] = ff >> 8
+        h[:, 21] = ff & 0xFF
+        h[:, 28] = 100 + (k >> 16)                           # source 172.31.(100 + k >> 16).2
+        h[:, 24] = 0
+        h[:, 25] = 0
+        w = h[:, 14:34:2].astype(np.uint64) + h[:, 15:34:2].astype(np.uint64) * 256
+        c = (~_fold(w.sum(1))) & 0xFFFF
+        h[:, 24] = c & 0xFF
+        h[:, 25] = c >> 8
+        view[:, pos:pos + 34] = h
+        view[:, pos + 34:pos + fs] = whole[:, 34 + j * fpl:34 + j * fpl + fs - 34]
+        pos += fs
+    # the UDP checksum covers the pseudo header's source address (+ (k >> 16) in the LE word of
+    # bytes 28-29): fold the change into the checksum in the first fragment (bytes 40-41)
+    hi = (k >> 16).astype(np.uint64)
+    if np.any(hi):
+        c = view[:, 40].astype(np.uint64) | (view[:, 41].astype(np.uint64) << 8)
+        c2 = (~_fold((~c & 0xFFFF) + hi)) & 0xFFFF
+        c2[c2 == 0] = 0xFFFF
+        view[:, 40] = (c2 & 0xFF).astype(np.uint8)
+        view[:, 41] = (c2 >> 8).astype(np.uint8)
+    off = (np.arange(n_dgrams, dtype=np.uint64)[:, None] * per +
+           np.cumsum([0] + sizes[:-1])[None, :]).reshape(-1).astype(np.uint32)
+    ln = np.tile(np.array(sizes, np.uint16), n_dgrams)
+    return Batch(flat, off, ln, total)
