@@ -164,7 +164,7 @@ __device__ void wave_copy(uint8_t *dst, __amdgpu_buffer_rsrc_t r, uint32_t src_o
 }
 
 // As wave_copy, with 16-byte stores once the destination is 16-byte aligned (byte-aligned
-// 16-byte loads from the source).
+// 16-byte loads from the source), up to four loads per lane in flight before their stores.
 __device__ void wave_copy16(uint8_t *dst, __amdgpu_buffer_rsrc_t r, uint32_t src_off, uint32_t len)
 {
     const uint32_t lane = __lane_id();
@@ -172,9 +172,22 @@ __device__ void wave_copy16(uint8_t *dst, __amdgpu_buffer_rsrc_t r, uint32_t src
     if (lane < head) dst[lane] = (uint8_t)ld32(r, src_off + lane);
     const uint32_t body = (len - head) >> 4;
     uint4 *d16 = reinterpret_cast<uint4 *>(dst + head);
-    for (uint32_t k = lane; k < body; k += 64) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(src_off + head + 16u * k), 0, 0);
-        d16[k] = make_uint4(v[0], v[1], v[2], v[3]);
+    const uint32_t sb = src_off + head;
+    for (uint32_t k0 = lane; k0 < body; k0 += 256u) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t k = k0 + 64u * u;
+            if (k < body) {
+                const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(sb + 16u * k), 0, 0);
+                v[u] = make_uint4(x[0], x[1], x[2], x[3]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t k = k0 + 64u * u;
+            if (k < body) d16[k] = v[u];
+        }
     }
     const uint32_t done = head + 16u * body, tail = len - done;
     if (lane < tail) dst[done + lane] = (uint8_t)ld32(r, src_off + done + lane);
