@@ -45,8 +45,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1500 B / IMIX side lines")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU time per baseline leg")
-    p.add_argument("--pipeline", type=int, default=2, choices=(1, 2),
-                   help="udpdk_gpu_pipeline_depth: 2 overlaps consecutive batches on two streams")
+    p.add_argument("--pipeline", type=int, default=3, choices=(1, 2, 3, 4),
+                   help="udpdk_gpu_pipeline_depth: d > 1 overlaps consecutive batches on d streams")
     p.add_argument("--timing-every", type=int, default=16,
                    help="per-kernel timing on every Nth call (dispatch-carried events)")
     return p.parse_args()
@@ -184,7 +184,7 @@ def cpu_baseline(w: F.Workload, target_s: float):
 def side_config(ctx, cfg: int, steps: int, rotate: int):
     w = F.config_batch(cfg)
     rx = Rx(ctx, w, rotate)
-    ctx.pipeline(2)
+    ctx.pipeline(3)
     wall, gpu_step, _, st = time_loop(rx, steps, 5, lambda: None, 0)
     ctx.pipeline(1)
     wall1, gpu_step1, kt, _ = time_loop(rx, steps, 5, lambda: None, 4)

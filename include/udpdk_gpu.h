@@ -202,10 +202,11 @@ typedef struct {
  * rx_compact1 (one lane and no fan-out in the snapshot) or rx_scan + rx_scatter. meta, lane_off
  * and lane_pkt are complete when the stream reaches the end of the sequence. */
 int udpdk_gpu_rx(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch, const udpdk_rx_out_t *out);
-/* Pipelining: with depth 2, consecutive udpdk_gpu_rx calls alternate between two internal
+/* Pipelining: with depth d in 2..4, consecutive udpdk_gpu_rx calls rotate over d internal
  * streams with their own workspaces, so one batch's launch, prologue and compaction overlap the
- * next batch's streaming. Calls must then not share output buffers with the previous call still
- * in flight. Depth 1 (default): every call in order on the context stream. Synchronises. */
+ * other batches' streaming (3 is fastest for 1 M x 64 B batches). Calls must then not share
+ * output buffers with the d - 1 previous calls still in flight. Depth 1 (default): every call in
+ * order on the context stream. Synchronises. */
 int udpdk_gpu_pipeline_depth(udpdk_gpu_ctx *ctx, int depth);
 /* Make the context stream (udpdk_gpu_stream) wait, on the device, for all work enqueued so far on
  * the other pipes (no host wait). memset/h2d/d2h/tx_build/rx_host join implicitly. */

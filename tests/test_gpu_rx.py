@@ -189,10 +189,12 @@ def test_rx_host_end_to_end(gpu_ctx):
     assert np.array_equal(np.array(st.counters[:], np.uint64), wc)
 
 
-def test_pipeline_depth2(gpu_ctx):
-    """Two pipes: consecutive calls on independent batches overlap; every call's outputs and the
-    last call's counters still equal the oracle's."""
-    ws = [F.config_batch(4, n=30000 + 1000 * i) for i in range(4)]     # same 1024-port lists
+@pytest.mark.parametrize("cfg,depth", [(4, 2), (4, 3), (4, 4), (2, 3)])
+def test_pipeline_depth(gpu_ctx, cfg, depth):
+    """Several pipes: consecutive calls on independent batches overlap; every call's outputs and
+    the last call's counters still equal the oracle's (config 4: scan + scatter path, config 2:
+    single-lane compaction)."""
+    ws = [F.config_batch(cfg, n=30000 + 1000 * i) for i in range(depth + 2)]   # same lists
     lists = ws[0].port_lists()
     gpu_ctx.upload_snapshot(abi.snapshot_from_lists(lists, ws[0].n_sockets))
     bt = O.bindtable_from_lists(lists)
@@ -201,7 +203,7 @@ def test_pipeline_depth2(gpu_ctx):
         db = abi.rx_upload(gpu_ctx, w.batch.frames, w.batch.offset, w.batch.length)
         db.frames_bytes = w.batch.frames_bytes
         runs.append((w, db, abi.rx_alloc_out(gpu_ctx, w.batch.n, w.n_sockets, w.batch.n)))
-    gpu_ctx.pipeline(2)
+    gpu_ctx.pipeline(depth)
     try:
         for w, db, out in runs:
             assert abi.rx_enqueue(gpu_ctx, db, out) == 0
@@ -249,7 +251,8 @@ def test_rx_host_sync_and_async(gpu_ctx):
         gpu_ctx.pipeline(1)
         return res
 
-    for fn, depth in ((L.udpdk_gpu_rx_host, 1), (L.udpdk_gpu_rx_host_async, 2)):
+    for fn, depth in ((L.udpdk_gpu_rx_host, 1), (L.udpdk_gpu_rx_host_async, 2),
+                      (L.udpdk_gpu_rx_host_async, 3)):
         for meta, loff, pkt, st in call(fn, depth):
             assert np.array_equal(meta, want[0])
             assert np.array_equal(loff, want[1])

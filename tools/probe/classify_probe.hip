@@ -61,29 +61,40 @@ int main()
     // STREAMS=2: consecutive launches alternate between two streams with their own outputs,
     // so two launches may run concurrently
     const int NS = getenv("STREAMS") ? atoi(getenv("STREAMS")) : 1;
-    hipStream_t ss[2];
-    uint32_t *meta2, *hist2, *tcnt2;
-    (void)hipMalloc(&meta2, (size_t)N * 4);
-    (void)hipMalloc(&hist2, tiles * 4);
-    (void)hipMalloc(&tcnt2, tiles * 64);
-    for (int k = 0; k < 2; ++k) (void)hipStreamCreateWithFlags(&ss[k], hipStreamNonBlocking);
-    uint32_t *lp1, *lp2, *lo1, *lo2, *tot1, *tot2;
-    (void)hipMalloc(&lp1, (size_t)N * 4); (void)hipMalloc(&lp2, (size_t)N * 4);
-    (void)hipMalloc(&lo1, 64); (void)hipMalloc(&lo2, 64); (void)hipMalloc(&tot1, 64); (void)hipMalloc(&tot2, 64);
+    hipStream_t ss[4];
+    uint32_t *metak[4], *histk[4], *tcntk[4], *lpk[4], *lok[4], *totk[4];
+    for (int k = 0; k < 4; ++k) {
+        (void)hipStreamCreateWithFlags(&ss[k], hipStreamNonBlocking);
+        if (k == 0) { metak[0] = meta; histk[0] = hist; tcntk[0] = tcnt; }
+        else {
+            (void)hipMalloc(&metak[k], (size_t)N * 4);
+            (void)hipMalloc(&histk[k], tiles * 4);
+            (void)hipMalloc(&tcntk[k], tiles * 64);
+        }
+        (void)hipMalloc(&lpk[k], (size_t)N * 4);
+        (void)hipMalloc(&lok[k], 64);
+        (void)hipMalloc(&totk[k], 64);
+    }
+    uint32_t *lp1 = lpk[0], *tot1 = totk[0];
     auto launch = [&](int i) {
         RxArgs b = a;
         b.frames = fr + (size_t)(i % COPIES) * N * FL;
         b.offset = off + (size_t)(i % COPIES) * N;
         b.length = len + (size_t)(i % COPIES) * N;
-        const int k = NS > 1 ? (i & 1) : 0;
-        if (k) { b.meta = meta2; b.hist = hist2; b.tile_cnt = tcnt2; }
+        const int k = i % NS;
+        b.meta = metak[k]; b.hist = histk[k]; b.tile_cnt = tcntk[k];
         hipLaunchKernelGGL(rx_classify, dim3(tiles), dim3(CLS_BLOCK), lds, ss[k], b);
         if (getenv("COMPACT")) {              // the single-lane compaction after it, same stream
             Compact1Args ca;
-            ca.meta = b.meta; ca.tile_count = b.hist; ca.lane_pkt = k ? lp2 : lp1;
-            ca.lane_off = k ? lo2 : lo1; ca.total = k ? tot2 : tot1; ca.n = N; ca.tile_frames = T;
+            ca.meta = b.meta; ca.tile_count = b.hist; ca.lane_pkt = lpk[k];
+            ca.lane_off = lok[k]; ca.total = totk[k]; ca.n = N; ca.tile_frames = T;
             ca.n_tiles = tiles; ca.lane_cap = N;
-            hipLaunchKernelGGL(rx_compact1, dim3(tiles), dim3(RX_BLOCK), 0, ss[k], ca);
+            const int tpb = getenv("TPB") ? atoi(getenv("TPB")) : 0;
+            if (tpb > 0)
+                hipLaunchKernelGGL(rx_compact1w, dim3((tiles + tpb - 1) / tpb), dim3(RX_BLOCK), 0, ss[k], ca,
+                                   (uint32_t)tpb);
+            else
+                hipLaunchKernelGGL(rx_compact1, dim3(tiles), dim3(RX_BLOCK), 0, ss[k], ca);
         }
     };
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
@@ -101,7 +112,13 @@ int main()
     std::vector<uint32_t> hm(16);
     (void)hipMemcpy(hm.data(), meta, 64, hipMemcpyDeviceToHost);
     (void)ms;
-    printf("rx_classify%s %7.2f us per launch, %d stream(s) (meta[0] = %08x)\n",
-           getenv("COMPACT") ? "+compact1" : "", us / R, NS, hm[0]);
+    uint32_t lp[4] = {0, 0, 0, 0}, tot = 0;
+    if (getenv("COMPACT")) {
+        (void)hipMemcpy(lp, lp1 + (N - 4), 16, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(&tot, tot1, 4, hipMemcpyDeviceToHost);
+    }
+    printf("rx_classify%s %7.2f us per launch, %d stream(s) (meta[0] = %08x, total %u, last %u)\n",
+           getenv("COMPACT") ? (getenv("TPB") ? "+compact1w" : "+compact1") : "", us / R, NS, hm[0],
+           tot, lp[3]);
     return 0;
 }

@@ -38,10 +38,12 @@ struct TimingSet {
     bool used[TIMED_KERNELS];
 };
 
-// One RX pipe = a stream and the per-call workspace. With pipelining depth 2, consecutive
-// udpdk_gpu_rx calls alternate between two pipes, so one batch's prologue, tail and compaction
-// overlap the next batch's streaming phase (the calls are independent: distinct batches and
-// output buffers).
+// One RX pipe = a stream and the per-call workspace. With pipelining depth d > 1, consecutive
+// udpdk_gpu_rx calls rotate over d pipes, so one batch's prologue, tail and compaction overlap
+// the other batches' streaming phases (the calls are independent: distinct batches and output
+// buffers). Depth 3 is the measured optimum for 1 M x 64 B (tools/probe/classify_probe: classify
+// + compaction 22.2 / 19.0 / 15.5 / 17.4 us per batch at 1 / 2 / 3 / 4 streams; 4 streams exceed
+// the box's 4 hardware queues with the context stream's own traffic).
 struct Pipe {
     hipStream_t stream = nullptr;
     uint32_t *hist = nullptr;
@@ -60,7 +62,7 @@ struct Pipe {
     uint8_t *st_out_d = nullptr; size_t st_out_cap = 0;
     udpdk_rx_stats_t *host_stats = nullptr;   // outstanding async host call: where its stats go
 };
-constexpr int MAX_PIPES = 2;
+constexpr int MAX_PIPES = 4;
 
 } // namespace
 
