@@ -171,7 +171,6 @@ __host__ __device__ constexpr uint32_t scatterw_lds_bytes(uint32_t n_lanes)
     return 4u * n_lanes + 2u * SCATTER_WAVES * n_lanes;
 }
 __global__ void rx_compact1(Compact1Args a);
-__global__ void rx_compact1w(Compact1Args a, uint32_t tpb);
 __global__ void rx_counters(const uint32_t *tile_cnt, uint32_t n_tiles, unsigned long long *counters);
 // RX reassembly (rx_reasm.hip): host-side table object driven by udpdk_gpu_rx_reassemble.
 struct Reasm;

@@ -681,81 +681,6 @@ rx_compact1(Compact1Args a)
 }
 
 // ------------------------------------------------------------------------------------------
-// rx_compact1w: rx_compact1 with each workgroup taking `tpb` consecutive tiles (fewer, longer
-// workgroups): the base of its first tile is read once, the next tile's verdict words are in
-// flight while the current tile's entries are written.
-// ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(RX_BLOCK)
-rx_compact1w(Compact1Args a, uint32_t tpb)
-{
-    __shared__ uint32_t red[2][RX_WAVES];
-    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    const uint32_t tb = blockIdx.x * tpb, te = min(a.n_tiles, tb + tpb);
-    const uint32_t steps = a.tile_frames / RX_BLOCK;        // 64-frame steps per wave per tile
-    const uint32_t plast = a.n - 1u;
-    uint32_t pre = 0;
-    for (uint32_t t = tid; t < tb; t += RX_BLOCK) pre += a.tile_count[t];
-    pre = wave_sum(pre);
-    if (lane == 0) red[0][w] = pre;
-    __syncthreads();
-    uint32_t run_base = 0;
-#pragma unroll
-    for (int i = 0; i < RX_WAVES; ++i) run_base += red[0][i];
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    constexpr uint32_t MAXU = 8;                            // steps held in registers
-    uint32_t mv[MAXU];
-    auto load_tile = [&](uint32_t t) {
-        const uint32_t wb = t * a.tile_frames + w * steps * 64;
-#pragma unroll
-        for (uint32_t u = 0; u < MAXU; ++u)
-            if (u < steps) mv[u] = a.meta[min(wb + u * 64 + lane, plast)];
-    };
-    if (tb < te) load_tile(tb);
-    for (uint32_t t = tb; t < te; ++t) {
-        const uint32_t t1 = min(a.n, (t + 1) * a.tile_frames);
-        const uint32_t wb = t * a.tile_frames + w * steps * 64;
-        unsigned long long m[MAXU];
-        uint32_t wcount = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < MAXU; ++u) {
-            m[u] = 0;
-            if (u < steps) {
-                const uint32_t p = wb + u * 64 + lane;
-                m[u] = __ballot(p < t1 && (mv[u] & 0xFu) == UDPDK_V_DELIVERED);
-                wcount += (uint32_t)__popcll(m[u]);
-            }
-        }
-        if (t + 1 < te) load_tile(t + 1);                   // next tile's words in flight
-        const uint32_t buf = (t - tb) & 1u;
-        if (lane == 0) red[buf][w] = wcount;
-        __syncthreads();
-        uint32_t before = 0, tcount = 0;
-#pragma unroll
-        for (int i = 0; i < RX_WAVES; ++i) {
-            tcount += red[buf][i];
-            before += (uint32_t)i < w ? red[buf][i] : 0u;
-        }
-        uint32_t run = run_base + before;
-#pragma unroll
-        for (uint32_t u = 0; u < MAXU; ++u) {
-            if (u < steps) {
-                if ((m[u] >> lane) & 1ull) {
-                    const uint32_t pos = run + (uint32_t)__popcll(m[u] & lt);
-                    if (pos < a.lane_cap) a.lane_pkt[pos] = wb + u * 64 + lane;
-                }
-                run += (uint32_t)__popcll(m[u]);
-            }
-        }
-        run_base += tcount;
-        if (t == a.n_tiles - 1u && tid == 0) {
-            a.lane_off[0] = 0u;
-            a.lane_off[1] = run_base;
-            *a.total = run_base;
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // rx_counters: counters[c] = sum over the last call's tiles of tile_cnt[t][c] (one workgroup,
 // launched by udpdk_gpu_rx_stats only, so a batch that nobody asks statistics for pays nothing)
 // ------------------------------------------------------------------------------------------
