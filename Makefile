@@ -9,7 +9,7 @@ INC       := -Iinclude -Iudpdk_amd/csrc
 LIB       := udpdk_amd/libudpdk_amd.so
 OBJDIR    := build/obj
 
-HIP_SRC   := udpdk_amd/csrc/rx_kernels.hip udpdk_amd/csrc/rx_gather.hip udpdk_amd/csrc/rx_reasm.hip udpdk_amd/csrc/tx_kernels.hip \
+HIP_SRC   := udpdk_amd/csrc/rx_kernels.hip udpdk_amd/csrc/rx_gather.hip udpdk_amd/csrc/rx_reasm.hip udpdk_amd/csrc/rx_rss.hip udpdk_amd/csrc/tx_kernels.hip \
              udpdk_amd/csrc/udpdk_gpu.hip
 C_SRC     := $(wildcard udpdk_amd/csrc/host/*.c)
 HIP_OBJ   := $(patsubst udpdk_amd/csrc/%.hip,$(OBJDIR)/%.o,$(HIP_SRC))

@@ -314,6 +314,43 @@ int udpdk_gpu_rx_reassemble(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch,
                             const uint32_t *meta_dev, uint64_t tms, udpdk_reasm_out_t *out);
 
 /* ---------------------------------------------------------------------------------------------
+ * Receive-side scaling: the reference configures ETH_MQ_RX_RSS with a single
+ * RX ring ("TODO add RSS support", udpdk_init.c:112-137) and polls queue 0 (udpdk_poller.c:516).
+ * udpdk_gpu_rss computes, per frame, the Toeplitz hash a NIC computes for rss_hf = IPv4 |
+ * non-fragmented IPv4 UDP and the redirection-table queue, and lists each queue's frames in
+ * arrival order: the split of one ingress batch over several pollers or GPUs by flow.
+ * ------------------------------------------------------------------------------------------- */
+#define UDPDK_RSS_KEY_BYTES   40u
+#define UDPDK_RSS_RETA_MAX    512u
+#define UDPDK_RSS_MAX_QUEUES  64u
+enum udpdk_rss_type {
+    UDPDK_RSS_IPV4            = 1u, /* 2-tuple (src, dst address) for IPv4 frames              */
+    UDPDK_RSS_NONFRAG_IPV4_UDP = 2u /* 4-tuple (+ src, dst port) for unfragmented UDP          */
+};
+typedef struct {
+    uint8_t  key[UDPDK_RSS_KEY_BYTES];  /* rss_key, byte 0 first                                */
+    uint32_t hash_types;                /* udpdk_rss_type bits                                   */
+    uint32_t n_queues;                  /* RX queues, 1..UDPDK_RSS_MAX_QUEUES                    */
+    uint32_t reta_size;                 /* power of two, 1..UDPDK_RSS_RETA_MAX                   */
+    uint16_t reta[UDPDK_RSS_RETA_MAX];  /* queue of entry hash & (reta_size - 1)                 */
+} udpdk_rss_conf_t;
+
+typedef struct {
+    uint32_t *hash_dev;       /* [n] the frame's RSS hash (mbuf hash.rss); 0 when no type applies */
+    uint32_t *queue_off_dev;  /* [n_queues + 1] exclusive prefix of per-queue frame counts        */
+    uint32_t *queue_pkt_dev;  /* [n] frame indices grouped by queue, arrival order kept           */
+} udpdk_rss_out_t;
+
+/* The widely used 40-byte Toeplitz key (the RSS verification suite's), both hash types, and a
+ * 128-entry redirection table spreading entries round-robin over n_queues. Host only. */
+int udpdk_gpu_rss_default_conf(udpdk_rss_conf_t *conf, uint32_t n_queues);
+/* rte_eth_dev_rss_hash_update + rte_eth_dev_rss_reta_update: the context's RSS configuration. */
+int udpdk_gpu_rss_config(udpdk_gpu_ctx *ctx, const udpdk_rss_conf_t *conf);
+/* Hash, queue and per-queue lists for one batch (async on the context stream). Frames the IPv4
+ * gate rejects (the rx_classify ptype rule) or with descriptors past frames_bytes get hash 0. */
+int udpdk_gpu_rss(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch, const udpdk_rss_out_t *out);
+
+/* ---------------------------------------------------------------------------------------------
  * TX: Eth/IPv4/UDP header build + rte_ipv4_cksum + payload copy (udpdk_syscall.c:314-356)
  * ------------------------------------------------------------------------------------------- */
 typedef struct {

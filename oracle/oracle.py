@@ -51,6 +51,11 @@ def lib() -> C.CDLL:
         L.oracle_reassemble.restype = C.c_int64
         L.oracle_reassemble.argtypes = [P, P, C.c_uint64, P, P, P, C.c_uint32, C.c_uint64, P,
                                         C.c_uint64, P, P, P, C.c_uint32, P]
+        L.oracle_toeplitz.restype = C.c_uint32
+        L.oracle_toeplitz.argtypes = [P, P, C.c_uint32]
+        L.oracle_rss.restype = C.c_int
+        L.oracle_rss.argtypes = [P, C.c_uint32, P, C.c_uint32, C.c_uint32, P, C.c_uint64, P, P, P,
+                                 C.c_uint32, P, P, P]
         L.oracle_recv_gather.argtypes = [P, P, P, P, C.c_uint32, C.c_uint32, C.c_uint32, P, P, P, P]
         _lib = L
     return _lib
@@ -224,3 +229,28 @@ def frag_hash(src: int, dst: int, pid: int):
     s2 = C.c_uint32()
     s1 = lib().oracle_frag_hash(src, dst, pid, C.byref(s2))
     return s1, s2.value
+
+
+def toeplitz(key: bytes, data: bytes) -> int:
+    return lib().oracle_toeplitz(C.create_string_buffer(key, 40), C.create_string_buffer(data, len(data)),
+                                 len(data))
+
+
+def rss(key: bytes, hash_types: int, reta, n_queues: int, frames: np.ndarray, frames_bytes: int,
+        offset, length, ptype=None):
+    """-> (hash u32[n], queue_off u32[Q+1], queue_pkt u32[n])."""
+    off = np.ascontiguousarray(offset, np.uint32)
+    ln = np.ascontiguousarray(length, np.uint16)
+    rt = np.ascontiguousarray(reta, np.uint16)
+    n = len(off)
+    h = np.zeros(max(1, n), np.uint32)
+    qo = np.zeros(n_queues + 1, np.uint32)
+    qp = np.zeros(max(1, n), np.uint32)
+    pt = np.ascontiguousarray(ptype, np.uint32) if ptype is not None else None
+    P = lambda a: a.ctypes.data_as(C.c_void_p)
+    rc = lib().oracle_rss(C.create_string_buffer(key, 40), hash_types, P(rt), len(rt), n_queues,
+                          P(np.ascontiguousarray(frames, np.uint8)), frames_bytes, P(off), P(ln),
+                          P(pt) if pt is not None else None, n, P(h), P(qo), P(qp))
+    if rc:
+        raise ValueError("oracle_rss")
+    return h[:n], qo, qp[:n]

@@ -101,6 +101,13 @@ int64_t oracle_reassemble(oracle_ftable *t, const uint8_t *frames, uint64_t fram
                           uint32_t *out_off, uint16_t *out_len, uint32_t *out_origin,
                           uint32_t out_max, uint64_t stats[ORACLE_RS_N]);
 
+/* Receive-side scaling (udpdk_oracle_rss.c): Toeplitz hash and redirection-table queues. */
+uint32_t oracle_toeplitz(const uint8_t key[40], const uint8_t *data, uint32_t len);
+int oracle_rss(const uint8_t key[40], uint32_t hash_types, const uint16_t *reta, uint32_t reta_size,
+               uint32_t n_queues, const uint8_t *frames, uint64_t frames_bytes,
+               const uint32_t *offset, const uint16_t *length, const uint32_t *ptype, uint32_t n,
+               uint32_t *hash_out, uint32_t *queue_off, uint32_t *queue_pkt);
+
 void oracle_recv_gather(const uint8_t *frames, const uint32_t *offset, const uint16_t *length,
                         const uint32_t *lane_pkt, uint32_t first, uint32_t count, uint32_t len,
                         uint8_t *out_payload, uint32_t *out_len, uint32_t *out_src_ip,

@@ -1,0 +1,73 @@
+"""Receive-side scaling parity (f4): udpdk_gpu_rss against the oracle's restatement (hash per
+frame, redirection table, per-queue lists in arrival order) on mixed batches with every verdict
+class, several redirection tables, hash-type sets and queue counts, ptype given or derived; frames
+built from the published verification vectors; and full-size config 5 frames over 8 queues."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle as O
+from udpdk_amd import abi, frames as F
+
+pytestmark = pytest.mark.gpu
+
+G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "rss_vectors.json")))
+KEY = bytes.fromhex(G["key"])
+
+
+def _both(ctx, b, cf, ptype=None):
+    reta = [cf.reta[i] for i in range(cf.reta_size)]
+    want = O.rss(bytes(cf.key), cf.hash_types, reta, cf.n_queues, b.frames, b.frames_bytes,
+                 b.offset, b.length, ptype)
+    db = abi.rx_upload(ctx, b.frames, b.offset, b.length, ptype)
+    db.frames_bytes = b.frames_bytes
+    got = abi.rss_run(ctx, db, cf)
+    for x in (db.frames, db.offset, db.length, db.ptype):
+        if x is not None:
+            x.free()
+    return want, got
+
+
+@pytest.mark.parametrize("nq,reta_size,types", [(8, 128, 3), (1, 1, 3), (64, 512, 3), (5, 64, 1),
+                                                (3, 256, 2), (16, 128, 0)])
+@pytest.mark.parametrize("with_ptype", [False, True])
+def test_rss_mixed(gpu_ctx, nq, reta_size, types, with_ptype):
+    b = F.mixed_batch(7 + nq, 5000, [10001, 10002, 10004], [9, 20000], ["172.31.100.1", "172.31.100.9"],
+                      with_ptype=with_ptype)
+    rng = np.random.default_rng(nq * 7 + reta_size)
+    cf = abi.rss_conf(nq, reta=rng.integers(0, nq, reta_size), hash_types=types)
+    (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, b, cf, b.ptype)
+    assert np.array_equal(wh, gh)
+    assert np.array_equal(wo, go)
+    assert np.array_equal(wp, gp)
+
+
+def test_rss_verification_frames(gpu_ctx):
+    """UDP frames carrying the verification suite's addresses and ports hash to its values."""
+    frames = []
+    for v in G["ipv4"]:
+        fr = bytearray(F.make_frame(np.random.default_rng(0), dport=v["dport"], dst_ip=v["dst"],
+                                    src_ip=v["src"]))
+        fr[34:36] = v["sport"].to_bytes(2, "big")
+        frames.append(bytes(fr))
+    off = np.cumsum([0] + [len(f) for f in frames[:-1]]).astype(np.uint32)
+    buf = np.zeros(int(off[-1]) + len(frames[-1]) + 64, np.uint8)
+    for o, f in zip(off, frames):
+        buf[o:o + len(f)] = np.frombuffer(f, np.uint8)
+    b = F.Batch(buf, off, np.array([len(f) for f in frames], np.uint16), len(buf) - 64)
+    cf = abi.rss_conf(4)
+    _, (gh, _, _) = _both(gpu_ctx, b, cf)
+    assert [int(x) for x in gh] == [int(v["ipv4_l4"], 16) for v in G["ipv4"]]
+    cf = abi.rss_conf(4, hash_types=1)
+    _, (gh, _, _) = _both(gpu_ctx, b, cf)
+    assert [int(x) for x in gh] == [int(v["ipv4"], 16) for v in G["ipv4"]]
+
+
+def test_rss_full_size_config5(gpu_ctx):
+    w = F.config_batch(5)                      # 4 M x 64 B over 4096 ports (Zipf)
+    (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, w.batch, abi.rss_conf(8))
+    assert np.array_equal(wh, gh) and np.array_equal(wo, go) and np.array_equal(wp, gp)
+    assert go[-1] == w.batch.n

@@ -96,6 +96,15 @@ class ReasmOut(C.Structure):
     _fields_ = [("batch", RxBatch), ("origin_dev", C.c_void_p), ("stats", C.c_uint64 * RS_N)]
 
 
+class RssConf(C.Structure):
+    _fields_ = [("key", C.c_uint8 * 40), ("hash_types", C.c_uint32), ("n_queues", C.c_uint32),
+                ("reta_size", C.c_uint32), ("reta", C.c_uint16 * 512)]
+
+
+class RssOut(C.Structure):
+    _fields_ = [("hash_dev", C.c_void_p), ("queue_off_dev", C.c_void_p), ("queue_pkt_dev", C.c_void_p)]
+
+
 class TxConfig(C.Structure):
     _fields_ = [("src_mac", C.c_uint8 * 6), ("dst_mac", C.c_uint8 * 6), ("src_ip", C.c_uint32)]
 
@@ -144,6 +153,9 @@ _PROTOS = {
                                       C.POINTER(RxGather)]),
     "udpdk_gpu_frag_table_create": (C.c_int, [_P, C.POINTER(FragTableCfg)]),
     "udpdk_gpu_rx_reassemble": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint64, C.POINTER(ReasmOut)]),
+    "udpdk_gpu_rss_default_conf": (C.c_int, [C.POINTER(RssConf), C.c_uint32]),
+    "udpdk_gpu_rss_config": (C.c_int, [_P, C.POINTER(RssConf)]),
+    "udpdk_gpu_rss": (C.c_int, [_P, C.POINTER(RxBatch), C.POINTER(RssOut)]),
     "udpdk_gpu_tx_build": (C.c_int, [_P, C.POINTER(TxConfig), C.POINTER(TxBatch), C.POINTER(TxOut)]),
     "udpdk_gpu_tx_build_mtu": (C.c_int, [_P, C.POINTER(TxConfig), C.POINTER(TxBatch),
                                          C.POINTER(TxOut), C.c_uint32]),
@@ -471,6 +483,38 @@ def rx_reassemble(ctx: GpuContext, b: RxDeviceBatch, meta: DeviceBuffer, tms: in
     rb = RxDeviceBatch(DevRef(ob.frames_dev or 0), int(ob.frames_bytes), DevRef(ob.offset_dev or 0),
                        DevRef(ob.length_dev or 0), DevRef(ob.ptype_dev or 0), int(ob.n))
     return rb, DevRef(o.origin_dev or 0), dict(zip(RS_STATS, list(o.stats)))
+
+
+def rss_conf(n_queues: int, reta=None, key: bytes | None = None, hash_types: int = 3) -> RssConf:
+    """udpdk_gpu_rss_default_conf, optionally with another redirection table / key / types."""
+    cf = RssConf()
+    _check(lib().udpdk_gpu_rss_default_conf(C.byref(cf), n_queues), "udpdk_gpu_rss_default_conf")
+    if reta is not None:
+        cf.reta_size = len(reta)
+        for i, q in enumerate(reta):
+            cf.reta[i] = int(q)
+    if key is not None:
+        for i in range(40):
+            cf.key[i] = key[i]
+    cf.hash_types = hash_types
+    return cf
+
+
+def rss_run(ctx: GpuContext, b: RxDeviceBatch, cf: RssConf):
+    """Configure RSS, run it over a device batch and download (hash, queue_off, queue_pkt)."""
+    _check(lib().udpdk_gpu_rss_config(ctx.handle, C.byref(cf)), "udpdk_gpu_rss_config")
+    n = b.n
+    h, qo, qp = ctx.alloc(4 * max(1, n)), ctx.alloc(4 * (cf.n_queues + 1)), ctx.alloc(4 * max(1, n))
+    bt = RxBatch(b.frames.ptr, b.frames_bytes, b.offset.ptr, b.length.ptr,
+                 b.ptype.ptr if b.ptype is not None else None, n)
+    _check(lib().udpdk_gpu_rss(ctx.handle, C.byref(bt), C.byref(RssOut(h.ptr, qo.ptr, qp.ptr))),
+           "udpdk_gpu_rss")
+    ctx.sync()
+    out = (ctx.download(h, np.uint32, n), ctx.download(qo, np.uint32, cf.n_queues + 1),
+           ctx.download(qp, np.uint32, n))
+    for x in (h, qo, qp):
+        x.free()
+    return out
 
 
 def download_ptr(ctx: GpuContext, ptr: int, dtype, count: int) -> np.ndarray:

@@ -172,6 +172,33 @@ __host__ __device__ constexpr uint32_t scatterw_lds_bytes(uint32_t n_lanes)
 }
 __global__ void rx_compact1(Compact1Args a);
 __global__ void rx_counters(const uint32_t *tile_cnt, uint32_t n_tiles, unsigned long long *counters);
+// Receive-side scaling (rx_rss.hip).
+constexpr uint32_t RSS_BLOCK = 256;
+constexpr uint32_t RSS_TILE = 1024;          // frames per workgroup
+constexpr uint32_t RSS_RETA_MAX = 512;
+constexpr uint32_t RSS_MAX_QUEUES = 64;
+struct RssArgs {
+    const uint8_t  *frames;
+    const uint32_t *offset;
+    const uint16_t *length;
+    const uint32_t *ptype;
+    const uint16_t *reta;     // [reta_size] queue per redirection entry
+    uint32_t *hash;           // [n] mbuf.hash.rss
+    uint8_t  *qid;            // [n] queue per frame
+    uint32_t *hist;           // [tiles][n_queues] -> scanned start positions
+    uint32_t *queue_pkt;      // [n] frame indices grouped by queue
+    uint64_t frames_bytes;
+    uint32_t rsrc_bytes;
+    uint32_t n;
+    uint32_t reta_size;       // power of two <= RSS_RETA_MAX
+    uint32_t n_queues;        // <= RSS_MAX_QUEUES
+    uint32_t q_bits;          // bits of a queue index
+    uint32_t hash_types;      // bit 0: IPv4 2-tuple, bit 1: unfragmented IPv4 UDP 4-tuple
+    uint8_t  key_be[40];      // Toeplitz key, byte 0 first
+};
+__global__ void rss_hash(RssArgs a);
+__global__ void rss_scatter(RssArgs a);
+
 // RX reassembly (rx_reasm.hip): host-side table object driven by udpdk_gpu_rx_reassemble.
 struct Reasm;
 int  reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_table_cfg_t *cfg,

@@ -1,0 +1,178 @@
+// rx_rss.hip — gfx950 receive-side scaling: the per-frame Toeplitz hash a
+// NIC computes for ETH_MQ_RX_RSS (the mode udpdk_init.c:137 asks for, with one RX ring and a
+// "TODO add RSS support" at :112) and the redirection-table lookup that picks the frame's RX
+// queue, then stable per-queue lists: queue q's frames in arrival order, the input for one
+// GPU (or poller) per queue.
+//
+// Hash input (rss_hf = IPv4 | non-fragmented IPv4 UDP): frame bytes [26, 38) = source address,
+// destination address, source port, destination port for an unfragmented UDP frame, bytes
+// [26, 34) for other IPv4 frames (fragments, other protocols), nothing (hash 0) for frames the
+// IPv4 gate rejects (the same ptype rule as rx_classify, fixed offsets as the reference parses).
+// Queue = reta[hash & (reta_size - 1)].
+//
+// Kernels: rss_hash (one workgroup per 1024-frame tile: a 12 x 256 table of key windows in LDS
+// turns the bit-serial Toeplitz product into 12 lookups per frame; hash and queue per frame; the
+// tile's queue histogram by wave multi-split), the tile-major scan shared with rx (rx_scan_*),
+// rss_scatter (per tile, each wave's contiguous quarter placed after the earlier quarters).
+// Bytes per frame: 26 header bytes read (one or two 32 B sectors) + 8 descriptor + 4 hash + 1
+// queue id written, then 1 + 4 (queue id read, list entry written) in the scatter.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "udpdk_gpu.h"
+#include "rx_common.h"
+
+namespace udpdk {
+
+namespace {
+
+__device__ __forceinline__ uint32_t ld32(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
+
+// Orders a wave's LDS accesses across lanes (its DS instructions execute in order).
+__device__ __forceinline__ void wsync()
+{
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Lanes of the wave holding the same key (key < 2^bits), from one ballot per key bit.
+__device__ __forceinline__ unsigned long long peers_of(uint32_t key, uint32_t bits, bool active)
+{
+    unsigned long long peers = __ballot(active);
+    for (uint32_t b = 0; b < bits; ++b) {
+        const bool kb = (key >> b) & 1u;
+        const unsigned long long bal = __ballot(kb);
+        peers &= kb ? bal : ~bal;
+    }
+    return peers;
+}
+
+} // namespace
+
+__global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
+{
+    __shared__ uint32_t tab[12][256];
+    __shared__ uint16_t reta[RSS_RETA_MAX];
+    __shared__ uint32_t hist[RSS_MAX_QUEUES];
+    const uint32_t tid = threadIdx.x, lane = __lane_id();
+    // key windows: win(b) = key bits [b, b + 32) (MSB first); tab[p][v] = XOR of win(8p + j) over
+    // the set bits j (MSB first) of byte value v at input position p
+    for (uint32_t e = tid; e < 12u * 256u; e += RSS_BLOCK) {
+        const uint32_t p = e >> 8, v = e & 255u;
+        uint32_t h = 0;
+        for (uint32_t j = 0; j < 8; ++j) {
+            if (!((v >> (7u - j)) & 1u)) continue;
+            const uint32_t b = 8u * p + j, k0 = b >> 3, s = b & 7u;
+            const unsigned long long w = ((unsigned long long)a.key_be[k0] << 32) |
+                                         ((unsigned long long)a.key_be[k0 + 1] << 24) |
+                                         ((unsigned long long)a.key_be[k0 + 2] << 16) |
+                                         ((unsigned long long)a.key_be[k0 + 3] << 8) |
+                                         (unsigned long long)a.key_be[k0 + 4];
+            h ^= (uint32_t)(w >> (8u - s));
+        }
+        tab[p][v] = h;
+    }
+    for (uint32_t e = tid; e < a.reta_size; e += RSS_BLOCK) reta[e] = a.reta[e];
+    for (uint32_t q = tid; q < a.n_queues; q += RSS_BLOCK) hist[q] = 0;
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.frames), (short)0, (int)a.rsrc_bytes, 0x00020000);
+    const uint32_t t0 = blockIdx.x * RSS_TILE, t1 = min(a.n, t0 + RSS_TILE);
+    for (uint32_t i0 = t0 + (tid & ~63u); i0 < t1; i0 += RSS_BLOCK) {
+        const uint32_t i = i0 + lane;
+        const bool in = i < t1;
+        uint32_t hash = 0;
+        if (in) {
+            const uint32_t o = a.offset[i], len = a.length[i];
+            const bool desc_ok = (uint64_t)o + len <= a.frames_bytes;
+            uint32_t w12 = 0, w20 = 0, src = 0, dst = 0, ports = 0;
+            if (desc_ok && len >= 34u) {
+                w12 = ld32(fr, o + 12);
+                w20 = ld32(fr, o + 20);
+                src = ld32(fr, o + 26);
+                dst = ld32(fr, o + 30);
+                if (len >= 38u) ports = ld32(fr, o + 34);
+            }
+            const uint32_t pt = a.ptype ? a.ptype[i] : ((w12 & 0xFFFFu) == 0x0008u ? 0x211u : 0x1u);
+            if (desc_ok && len >= 34u && (pt & 0x10u)) {
+                const uint32_t ff = ((w20 & 0xFFu) << 8) | ((w20 >> 8) & 0xFFu);
+                const bool frag = (ff & 0x3FFFu) != 0u;
+                const bool udp4 = !frag && ((w20 >> 24) & 0xFFu) == 17u && len >= 38u && (a.hash_types & 2u);
+                if (udp4 || (a.hash_types & 1u)) {
+                    hash = tab[0][src & 255u] ^ tab[1][(src >> 8) & 255u] ^ tab[2][(src >> 16) & 255u] ^
+                           tab[3][src >> 24] ^ tab[4][dst & 255u] ^ tab[5][(dst >> 8) & 255u] ^
+                           tab[6][(dst >> 16) & 255u] ^ tab[7][dst >> 24];
+                    if (udp4)
+                        hash ^= tab[8][ports & 255u] ^ tab[9][(ports >> 8) & 255u] ^
+                                tab[10][(ports >> 16) & 255u] ^ tab[11][ports >> 24];
+                }
+            }
+        }
+        const uint32_t q = reta[hash & (a.reta_size - 1u)];
+        if (in) {
+            a.hash[i] = hash;
+            a.qid[i] = (uint8_t)q;
+        }
+        const unsigned long long peers = peers_of(q, a.q_bits, in);
+        if (in && lane == (uint32_t)__ffsll((long long)peers) - 1u)
+            atomicAdd(&hist[q], (uint32_t)__popcll(peers));
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < a.n_queues; q += RSS_BLOCK)
+        a.hist[(size_t)blockIdx.x * a.n_queues + q] = hist[q];
+}
+
+// Per tile: wave w owns frames [t0 + 256 w, t0 + 256 w + 256); its base for queue q is the
+// tile's scanned start for q plus the earlier waves' counts.
+__global__ void __launch_bounds__(RSS_BLOCK) rss_scatter(RssArgs a)
+{
+    __shared__ uint32_t cnt[RSS_BLOCK / 64][RSS_MAX_QUEUES], run[RSS_BLOCK / 64][RSS_MAX_QUEUES];
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+    const uint32_t t0 = blockIdx.x * RSS_TILE, t1 = min(a.n, t0 + RSS_TILE);
+    const uint32_t wb = t0 + w * (RSS_TILE / (RSS_BLOCK / 64));
+    constexpr uint32_t STEPS = RSS_TILE / RSS_BLOCK;
+    for (uint32_t q = lane; q < a.n_queues; q += 64) cnt[w][q] = 0;
+    uint32_t qv[STEPS];
+#pragma unroll
+    for (uint32_t s = 0; s < STEPS; ++s) {
+        const uint32_t i = wb + 64u * s + lane;
+        qv[s] = i < t1 ? a.qid[i] : 0u;
+    }
+    wsync();
+#pragma unroll
+    for (uint32_t s = 0; s < STEPS; ++s) {
+        const uint32_t i = wb + 64u * s + lane;
+        const unsigned long long peers = peers_of(qv[s], a.q_bits, i < t1);
+        if (i < t1 && lane == (uint32_t)__ffsll((long long)peers) - 1u) cnt[w][qv[s]] += (uint32_t)__popcll(peers);
+        wsync();
+    }
+    __syncthreads();
+    // running position per queue for this wave (row w of run[] is wave w's alone)
+    for (uint32_t q = lane; q < a.n_queues; q += 64) {
+        uint32_t b = a.hist[(size_t)blockIdx.x * a.n_queues + q];
+        for (uint32_t v = 0; v < w; ++v) b += cnt[v][q];
+        run[w][q] = b;
+    }
+    wsync();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (uint32_t s = 0; s < STEPS; ++s) {
+        const uint32_t i = wb + 64u * s + lane;
+        const bool in = i < t1;
+        const uint32_t q = qv[s];
+        const unsigned long long peers = peers_of(q, a.q_bits, in);
+        const uint32_t base = in ? run[w][q] : 0u;
+        wsync();
+        if (in) {
+            const uint32_t pos = base + (uint32_t)__popcll(peers & lt);
+            a.queue_pkt[pos] = i;
+            if (lane == (uint32_t)__ffsll((long long)peers) - 1u) run[w][q] = base + (uint32_t)__popcll(peers);
+        }
+        wsync();
+    }
+}
+
+} // namespace udpdk

@@ -95,6 +95,12 @@ struct udpdk_gpu_ctx {
 
     unsigned long long *dbg = nullptr;        // diagnostic stamp buffer (UDPDK_STAMPS builds)
     Reasm *reasm = nullptr;                   // udpdk_gpu_frag_table_create
+    // receive-side scaling (udpdk_gpu_rss_config)
+    bool rss_ready = false;
+    RssArgs rss{};
+    uint16_t *rss_reta = nullptr;
+    uint8_t *rss_qid = nullptr;
+    uint32_t *rss_hist = nullptr, *rss_partial = nullptr, *rss_total = nullptr;
 
     // timing
     uint32_t timing_every = 0;                // 0 off, N: events on every Nth call
@@ -306,6 +312,9 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
         if (P.stream) (void)hipStreamSynchronize(P.stream);
     reasm_destroy(c->reasm);
     c->reasm = nullptr;
+    for (void *p : {(void *)c->rss_reta, (void *)c->rss_qid, (void *)c->rss_hist,
+                    (void *)c->rss_partial, (void *)c->rss_total})
+        if (p) (void)hipFree(p);
     void *dev[] = {c->port_tab, c->binds, c->slots};
     for (void *p : dev) if (p) (void)hipFree(p);
     for (Pipe &P : c->pipes) {
@@ -845,6 +854,111 @@ int udpdk_gpu_rx_gather(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
     }
+    return 0;
+}
+
+int udpdk_gpu_rss_default_conf(udpdk_rss_conf_t *conf, uint32_t n_queues)
+{
+    static const uint8_t key[UDPDK_RSS_KEY_BYTES] = {
+        0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
+        0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
+        0x80, 0x30, 0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
+    if (!conf || !n_queues || n_queues > UDPDK_RSS_MAX_QUEUES) return -EINVAL;
+    memset(conf, 0, sizeof(*conf));
+    memcpy(conf->key, key, sizeof(key));
+    conf->hash_types = UDPDK_RSS_IPV4 | UDPDK_RSS_NONFRAG_IPV4_UDP;
+    conf->n_queues = n_queues;
+    conf->reta_size = 128;
+    for (uint32_t i = 0; i < conf->reta_size; ++i) conf->reta[i] = (uint16_t)(i % n_queues);
+    return 0;
+}
+
+int udpdk_gpu_rss_config(udpdk_gpu_ctx *c, const udpdk_rss_conf_t *conf)
+{
+    if (!c || !conf) return -EINVAL;
+    if (!conf->n_queues || conf->n_queues > UDPDK_RSS_MAX_QUEUES || !conf->reta_size ||
+        conf->reta_size > UDPDK_RSS_RETA_MAX || (conf->reta_size & (conf->reta_size - 1)) ||
+        (conf->hash_types & ~3u))
+        return -EINVAL;
+    for (uint32_t i = 0; i < conf->reta_size; ++i)
+        if (conf->reta[i] >= conf->n_queues) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    { int r = join_pipes(c); if (r) return r; }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    const uint32_t tiles = ceil_div(std::max<uint32_t>(c->max_frames, 1), RSS_TILE);
+    if (!c->rss_reta) {
+        HIPC(c, hipMalloc((void **)&c->rss_reta, RSS_RETA_MAX * sizeof(uint16_t)));
+        HIPC(c, hipMalloc((void **)&c->rss_qid, std::max<uint32_t>(c->max_frames, 1)));
+        HIPC(c, hipMalloc((void **)&c->rss_hist, (size_t)tiles * RSS_MAX_QUEUES * 4));
+        HIPC(c, hipMalloc((void **)&c->rss_partial, (size_t)ceil_div(tiles, SCAN_COL_CHUNK) * RSS_MAX_QUEUES * 4));
+        HIPC(c, hipMalloc((void **)&c->rss_total, 64));
+    }
+    HIPC(c, hipMemcpy(c->rss_reta, conf->reta, conf->reta_size * sizeof(uint16_t), hipMemcpyHostToDevice));
+    RssArgs &r = c->rss;
+    memset(&r, 0, sizeof(r));
+    memcpy(r.key_be, conf->key, UDPDK_RSS_KEY_BYTES);
+    r.reta = c->rss_reta;
+    r.qid = c->rss_qid;
+    r.hist = c->rss_hist;
+    r.reta_size = conf->reta_size;
+    r.n_queues = conf->n_queues;
+    uint32_t qb = 0;
+    while ((1u << qb) < conf->n_queues) ++qb;
+    r.q_bits = qb;
+    r.hash_types = conf->hash_types;
+    c->rss_ready = true;
+    return 0;
+}
+
+int udpdk_gpu_rss(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rss_out_t *o)
+{
+    if (!c || !bt || !o || !c->rss_ready) return -EINVAL;
+    if (bt->n > c->max_frames || bt->frames_bytes >= (1ull << 32)) return -EINVAL;
+    if (bt->n && (!bt->frames_dev || !bt->offset_dev || !bt->length_dev || !o->hash_dev ||
+                  !o->queue_off_dev || !o->queue_pkt_dev))
+        return -EINVAL;
+    if (!o->queue_off_dev) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    { int r = join_pipes(c); if (r) return r; }
+    hipStream_t st = c->stream;
+    RssArgs a = c->rss;
+    const uint32_t S = a.n_queues;
+    if (!bt->n) {
+        HIPC(c, hipMemsetAsync(o->queue_off_dev, 0, (S + 1) * sizeof(uint32_t), st));
+        return 0;
+    }
+    a.frames = bt->frames_dev;
+    a.offset = bt->offset_dev;
+    a.length = bt->length_dev;
+    a.ptype = bt->ptype_dev;
+    a.hash = o->hash_dev;
+    a.queue_pkt = o->queue_pkt_dev;
+    a.frames_bytes = bt->frames_bytes;
+    a.rsrc_bytes = frames_rsrc_bytes(bt->frames_bytes);
+    a.n = bt->n;
+    const uint32_t tiles = ceil_div(bt->n, RSS_TILE);
+    hipLaunchKernelGGL(rss_hash, dim3(tiles), dim3(RSS_BLOCK), 0, st, a);
+    HIPC(c, hipGetLastError());
+    ScanArgs sa;
+    sa.hist = c->rss_hist;
+    sa.partial = c->rss_partial;
+    sa.lane_off = o->queue_off_dev;
+    sa.total = c->rss_total;
+    sa.n_elems = tiles * S;
+    sa.n_tiles = tiles;
+    sa.n_lanes = S;
+    if (sa.n_elems <= SCAN_SMALL_MAX && tiles <= SCAN_SMALL_TILES) {
+        hipLaunchKernelGGL(rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 4u * S, st, sa);
+    } else {
+        const uint32_t nc = ceil_div(tiles, SCAN_COL_CHUNK);
+        const dim3 grid(nc, ceil_div(S, (uint32_t)SCAN_BLOCK));
+        hipLaunchKernelGGL(rx_scan_reduce, grid, dim3(SCAN_BLOCK), 0, st, sa);
+        hipLaunchKernelGGL(rx_scan_top, dim3(1), dim3(SCAN_TOP_BLOCK), 4u * S, st, sa, nc);
+        hipLaunchKernelGGL(rx_scan_down, grid, dim3(SCAN_BLOCK), 0, st, sa);
+    }
+    HIPC(c, hipGetLastError());
+    hipLaunchKernelGGL(rss_scatter, dim3(tiles), dim3(RSS_BLOCK), 0, st, a);
+    HIPC(c, hipGetLastError());
     return 0;
 }
 
