@@ -287,6 +287,42 @@ def reasm_line(ctx, n_dgrams: int, payload_len: int, reps: int):
             "timing": "host wall clock per synchronous call"}
 
 
+def rss_line(ctx, cfg: int, n_queues: int, steps: int):
+    """udpdk_gpu_rss (f4) over one batch of config `cfg`: Toeplitz hash, redirection table and
+    per-queue lists, GPU time from events around `steps` back-to-back calls. Algorithmic bytes
+    per frame: 26 header bytes + 6 descriptor read, 4 hash + 1 queue id written, 1 queue id
+    read + 4 list entry written."""
+    w = F.config_batch(cfg)
+    b = w.batch
+    cf = abi.rss_conf(n_queues)
+    abi._check(abi.lib().udpdk_gpu_rss_config(ctx.handle, C.byref(cf)), "udpdk_gpu_rss_config")
+    db = abi.rx_upload(ctx, b.frames, b.offset, b.length)
+    db.frames_bytes = b.frames_bytes
+    h, qo, qp = ctx.alloc(4 * b.n), ctx.alloc(4 * (n_queues + 1)), ctx.alloc(4 * b.n)
+    bt = abi.RxBatch(db.frames.ptr, db.frames_bytes, db.offset.ptr, db.length.ptr, None, b.n)
+    ro = abi.RssOut(h.ptr, qo.ptr, qp.ptr)
+    f = abi.lib().udpdk_gpu_rss
+    for _ in range(3):
+        abi._check(f(ctx.handle, C.byref(bt), C.byref(ro)), "udpdk_gpu_rss")
+    ev = HipEvents(ctx)
+    ctx.sync()
+    ev.record(0)
+    for _ in range(steps):
+        f(ctx.handle, C.byref(bt), C.byref(ro))
+    ev.record(1)
+    ctx.sync()
+    us = 1e3 * ev.elapsed_ms() / steps
+    ev.close()
+    counts = np.diff(ctx.download(qo, np.uint32, n_queues + 1).astype(np.int64))
+    for x in (db.frames, db.offset, db.length, h, qo, qp):
+        x.free()
+    nbytes = (26 + 6 + 4 + 1 + 1 + 4) * b.n
+    return {"workload": f"RSS {w.name} over {n_queues} queues", "mpkt_s": round(b.n / us, 1),
+            "us_per_call": round(us, 2), "gbps": round(nbytes / us / 1e3, 1),
+            "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
+            "queue_min_max": [int(counts.min()), int(counts.max())]}
+
+
 def gather_line(ctx, cfg: int, steps: int, slot: int = 2048):
     """udpdk_gpu_rx_gather (f1, the batch form of recvfrom) over every delivery of one RX batch
     of config `cfg`: payload slots of `slot` bytes + length + source address per datagram, GPU
@@ -534,6 +570,13 @@ def main():
             line["reassembly"] = [reasm_line(ctx, 1 << 18, 2952, 10)]
         except Exception as e:
             line["reassembly"] = [{"error": repr(e)}]
+        rs = []
+        for cfg, nq in ((2, 8), (5, 8)):
+            try:
+                rs.append(rss_line(ctx, cfg, nq, 50))
+            except Exception as e:
+                rs.append({"config": cfg, "error": repr(e)})
+        line["rss"] = rs
         ga = []
         for cfg in (2, 3):
             try:

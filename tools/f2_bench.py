@@ -1,4 +1,4 @@
-"""Runs bench.py's f2 lines alone (fragmented TX, reassembly) and prints them as JSON."""
+"""Runs bench.py's f2/f4 lines alone (fragmented TX, reassembly, RSS) and prints them as JSON."""
 import json
 import os
 import sys
@@ -13,6 +13,9 @@ if what in ("all", "tx"):
     print(json.dumps(bench.tx_line(ctx, 22, 1 << 20, 50)), flush=True)
     print(json.dumps(bench.tx_line(ctx, 1458, 1 << 20, 50)), flush=True)
     print(json.dumps(bench.tx_line(ctx, 2952, 1 << 18, 50, mtu=1500)), flush=True)
+if what in ("all", "rss"):
+    print(json.dumps(bench.rss_line(ctx, 2, 8, 50)), flush=True)
+    print(json.dumps(bench.rss_line(ctx, 5, 8, 50)), flush=True)
 if what in ("all", "reasm"):
     print(json.dumps(bench.reasm_line(ctx, 1 << 18, 2952, 10)), flush=True)
 ctx.close()

@@ -183,6 +183,7 @@ struct RssArgs {
     const uint16_t *length;
     const uint32_t *ptype;
     const uint16_t *reta;     // [reta_size] queue per redirection entry
+    const uint32_t *ktab;     // [12][256] Toeplitz key windows per input byte (host-built)
     uint32_t *hash;           // [n] mbuf.hash.rss
     uint8_t  *qid;            // [n] queue per frame
     uint32_t *hist;           // [tiles][n_queues] -> scanned start positions
@@ -194,7 +195,6 @@ struct RssArgs {
     uint32_t n_queues;        // <= RSS_MAX_QUEUES
     uint32_t q_bits;          // bits of a queue index
     uint32_t hash_types;      // bit 0: IPv4 2-tuple, bit 1: unfragmented IPv4 UDP 4-tuple
-    uint8_t  key_be[40];      // Toeplitz key, byte 0 first
 };
 __global__ void rss_hash(RssArgs a);
 __global__ void rss_scatter(RssArgs a);

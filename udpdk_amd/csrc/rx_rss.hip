@@ -10,8 +10,9 @@
 // IPv4 gate rejects (the same ptype rule as rx_classify, fixed offsets as the reference parses).
 // Queue = reta[hash & (reta_size - 1)].
 //
-// Kernels: rss_hash (one workgroup per 1024-frame tile: a 12 x 256 table of key windows in LDS
-// turns the bit-serial Toeplitz product into 12 lookups per frame; hash and queue per frame; the
+// Kernels: rss_hash (one workgroup per 1024-frame tile: a 12 x 256 table of key windows, built
+// once on the host and staged into LDS, turns the bit-serial Toeplitz product into 12 lookups
+// per frame; hash and queue per frame; the
 // tile's queue histogram by wave multi-split), the tile-major scan shared with rx (rx_scan_*),
 // rss_scatter (per tile, each wave's contiguous quarter placed after the earlier quarters).
 // Bytes per frame: 26 header bytes read (one or two 32 B sectors) + 8 descriptor + 4 hash + 1
@@ -54,61 +55,63 @@ __device__ __forceinline__ unsigned long long peers_of(uint32_t key, uint32_t bi
 
 __global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
 {
-    __shared__ uint32_t tab[12][256];
+    __shared__ __attribute__((aligned(16))) uint32_t tab[12][256];
     __shared__ uint16_t reta[RSS_RETA_MAX];
     __shared__ uint32_t hist[RSS_MAX_QUEUES];
     const uint32_t tid = threadIdx.x, lane = __lane_id();
-    // key windows: win(b) = key bits [b, b + 32) (MSB first); tab[p][v] = XOR of win(8p + j) over
-    // the set bits j (MSB first) of byte value v at input position p
-    for (uint32_t e = tid; e < 12u * 256u; e += RSS_BLOCK) {
-        const uint32_t p = e >> 8, v = e & 255u;
-        uint32_t h = 0;
-        for (uint32_t j = 0; j < 8; ++j) {
-            if (!((v >> (7u - j)) & 1u)) continue;
-            const uint32_t b = 8u * p + j, k0 = b >> 3, s = b & 7u;
-            const unsigned long long w = ((unsigned long long)a.key_be[k0] << 32) |
-                                         ((unsigned long long)a.key_be[k0 + 1] << 24) |
-                                         ((unsigned long long)a.key_be[k0 + 2] << 16) |
-                                         ((unsigned long long)a.key_be[k0 + 3] << 8) |
-                                         (unsigned long long)a.key_be[k0 + 4];
-            h ^= (uint32_t)(w >> (8u - s));
-        }
-        tab[p][v] = h;
+    // the key-window table (udpdk_gpu_rss_config builds it: tab[p][v] = XOR of the key windows
+    // key bits [8p + j, 8p + j + 32) over the set bits j, MSB first, of byte value v at input
+    // position p), staged with 16-byte loads
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.ktab);
+        uint4 *dst = reinterpret_cast<uint4 *>(&tab[0][0]);
+        for (uint32_t e = tid; e < 12u * 256u / 4u; e += RSS_BLOCK) dst[e] = src[e];
     }
     for (uint32_t e = tid; e < a.reta_size; e += RSS_BLOCK) reta[e] = a.reta[e];
-    for (uint32_t q = tid; q < a.n_queues; q += RSS_BLOCK) hist[q] = 0;
-    __syncthreads();
     const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.frames), (short)0, (int)a.rsrc_bytes, 0x00020000);
-    const uint32_t t0 = blockIdx.x * RSS_TILE, t1 = min(a.n, t0 + RSS_TILE);
-    for (uint32_t i0 = t0 + (tid & ~63u); i0 < t1; i0 += RSS_BLOCK) {
-        const uint32_t i = i0 + lane;
+    for (uint32_t q = tid; q < a.n_queues; q += RSS_BLOCK) hist[q] = 0;
+    __syncthreads();
+    const uint32_t tile = blockIdx.x;
+    const uint32_t t0 = tile * RSS_TILE, t1 = min(a.n, t0 + RSS_TILE);
+    constexpr uint32_t STEPS = RSS_TILE / RSS_BLOCK;
+    // all of the thread's frames' loads first (descriptors, then header words), then the work
+    uint32_t o[STEPS], len[STEPS], w12[STEPS], w20[STEPS], src[STEPS], dst[STEPS], ports[STEPS];
+#pragma unroll
+    for (uint32_t s = 0; s < STEPS; ++s) {
+        const uint32_t i = t0 + s * RSS_BLOCK + (tid & ~63u) + lane;
+        o[s] = i < t1 ? a.offset[i] : 0u;
+        len[s] = i < t1 ? a.length[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t s = 0; s < STEPS; ++s) {
+        const bool ok = (uint64_t)o[s] + len[s] <= a.frames_bytes && len[s] >= 34u;
+        const uint32_t b0 = ok ? o[s] : 0u;
+        w12[s] = ok ? ld32(fr, b0 + 12) : 0u;
+        w20[s] = ok ? ld32(fr, b0 + 20) : 0u;
+        src[s] = ok ? ld32(fr, b0 + 26) : 0u;
+        dst[s] = ok ? ld32(fr, b0 + 30) : 0u;
+        ports[s] = ok && len[s] >= 38u ? ld32(fr, b0 + 34) : 0u;
+    }
+#pragma unroll
+    for (uint32_t s = 0; s < STEPS; ++s) {
+        const uint32_t i = t0 + s * RSS_BLOCK + (tid & ~63u) + lane;
         const bool in = i < t1;
         uint32_t hash = 0;
-        if (in) {
-            const uint32_t o = a.offset[i], len = a.length[i];
-            const bool desc_ok = (uint64_t)o + len <= a.frames_bytes;
-            uint32_t w12 = 0, w20 = 0, src = 0, dst = 0, ports = 0;
-            if (desc_ok && len >= 34u) {
-                w12 = ld32(fr, o + 12);
-                w20 = ld32(fr, o + 20);
-                src = ld32(fr, o + 26);
-                dst = ld32(fr, o + 30);
-                if (len >= 38u) ports = ld32(fr, o + 34);
-            }
-            const uint32_t pt = a.ptype ? a.ptype[i] : ((w12 & 0xFFFFu) == 0x0008u ? 0x211u : 0x1u);
-            if (desc_ok && len >= 34u && (pt & 0x10u)) {
-                const uint32_t ff = ((w20 & 0xFFu) << 8) | ((w20 >> 8) & 0xFFu);
-                const bool frag = (ff & 0x3FFFu) != 0u;
-                const bool udp4 = !frag && ((w20 >> 24) & 0xFFu) == 17u && len >= 38u && (a.hash_types & 2u);
-                if (udp4 || (a.hash_types & 1u)) {
-                    hash = tab[0][src & 255u] ^ tab[1][(src >> 8) & 255u] ^ tab[2][(src >> 16) & 255u] ^
-                           tab[3][src >> 24] ^ tab[4][dst & 255u] ^ tab[5][(dst >> 8) & 255u] ^
-                           tab[6][(dst >> 16) & 255u] ^ tab[7][dst >> 24];
-                    if (udp4)
-                        hash ^= tab[8][ports & 255u] ^ tab[9][(ports >> 8) & 255u] ^
-                                tab[10][(ports >> 16) & 255u] ^ tab[11][ports >> 24];
-                }
+        const bool ok = in && (uint64_t)o[s] + len[s] <= a.frames_bytes && len[s] >= 34u;
+        const uint32_t pt = ok ? (a.ptype ? a.ptype[i] : ((w12[s] & 0xFFFFu) == 0x0008u ? 0x211u : 0x1u)) : 0u;
+        if (ok && (pt & 0x10u)) {
+            const uint32_t ff = ((w20[s] & 0xFFu) << 8) | ((w20[s] >> 8) & 0xFFu);
+            const bool frag = (ff & 0x3FFFu) != 0u;
+            const bool udp4 = !frag && ((w20[s] >> 24) & 0xFFu) == 17u && len[s] >= 38u && (a.hash_types & 2u);
+            if (udp4 || (a.hash_types & 1u)) {
+                const uint32_t sa = src[s], da = dst[s], pp = ports[s];
+                hash = tab[0][sa & 255u] ^ tab[1][(sa >> 8) & 255u] ^ tab[2][(sa >> 16) & 255u] ^
+                       tab[3][sa >> 24] ^ tab[4][da & 255u] ^ tab[5][(da >> 8) & 255u] ^
+                       tab[6][(da >> 16) & 255u] ^ tab[7][da >> 24];
+                if (udp4)
+                    hash ^= tab[8][pp & 255u] ^ tab[9][(pp >> 8) & 255u] ^ tab[10][(pp >> 16) & 255u] ^
+                            tab[11][pp >> 24];
             }
         }
         const uint32_t q = reta[hash & (a.reta_size - 1u)];
@@ -122,7 +125,7 @@ __global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
     }
     __syncthreads();
     for (uint32_t q = tid; q < a.n_queues; q += RSS_BLOCK)
-        a.hist[(size_t)blockIdx.x * a.n_queues + q] = hist[q];
+        a.hist[(size_t)tile * a.n_queues + q] = hist[q];
 }
 
 // Per tile: wave w owns frames [t0 + 256 w, t0 + 256 w + 256); its base for queue q is the

@@ -99,6 +99,7 @@ struct udpdk_gpu_ctx {
     bool rss_ready = false;
     RssArgs rss{};
     uint16_t *rss_reta = nullptr;
+    uint32_t *rss_ktab = nullptr;             // [12][256] key windows
     uint8_t *rss_qid = nullptr;
     uint32_t *rss_hist = nullptr, *rss_partial = nullptr, *rss_total = nullptr;
 
@@ -312,7 +313,7 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
         if (P.stream) (void)hipStreamSynchronize(P.stream);
     reasm_destroy(c->reasm);
     c->reasm = nullptr;
-    for (void *p : {(void *)c->rss_reta, (void *)c->rss_qid, (void *)c->rss_hist,
+    for (void *p : {(void *)c->rss_reta, (void *)c->rss_ktab, (void *)c->rss_qid, (void *)c->rss_hist,
                     (void *)c->rss_partial, (void *)c->rss_total})
         if (p) (void)hipFree(p);
     void *dev[] = {c->port_tab, c->binds, c->slots};
@@ -888,16 +889,35 @@ int udpdk_gpu_rss_config(udpdk_gpu_ctx *c, const udpdk_rss_conf_t *conf)
     const uint32_t tiles = ceil_div(std::max<uint32_t>(c->max_frames, 1), RSS_TILE);
     if (!c->rss_reta) {
         HIPC(c, hipMalloc((void **)&c->rss_reta, RSS_RETA_MAX * sizeof(uint16_t)));
+        HIPC(c, hipMalloc((void **)&c->rss_ktab, 12 * 256 * sizeof(uint32_t)));
         HIPC(c, hipMalloc((void **)&c->rss_qid, std::max<uint32_t>(c->max_frames, 1)));
         HIPC(c, hipMalloc((void **)&c->rss_hist, (size_t)tiles * RSS_MAX_QUEUES * 4));
         HIPC(c, hipMalloc((void **)&c->rss_partial, (size_t)ceil_div(tiles, SCAN_COL_CHUNK) * RSS_MAX_QUEUES * 4));
         HIPC(c, hipMalloc((void **)&c->rss_total, 64));
     }
     HIPC(c, hipMemcpy(c->rss_reta, conf->reta, conf->reta_size * sizeof(uint16_t), hipMemcpyHostToDevice));
+    // Toeplitz key windows per (input byte position, byte value): win(b) = key bits [b, b + 32)
+    // MSB first; the hash of a 12-byte input is the XOR of 12 table entries
+    {
+        std::vector<uint32_t> tab(12 * 256);
+        auto win = [&](uint32_t b) {
+            uint64_t w = 0;
+            for (uint32_t k = 0; k < 5; ++k) w = (w << 8) | conf->key[(b >> 3) + k];
+            return (uint32_t)(w >> (8u - (b & 7u)));
+        };
+        for (uint32_t p = 0; p < 12; ++p)
+            for (uint32_t v = 0; v < 256; ++v) {
+                uint32_t h = 0;
+                for (uint32_t j = 0; j < 8; ++j)
+                    if ((v >> (7u - j)) & 1u) h ^= win(8u * p + j);
+                tab[p * 256 + v] = h;
+            }
+        HIPC(c, hipMemcpy(c->rss_ktab, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     RssArgs &r = c->rss;
     memset(&r, 0, sizeof(r));
-    memcpy(r.key_be, conf->key, UDPDK_RSS_KEY_BYTES);
     r.reta = c->rss_reta;
+    r.ktab = c->rss_ktab;
     r.qid = c->rss_qid;
     r.hist = c->rss_hist;
     r.reta_size = conf->reta_size;
