@@ -852,15 +852,21 @@ rx_scatterw(ScatterArgs a)
     const uint32_t plast = a.n - 1u;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     uint16_t *mine = woff + w * S;
-    constexpr int PF = 4;
+    // the wave's whole slice of verdict words in registers (<= RX_TILE_MAX / W frames = 16 per
+    // lane), loaded once for both passes: no load in the counting or the placing loop
+    constexpr uint32_t MV = RX_TILE_MAX / (64 * SCATTER_WAVES);
+    uint32_t mv[MV];
+#pragma unroll
+    for (uint32_t i = 0; i < MV; ++i) {
+        const uint32_t p = wb + i * 64 + lane;
+        mv[i] = (i * 64 < q) ? a.meta[min(p, plast)] : 0u;
+    }
     for (int pass = 0; pass < 2; ++pass) {
-        for (uint32_t g0 = wb; g0 < we; g0 += 64 * PF) {
-            uint32_t mv[PF];
 #pragma unroll
-            for (int i = 0; i < PF; ++i) mv[i] = a.meta[min(g0 + i * 64 + lane, plast)];
-#pragma unroll
-            for (int i = 0; i < PF; ++i) {
-                const uint32_t p = g0 + i * 64 + lane;
+        for (uint32_t i = 0; i < MV; ++i) {
+            if (i * 64 >= q) break;                        // uniform
+            {
+                const uint32_t p = wb + i * 64 + lane;
                 const bool deliver = p < we && UDPDK_META_VERDICT(mv[i]) == UDPDK_V_DELIVERED;
                 const uint32_t key = UDPDK_META_SOCKFD(mv[i]) & a.lane_mask;
                 unsigned long long peers = __ballot(deliver);
