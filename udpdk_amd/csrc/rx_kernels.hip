@@ -300,10 +300,93 @@ rx_classify(RxArgs a)
     Win W = load_win(st, c_off, c_lp & 0xFFFFu);
     STAMP(0);
 
-    // rounds of RX_ROUND frames: SPR steps per wave, then the wave's tail pass for them (the
-    // next round's first window is already in flight during the tail pass)
+    // ---- tail pass: UDP checksums of the datagrams that extend past the header window ----
+    // Run for each step right after it (while the frames' first lines are still in L2: a pass
+    // per round of four steps re-fetched the line shared by a frame's header window and its
+    // first tail chunk from HBM). The step's pending frames (state 3): frame bytes [64, dge) as
+    // 64-byte super-chunks, chunk j = frame bytes [64 + 64 j, 128 + 64 j) loaded as 4
+    // byte-aligned 16-byte pieces (so the words are frame-relative whatever the frame's offset,
+    // and only a frame's last chunk needs byte masks), swept across the wave's lanes: lane i of a
+    // group takes chunk k0 + i of the step's chunk space (its frame found by binary search over
+    // the per-frame chunk starts in LDS), so a group is 4 KiB of dense frame bytes. Per-frame sums
+    // are segment sums of a DPP prefix scan; two groups in flight.
+    uint32_t *l_cs = reinterpret_cast<uint32_t *>(smem + TP_OFF) + w * 192;  // [64] chunk starts
+    uint32_t *l_off = l_cs + 64, *l_dge = l_cs + 128;                       // [64] offset, dge
+    auto tail_step = [&](uint32_t s2) {
+            const uint32_t i = s2 * 64 + lane;
+            const uint32_t m = mstage[i];
+            const bool pd = t0 + i < t1 && ((m >> 5) & 3u) == 3u;
+            if (!__ballot(pd)) return;
+            // the frame's offset: the staged descriptor of a single-round tile, else global
+            const uint32_t fo = nbuf == 1u ? d_off[i] : a.offset[min(t0 + i, plast)];
+            const uint32_t dw = dgl[i & (RX_ROUND - 1u)];
+            const uint32_t de = pd ? dw & 0xFFFFu : 64u;
+            const uint32_t my_nt = (de - 64u + 63u) >> 6;
+            const uint32_t inc = scan_dpp(my_nt);
+            const uint32_t my_cs = inc - my_nt;
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            l_cs[lane] = my_cs;
+            l_off[lane] = fo;
+            l_dge[lane] = de;
+            wave_sync();
+            uint32_t tsum = 0;
+            auto issue = [&](uint32_t k0, uint32_t &q, uint4 (&R)[4]) {
+                const uint32_t k = k0 + lane;
+                q = 0;
+#pragma unroll
+                for (int sft = 32; sft >= 1; sft >>= 1)
+                    if (l_cs[q + sft] <= k) q += sft;
+                const uint32_t base = k < total ? l_off[q] + 64u + 64u * (k - l_cs[q]) : 0u;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) R[c] = load16(fr, base + 16u * c);
+            };
+            // The full-chunk sum reads every loaded register unconditionally, so the compiler's
+            // wait for this group is placed here on every path (a first use only inside a lane
+            // branch leaves the loads "pending" at the loop header, where it then waits for
+            // every load in flight, the next group's included).
+            auto consume = [&](uint32_t k0, uint32_t q, const uint4 (&R)[4]) {
+                const uint32_t k = k0 + lane;
+                uint32_t part = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) part += sum16(R[c].x) + sum16(R[c].y) + sum16(R[c].z) + sum16(R[c].w);
+                const int left = (int)l_dge[q] - 64 - 64 * (int)(k - l_cs[q]);   // chunk bytes in the datagram
+                if (left < 64) {                                       // the frame's last chunk
+                    part = 0;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) part += chunk_sum(R[c], 0, left - 16 * c);
+                }
+                part = k < total ? part : 0u;
+                const uint32_t P = scan_dpp(part);
+                const uint32_t lo = max(my_cs, k0), hi = min(my_cs + my_nt, k0 + 64u);
+                const uint32_t ph = __shfl(P, (int)((hi > k0 ? hi - 1u - k0 : 0u) & 63u), 64);
+                const uint32_t pl = __shfl(P, (int)((lo > k0 ? lo - 1u - k0 : 0u) & 63u), 64);
+                if (lo < hi) tsum += ph - (lo > k0 ? pl : 0u);
+            };
+            // Two groups in flight; one back edge, after the second group is consumed (a loop
+            // exit between the two halves leaves the second group's loads pending at the
+            // header, which then waits for everything). Groups past the end load from offset 0
+            // and contribute nothing.
+            uint32_t qa, qb;
+            uint4 Ra[4], Rb[4];
+            issue(0, qa, Ra);
+            for (uint32_t k0 = 0;; k0 += 128) {
+                issue(k0 + 64, qb, Rb);
+                consume(k0, qa, Ra);
+                issue(k0 + 128, qa, Ra);
+                consume(k0 + 64, qb, Rb);
+                if (k0 + 128 >= total) break;
+            }
+            wave_sync();
+            if (pd) {
+                const bool ok = fold32(fold32(tsum) + (dw >> 16)) == 0xFFFFu;
+                mstage[i] = (m & ~0x60u) | ((ok ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD) << 5);
+                acc_f0 += ok ? 0x10000u : 0x1000000u;
+            }
+    };
+
+    // rounds of RX_ROUND frames: SPR steps per wave (each followed by its tail pass when a frame
+    // of the step is pending), then the round's demux pass
     for (uint32_t rnd = 0; rnd < steps / 16u; ++rnd) {
-        bool tail_any = false;     // some frame of the wave's steps waits for the tail pass (SGPR)
 #pragma unroll 1
         for (uint32_t jstep = 0; jstep < SPR; ++jstep) {
             const uint32_t p = t0 + st * 64 + lane;
@@ -356,7 +439,6 @@ rx_classify(RxArgs a)
             }
             const uint32_t us = ws + (g[5] >> 16) + (g[3] >> 16) + (g[4] & 0xFFFFu) + (dip & 0xFFFFu) +
                                 (dip >> 16) + 0x1100u + ulen_raw;
-            tail_any = tail_any || __ballot(pend) != 0ull;
             dgl[(st * 64 + lane) & (RX_ROUND - 1u)] = dge | fold32(us) << 16;
             STAMP(2);
 
@@ -388,6 +470,7 @@ rx_classify(RxArgs a)
             // the port-table lookup waits for the round's demux pass: verdict field 0xF until then
             mstage[st * 64 + lane] = (pre == 0xFFu ? 0xFu : pre) | l3f | udpf;
             dstash[(st * 64 + lane) & (RX_ROUND - 1u)] = make_uint2(dport | (is_udp ? 0x10000u : 0u), dip);
+            if (__ballot(pend)) tail_step(st);
             STAMP(6);
             // next round's descriptors into the other buffer at the wave's next-to-last step of a
             // round (its steps of round r are 16 r + w + CLS_WAVES j, j < SPR): the last reads of that
@@ -478,81 +561,6 @@ rx_classify(RxArgs a)
         // lanes: lane i of a group takes chunk k0 + i of the step's chunk space (its frame found by
         // binary search over the per-frame chunk starts in LDS), so a group is 4 KiB of dense frame
         // bytes. Per-frame sums are segment sums of a DPP prefix scan; two groups in flight.
-        if (tail_any) {
-            uint32_t *l_cs = reinterpret_cast<uint32_t *>(smem + TP_OFF) + w * 192;  // [64] chunk starts
-            uint32_t *l_off = l_cs + 64, *l_dge = l_cs + 128;                       // [64] offset, dge
-            for (uint32_t s2 = st - 16u; s2 < st; s2 += CLS_WAVES) {      // this round's steps
-                const uint32_t i = s2 * 64 + lane;
-                const uint32_t m = mstage[i];
-                const bool pd = t0 + i < t1 && ((m >> 5) & 3u) == 3u;
-                if (!__ballot(pd)) continue;
-                // the frame's offset: the staged descriptor of a single-round tile, else global
-                const uint32_t fo = nbuf == 1u ? d_off[i] : a.offset[min(t0 + i, plast)];
-                const uint32_t dw = dgl[i & (RX_ROUND - 1u)];
-                const uint32_t de = pd ? dw & 0xFFFFu : 64u;
-                const uint32_t my_nt = (de - 64u + 63u) >> 6;
-                const uint32_t inc = scan_dpp(my_nt);
-                const uint32_t my_cs = inc - my_nt;
-                const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-                l_cs[lane] = my_cs;
-                l_off[lane] = fo;
-                l_dge[lane] = de;
-                wave_sync();
-                uint32_t tsum = 0;
-                auto issue = [&](uint32_t k0, uint32_t &q, uint4 (&R)[4]) {
-                    const uint32_t k = k0 + lane;
-                    q = 0;
-#pragma unroll
-                    for (int sft = 32; sft >= 1; sft >>= 1)
-                        if (l_cs[q + sft] <= k) q += sft;
-                    const uint32_t base = k < total ? l_off[q] + 64u + 64u * (k - l_cs[q]) : 0u;
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) R[c] = load16(fr, base + 16u * c);
-                };
-                // The full-chunk sum reads every loaded register unconditionally, so the compiler's
-                // wait for this group is placed here on every path (a first use only inside a lane
-                // branch leaves the loads "pending" at the loop header, where it then waits for
-                // every load in flight, the next group's included).
-                auto consume = [&](uint32_t k0, uint32_t q, const uint4 (&R)[4]) {
-                    const uint32_t k = k0 + lane;
-                    uint32_t part = 0;
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) part += sum16(R[c].x) + sum16(R[c].y) + sum16(R[c].z) + sum16(R[c].w);
-                    const int left = (int)l_dge[q] - 64 - 64 * (int)(k - l_cs[q]);   // chunk bytes in the datagram
-                    if (left < 64) {                                       // the frame's last chunk
-                        part = 0;
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) part += chunk_sum(R[c], 0, left - 16 * c);
-                    }
-                    part = k < total ? part : 0u;
-                    const uint32_t P = scan_dpp(part);
-                    const uint32_t lo = max(my_cs, k0), hi = min(my_cs + my_nt, k0 + 64u);
-                    const uint32_t ph = __shfl(P, (int)((hi > k0 ? hi - 1u - k0 : 0u) & 63u), 64);
-                    const uint32_t pl = __shfl(P, (int)((lo > k0 ? lo - 1u - k0 : 0u) & 63u), 64);
-                    if (lo < hi) tsum += ph - (lo > k0 ? pl : 0u);
-                };
-                // Two groups in flight; one back edge, after the second group is consumed (a loop
-                // exit between the two halves leaves the second group's loads pending at the
-                // header, which then waits for everything). Groups past the end load from offset 0
-                // and contribute nothing.
-                uint32_t qa, qb;
-                uint4 Ra[4], Rb[4];
-                issue(0, qa, Ra);
-                for (uint32_t k0 = 0;; k0 += 128) {
-                    issue(k0 + 64, qb, Rb);
-                    consume(k0, qa, Ra);
-                    issue(k0 + 128, qa, Ra);
-                    consume(k0 + 64, qb, Rb);
-                    if (k0 + 128 >= total) break;
-                }
-                wave_sync();
-                if (pd) {
-                    const bool ok = fold32(fold32(tsum) + (dw >> 16)) == 0xFFFFu;
-                    mstage[i] = (m & ~0x60u) | ((ok ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD) << 5);
-                    acc_f0 += ok ? 0x10000u : 0x1000000u;
-                }
-            }
-        }
     }
 
     // ---- tile counters: one row per wave (lanes 0-15), summed by the readers ----
