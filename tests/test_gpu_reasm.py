@@ -154,3 +154,27 @@ def test_tx_fragments_come_back(gpu_ctx):
     for k in range(n):
         assert glen[k] == lens[k] and gp[k, :lens[k]].tobytes() == pays[k], k
     assert np.all(gport == abi.raw_port(10000)) and np.all(gip == abi.raw_ip("172.31.100.2"))
+
+
+def test_reassembly_edges(gpu_ctx):
+    """Bad table geometry -> EINVAL; an empty batch and a batch without fragments give no
+    datagrams."""
+    import ctypes as C
+    from reasm_util import udp_datagram, ip_frame, raw_ip
+    bad = abi.FragTableCfg(0, 16, 100, 65515)
+    assert abi.lib().udpdk_gpu_frag_table_create(gpu_ctx.handle, C.byref(bad)) == -22
+    bad = abi.FragTableCfg(16, 3, 100, 65515)                 # bucket_entries not a power of two
+    assert abi.lib().udpdk_gpu_frag_table_create(gpu_ctx.handle, C.byref(bad)) == -22
+    bad = abi.FragTableCfg(16, 16, 100, 70000)                # max_dgram past IPv4
+    assert abi.lib().udpdk_gpu_frag_table_create(gpu_ctx.handle, C.byref(bad)) == -22
+    abi.frag_table_create(gpu_ctx, 16, 16, 100, 4096)
+    frames = [ip_frame(raw_ip("10.0.0.1"), raw_ip("172.31.100.1"), 1, 0, udp_datagram(1, 2, b"x" * 40), False)]
+    buf, off, ln = batch(frames)
+    db = abi.rx_upload(gpu_ctx, buf, off, ln)
+    db.frames_bytes = len(buf) - 64
+    meta = gpu_ctx.upload(O.rx(O.BindTable(), buf, len(buf) - 64, off, ln, None, 1)[0])
+    rb, _, st = abi.rx_reassemble(gpu_ctx, db, meta, 0)
+    assert rb.n == 0 and st["frags"] == 0
+    db.n = 0
+    rb, _, st = abi.rx_reassemble(gpu_ctx, db, meta, 0)
+    assert rb.n == 0 and sum(st.values()) == 0

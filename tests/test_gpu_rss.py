@@ -71,3 +71,28 @@ def test_rss_full_size_config5(gpu_ctx):
     (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, w.batch, abi.rss_conf(8))
     assert np.array_equal(wh, gh) and np.array_equal(wo, go) and np.array_equal(wp, gp)
     assert go[-1] == w.batch.n
+
+
+def test_rss_edges(gpu_ctx):
+    """Empty batch, bad configurations, a single frame; the RSS call needs a configuration."""
+    import ctypes as C
+    cf = abi.rss_conf(4)
+    assert abi.lib().udpdk_gpu_rss_config(gpu_ctx.handle, C.byref(cf)) == 0
+    qo = gpu_ctx.alloc(4 * 5)
+    bt = abi.RxBatch(None, 0, None, None, None, 0)
+    assert abi.lib().udpdk_gpu_rss(gpu_ctx.handle, C.byref(bt), C.byref(abi.RssOut(None, qo.ptr, None))) == 0
+    gpu_ctx.sync()
+    assert np.array_equal(gpu_ctx.download(qo, np.uint32, 5), np.zeros(5, np.uint32))
+    qo.free()
+    for bad in (dict(n_queues=0), dict(n_queues=65), dict(reta_size=3), dict(reta_size=1024),
+                dict(hash_types=4)):
+        c2 = abi.rss_conf(4)
+        for k, v in bad.items():
+            setattr(c2, k, v)
+        assert abi.lib().udpdk_gpu_rss_config(gpu_ctx.handle, C.byref(c2)) == -22, bad
+    c3 = abi.rss_conf(4)
+    c3.reta[0] = 4                                     # queue out of range
+    assert abi.lib().udpdk_gpu_rss_config(gpu_ctx.handle, C.byref(c3)) == -22
+    b = F.mixed_batch(1, 1, [10001], [9], ["172.31.100.1"])
+    (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, b, abi.rss_conf(3))
+    assert np.array_equal(wh, gh) and np.array_equal(wo, go) and np.array_equal(wp, gp)
