@@ -162,14 +162,30 @@ def time_loop(rx: Rx, steps: int, warmup: int, barrier, timing_every: int):
     return (t1 - t0), gpu_ms / steps, kt, st
 
 
-def cpu_baseline(w: F.Workload, target_s: float):
+def _digest(*arrays) -> str:
+    import hashlib
+    h = hashlib.blake2b(digest_size=8)
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def cpu_baseline(w: F.Workload, target_s: float, gpu_out=None):
     """Oracle (the C restatement, kind "port") on the host cores: 1 thread and min(nproc, 16)
-    threads, one independent shard per pinned thread, with the RX checksum verification."""
+    threads, one independent shard per pinned thread, with the RX checksum verification. With
+    gpu_out = (meta, lane_off, lane_pkt) of the measured batch, the same leg also runs the
+    restatement once on that batch and compares 64-bit digests of the outputs (SURVEY.md §8(d)
+    "parity mode")."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     b = w.batch
     bt = O.bindtable_from_lists(w.port_lists())
-    res = {}
+    parity = None
+    if gpu_out is not None:
+        wm, wl, wp, _ = O.rx(bt, b.frames, b.frames_bytes, b.offset, b.length, None, w.n_sockets)
+        parity = {"oracle": _digest(wm, wl, wp), "gpu": _digest(*gpu_out)}
+        parity["match"] = parity["oracle"] == parity["gpu"]
+    res = {"parity": parity}
     threads_all = max(1, min(os.cpu_count() or 1, 16))
     for th in sorted({1, threads_all}):
         for csum in (True, False):
@@ -473,6 +489,16 @@ def main():
     ctx.pipeline(1)
     k_steps = max(16, args.steps // 2)
     wall1, gpu_step1, kt, _ = time_loop(rx, k_steps, 5, barrier, args.timing_every)
+    # one isolated call (a single launch beside the steady state): events around
+    # one udpdk_gpu_rx on an idle GPU, on a device copy not touched by the previous calls
+    ev1 = HipEvents(ctx)
+    ctx.sync()
+    ev1.record(0)
+    rx.step(k_steps + 5 + rx.copies // 2)
+    ev1.record(1)
+    ctx.sync()
+    single_us = 1e3 * ev1.elapsed_ms()
+    ev1.close()
     if dist is not None:
         t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -511,6 +537,7 @@ def main():
                    "parallelism": f"shard{world}", "device_copies_rotated": rx.copies},
         "gbps_pipeline": round(rx.pipeline_bytes() * args.steps * world / wall / 1e9, 1),
         "gpu_us_per_step": round(1e3 * gpu_step, 3),
+        "single_call_us": round(single_us, 3),
         "pipeline_depth": args.pipeline,
         "depth1": {"mpkt_s": round(rx.n * k_steps / wall1 / 1e6, 2), "gpu_us_per_step": round(1e3 * gpu_step1, 3),
                    "note": "the same calls one at a time on one stream (kernel timing loop)"},
@@ -524,7 +551,16 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res, thr = cpu_baseline(F.config_batch(args.config, n=min(rx.n, 1 << 20)), args.cpu_seconds)
+        gpu_out = None
+        if rx.n <= (1 << 20):            # the measured batch itself: digest of its outputs
+            a0 = rx.args[0]
+            out = a0[5]
+            gpu_out = (ctx.download(out.meta, np.uint32, rx.n),
+                       ctx.download(out.lane_off, np.uint32, rx.w.n_sockets + 1),
+                       None)
+            gpu_out = (gpu_out[0], gpu_out[1], ctx.download(out.lane_pkt, np.uint32, int(gpu_out[1][-1])))
+        res, thr = cpu_baseline(F.config_batch(args.config, n=min(rx.n, 1 << 20)), args.cpu_seconds,
+                                gpu_out)
         v, reps, secs = res[(thr, True)]
         line["cpu_baseline"] = {
             "value": round(v, 2), "unit": "Mpkt/s", "cores": thr, "kind": "port",
@@ -533,6 +569,7 @@ def main():
             "one_thread": round(res[(1, True)][0], 2),
             "one_thread_no_csum": round(res[(1, False)][0], 2),
             f"{thr}_threads_no_csum": round(res[(thr, False)][0], 2),
+            "parity": res["parity"],
         }
     if rank == 0 and world == 1 and not args.no_extra:
         extra = []
