@@ -1,0 +1,57 @@
+"""The reference's socket surface end to end on the GPU: udpdk_init (config file), bind,
+udpdk_poll_rx (the poller's RX half: GPU classify/demux, device reassembly of IPv4 fragments,
+per-socket rings in the reference's order) and udpdk_recvfrom; a reassembled datagram arrives at
+the position of the fragment that completed it (udpdk_poller.c:338-412), across poll calls."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from reasm_util import batch, ip_frame, raw_ip, split, udp_datagram
+from udpdk_amd import abi
+
+pytestmark = pytest.mark.gpu
+
+
+def _port(p):
+    return int.from_bytes(p.to_bytes(2, "big"), "little")
+
+
+def test_poll_rx_delivers_reassembled_datagrams_in_order(tmp_path, host_api):
+    ini = tmp_path / "udpdk.ini"
+    ini.write_text("[port0]\nmac_addr = 68:05:ca:95:f8:ec\nip_addr = 172.31.100.1\n"
+                   "[port0_dst]\nmac_addr = 68:05:ca:95:fa:64\n"
+                   "[gpu]\ndevice = 0\nmax_frames = 65536\nmax_lanes = 16\n"
+                   "frag_buckets = 16\nfrag_bucket_entries = 16\nfrag_max_dgram = 16384\n")
+    L = abi.lib()
+    argv = (C.c_char_p * 4)(b"prog", b"-c", str(ini).encode(), None)
+    assert L.udpdk_init(3, argv) == 0
+    try:
+        s0, s1 = host_api.socket(), host_api.socket()
+        assert host_api.bind(s0, "0.0.0.0", 10001) == 0
+        assert host_api.bind(s1, "0.0.0.0", 10002) == 0
+        src, dst = raw_ip("10.9.8.7"), raw_ip("172.31.100.1")
+
+        def plain(port, payload, pid):
+            return ip_frame(src, dst, pid, 0, udp_datagram(_port(4000), _port(port), payload), False)
+        d1 = udp_datagram(_port(4000), _port(10001), bytes(range(256)) * 12)        # 3080 B
+        d2 = udp_datagram(_port(4000), _port(10002), bytes(range(100, 200)) * 20)   # 2008 B
+        f1 = split(src, dst, 77, d1, [1480, 1480, 120])
+        f2 = split(src, dst, 78, d2, [1480, 528])
+        b1 = [plain(10001, b"A" * 10, 1), f1[2], plain(10002, b"B" * 20, 2), f1[0],
+              plain(10001, b"C" * 30, 3), f2[1]]
+        b2 = [f1[1], plain(10001, b"D" * 40, 4), f2[0], plain(10002, b"E" * 50, 5)]
+        for fr in (b1, b2):
+            buf, off, ln = batch(fr)
+            st = abi.RxStats()
+            assert L.udpdk_poll_rx(buf.ctypes.data, len(buf) - 64, off.ctypes.data, ln.ctypes.data,
+                                   None, len(off), C.byref(st)) == 0
+        want0 = [b"A" * 10, b"C" * 30, d1[8:], b"D" * 40]      # d1 completes at b2[0]
+        want1 = [b"B" * 20, d2[8:], b"E" * 50]                 # d2 completes at b2[2]
+        for s, want in ((s0, want0), (s1, want1)):
+            for w in want:
+                n, data, addr = host_api.recvfrom(s, 8192)
+                assert n == len(w) and data == w, (s, n)
+                assert addr == ("10.9.8.7", 4000)
+    finally:
+        L.udpdk_cleanup()

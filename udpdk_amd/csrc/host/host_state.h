@@ -55,6 +55,16 @@ struct h_state {
     uint32_t gpu_max_frames, gpu_max_lanes;
     uint64_t snap_version;   /* version uploaded to the GPU (UINT64_MAX = none) */
     int      snap_compat;
+    /* fragments (udpdk_poller.c:338-361): the device reassembly table, created on the first
+     * FRAG frame; geometry from the [gpu] frag_* ini keys (defaults: the poller's table) */
+    int      frag_ready;
+    uint32_t frag_buckets, frag_entries, frag_max_dgram;
+    uint64_t frag_ttl_ms;
+    void    *fd_frames, *fd_offset, *fd_length, *fd_meta;      /* device copies, grow-only */
+    uint64_t fd_frames_cap;
+    uint32_t fd_n_cap;
+    void    *fd_meta2, *fd_loff2, *fd_lpkt2;
+    uint32_t fd_out_cap;
     /* TX queue of built frames (the tx_q rings + TX half of the poller, poller.c:452-514) */
     uint8_t *txq;
     uint64_t txq_bytes, txq_cap;
