@@ -41,6 +41,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--config", type=int, default=2, help="BASELINE.json config number (2..5)")
     p.add_argument("--frames", type=int, default=None, help="override frames per GPU")
+    p.add_argument("--strong-total", type=int, default=None,
+                   help="strong scaling: this many frames in total, split into contiguous equal "
+                        "shards over the ranks (SURVEY.md 8(e): one 32 M batch)")
     p.add_argument("--rotate-mib", type=int, default=640, help="device bytes cycled by the loop")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1500 B / IMIX side lines")
@@ -478,7 +481,10 @@ def main():
     if ndev < 1:
         raise SystemExit("bench.py needs a GPU (no HIP device visible)")
     device = local % ndev
-    w = F.config_batch(args.config, n=args.frames, shard=rank)
+    frames = args.frames
+    if args.strong_total:
+        frames = -(-args.strong_total // world)          # this rank's contiguous shard
+    w = F.config_batch(args.config, n=frames, shard=rank)
     ctx = abi.GpuContext(device, max_frames=max(w.batch.n, 1 << 22), max_lanes=4096)
     rx = Rx(ctx, w, args.rotate_mib << 20)
     # the timed region (value): consecutive batches pipelined over two streams, no events inside
@@ -528,7 +534,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong_total else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (SURVEY.md §8(d) recipe, seeded per rank)",

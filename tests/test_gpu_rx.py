@@ -260,3 +260,30 @@ def test_rx_host_sync_and_async(gpu_ctx):
             assert d == int(want[1][-1])
             assert np.array_equal(pkt[:d], want[2])
             assert np.array_equal(np.array(st.counters[:], np.uint64), want[3])
+
+
+def test_single_lane_many_tiles():
+    """5 M frames in one batch (5120 tiles: past COMPACT1_DIRECT_TILES the compaction takes its
+    tile bases from rx_tile_base): every frame delivered except every 997th, whose destination
+    port is unbound; the lane lists the others in order."""
+    w = F.config_batch(2, n=5 * (1 << 20))
+    b = w.batch
+    n = b.n
+    drop = np.arange(0, n, 997)
+    v = b.frames[:n * 64].reshape(n, 64)
+    v[drop, 36] = 0x4E                                  # dst port 20000: not bound
+    v[drop, 37] = 0x20
+    ctx = abi.GpuContext(0, max_frames=6 << 20, max_lanes=16)
+    ctx.upload_snapshot(abi.snapshot_from_lists(w.port_lists(), 1))
+    db = abi.rx_upload(ctx, b.frames, b.offset, b.length)
+    db.frames_bytes = b.frames_bytes
+    out = abi.rx_alloc_out(ctx, n, 1, n)
+    meta, loff, pkt, cnt, rc = abi.rx_run(ctx, db, out)
+    keep = np.ones(n, bool)
+    keep[drop] = False
+    assert rc == 0 and int(loff[1]) == int(keep.sum())
+    assert np.array_equal(pkt, np.nonzero(keep)[0].astype(np.uint32))
+    assert np.all(abi.meta_verdict(meta[drop]) == abi.V_NO_BIND)
+    for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt):
+        x.free()
+    ctx.close()

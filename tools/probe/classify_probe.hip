@@ -166,7 +166,7 @@ int main()
             Compact1Args ca;
             ca.meta = b.meta; ca.tile_count = b.hist; ca.lane_pkt = lpk[k];
             ca.lane_off = lok[k]; ca.total = totk[k]; ca.n = N; ca.tile_frames = T;
-            ca.n_tiles = tiles; ca.lane_cap = N;
+            ca.n_tiles = tiles; ca.lane_cap = N; ca.base = nullptr;
             const int tpb = getenv("TPB") ? atoi(getenv("TPB")) : 0;
             if (tpb > 0)
                 hipLaunchKernelGGL(rx_compact1w, dim3((tiles + tpb - 1) / tpb), dim3(RX_BLOCK), 0, ss[k], ca,

@@ -23,6 +23,7 @@ constexpr int CLS_WAVES = CLS_BLOCK / 64;
 
 constexpr int SCAN_BLOCK = 256;
 constexpr int SCAN_TOP_BLOCK = 1024;
+constexpr uint32_t COMPACT1_DIRECT_TILES = 4096; // rx_compact1 sums its predecessors' counts itself
 constexpr uint32_t SCAN_COL_CHUNK = 32;     // tiles per chunk of the 3-pass column scan
 constexpr uint32_t SCAN_SMALL_MAX = 16384;  // single-workgroup scan up to this many elements
 constexpr uint32_t SCAN_SMALL_TILES = 32;   // ... and this many tiles (serial per lane)
@@ -115,6 +116,7 @@ struct Compact1Args {
     uint32_t tile_frames;
     uint32_t n_tiles;
     uint32_t lane_cap;
+    const uint32_t *base;         // [n_tiles] exclusive prefix of tile_count (rx_tile_base), or null
 };
 
 struct TxArgs {
@@ -171,6 +173,7 @@ __host__ __device__ constexpr uint32_t scatterw_lds_bytes(uint32_t n_lanes)
     return 4u * n_lanes + 2u * SCATTER_WAVES * n_lanes;
 }
 __global__ void rx_compact1(Compact1Args a);
+__global__ void rx_tile_base(const uint32_t *cnt, uint32_t *base, uint32_t n);
 __global__ void rx_counters(const uint32_t *tile_cnt, uint32_t n_tiles, unsigned long long *counters);
 // Receive-side scaling (rx_rss.hip).
 constexpr uint32_t RSS_BLOCK = 256;

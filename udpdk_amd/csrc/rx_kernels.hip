@@ -658,12 +658,16 @@ rx_compact1(Compact1Args a)
             wcount += (uint32_t)__popcll(m);
         }
     }
-    uint32_t pre = (tid < tile ? c0 : 0u) + (tid + RX_BLOCK < tile ? c1 : 0u);
-    for (uint32_t t = tid + 2 * RX_BLOCK; t < tile; t += RX_BLOCK) pre += a.tile_count[t];
-    pre = wave_sum(pre);
+    uint32_t pre = 0;
+    if (!a.base) {
+        pre = (tid < tile ? c0 : 0u) + (tid + RX_BLOCK < tile ? c1 : 0u);
+        for (uint32_t t = tid + 2 * RX_BLOCK; t < tile; t += RX_BLOCK) pre += a.tile_count[t];
+        pre = wave_sum(pre);
+    }
     if (lane == 0) { red[w] = pre; red[RX_WAVES + w] = wcount; }
     __syncthreads();
-    uint32_t base = 0, tcount = 0, before = 0;
+    // many tiles: the base comes from rx_tile_base (the all-predecessor sum grows with tiles^2)
+    uint32_t base = a.base ? a.base[tile] : 0u, tcount = 0, before = 0;
 #pragma unroll
     for (int i = 0; i < RX_WAVES; ++i) {
         base += red[i];
@@ -685,6 +689,29 @@ rx_compact1(Compact1Args a)
             if (pos < a.lane_cap) a.lane_pkt[pos] = wb + s * 64 + lane;
         }
         run += (uint32_t)__popcll(m);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// rx_tile_base: exclusive prefix of the per-tile delivery counts for rx_compact1 when a batch
+// has many tiles (one workgroup: a contiguous block of tiles per thread + a block scan).
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024)
+rx_tile_base(const uint32_t *cnt, uint32_t *base, uint32_t n)
+{
+    __shared__ uint32_t wsum[16];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const uint32_t per = (n + 1023u) / 1024u, b0 = min(n, tid * per), b1 = min(n, b0 + per);
+    uint32_t s = 0;
+    for (uint32_t i = b0; i < b1; ++i) s += cnt[i];
+    const uint32_t incl = wave_incl_scan(s);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t before = incl - s;
+    for (uint32_t i = 0; i < w; ++i) before += wsum[i];
+    for (uint32_t i = b0; i < b1; ++i) {
+        base[i] = before;
+        before += cnt[i];
     }
 }
 

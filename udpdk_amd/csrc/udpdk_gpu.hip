@@ -588,6 +588,15 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
         ca.tile_frames = T;
         ca.n_tiles = tiles;
         ca.lane_cap = o->lane_cap;
+        ca.base = nullptr;
+        if (tiles > COMPACT1_DIRECT_TILES && tiles <= c->partial_cap) {
+            // past a few thousand tiles each workgroup's sum over its predecessors costs more
+            // than one extra launch scanning the counts once
+            hipLaunchKernelGGL(rx_tile_base, dim3(1), dim3(1024), 0, st, (const uint32_t *)P.hist,
+                               P.partial, tiles);
+            HIPC(c, hipGetLastError());
+            ca.base = P.partial;
+        }
         HIPC(c, launch(st, ts, 2, true, true, rx_compact1, dim3(tiles), dim3(RX_BLOCK), 0u, ca));
         return 0;
     }

@@ -158,8 +158,13 @@ class Workload:
         return {raw_port(self.base_port + i): [(0, i, 0)] for i in range(self.n_sockets)}
 
 
+def _nlabel(n: int) -> str:
+    return f"{n >> 20}M" if n % (1 << 20) == 0 else str(n)
+
+
 def config_batch(cfg: int, n: int | None = None, shard: int = 0) -> Workload:
-    """BASELINE.json configs[cfg] (1-based as in BASELINE.md: 1 = CPU pktgen case)."""
+    """BASELINE.json configs[cfg] (1-based as in BASELINE.md: 1 = CPU pktgen case). The workload
+    name carries the frame count (profiles/traffic.json is keyed by it)."""
     if cfg == 1:   # apps/pktgen -s 64: 64 B payload -> 106 B frames, one socket ANY:10001
         n = n or (1 << 20)
         b = build_frames(np.full(n, 106, np.uint32), np.full(n, PORT_RECV, np.uint32), 0x5EED ^ shard)
@@ -167,24 +172,24 @@ def config_batch(cfg: int, n: int | None = None, shard: int = 0) -> Workload:
     if cfg == 2:
         n = n or (1 << 20)
         b = build_frames(np.full(n, 64, np.uint32), np.full(n, PORT_RECV, np.uint32), 0x5EED ^ shard)
-        return Workload("1M-64B-1port", b, 1, PORT_RECV)
+        return Workload(f"{_nlabel(n)}-64B-1port", b, 1, PORT_RECV)
     if cfg == 3:
         n = n or (1 << 20)
         b = build_frames(np.full(n, 1500, np.uint32), np.full(n, PORT_RECV, np.uint32), 0x5EED ^ shard)
-        return Workload("1M-1500B-1port", b, 1, PORT_RECV)
+        return Workload(f"{_nlabel(n)}-1500B-1port", b, 1, PORT_RECV)
     if cfg == 4:
         n = n or (1 << 20)
         rng = np.random.default_rng(4 + shard)
         sizes = IMIX_SIZES[rng.choice(3, size=n, p=IMIX_WEIGHTS / IMIX_WEIGHTS.sum())]
         ports = 10000 + rng.integers(0, 1024, n, dtype=np.uint32)
         b = build_frames(sizes, ports, 0x5EED ^ shard)
-        return Workload("IMIX-1024ports-uniform", b, 1024, 10000)
+        return Workload("IMIX-1024ports-uniform" + ("" if n == 1 << 20 else f"-{_nlabel(n)}"), b, 1024, 10000)
     if cfg == 5:
         n = n or (1 << 22)
         rng = np.random.default_rng(1000 + shard)
         ports = 10000 + zipf_ports(rng, n, 4096)
         b = build_frames(np.full(n, 64, np.uint32), ports, 0x5EED ^ shard)
-        return Workload("4M-64B-4096ports-zipf0.99", b, 4096, 10000)
+        return Workload(f"{_nlabel(n)}-64B-4096ports-zipf0.99", b, 4096, 10000)
     raise ValueError(cfg)
 
 
