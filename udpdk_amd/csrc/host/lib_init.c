@@ -245,7 +245,6 @@ static int h_frag_pass(const uint8_t *frames, uint64_t frames_bytes, const uint3
         if (rc) { errno = -rc; return -1; }
         g_udpdk.frag_ready = 1;
     }
-    uint64_t ncap = g_udpdk.fd_n_cap;
     if (h_grow_dev(&g_udpdk.fd_frames, &g_udpdk.fd_frames_cap, frames_bytes + UDPDK_GPU_FRAMES_TAILROOM)) return -1;
     if (n > g_udpdk.fd_n_cap) {
         uint64_t c0 = 0, c1 = 0, c2 = 0;
@@ -254,7 +253,6 @@ static int h_frag_pass(const uint8_t *frames, uint64_t frames_bytes, const uint3
             return -1;
         g_udpdk.fd_n_cap = n;
     }
-    (void)ncap;
     if ((rc = udpdk_gpu_h2d(g, g_udpdk.fd_frames, frames, frames_bytes)) ||
         (rc = udpdk_gpu_h2d(g, g_udpdk.fd_offset, offset, 4ull * n)) ||
         (rc = udpdk_gpu_h2d(g, g_udpdk.fd_length, length, 2ull * n)) ||
