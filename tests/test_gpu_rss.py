@@ -66,9 +66,12 @@ def test_rss_verification_frames(gpu_ctx):
     assert [int(x) for x in gh] == [int(v["ipv4"], 16) for v in G["ipv4"]]
 
 
-def test_rss_full_size_config5(gpu_ctx):
-    w = F.config_batch(5)                      # 4 M x 64 B over 4096 ports (Zipf)
-    (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, w.batch, abi.rss_conf(8))
+@pytest.mark.parametrize("nq", [8, 64])
+def test_rss_full_size_config5(gpu_ctx, nq):
+    """4 M x 64 B over 4096 ports (Zipf): 8 queues take the one-workgroup base scan (rss_base),
+    64 queues (4096 tiles x 64 entries) the three-pass column scan."""
+    w = F.config_batch(5)
+    (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, w.batch, abi.rss_conf(nq))
     assert np.array_equal(wh, gh) and np.array_equal(wo, go) and np.array_equal(wp, gp)
     assert go[-1] == w.batch.n
 

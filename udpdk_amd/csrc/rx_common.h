@@ -179,6 +179,7 @@ __global__ void rx_counters(const uint32_t *tile_cnt, uint32_t n_tiles, unsigned
 constexpr uint32_t RSS_BLOCK = 256;
 constexpr uint32_t RSS_TILE = 1024;          // frames per workgroup
 constexpr uint32_t RSS_RETA_MAX = 512;
+constexpr uint32_t RSS_BASE_MAX = 32768;    // histogram entries scanned by one rss_base workgroup
 constexpr uint32_t RSS_MAX_QUEUES = 64;
 struct RssArgs {
     const uint8_t  *frames;
@@ -189,7 +190,8 @@ struct RssArgs {
     const uint32_t *ktab;     // [12][256] Toeplitz key windows per input byte (host-built)
     uint32_t *hash;           // [n] mbuf.hash.rss
     uint8_t  *qid;            // [n] queue per frame
-    uint32_t *hist;           // [tiles][n_queues] -> scanned start positions
+    uint32_t *hist;           // queue counts per tile -> scanned start positions; [n_queues][tiles]
+                              // when qmajor (the rss_base scan), else [tiles][n_queues]
     uint32_t *queue_pkt;      // [n] frame indices grouped by queue
     uint64_t frames_bytes;
     uint32_t rsrc_bytes;
@@ -198,9 +200,12 @@ struct RssArgs {
     uint32_t n_queues;        // <= RSS_MAX_QUEUES
     uint32_t q_bits;          // bits of a queue index
     uint32_t hash_types;      // bit 0: IPv4 2-tuple, bit 1: unfragmented IPv4 UDP 4-tuple
+    uint32_t n_tiles;
+    uint32_t qmajor;
 };
 __global__ void rss_hash(RssArgs a);
 __global__ void rss_scatter(RssArgs a);
+__global__ void rss_base(uint32_t *hist, uint32_t n, uint32_t T, uint32_t *queue_off, uint32_t *total);
 
 // RX reassembly (rx_reasm.hip): host-side table object driven by udpdk_gpu_rx_reassemble.
 struct Reasm;

@@ -12,7 +12,7 @@
 // bucket pair (then which flow gets it depends on timing, as it would on arrival order).
 //
 // Launch sequence (udpdk_gpu_rx_reassemble, synchronous):
-//   reasm_collect   FRAG verdicts -> fragment list + (id << 32 | index) sort keys
+//   reasm_collect   FRAG verdicts -> fragment list + (id << ib | index) sort keys
 //   radix sort 1    by (id, index); reasm_keys: src|dst keys in that order; radix sort 2 (stable)
 //   reasm_process   one wave per flow segment: table find (2 x assoc slots scanned by the lanes,
 //                   entry locks), ip_frag_process on lane 0, completion records, store jobs
@@ -49,6 +49,9 @@ constexpr uint32_t RS_VIRTUAL = 0xFFFFFFFEu;    // flow state only in LDS (no ta
 constexpr uint32_t RS_MAX_FRAG = 4;             // RTE_LIBRTE_IP_FRAG_MAX_FRAG
 constexpr uint32_t RS_SPIN = 1u << 20;          // bound on lock spins / find retries
 
+// Bits to hold every value in [0, v]
+inline uint32_t bits_for(uint32_t v) { return v ? 32u - (uint32_t)__builtin_clz(v) : 1u; }
+
 // One table entry (struct ip_frag_pkt) as 20 u32 words, every one accessed with agent-scope
 // relaxed atomics; a wave holding the entry's lock owns the words after E_ID.
 enum : uint32_t {
@@ -76,8 +79,9 @@ struct ReasmArgs {
     const uint16_t *length;
     const uint32_t *meta;
     uint32_t n, rsrc_bytes;
+    uint32_t ib;                       // index bits of the sort-1 key: n - 1 < 2^ib
     uint32_t *frag_list;               // [F] (unordered)
-    unsigned long long *k1;            // [F] id << 32 | index
+    unsigned long long *k1;            // [F] id << ib | index
     const uint32_t *v1s;               // [F] frame indices sorted by (id, index)
     unsigned long long *k2;            // [F] src | dst << 32 in v1s order
     const uint32_t *order;             // [F] frame indices sorted by (src, dst, id, index)
@@ -230,7 +234,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_collect(ReasmArgs a)
             const uint32_t j = s_base + off + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
             const uint32_t id = ld32(fr, a.offset[i] + 16) >> 16;
             a.frag_list[j] = i;
-            a.k1[j] = ((unsigned long long)id << 32) | i;
+            a.k1[j] = ((unsigned long long)id << a.ib) | i;
         }
     }
 }
@@ -811,6 +815,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     a.dv = r->dv;
     a.jobs = r->jobs;
     a.tag_base = 0;
+    a.ib = bits_for(n - 1u);
     RS_HIP(hipMemsetAsync(r->counts, 0, 4 * sizeof(uint32_t), st));
     RS_HIP(hipMemsetAsync(r->stats, 0, UDPDK_RS_N * sizeof(unsigned long long), st));
     RS_HIP(hipMemsetAsync(r->out_bytes, 0, sizeof(unsigned long long), st));
@@ -823,7 +828,8 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     memset(o, 0, sizeof(*o));
     if (F) {
         size_t tb = r->tmp_bytes;
-        RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k1, r->k1s, r->frag_list, r->v1s, (size_t)F, 0, 48, st));
+        RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k1, r->k1s, r->frag_list, r->v1s, (size_t)F, 0,
+                                                  16 + a.ib, st));
         const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((F + RS_BLOCK - 1) / RS_BLOCK, 4096));
         hipLaunchKernelGGL(reasm_keys, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
         RS_HIP(hipGetLastError());
@@ -866,7 +872,9 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         // frame offsets
         const uint32_t gC = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_BLOCK - 1) / RS_BLOCK, 4096));
         size_t tb = r->tmp_bytes;
-        RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->dk, r->dks, r->dv, r->perm, (size_t)F, 0, 32, st));
+        // (origins are < n < 2^bits_for(n); the all-ones keys of positions without one stay last)
+        RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->dk, r->dks, r->dv, r->perm, (size_t)F, 0,
+                                                  bits_for(n), st));
         hipLaunchKernelGGL(reasm_sizes, dim3(gC), dim3(RS_BLOCK), 0, st, (const ReasmDone *)r->done,
                            (const uint32_t *)r->perm, r->sizes, Cn);
         RS_HIP(hipGetLastError());

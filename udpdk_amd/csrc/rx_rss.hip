@@ -59,19 +59,8 @@ __global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
     __shared__ uint16_t reta[RSS_RETA_MAX];
     __shared__ uint32_t hist[RSS_MAX_QUEUES];
     const uint32_t tid = threadIdx.x, lane = __lane_id();
-    // the key-window table (udpdk_gpu_rss_config builds it: tab[p][v] = XOR of the key windows
-    // key bits [8p + j, 8p + j + 32) over the set bits j, MSB first, of byte value v at input
-    // position p), staged with 16-byte loads
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(a.ktab);
-        uint4 *dst = reinterpret_cast<uint4 *>(&tab[0][0]);
-        for (uint32_t e = tid; e < 12u * 256u / 4u; e += RSS_BLOCK) dst[e] = src[e];
-    }
-    for (uint32_t e = tid; e < a.reta_size; e += RSS_BLOCK) reta[e] = a.reta[e];
     const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(a.frames), (short)0, (int)a.rsrc_bytes, 0x00020000);
-    for (uint32_t q = tid; q < a.n_queues; q += RSS_BLOCK) hist[q] = 0;
-    __syncthreads();
     const uint32_t tile = blockIdx.x;
     const uint32_t t0 = tile * RSS_TILE, t1 = min(a.n, t0 + RSS_TILE);
     constexpr uint32_t STEPS = RSS_TILE / RSS_BLOCK;
@@ -83,6 +72,15 @@ __global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
         o[s] = i < t1 ? a.offset[i] : 0u;
         len[s] = i < t1 ? a.length[i] : 0u;
     }
+    // the key-window table (udpdk_gpu_rss_config builds it: tab[p][v] = XOR of the key windows
+    // key bits [8p + j, 8p + j + 32) over the set bits j, MSB first, of byte value v at input
+    // position p): its 16-byte loads go out while the descriptors are in flight, the LDS stores
+    // after the header loads are issued
+    constexpr uint32_t KV = 12u * 256u / 4u / RSS_BLOCK;
+    uint4 kv[KV];
+    const uint4 *ksrc = reinterpret_cast<const uint4 *>(a.ktab);
+#pragma unroll
+    for (uint32_t e = 0; e < KV; ++e) kv[e] = ksrc[e * RSS_BLOCK + tid];
 #pragma unroll
     for (uint32_t s = 0; s < STEPS; ++s) {
         const bool ok = (uint64_t)o[s] + len[s] <= a.frames_bytes && len[s] >= 34u;
@@ -93,6 +91,14 @@ __global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
         dst[s] = ok ? ld32(fr, b0 + 30) : 0u;
         ports[s] = ok && len[s] >= 38u ? ld32(fr, b0 + 34) : 0u;
     }
+    {
+        uint4 *dst = reinterpret_cast<uint4 *>(&tab[0][0]);
+#pragma unroll
+        for (uint32_t e = 0; e < KV; ++e) dst[e * RSS_BLOCK + tid] = kv[e];
+    }
+    for (uint32_t e = tid; e < a.reta_size; e += RSS_BLOCK) reta[e] = a.reta[e];
+    for (uint32_t q = tid; q < a.n_queues; q += RSS_BLOCK) hist[q] = 0;
+    __syncthreads();
 #pragma unroll
     for (uint32_t s = 0; s < STEPS; ++s) {
         const uint32_t i = t0 + s * RSS_BLOCK + (tid & ~63u) + lane;
@@ -125,7 +131,69 @@ __global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
     }
     __syncthreads();
     for (uint32_t q = tid; q < a.n_queues; q += RSS_BLOCK)
-        a.hist[(size_t)tile * a.n_queues + q] = hist[q];
+        a.hist[a.qmajor ? (size_t)q * a.n_tiles + tile : (size_t)tile * a.n_queues + q] = hist[q];
+}
+
+// The scan between rss_hash and rss_scatter for up to RSS_BASE_MAX histogram entries, in one
+// workgroup: rss_hash wrote the histogram queue-major ([n_queues][T]), so an exclusive scan of it
+// as one array turns entry (q, t) into queue q's list start plus the earlier tiles' counts for q,
+// and queue_off[q] is the value at q * T. Thread tid owns entries [32 tid, 32 tid + 32) (eight
+// 16-byte loads, all in flight at once), sums them serially, and one wave scan plus one scan of
+// the 16 wave sums gives its start. (Row-per-wave ownership with a wave scan per row measured
+// 13-16 us: 32 dependent shuffle chains per wave; this form has one.)
+__global__ void __launch_bounds__(1024)
+rss_base(uint32_t *hist, uint32_t n, uint32_t T, uint32_t *queue_off, uint32_t *total)
+{
+    constexpr uint32_t PER = RSS_BASE_MAX / 1024u;
+    __shared__ uint32_t wsum[16];
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+    // range-checked per dword: entries past n read as 0 and are never written
+    const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(hist, (short)0, (int)(4u * n), 0x00020000);
+    const uint32_t k0 = PER * tid;
+    uint32_t v[PER];
+#pragma unroll
+    for (uint32_t i = 0; i < PER / 4u; ++i) {
+        const uint4 q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(hr, (int)(4u * k0 + 16u * i), 0, 0));
+        v[4 * i] = q.x; v[4 * i + 1] = q.y; v[4 * i + 2] = q.z; v[4 * i + 3] = q.w;
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) sum += v[i];
+    uint32_t incl = sum;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += u;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum, grand = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) {
+        run += i < w ? wsum[i] : 0u;
+        grand += wsum[i];
+    }
+    // queue starts: the multiples of T inside this thread's range
+    uint32_t next = k0 < n ? ((k0 + T - 1u) / T) * T : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t i = 0; i < PER; ++i) {
+        if (k0 + i == next) {
+            queue_off[next / T] = run;
+            next += T;
+        }
+        const uint32_t x = v[i];
+        v[i] = run;
+        run += x;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < PER / 4u; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, make_uint4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3])),
+            hr, (int)(4u * k0 + 16u * i), 0, 0);
+    if (tid == 0) {
+        queue_off[n / T] = grand;
+        *total = grand;
+    }
 }
 
 // Per tile: wave w owns frames [t0 + 256 w, t0 + 256 w + 256); its base for queue q is the
@@ -155,7 +223,7 @@ __global__ void __launch_bounds__(RSS_BLOCK) rss_scatter(RssArgs a)
     __syncthreads();
     // running position per queue for this wave (row w of run[] is wave w's alone)
     for (uint32_t q = lane; q < a.n_queues; q += 64) {
-        uint32_t b = a.hist[(size_t)blockIdx.x * a.n_queues + q];
+        uint32_t b = a.hist[a.qmajor ? (size_t)q * a.n_tiles + blockIdx.x : (size_t)blockIdx.x * a.n_queues + q];
         for (uint32_t v = 0; v < w; ++v) b += cnt[v][q];
         run[w][q] = b;
     }

@@ -966,6 +966,8 @@ int udpdk_gpu_rss(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rss_
     a.rsrc_bytes = frames_rsrc_bytes(bt->frames_bytes);
     a.n = bt->n;
     const uint32_t tiles = ceil_div(bt->n, RSS_TILE);
+    a.n_tiles = tiles;
+    a.qmajor = tiles * S <= RSS_BASE_MAX ? 1u : 0u;
     hipLaunchKernelGGL(rss_hash, dim3(tiles), dim3(RSS_BLOCK), 0, st, a);
     HIPC(c, hipGetLastError());
     ScanArgs sa;
@@ -976,8 +978,9 @@ int udpdk_gpu_rss(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rss_
     sa.n_elems = tiles * S;
     sa.n_tiles = tiles;
     sa.n_lanes = S;
-    if (sa.n_elems <= SCAN_SMALL_MAX && tiles <= SCAN_SMALL_TILES) {
-        hipLaunchKernelGGL(rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 4u * S, st, sa);
+    if (a.qmajor) {
+        hipLaunchKernelGGL(rss_base, dim3(1), dim3(1024), 0, st, c->rss_hist, tiles * S, tiles,
+                           o->queue_off_dev, c->rss_total);
     } else {
         const uint32_t nc = ceil_div(tiles, SCAN_COL_CHUNK);
         const dim3 grid(nc, ceil_div(S, (uint32_t)SCAN_BLOCK));
