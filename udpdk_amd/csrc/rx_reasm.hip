@@ -96,7 +96,7 @@ struct ReasmArgs {
     uint32_t mask, assoc, max_dgram, stride;
     unsigned long long max_cycles, tms;
     ReasmDone *done;                   // [F] at the completing fragment's position
-    unsigned long long *dk;            // [F] origin of the completion there, or ~0
+    uint32_t *dk;                      // [F] origin of the completion there, or ~0
     uint32_t *dv;                      // [F] 0..F-1
     ReasmJob *jobs;                    // [F] at the stored fragment's position (frame ~0: none)
     uint32_t tag_base;
@@ -685,7 +685,7 @@ struct Reasm {
     unsigned long long *out_bytes = nullptr;
     ReasmDone *done = nullptr;
     ReasmJob *jobs = nullptr;
-    unsigned long long *dk = nullptr, *dks = nullptr;
+    uint32_t *dk = nullptr, *dks = nullptr;
     uint32_t *dv = nullptr, *perm = nullptr, *sizes = nullptr, *offs = nullptr;
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
@@ -769,15 +769,16 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
         return rc;
     }
     // rocPRIM temporary storage for the largest call (sorts of u64 keys / u32 values, u32 scan)
-    size_t t1 = 0, t2 = 0;
+    size_t t1 = 0, t2 = 0, t3 = 0;
     if ((e = rocprim::radix_sort_pairs(nullptr, t1, r->k1, r->k1s, r->v1s, r->v2s, (size_t)C, 0, 64)) != hipSuccess ||
+        (e = rocprim::radix_sort_pairs(nullptr, t3, r->dk, r->dks, r->v1s, r->v2s, (size_t)C, 0, 32)) != hipSuccess ||
         (e = rocprim::exclusive_scan(nullptr, t2, r->sizes, r->offs, 0u, (size_t)C, rocprim::plus<uint32_t>())) != hipSuccess ||
-        (e = hipMalloc(&r->tmp, std::max<size_t>(std::max(t1, t2), 256))) != hipSuccess) {
+        (e = hipMalloc(&r->tmp, std::max<size_t>(std::max(std::max(t1, t2), t3), 256))) != hipSuccess) {
         fail(e);
         reasm_destroy(r);
         return rc;
     }
-    r->tmp_bytes = std::max<size_t>(std::max(t1, t2), 256);
+    r->tmp_bytes = std::max<size_t>(std::max(std::max(t1, t2), t3), 256);
     *out = r;
     return 0;
 }
@@ -844,7 +845,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         a.s_meta = a.s_sig + F;
         hipLaunchKernelGGL(reasm_prep, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
         RS_HIP(hipGetLastError());
-        RS_HIP(hipMemsetAsync(r->dk, 0xFF, (size_t)F * sizeof(unsigned long long), st));
+        RS_HIP(hipMemsetAsync(r->dk, 0xFF, (size_t)F * sizeof(uint32_t), st));
         RS_HIP(hipMemsetAsync(r->jobs, 0xFF, (size_t)F * sizeof(ReasmJob), st));
         a.tag_base = (r->calls++ & 0x3FFu) << 20;
         const uint32_t waves = (F + 63u) / 64u;
