@@ -84,6 +84,42 @@ def test_tx_random_batch(gpu_ctx):
         assert got == want, f"frame {i} len {lens[i]} off {fo[i]}"
 
 
+@pytest.mark.parametrize("gap", [0, 3])
+def test_tx_small_frames(gpu_ctx, gap):
+    """Waves whose frames are all <= 80 bytes take the lane-per-frame path (tx_small): every
+    payload length 0-38 at odd payload and frame offsets, frames back to back (gap 0: frame ends
+    share 16-byte pieces with the next frame) or with 3 untouched bytes between them; some waves
+    carry one larger frame (the chunk-sweep path) and some lanes an invalid socket (no frame)."""
+    rng = np.random.default_rng(11 + gap)
+    slots = [(0, 10000, 1), (abi.raw_ip("10.1.2.3"), 5353, 1), (abi.raw_ip("10.9.9.9"), 7, 0)]
+    n = 64 * 40 + 17
+    lens = rng.integers(0, 39, n)
+    lens[:39] = np.arange(39)
+    for g in range(0, n // 64, 3):                     # every third wave: one 300-byte frame
+        lens[g * 64 + int(rng.integers(0, 64))] = 300
+    payloads = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
+    sock = rng.integers(0, 3, n)
+    sock[rng.integers(0, n, 20)] = 7                    # out of range: nothing written
+    dip = rng.integers(0, 2**32, n, dtype=np.uint64)
+    dport = rng.integers(0, 65536, n)
+    fo = np.zeros(n, np.uint32)
+    pos = 7
+    for i in range(n):
+        fo[i] = pos
+        pos += int(lens[i]) + 42 + gap
+    cap = pos + 64
+    res = _tx_gpu(gpu_ctx, slots, sock, dip, dport, payloads, fo, cap)
+    want_buf = np.full(cap, 0xEE, np.uint8)
+    for i in range(n):
+        if sock[i] >= len(slots):
+            continue
+        ip, port, bound = slots[sock[i]]
+        want = O.tx_frame(SRC_MAC, DST_MAC, SRC_IP, bound, ip, port, int(dip[i]), int(dport[i]), payloads[i])
+        want_buf[fo[i]:fo[i] + len(want)] = np.frombuffer(want, np.uint8)
+    bad = np.nonzero(res != want_buf)[0]
+    assert bad.size == 0, f"first differing byte {bad[0]} (frame {np.searchsorted(fo, bad[0], 'right') - 1})"
+
+
 def test_tx_golden_vectors(gpu_ctx):
     with open(os.path.join(os.path.dirname(__file__), "golden", "tx_vectors.json")) as f:
         g = json.load(f)

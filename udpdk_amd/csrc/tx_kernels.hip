@@ -88,6 +88,73 @@ __device__ __forceinline__ uint32_t ipv4_cksum_nic(uint32_t raw) { return ~raw &
 constexpr int TX_WIN = 64;  // bytes of header window per frame (16 dwords)
 constexpr int TXW = TX_BLOCK / 64;
 
+constexpr uint32_t TX_SMALL_SPAN = 80;       // frames up to this size take tx_small
+constexpr uint32_t TX_SMALL_LOADS = (TX_SMALL_SPAN - 42u + 15u) / 16u;
+
+// The frame of datagram i built in this lane's registers and stored as 16-byte pieces: for waves
+// whose frames are all <= TX_SMALL_SPAN bytes and unfragmented. The payload loads go out with
+// the slot lookup (byte-aligned 16-byte buffer loads; pieces past the payload are addressed out
+// of range, so they cost no memory access and read as 0), so a wave's frames take one round
+// trip after the descriptors instead of one per 64-chunk sweep step.
+__device__ __forceinline__ void tx_small(const TxArgs &a, uint32_t i, uint32_t fo, uint32_t L,
+                                         uint32_t po, int32_t sock)
+{
+    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.payload), (short)0, (int)a.payload_rsrc, 0x00020000);
+    const __amdgpu_buffer_rsrc_t fw = __builtin_amdgcn_make_buffer_rsrc(
+        a.frames, (short)0, (int)a.frames_bytes, 0x00020000);
+    const uint32_t span = L + 42u;
+    const bool ok = i < a.n && (uint64_t)fo + span <= a.frames_bytes &&
+                    (uint64_t)po + L <= a.payload_bytes && sock >= 0 && (uint32_t)sock < a.n_slots;
+    uint32_t P[4 * TX_SMALL_LOADS + 1];
+#pragma unroll
+    for (uint32_t m = 0; m < TX_SMALL_LOADS; ++m) {
+        const uint32_t off = ok && 16u * m < L ? po + 16u * m : 0x80000000u;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)off, 0, 0);
+        P[4 * m] = v[0]; P[4 * m + 1] = v[1]; P[4 * m + 2] = v[2]; P[4 * m + 3] = v[3];
+    }
+    P[4 * TX_SMALL_LOADS] = 0u;
+    if (!ok) return;
+    const uint4 sl = a.slots[sock];
+    const uint32_t sq = (sl.z && sl.x != 0u) ? sl.x : a.src_ip;                    // :329-334
+    const uint32_t dq = a.dst_ip[i];                                               // :335
+    const uint32_t ptq = (sl.y & 0xFFFFu) | ((uint32_t)a.dst_port[i] << 16);        // :341-342
+    const uint32_t tl = L + 28u, ul = L + 8u;                                      // :336, :344
+    uint32_t H[10];
+    H[0] = a.mac_lo[0]; H[1] = a.mac_lo[1]; H[2] = a.mac_lo[2];                    // :315-317
+    H[3] = 0x00450008u;
+    H[4] = bswap16(tl);
+    H[5] = 0x11400000u;
+    H[6] = ipv4_cksum(ipv4_raw(tl, 0u, sq, dq)) | ((sq & 0xFFFFu) << 16);          // :337
+    H[7] = (sq >> 16) | ((dq & 0xFFFFu) << 16);
+    H[8] = (dq >> 16) | ((ptq & 0xFFFFu) << 16);
+    H[9] = (ptq >> 16) | (bswap16(ul) << 16);
+    // frame dword d: the header for d < 10; then frame byte 42 + t = payload byte t, so dword
+    // d >= 10 = payload bytes [4d - 42, 4d - 38) (bytes 40-41: UDP checksum 0)
+    auto F = [&](uint32_t d) -> uint32_t {
+        return d < 10u ? H[d] : (d == 10u ? P[0] << 16 : __builtin_amdgcn_alignbyte(P[d - 10u], P[d - 11u], 2));
+    };
+    // whole 16-byte pieces, then the frame's last 0-15 bytes as dword / byte stores
+#pragma unroll
+    for (uint32_t c = 0; c < TX_SMALL_SPAN / 16; ++c) {
+        if (16u * c + 16u <= span) {
+            const __attribute__((ext_vector_type(4))) uint32_t v = {F(4 * c), F(4 * c + 1), F(4 * c + 2), F(4 * c + 3)};
+            __builtin_amdgcn_raw_buffer_store_b128(v, fw, (int)(fo + 16u * c), 0, 0);
+        } else if (16u * c < span) {
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t) {
+                const uint32_t b = 16u * c + 4u * t;
+                if (b + 4u <= span) {
+                    __builtin_amdgcn_raw_buffer_store_b32(F(4 * c + t), fw, (int)(fo + b), 0, 0);
+                } else if (b < span) {
+                    for (uint32_t k = 0; b + k < span; ++k)
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(F(4 * c + t) >> (8 * k)), fw, (int)(fo + b + k), 0, 0);
+                }
+            }
+        }
+    }
+}
+
 } // namespace
 
 __global__ void __launch_bounds__(TX_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8)))
@@ -106,11 +173,19 @@ tx_build(TxArgs a)
     for (uint32_t g = blockIdx.x * TXW + w; g * 64 < a.n; g += waves_total) {
         const uint32_t i = g * 64 + lane;
         uint32_t nf = 0, fo = 0, L = 0, po = 0, src = 0, dst = 0, pt = 0;
+        int32_t sock = -1;
         if (i < a.n) {
             fo = a.frame_off[i];
             L = a.payload_len[i];
             po = a.payload_off[i];
-            const int32_t sock = a.sockfd[i];
+            sock = a.sockfd[i];
+        }
+        // a wave of small unfragmented frames: one lane builds and stores its own frame
+        if (!__ballot(i < a.n && (L + 42u > TX_SMALL_SPAN || (a.mtu && L + 42u > a.mtu)))) {
+            tx_small(a, i, fo, L, po, sock);
+            continue;
+        }
+        if (i < a.n) {
             const bool frag = a.mtu && L + 42u > a.mtu;                    // poller.c:466
             const uint32_t n_fr = frag ? (L + 8u + fpl - 1u) / fpl : 1u;
             const uint32_t span = frag ? L + 8u + 34u * n_fr : L + 42u;
