@@ -33,6 +33,16 @@ __global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
         const uint32_t o = a.offset[i];
         const uint32_t len = a.length[i];
         const auto h = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)(o + 26u), 0, 0);  // bytes 26..41
+        // a short frame's first 64 payload bytes go out with the header load (the frame length
+        // bounds them; pieces past it are addressed out of range: no memory access)
+        const uint32_t fseg = len >= 42u ? len - 42u : 0u;
+        uint4 v0[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            const uint32_t off = valid && fseg <= 64u && 16u * u < fseg ? o + 42u + 16u * u : 0x80000000u;
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)off, 0, 0);
+            v0[u] = make_uint4(x[0], x[1], x[2], x[3]);
+        }
         const uint32_t dlr = h[3] & 0xFFFFu;                                           // dgram_len, BE
         const uint32_t dl = ((dlr & 0xFFu) << 8) | (dlr >> 8);
         const uint32_t pl = (dl - 8u) & 0xFFFFu;                 // uint16_t dgram_payl_len (:436)
@@ -49,10 +59,15 @@ __global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
             uint8_t *dst = a.payload + (size_t)k * a.slot_bytes;
             for (uint32_t c = 0; c < n; c += 64u) {
                 uint4 v[4];
+                if (c == 0u && fseg <= 64u) {
 #pragma unroll
-                for (uint32_t u = 0; u < 4; ++u) {
-                    const auto x = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)(o + 42u + c + 16u * u), 0, 0);
-                    v[u] = make_uint4(x[0], x[1], x[2], x[3]);
+                    for (uint32_t u = 0; u < 4; ++u) v[u] = v0[u];
+                } else {
+#pragma unroll
+                    for (uint32_t u = 0; u < 4; ++u) {
+                        const auto x = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)(o + 42u + c + 16u * u), 0, 0);
+                        v[u] = make_uint4(x[0], x[1], x[2], x[3]);
+                    }
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < 4; ++u)
