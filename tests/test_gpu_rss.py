@@ -99,3 +99,14 @@ def test_rss_edges(gpu_ctx):
     b = F.mixed_batch(1, 1, [10001], [9], ["172.31.100.1"])
     (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, b, abi.rss_conf(3))
     assert np.array_equal(wh, gh) and np.array_equal(wo, go) and np.array_equal(wp, gp)
+
+
+def test_rss_repeats_of_different_sizes(gpu_ctx):
+    """Calls of different sizes and queue counts alternate on one context (per-call histogram
+    and list state): 1 M frames (4096 ports, Zipf) over 8 and 16 queues and a small mixed batch."""
+    w = F.config_batch(5, n=1 << 20)
+    small = F.mixed_batch(11, 3000, [10001, 10002, 10004], [9, 20000], ["172.31.100.1"])
+    for b, nq in ((w.batch, 8), (small, 8), (w.batch, 16), (w.batch, 8), (small, 3), (w.batch, 8)):
+        (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, b, abi.rss_conf(nq))
+        assert np.array_equal(wh, gh) and np.array_equal(wo, go) and np.array_equal(wp, gp)
+        assert go[-1] == b.n
