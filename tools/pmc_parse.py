@@ -28,7 +28,7 @@ for cfg in (1, 2, 3, 4, 5):
         vals[ctr] = {k: sum(v) / len(v) for k, v in agg.items()}
     if len(vals) < 2:
         continue
-    name = F.config_batch(cfg, n=1).name
+    name = F.config_batch(cfg).name     # the bench workload (its default frame count)
     kern = {}
     for k in vals["FETCH_SIZE"]:
         if not k.startswith("udpdk::"):
