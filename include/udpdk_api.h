@@ -2,7 +2,8 @@
  * udpdk_api.h — POSIX-like UDP socket surface, source compatible with the reference's
  * udpdk/udpdk_api.h:19-41 (same ten functions, same argument meaning, -1 + errno on error) plus
  * udpdk_dump_payload (udpdk_api.symlist:11). Applications written against the reference
- * (apps/pktgen, apps/pingpong) compile against this header unchanged.
+ * (apps/pktgen, apps/pingpong) compile against this header and link against libudpdk_amd.so
+ * unchanged (tests/test_ref_apps.py builds both from /root/reference in place).
  *
  * What changed underneath: there is no forked DPDK poller. The per-packet RX work of
  * udpdk_poller.c runs as HIP kernels on an MI355X through udpdk_gpu.h; udpdk_init() creates the
@@ -17,7 +18,12 @@
 #ifndef UDPDK_API_H
 #define UDPDK_API_H
 
+/* What the reference header supplied to applications transitively through udpdk_types.h:19-23
+ * (apps/pktgen/main.c:54-58 uses bool without including <stdbool.h> itself). */
+#include <netinet/in.h>
+#include <stdbool.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <sys/socket.h>
 #include <sys/types.h>
 #include <unistd.h>
