@@ -4,9 +4,14 @@ A step = one udpdk_gpu_rx call over one batch of frames already resident in HBM 
 batches: rx_classify + rx_compact1; otherwise rx_classify + rx_scan + rx_scatter). The timed
 region's GPU time comes from two events on the library stream around all K steps; per-kernel
 durations from events carried by the kernel dispatches themselves (hipExtLaunchKernelGGL), so
-they agree with rocprofv3's kernel trace. Default workload = BASELINE.json configs[1]: 1 M synthetic 64 B
-Eth/IPv4/UDP frames, 1 bound port, per GPU. With N GPUs (torchrun) every rank processes its own
-independent shard (seed 0x5EED ^ rank) with no data-path collective: weak scaling.
+they agree with rocprofv3's kernel trace. Default workload at N = 1: BASELINE.json configs[1], 1 M synthetic 64 B Eth/IPv4/UDP frames, 1 bound
+port. At N > 1 the default is the scaling workload BASELINE.json configs[4] (config 5): every rank
+processes its own independent 4 M x 64 B shard over 4096 ports, Zipf-0.99 (ports seeded 1000 +
+rank, frames 0x5EED ^ rank) with no data-path collective: weak scaling.
+
+`--gpus N` is honoured two ways: under torchrun (WORLD_SIZE set) it must equal WORLD_SIZE; run
+directly with N > 1, bench.py spawns N worker processes itself (one per GPU, gloo rendezvous on
+127.0.0.1) before anything touches HIP, and prints rank 0's line.
 
 To keep the 256 MiB Infinity Cache from serving the 64 B batch (≈80 MB) out of cache, the timed
 loop rotates over enough device copies of the batch that a copy is evicted before its reuse
@@ -36,10 +41,12 @@ HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak, MI355X_MICROARCH.md chip table
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (one process each); default WORLD_SIZE, else 1")
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--config", type=int, default=2, help="BASELINE.json config number (2..5)")
+    p.add_argument("--config", type=int, default=None,
+                   help="BASELINE.json config number (1..5); default 2 at N = 1, 5 at N > 1")
     p.add_argument("--frames", type=int, default=None, help="override frames per GPU")
     p.add_argument("--strong-total", type=int, default=None,
                    help="strong scaling: this many frames in total, split into contiguous equal "
@@ -52,7 +59,32 @@ def parse():
                    help="udpdk_gpu_pipeline_depth: d > 1 overlaps consecutive batches on d streams")
     p.add_argument("--timing-every", type=int, default=16,
                    help="per-kernel timing on every Nth call (dispatch-carried events)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="no GPU: rendezvous, build each rank's workload, print the plan line")
     return p.parse_args()
+
+
+def spawn_workers(n: int) -> int:
+    """`bench.py --gpus N` without torchrun: start N copies of this script as ranks 0..N-1
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), each on GPU
+    LOCAL_RANK. Called before any HIP call in this process, which never touches the GPU. Rank
+    0's stdout (the JSON line) is passed through; the exit code is the first failing rank's."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].communicate()[0]
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    sys.stdout.write(out.decode())
+    sys.stdout.flush()
+    return next((rc for rc in rcs if rc), 0)
 
 
 class Rx:
@@ -173,31 +205,78 @@ def _digest(*arrays) -> str:
     return h.hexdigest()
 
 
-def cpu_baseline(w: F.Workload, target_s: float, gpu_out=None):
-    """Oracle (the C restatement, kind "port") on the host cores: 1 thread and min(nproc, 16)
-    threads, one independent shard per pinned thread, with the RX checksum verification. With
-    gpu_out = (meta, lane_off, lane_pkt) of the measured batch, the same leg also runs the
-    restatement once on that batch and compares 64-bit digests of the outputs (SURVEY.md §8(d)
-    "parity mode")."""
+def host_cores() -> int:
+    """CPUs this process may run on (its affinity mask): all online cores unless the host
+    partitions them; the count the CPU baseline's "cores" states."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def oracle_digest(w: F.Workload):
+    """64-bit digest of the oracle's verdict words and lanes for workload w (parity mode,
+    SURVEY.md §8(d)); compared with the digest of the GPU outputs of the same batch."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    b = w.batch
+    wm, wl, wp, _ = O.rx(O.bindtable_from_lists(w.port_lists()), b.frames, b.frames_bytes, b.offset,
+                         b.length, None, w.n_sockets)
+    return _digest(wm, wl, wp)
+
+
+def gpu_digest(ctx, out, n: int, n_lanes: int):
+    meta = ctx.download(out.meta, np.uint32, n)
+    loff = ctx.download(out.lane_off, np.uint32, n_lanes + 1)
+    pkt = ctx.download(out.lane_pkt, np.uint32, int(loff[-1]))
+    return _digest(meta, loff, pkt)
+
+
+def cpu_baseline(w: F.Workload, target_s: float, gpu_dig: str | None = None):
+    """Oracle (the C restatement, kind "port") on the host cores, one independent shard per
+    pinned thread, with the RX checksum verification: 1 thread, 16 threads (the per-GPU CPU
+    share of the box) and every core the process may run on (`host_cores()`, nproc unless the
+    host partitions it). With gpu_dig (digest of the GPU outputs of the measured batch) the leg
+    also runs the restatement once on that batch and compares digests (SURVEY.md §8(d) "parity
+    mode")."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     b = w.batch
     bt = O.bindtable_from_lists(w.port_lists())
     parity = None
-    if gpu_out is not None:
-        wm, wl, wp, _ = O.rx(bt, b.frames, b.frames_bytes, b.offset, b.length, None, w.n_sockets)
-        parity = {"oracle": _digest(wm, wl, wp), "gpu": _digest(*gpu_out)}
+    if gpu_dig is not None:
+        parity = {"oracle": oracle_digest(w), "gpu": gpu_dig}
         parity["match"] = parity["oracle"] == parity["gpu"]
     res = {"parity": parity}
-    threads_all = max(1, min(os.cpu_count() or 1, 16))
-    for th in sorted({1, threads_all}):
-        for csum in (True, False):
-            # calibrate reps so each leg takes ~target_s
-            t1 = O.rx_parallel(bt, b.frames, b.frames_bytes, b.offset, b.length, w.n_sockets, csum, th, 1)
-            reps = max(1, int(target_s / max(t1, 1e-6)))
+    cores = host_cores()
+    legs = [(1, True), (1, False), (min(16, cores), True), (cores, True), (cores, False)]
+    for th, csum in dict.fromkeys(legs):
+        # calibrate reps so the timed leg takes ~target_s: grow the pass count until a run
+        # lasts >= 0.2 s (a single pass of many threads is dominated by starting them)
+        reps, secs = 1, 0.0
+        while True:
             secs = O.rx_parallel(bt, b.frames, b.frames_bytes, b.offset, b.length, w.n_sockets, csum, th, reps)
-            res[(th, csum)] = (b.n * reps / secs / 1e6, reps, secs)
-    return res, threads_all
+            if secs >= 0.2 or reps >= 1 << 20:
+                break
+            reps *= 4
+        reps = max(1, int(reps * target_s / max(secs, 1e-6)))
+        secs = O.rx_parallel(bt, b.frames, b.frames_bytes, b.offset, b.length, w.n_sockets, csum, th, reps)
+        res[(th, csum)] = (b.n * reps / secs / 1e6, reps, secs)
+    return res, cores
+
+
+def config1_line(target_s: float):
+    """BASELINE.json configs[0]: apps/pktgen's traffic (64 B UDP payload = 106 B frames,
+    apps/pktgen/main.c:53,156; one socket bound ANY:10001, main.c:183-191) through the CPU poller
+    path, here the C restatement of reassemble() + flush_rx_queue (the reference needs DPDK,
+    absent), on 1 thread and on every host core."""
+    w = F.config_batch(1)
+    res, cores = cpu_baseline(w, target_s)
+    return {"workload": w.name, "kind": "port",
+            "one_thread_mpkt_s": round(res[(1, True)][0], 2),
+            "one_thread_no_csum_mpkt_s": round(res[(1, False)][0], 2),
+            "all_cores_mpkt_s": round(res[(cores, True)][0], 2), "cores": cores,
+            "gbps_all_cores": round(res[(cores, True)][0] * 106 / 1e3, 2)}
 
 
 def side_config(ctx, cfg: int, steps: int, rotate: int):
@@ -208,13 +287,18 @@ def side_config(ctx, cfg: int, steps: int, rotate: int):
     ctx.pipeline(1)
     wall1, gpu_step1, kt, _ = time_loop(rx, steps, 5, lambda: None, 4)
     cls_gbps = rx.classify_bytes() / (kt.get("rx_classify", 1e3 * gpu_step1) / 1e6) / 1e9
+    a0 = rx.args[0]
+    dg = gpu_digest(ctx, a0[5], rx.n, w.n_sockets)
+    od = oracle_digest(w)
     out = {"workload": w.name, "mpkt_s": round(rx.n * steps / wall / 1e6, 1),
            "gbps_pipeline": round(rx.pipeline_bytes() * steps / wall / 1e9, 1),
            "gpu_us_per_step": round(1e3 * gpu_step, 2),
            "depth1_mpkt_s": round(rx.n * steps / wall1 / 1e6, 1),
            "kernel_us": {k: round(v, 2) for k, v in kt.items()},
            "classify_gbps": round(cls_gbps, 1),
-           "frac_hbm_classify": round(cls_gbps / HBM_PEAK_GBS, 4)}
+           "frac_hbm_classify": round(cls_gbps / HBM_PEAK_GBS, 4),
+           "frac_hbm_pipeline": round(rx.pipeline_bytes() * steps / wall / 1e9 / HBM_PEAK_GBS, 4),
+           "parity": {"gpu": dg, "oracle": od, "match": dg == od}}
     for a in rx.args:
         a[4].frames.free(); a[4].offset.free(); a[4].length.free()
         a[5].meta.free(); a[5].lane_off.free(); a[5].lane_pkt.free()
@@ -464,14 +548,32 @@ def end_to_end(ctx, cfg: int, reps: int):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        raise SystemExit(spawn_workers(args.gpus))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config is None:
+        args.config = 2 if world == 1 else 5
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # gloo prints its connection notice on stdout: keep stdout for the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(os.open(os.devnull, os.O_WRONLY), 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     import torch
+    if args.dry_run:
+        return dry_run(args, world, rank, dist)
 
     def barrier():
         if dist is not None:
@@ -505,14 +607,23 @@ def main():
     ctx.sync()
     single_us = 1e3 * ev1.elapsed_ms()
     ev1.close()
+    cls_bytes = rx.classify_bytes()
+    mine = {"rank": rank, "device": device, "frames": rx.n,
+            "mpkt_s": round(rx.n * args.steps / wall / 1e6, 2),
+            "gbps": round(rx.pipeline_bytes() * args.steps / wall / 1e9, 1),
+            "classify_us": round(kt.get("rx_classify", 0.0), 3),
+            "classify_gbps": round(cls_bytes / kt["rx_classify"] / 1e3, 1) if kt.get("rx_classify") else None,
+            "kernel_us": {k: round(v, 3) for k, v in kt.items()}}
+    per_rank = [mine]
     if dist is not None:
         t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     total_pkts = rx.n * args.steps * world
     mpkt_s = total_pkts / wall / 1e6
     ms_step = 1e3 * wall / args.steps
-    cls_bytes = rx.classify_bytes()
     cls_us = kt.get("rx_classify", 1e3 * gpu_step1)    # timing off: the whole step, an upper bound
     achieved = cls_bytes / (cls_us / 1e6) / 1e9
 
@@ -556,30 +667,30 @@ def main():
                      "algorithmic_bytes_per_launch": cls_bytes},
         "cpu_baseline": None,
     }
+    if world > 1:
+        line["per_rank"] = per_rank
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        gpu_out = None
-        if rx.n <= (1 << 20):            # the measured batch itself: digest of its outputs
-            a0 = rx.args[0]
-            out = a0[5]
-            gpu_out = (ctx.download(out.meta, np.uint32, rx.n),
-                       ctx.download(out.lane_off, np.uint32, rx.w.n_sockets + 1),
-                       None)
-            gpu_out = (gpu_out[0], gpu_out[1], ctx.download(out.lane_pkt, np.uint32, int(gpu_out[1][-1])))
-        res, thr = cpu_baseline(F.config_batch(args.config, n=min(rx.n, 1 << 20)), args.cpu_seconds,
-                                gpu_out)
-        v, reps, secs = res[(thr, True)]
+        gdig = gpu_digest(ctx, rx.args[0][5], rx.n, w.n_sockets) if rx.n <= (1 << 22) else None
+        res, cores = cpu_baseline(w, args.cpu_seconds, gdig)
+        v, reps, secs = res[(cores, True)]
         line["cpu_baseline"] = {
-            "value": round(v, 2), "unit": "Mpkt/s", "cores": thr, "kind": "port",
-            "sample": f"{min(rx.n, 1 << 20)} frames of {w.name} x {reps} passes, {thr} pinned "
-                      f"threads (one shard each), RX checksum verification on",
+            "value": round(v, 2), "unit": "Mpkt/s", "cores": cores, "kind": "port",
+            "sample": f"{rx.n} frames of {w.name} x {reps} passes ({secs:.1f} s), {cores} pinned "
+                      f"threads = every host core this process may use (one shard each), RX "
+                      f"checksum verification on",
             "one_thread": round(res[(1, True)][0], 2),
             "one_thread_no_csum": round(res[(1, False)][0], 2),
-            f"{thr}_threads_no_csum": round(res[(thr, False)][0], 2),
+            f"{min(16, cores)}_threads": round(res[(min(16, cores), True)][0], 2),
+            f"{cores}_threads_no_csum": round(res[(cores, False)][0], 2),
             "parity": res["parity"],
         }
+        try:
+            line["config1_cpu"] = config1_line(args.cpu_seconds / 2)
+        except Exception as e:
+            line["config1_cpu"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_extra:
         extra = []
-        for cfg in (3, 4, 5):
+        for cfg in (1, 3, 4, 5):
             if cfg != args.config:
                 try:
                     extra.append(side_config(ctx, cfg, max(10, args.steps // 4), args.rotate_mib << 20))
@@ -630,6 +741,35 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def dry_run(args, world, rank, dist):
+    """The multi-rank plumbing without a GPU: each rank builds its shard of the workload (small
+    --frames keeps it quick), the ranks rendezvous, and rank 0 prints what every rank would
+    measure (workload, frames, seeds) plus the barrier/max-over-ranks reduction of a dummy
+    wall time."""
+    frames = args.frames
+    if args.strong_total:
+        frames = -(-args.strong_total // world)
+    w = F.config_batch(args.config, n=frames, shard=rank)
+    mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "workload": w.name,
+            "frames": w.batch.n, "digest": _digest(w.batch.frames[:w.batch.frames_bytes], w.batch.length)}
+    per_rank = [mine]
+    wall = 1.0 + rank
+    if dist is not None:
+        import torch
+        dist.barrier()
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "baseline_config": args.config,
+                          "scaling": "strong" if args.strong_total else "weak",
+                          "max_wall": wall, "per_rank": per_rank}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

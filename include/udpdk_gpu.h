@@ -200,7 +200,14 @@ typedef struct {
 
 /* Enqueue the RX pipeline for one batch on the context stream (async): rx_classify, then either
  * rx_compact1 (one lane and no fan-out in the snapshot) or rx_scan + rx_scatter. meta, lane_off
- * and lane_pkt are complete when the stream reaches the end of the sequence. */
+ * and lane_pkt are complete when the stream reaches the end of the sequence.
+ *
+ * Tailroom contract: batch->frames_dev must be readable for frames_bytes +
+ * UDPDK_GPU_FRAMES_TAILROOM bytes. The kernels read frame bytes with byte-aligned dword loads
+ * that are range-checked against frames_bytes rounded up to a dword, so the last frame of a batch
+ * whose frames_bytes % 4 != 0 may be read up to 3 bytes past frames_bytes (never used in a
+ * result). The library cannot check the allocation size behind a device pointer: a buffer that
+ * ends exactly at frames_bytes may fault (tests/test_gpu_rx.py::test_tailroom_exact_allocation). */
 int udpdk_gpu_rx(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch, const udpdk_rx_out_t *out);
 /* Pipelining: with depth d in 2..4, consecutive udpdk_gpu_rx calls rotate over d internal
  * streams with their own workspaces, so one batch's launch, prologue and compaction overlap the

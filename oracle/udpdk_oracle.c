@@ -425,7 +425,13 @@ double oracle_rx_parallel(const oracle_btable *bt, const uint8_t *frames, uint64
     pthread_t *th = calloc((size_t)nthreads, sizeof(*th));
     pthread_barrier_t bar;
     pthread_barrier_init(&bar, NULL, (unsigned)nthreads + 1);
-    int ncpu = (int)sysconf(_SC_NPROCESSORS_ONLN);
+    /* thread t pinned to the t-th CPU this process may run on (its affinity mask: on a
+     * partitioned host that is the share the process was given, not every online CPU) */
+    int cpus[CPU_SETSIZE], ncpu = 0;
+    cpu_set_t allowed;
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0)
+        for (int c = 0; c < CPU_SETSIZE; c++)
+            if (CPU_ISSET(c, &allowed)) cpus[ncpu++] = c;
     double secs = -1.0;
     uint32_t per = (n + (uint32_t)nthreads - 1) / (uint32_t)nthreads;
     for (int t = 0; t < nthreads; t++) {
@@ -435,7 +441,7 @@ double oracle_rx_parallel(const oracle_btable *bt, const uint8_t *frames, uint64
         j->bt = bt; j->frames = frames; j->frames_bytes = frames_bytes;
         j->offset = offset + a; j->length = length + a; j->n = b - a;
         j->lane_mask = lane_mask; j->n_lanes = n_lanes; j->do_csum = do_csum; j->reps = reps;
-        j->cpu = ncpu > 0 ? t % ncpu : 0;
+        j->cpu = ncpu > 0 ? cpus[t % ncpu] : 0;
         j->meta = malloc(((size_t)j->n + 1) * 4);
         j->lane_off = malloc(((size_t)n_lanes + 1) * 4);
         j->lane_pkt = malloc(((size_t)j->n * 8u + 64u) * 4);

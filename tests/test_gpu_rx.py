@@ -287,3 +287,71 @@ def test_single_lane_many_tiles():
     for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt):
         x.free()
     ctx.close()
+
+
+@pytest.mark.parametrize("tail", [1, 2, 3])
+def test_tailroom_exact_allocation(gpu_ctx, tail):
+    """The tailroom contract at its edge: frames_bytes % 4 == tail, the device allocation is
+    exactly frames_bytes + UDPDK_GPU_FRAMES_TAILROOM, and the batch's last frame ends exactly at
+    frames_bytes (its UDP checksum covers the last byte). Round 1 faulted on a buffer loaded 16 B
+    past an exactly-sized allocation; this pins the fixed range."""
+    import ctypes as C
+    lists = {abi.raw_port(F.PORT_RECV): [(0, 0, 0)]}
+    sizes = np.array([64, 1500, 97, 333, 60 + tail + 4 * 7], np.uint32)
+    sizes[-1] += (tail - int(sizes.sum()) % 4) % 4          # frames_bytes % 4 == tail
+    b = F.build_frames(sizes, np.full(len(sizes), F.PORT_RECV, np.uint32), 77 + tail)
+    fb = int(b.length.astype(np.int64).sum())
+    assert fb % 4 == tail and int(b.offset[-1]) + int(b.length[-1]) == fb
+    gpu_ctx.upload_snapshot(abi.snapshot_from_lists(lists, 1))
+    exact = gpu_ctx.alloc(fb + abi.FRAMES_TAILROOM)           # exactly the contract, no slack
+    abi._check(abi.lib().udpdk_gpu_h2d(gpu_ctx.handle, C.c_void_p(exact.ptr),
+                                       b.frames.ctypes.data_as(C.c_void_p), fb), "h2d")
+    gpu_ctx.sync()
+    db = abi.RxDeviceBatch(exact, fb, gpu_ctx.upload(b.offset.astype(np.uint32)),
+                           gpu_ctx.upload(b.length.astype(np.uint16)), None, b.n)
+    out = abi.rx_alloc_out(gpu_ctx, b.n, 1, b.n)
+    got = abi.rx_run(gpu_ctx, db, out)
+    want = O.rx(O.bindtable_from_lists(lists), b.frames, fb, b.offset, b.length, None, 1)
+    _assert_same(want, got, f"tail={tail}")
+    assert np.all(abi.meta_udp(got[0]) == abi.UDP_OK)
+    for x in (exact, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt):
+        x.free()
+
+
+def test_config4_full_size(gpu_ctx):
+    """BASELINE.json configs[3] at its full size: 1 M IMIX frames over 1024 ports, exact against
+    the oracle (verdict words, lanes, counters), plus lane stability."""
+    w = F.config_batch(4)
+    want, got = _rx_both(gpu_ctx, w.batch, w.port_lists(), w.n_sockets)
+    _assert_same(want, got, w.name)
+    loff, pkt = got[1].astype(np.int64), got[2].astype(np.int64)
+    assert int(loff[-1]) == w.batch.n
+    d = np.diff(pkt)
+    inner = np.ones(len(d), bool)
+    inner[loff[1:-1][loff[1:-1] > 0] - 1] = False            # lane boundaries may step down
+    assert np.all(d[inner] > 0)
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_sharded_hip_merge(gpu_ctx, shards):
+    """SURVEY.md §8(e) through the HIP path: config 5's Zipf-0.99 batch over 4096 ports cut into
+    contiguous shards, each shard a separate udpdk_gpu_rx call (on device 0, as one rank per GPU
+    would run it), merged with shard.merge_lanes; equal to the single-batch HIP result and to the
+    oracle."""
+    from udpdk_amd import shard as S
+    w = F.config_batch(5, n=1 << 20)
+    b = w.batch
+    want, got = _rx_both(gpu_ctx, b, w.port_lists(), w.n_sockets)
+    _assert_same(want, got, "single batch")
+    parts, metas = [], []
+    for r in range(shards):
+        a, e = S.shard_range(b.n, shards, r)
+        sb = F.Batch(b.frames, b.offset[a:e].copy(), b.length[a:e].copy(), b.frames_bytes, None)
+        _, sg = _rx_both(gpu_ctx, sb, w.port_lists(), w.n_sockets)
+        assert sg[4] == 0
+        parts.append((sg[1], sg[2], a))
+        metas.append(sg[0])
+    goff, gpkt = S.merge_lanes(parts, w.n_sockets)
+    assert np.array_equal(np.concatenate(metas), got[0])
+    assert np.array_equal(goff, got[1]) and np.array_equal(gpkt, got[2])
+    assert np.array_equal(goff, want[1]) and np.array_equal(gpkt, want[2])
