@@ -82,14 +82,24 @@ struct ScanArgs {
     uint32_t *partial;
     uint32_t *lane_off;
     uint32_t *total;
+    uint32_t *tot;        // rx_scan_cols: [n_lanes] lane totals
     uint32_t n_elems;
     uint32_t n_tiles;
     uint32_t n_lanes;
 };
 
+// rx_scan_cols: one launch, workgroup = a block of 2^lb lanes x every tile; each thread keeps up
+// to SCAN_COLS_TPT tiles of one lane in registers, so tiles <= SCAN_COLS_TPT * (256 >> lb).
+constexpr int SCAN_COLS_BLOCK = 256;
+constexpr uint32_t SCAN_COLS_TPT = 64;
+constexpr uint32_t SCAN_COLS_MAX_TILES = SCAN_COLS_TPT * SCAN_COLS_BLOCK;
+
 struct ScatterArgs {
     const uint32_t *meta;
-    const uint32_t *base;  // scanned hist
+    const uint32_t *base;  // scanned hist: per-lane exclusive prefix over the earlier tiles
+    const uint32_t *tot;   // lane totals (rx_scan_cols); null: base already includes lane_off
+    uint32_t *lane_off;    // written by the workgroup of tile 0 when tot is given
+    uint32_t *total;
     const uint8_t  *frames;
     const uint32_t *offset;
     const uint4    *port_tab;
@@ -102,6 +112,7 @@ struct ScatterArgs {
     uint32_t lane_mask;
     uint32_t key_bits;
     uint32_t lane_cap;
+    unsigned long long *dbg;   // diagnostic stamps (UDPDK_STAMPS builds), may be null
 };
 
 // Single-lane compaction (rx_compact1): lane_pkt = indices of delivered frames in frame order,
@@ -160,7 +171,7 @@ struct GatherArgs {
 
 __global__ void rx_classify(RxArgs a);
 __global__ void rx_gather(GatherArgs a);
-__global__ void rx_scan_small(ScanArgs a);
+__global__ void rx_scan_cols(ScanArgs a, uint32_t lb);
 __global__ void rx_scan_reduce(ScanArgs a);
 __global__ void rx_scan_top(ScanArgs a, uint32_t n_part);
 __global__ void rx_scan_down(ScanArgs a);
@@ -170,7 +181,15 @@ constexpr uint32_t SCATTER_WAVES = 8;           // rx_scatterw workgroup: 8 wave
 constexpr uint32_t SCATTERW_MAX_LANES = 4096;   // rx_scatterw LDS: (4 + 2 x 8) x lanes bytes
 __host__ __device__ constexpr uint32_t scatterw_lds_bytes(uint32_t n_lanes)
 {
-    return 4u * n_lanes + 2u * SCATTER_WAVES * n_lanes;
+    // cursors + per-wave slice offsets (u16), which double as the prologue's S + 16 words of
+    // scratch: 80 KiB at 4096 lanes, so two workgroups share a CU's 160 KiB
+    return 4u * n_lanes + (2u * SCATTER_WAVES * n_lanes > 4u * n_lanes + 64u
+                           ? 2u * SCATTER_WAVES * n_lanes : 4u * n_lanes + 64u);
+}
+constexpr int SCATTER1_BLOCK = 256;             // rx_scatter: prologue by 4 waves, walk by wave 0
+__host__ __device__ constexpr uint32_t scatter1_lds_bytes(uint32_t n_lanes)
+{
+    return 8u * n_lanes + 64u;                  // cursors + the base row staged for the prologue
 }
 __global__ void rx_compact1(Compact1Args a);
 __global__ void rx_tile_base(const uint32_t *cnt, uint32_t *base, uint32_t n);

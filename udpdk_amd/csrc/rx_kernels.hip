@@ -770,27 +770,45 @@ __device__ void scan_lane_totals(const uint32_t *tot, uint32_t n_lanes, uint32_t
     if (tid == 0) { lane_off[n_lanes] = total; *total_out = total; }
 }
 
-__global__ void __launch_bounds__(SCAN_BLOCK)
-rx_scan_small(ScanArgs a)
+// rx_scan_cols: the whole column scan in one launch. Workgroup = a block of LB = 2^lb lanes
+// and every tile; thread (c, l) holds lane l's counts of the c-th of 256 / LB contiguous tile
+// chunks (<= SCAN_COLS_TPT tiles) in registers, all loaded at once (LB lanes x 4 B contiguous per
+// tile row). The chunk sums meet in LDS; each thread then writes its chunk's running prefix back
+// in place: hist[t][l] = sum over t' < t of hist[t'][l] (lane_off NOT included), and the lane
+// total goes to tot[l]. lane_off = exclusive scan of tot is folded into the scatter's prologue
+// (lane_cursors), so no launch waits for a scan over lanes. One read and one write of the
+// histogram, in place of the reduce / top / down chain's three launches.
+__global__ void __launch_bounds__(SCAN_COLS_BLOCK)
+rx_scan_cols(ScanArgs a, uint32_t lb)
 {
-    extern __shared__ uint32_t tot[];                       // [n_lanes]
-    __shared__ uint32_t lds16[SCAN_BLOCK / 64];
-    const uint32_t S = a.n_lanes;
-    for (uint32_t l = threadIdx.x; l < S; l += SCAN_BLOCK) {
-        uint32_t run = 0;
-        for (uint32_t t = 0; t < a.n_tiles; ++t) {
-            const uint32_t v = a.hist[(size_t)t * S + l];
-            a.hist[(size_t)t * S + l] = run;
-            run += v;
-        }
-        tot[l] = run;
+    __shared__ uint32_t part[SCAN_COLS_BLOCK];
+    const uint32_t LB = 1u << lb, C = (uint32_t)SCAN_COLS_BLOCK >> lb;
+    const uint32_t l = threadIdx.x & (LB - 1u), c = threadIdx.x >> lb;
+    const uint32_t S = a.n_lanes, lanei = blockIdx.x * LB + l;
+    const uint32_t tpc = (a.n_tiles + C - 1u) / C;
+    const uint32_t t0 = min(a.n_tiles, c * tpc), t1 = min(a.n_tiles, t0 + tpc);
+    const bool ok = lanei < S;
+    uint32_t *col = a.hist + lanei;
+    uint32_t v[SCAN_COLS_TPT];
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_COLS_TPT; ++k)
+        v[k] = (ok && t0 + k < t1) ? col[(size_t)(t0 + k) * S] : 0u;
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_COLS_TPT; ++k) sum += v[k];
+    part[c * LB + l] = sum;
+    __syncthreads();
+    uint32_t run = 0, tot = 0;
+    for (uint32_t i = 0; i < C; ++i) {
+        const uint32_t x = part[i * LB + l];
+        run += i < c ? x : 0u;
+        tot += x;
     }
-    __syncthreads();
-    scan_lane_totals(tot, S, a.lane_off, a.total, lds16);
-    __syncthreads();
-    for (uint32_t l = threadIdx.x; l < S; l += SCAN_BLOCK) {
-        const uint32_t base = a.lane_off[l];
-        for (uint32_t t = 0; t < a.n_tiles; ++t) a.hist[(size_t)t * S + l] += base;
+    if (ok && c == 0) a.tot[lanei] = tot;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_COLS_TPT; ++k) {
+        if (ok && t0 + k < t1) col[(size_t)(t0 + k) * S] = run;
+        run += v[k];
     }
 }
 
@@ -857,12 +875,84 @@ rx_scan_down(ScanArgs a)
     }
 }
 
+// Tile of workgroup b out of n so that each XCD walks a contiguous run of tiles (blocks are dealt
+// round-robin over the 8 XCDs, MI355X_MICROARCH.md §Workgroup dispatch; b % 8 labels the blocks
+// sharing one). Bijective for any n. A lane's entries from consecutive tiles are adjacent in
+// lane_pkt, so with this order the partial lines one tile leaves in a lane are completed by the
+// next tiles in the SAME L2 and written back once, instead of once per XCD that touched them.
+// Placement is a speed choice only: any order gives the same output.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n)
+{
+    const uint32_t x = b & 7u, q = n >> 3, r = n & 7u;
+    return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + (b >> 3);
+}
+
+// Scatter prologue: cur[k] = lane_off[k] + base[tile][k] for the S lanes, where lane_off is the
+// exclusive scan of the lane totals (every workgroup scans them itself, S <= 16384 words from L2;
+// the workgroup of tile 0 also stores lane_off[0..S] and the total). tmp: >= S + 16 words of LDS
+// scratch (no static LDS here: rx_scatterw's dynamic carve is sized so two workgroups share a
+// CU, and one more word would halve that). With a.tot == null (the 3-launch scan) base is
+// already absolute.
+__device__ void lane_cursors(const ScatterArgs &a, uint32_t tile, uint32_t *cur, uint32_t *tmp)
+{
+    const uint32_t tid = threadIdx.x, NT = blockDim.x, S = a.n_lanes;
+    const uint32_t *base = a.base + (size_t)tile * S;
+    if (!a.tot) {
+        for (uint32_t k = tid; k < S; k += NT) cur[k] = base[k];
+        __syncthreads();
+        return;
+    }
+    for (uint32_t k = tid; k < S; k += NT) {
+        cur[k] = a.tot[k];
+        tmp[k] = base[k];
+    }
+    __syncthreads();
+    const uint32_t L = (S + NT - 1u) / NT, l0 = min(S, tid * L), l1 = min(S, l0 + L);
+    uint32_t s = 0;
+    for (uint32_t k = l0; k < l1; ++k) s += cur[k];
+    uint32_t *wsum = tmp + S;
+    const uint32_t inc = scan_dpp(s), w = tid >> 6;
+    if (lane_id() == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t pre = inc - s, total = 0;
+    for (uint32_t i = 0; i < NT / 64u; ++i) {
+        const uint32_t x = wsum[i];
+        pre += i < w ? x : 0u;
+        total += x;
+    }
+    for (uint32_t k = l0; k < l1; ++k) {
+        const uint32_t v = cur[k];
+        cur[k] = pre;
+        pre += v;
+    }
+    __syncthreads();
+    const bool first = tile == 0;
+    for (uint32_t k = tid; k < S; k += NT) {
+        const uint32_t o = cur[k];
+        if (first) a.lane_off[k] = o;
+        cur[k] = o + tmp[k];
+    }
+    if (first && tid == 0) {
+        a.lane_off[S] = total;
+        *a.total = total;
+    }
+    __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------
 // rx_scatterw: stable per-lane compaction without fan-out, SCATTER_WAVES waves per tile. Wave w
-// owns the w-th slice of the tile. Pass 1 counts each wave's deliveries per lane key (wave
-// multi-split: one LDS update per distinct key per 64 frames); each key's wave offsets become
-// the exclusive prefix over the earlier slices (16-bit: a tile has <= 16384 frames); pass 2
-// re-reads the verdict words and writes each delivery at cursor + wave offset + rank.
+// owns the w-th contiguous slice of the tile. Pass 1 counts each wave's deliveries per lane key
+// with LDS atomics; each key's wave offsets become the exclusive prefix over the earlier slices;
+// pass 2 places every delivery at cursor + atomicAdd's return on its wave's counter.
+//
+// Stability comes from the order in which a ds_add_rtn_u32 resolves lanes of one instruction
+// that hit the same word: lane order on gfx950 (tools/probe/lds_order_probe.hip: 1.3e10 same-key
+// lane pairs over 1-4096 keys, none out of order), and one wave's instructions execute in
+// program order, so the returns number a key's frames of the slice in arrival order. (The first
+// form ranked lanes by a wave multi-split over the key bits, 12 ballots per 64 frames at 4096
+// lanes: 11 us per pass at config 5, instruction-bound; the atomics make a pass a few
+// instructions per 64 frames.) Counters hold two waves each, 16 bits per wave (a tile has
+// <= 8192 frames, so neither half can carry into the other).
 // LDS: 4 x n_lanes (cursors) + 2 x SCATTER_WAVES x n_lanes bytes.
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(64 * SCATTER_WAVES)
@@ -870,25 +960,20 @@ rx_scatterw(ScatterArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smw[];
     const uint32_t S = a.n_lanes;
-    uint32_t *cur = smw;                                               // [S]
-    uint16_t *woff = reinterpret_cast<uint16_t *>(smw + S);            // [W][S]
     constexpr uint32_t W = SCATTER_WAVES;
+    uint32_t *cur = smw;                                               // [S]
+    uint32_t *cnt = smw + S;                                           // [W / 2][S] packed pairs
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    const uint32_t tile = blockIdx.x;
-    for (uint32_t k = tid; k < S; k += 64 * W) {
-        cur[k] = a.base[(size_t)tile * S + k];
-#pragma unroll
-        for (uint32_t i = 0; i < W; ++i) woff[i * S + k] = 0;
-    }
-    __syncthreads();
+    const uint32_t tile = xcd_tile(blockIdx.x, a.n_tiles);
     const uint32_t t1 = min(a.n, (tile + 1) * a.tile_frames);
     const uint32_t q = a.tile_frames / W;
     const uint32_t wb = tile * a.tile_frames + w * q, we = min(t1, wb + q);
     const uint32_t plast = a.n - 1u;
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    uint16_t *mine = woff + w * S;
+    uint32_t *mine = cnt + (w >> 1) * S;
+    const uint32_t inc = (w & 1u) ? 0x10000u : 1u, sh = (w & 1u) * 16u;
     // the wave's whole slice of verdict words in registers (<= RX_TILE_MAX / W frames = 16 per
-    // lane), loaded once for both passes: no load in the counting or the placing loop
+    // lane), loaded once for both passes (no load in the counting or the placing loop) and
+    // issued first, so they are in flight during the cursor prologue
     constexpr uint32_t MV = RX_TILE_MAX / (64 * SCATTER_WAVES);
     uint32_t mv[MV];
 #pragma unroll
@@ -896,71 +981,86 @@ rx_scatterw(ScatterArgs a)
         const uint32_t p = wb + i * 64 + lane;
         mv[i] = (i * 64 < q) ? a.meta[min(p, plast)] : 0u;
     }
-    for (int pass = 0; pass < 2; ++pass) {
+#ifdef UDPDK_STAMPS
+    unsigned long long sacc[16] = {0}, slast = __builtin_amdgcn_s_memtime();
+    sacc[12] = __builtin_amdgcn_s_memrealtime();
+#define SSTAMP(k)                                                         \
+    do {                                                                  \
+        if (w == 0) {                                                     \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+            sacc[k] += t_ - slast;                                        \
+            slast = t_;                                                   \
+        }                                                                 \
+    } while (0)
+#else
+#define SSTAMP(k) do {} while (0)
+#endif
+    lane_cursors(a, tile, cur, cnt);                                   // cnt doubles as scratch
+    SSTAMP(0);
+    for (uint32_t k = tid; k < (W / 2) * S; k += 64 * W) cnt[k] = 0;
+    __syncthreads();
+    SSTAMP(1);
+    // pass 1: per-wave counts
 #pragma unroll
-        for (uint32_t i = 0; i < MV; ++i) {
-            if (i * 64 >= q) break;                        // uniform
-            {
-                const uint32_t p = wb + i * 64 + lane;
-                const bool deliver = p < we && UDPDK_META_VERDICT(mv[i]) == UDPDK_V_DELIVERED;
-                const uint32_t key = UDPDK_META_SOCKFD(mv[i]) & a.lane_mask;
-                unsigned long long peers = __ballot(deliver);
-                if (!peers) continue;                      // wave-uniform
-                for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
-                    const bool kb = (key >> bit) & 1u;
-                    const unsigned long long bal = __ballot(kb);
-                    peers &= kb ? bal : ~bal;
-                }
-                const uint32_t leader = deliver ? (uint32_t)__ffsll((long long)peers) - 1u : 64u;
-                const uint32_t cnt = (uint32_t)__popcll(peers);
-                if (pass == 0) {
-                    if (deliver && lane == leader) mine[key] = (uint16_t)(mine[key] + cnt);
-                } else {
-                    uint32_t c = 0;
-                    if (deliver && lane == leader) {
-                        const uint32_t o = mine[key];
-                        mine[key] = (uint16_t)(o + cnt);
-                        c = cur[key] + o;
-                    }
-                    c = __shfl(c, deliver ? (int)leader : 0, 64);
-                    const uint32_t pos = c + (uint32_t)__popcll(peers & lt_mask);
-                    if (deliver && pos < a.lane_cap) a.lane_pkt[pos] = p;
-                }
-            }
-        }
-        if (pass == 0) {
-            __syncthreads();
-            for (uint32_t k = tid; k < S; k += 64 * W) {   // slice offsets: earlier slices' counts
-                uint32_t c = 0;
+    for (uint32_t i = 0; i < MV; ++i) {
+        if (i * 64 >= q) break;                                        // uniform
+        const uint32_t p = wb + i * 64 + lane;
+        if (p < we && UDPDK_META_VERDICT(mv[i]) == UDPDK_V_DELIVERED)
+            atomicAdd(&mine[UDPDK_META_SOCKFD(mv[i]) & a.lane_mask], inc);
+    }
+    __syncthreads();
+    SSTAMP(2);
+    // slice offsets: each wave's counts become the sum of the earlier slices' counts
+    for (uint32_t k = tid; k < S; k += 64 * W) {
+        uint32_t c = 0;
 #pragma unroll
-                for (uint32_t i = 0; i < W; ++i) {
-                    const uint32_t v = woff[i * S + k];
-                    woff[i * S + k] = (uint16_t)c;
-                    c += v;
-                }
-            }
-            __syncthreads();
+        for (uint32_t j = 0; j < W / 2; ++j) {
+            const uint32_t v = cnt[j * S + k];
+            const uint32_t lo = c, hi = c + (v & 0xFFFFu);
+            cnt[j * S + k] = lo | (hi << 16);
+            c = hi + (v >> 16);
         }
     }
+    __syncthreads();
+    SSTAMP(3);
+    // pass 2: placement
+#pragma unroll
+    for (uint32_t i = 0; i < MV; ++i) {
+        if (i * 64 >= q) break;                                        // uniform
+        const uint32_t p = wb + i * 64 + lane;
+        const uint32_t key = UDPDK_META_SOCKFD(mv[i]) & a.lane_mask;
+        if (p < we && UDPDK_META_VERDICT(mv[i]) == UDPDK_V_DELIVERED) {
+            const uint32_t o = atomicAdd(&mine[key], inc);
+            const uint32_t pos = cur[key] + ((o >> sh) & 0xFFFFu);
+            if (pos < a.lane_cap) a.lane_pkt[pos] = p;
+        }
+    }
+    SSTAMP(4);
+#ifdef UDPDK_STAMPS
+    sacc[13] = __builtin_amdgcn_s_memrealtime();
+    sacc[14] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+               ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+    sacc[15] = tile;
+    if (a.dbg && w == 0 && lane < 16) a.dbg[(size_t)(RX_TILE_MAX * 2 + tile) * 16 + lane] = sacc[lane];
+#endif
+#undef SSTAMP
 }
 
 // ------------------------------------------------------------------------------------------
 // rx_scatter: stable per-lane compaction, one wave per tile
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(SCATTER1_BLOCK)
 rx_scatter(ScatterArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t *cur = reinterpret_cast<uint32_t *>(smem);   // running position per lane
     const uint32_t lane = lane_id();
-    const uint32_t tile = blockIdx.x;
-    // cursor of every lane for this tile (independent loads, one latency)
-#pragma unroll 8
-    for (uint32_t s = lane; s < a.n_lanes; s += 64) cur[s] = a.base[(size_t)tile * a.n_lanes + s];
-    wave_sync();
+    const uint32_t tile = xcd_tile(blockIdx.x, a.n_tiles);
+    // cursor of every lane for this tile: the whole workgroup runs the prologue, wave 0 the walk
+    lane_cursors(a, tile, cur, cur + a.n_lanes);
+    if (threadIdx.x >= 64) return;
     const uint32_t t0 = tile * a.tile_frames;
     const uint32_t t1 = min(a.n, t0 + a.tile_frames);
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
 
     constexpr int PF = 8;                                 // verdict words prefetched per lane
     for (uint32_t g0 = t0; g0 < t1; g0 += 64 * PF) {
@@ -981,23 +1081,12 @@ rx_scatter(ScatterArgs a)
             const uint32_t fan = UDPDK_META_FANOUT(m);
             const unsigned long long multi = __ballot(deliver && fan > 1u);
             if (multi == 0ull) {
-                // one delivery per frame: wave multi-split on the lane key
-                const uint32_t key = UDPDK_META_SOCKFD(m) & a.lane_mask;
-                unsigned long long peers = __ballot(deliver);
-                for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
-                    const bool kb = (key >> bit) & 1u;
-                    const unsigned long long bal = __ballot(kb);
-                    peers &= kb ? bal : ~bal;
+                // one delivery per frame: the LDS atomic on the lane's cursor returns the
+                // position, lanes of one key numbered in lane order (see rx_scatterw)
+                if (deliver) {
+                    const uint32_t pos = atomicAdd(&cur[UDPDK_META_SOCKFD(m) & a.lane_mask], 1u);
+                    if (pos < a.lane_cap) a.lane_pkt[pos] = p;
                 }
-                const uint32_t leader = deliver ? (uint32_t)__ffsll((long long)peers) - 1u : 64u;
-                uint32_t c = 0;
-                if (deliver && lane == leader) {
-                    c = cur[key];
-                    cur[key] = c + (uint32_t)__popcll(peers);
-                }
-                c = __shfl(c, deliver ? (int)leader : 0, 64);
-                const uint32_t pos = c + (uint32_t)__popcll(peers & lt_mask);
-                if (deliver && pos < a.lane_cap) a.lane_pkt[pos] = p;
             } else if (lane == 0) {
                 // fan-out (SO_REUSEADDR/SO_REUSEPORT clones, poller.c:396-399): deliveries in
                 // frame order then list order, re-derived from the frame header. Serial.

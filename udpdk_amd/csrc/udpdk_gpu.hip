@@ -48,6 +48,7 @@ struct Pipe {
     hipStream_t stream = nullptr;
     uint32_t *hist = nullptr;
     uint32_t *partial = nullptr;
+    uint32_t *tot = nullptr;                  // [max_lanes] lane totals (rx_scan_cols)
     uint32_t *tile_cnt = nullptr;
     DevResult *res = nullptr;                 // counters, total (device)
     DevResult *h_res = nullptr;               // pinned mirror, filled by udpdk_gpu_rx_stats
@@ -276,6 +277,7 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
         for (Pipe &P : c->pipes) {
             ok = ok && hipMalloc((void **)&P.hist, e_cap * 4) == hipSuccess;
             ok = ok && hipMalloc((void **)&P.partial, c->partial_cap * 4) == hipSuccess;
+            ok = ok && hipMalloc((void **)&P.tot, ((size_t)max_lanes + 1) * 4) == hipSuccess;
             ok = ok && hipMalloc((void **)&P.tile_cnt, c->tiles_cap * UDPDK_N_COUNTERS * 4) == hipSuccess;
             ok = ok && hipMalloc((void **)&P.res, sizeof(DevResult)) == hipSuccess;
             ok = ok && hipMemset(P.res, 0, sizeof(DevResult)) == hipSuccess;
@@ -286,12 +288,10 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
         if (hipFuncSetAttribute((const void *)rx_classify, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)classify_lds_bytes(UDPDK_GPU_MAX_LANES, RX_TILE_MAX)) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024) != hipSuccess) break;
+                                (int)scatter1_lds_bytes(UDPDK_GPU_MAX_LANES)) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatterw, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 scatterw_lds_bytes(SCATTERW_MAX_LANES)) != hipSuccess) break;
         // lane totals: 4 B per lane, up to UDPDK_GPU_MAX_LANES (64 KiB) beside a few static words
-        if (hipFuncSetAttribute((const void *)rx_scan_small, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                4 * UDPDK_GPU_MAX_LANES) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scan_top, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 4 * UDPDK_GPU_MAX_LANES) != hipSuccess) break;
         rc = 0;
@@ -321,7 +321,7 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
     for (Pipe &P : c->pipes) {
         void *ph[] = {P.st_frames_h, P.st_desc_h};
         for (void *p : ph) if (p) (void)hipHostFree(p);
-        void *pd[] = {P.hist, P.partial, P.tile_cnt, P.res, P.st_frames_d, P.st_desc_d, P.st_out_d};
+        void *pd[] = {P.hist, P.partial, P.tot, P.tile_cnt, P.res, P.st_frames_d, P.st_desc_d, P.st_out_d};
         for (void *p : pd) if (p) (void)hipFree(p);
         if (P.h_res) (void)hipHostFree(P.h_res);
         if (P.tail) (void)hipEventDestroy(P.tail);
@@ -606,11 +606,22 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     sa.partial = P.partial;
     sa.lane_off = o->lane_off_dev;
     sa.total = &P.res->total;
+    sa.tot = P.tot;
     sa.n_elems = (uint32_t)E;
     sa.n_tiles = tiles;
     sa.n_lanes = S;
-    if (E <= SCAN_SMALL_MAX && tiles <= SCAN_SMALL_TILES) {
-        HIPC(c, launch(st, ts, 1, true, true, rx_scan_small, dim3(1), dim3(SCAN_BLOCK), 4u * S, sa));
+    // one-launch column scan while each thread's tile chunk fits its registers; beyond (very
+    // large batches over few lanes) the reduce / top / down chain, which also writes lane_off
+    const bool cols = tiles <= SCAN_COLS_MAX_TILES;
+    if (cols) {
+        // lanes per workgroup: as many as the chunking allows (<= 64, 256 B rows), then fewer
+        // until the grid has >= 128 workgroups, never under 8 lanes (32 B row segments)
+        const uint32_t cmin = ceil_div(tiles, SCAN_COLS_TPT);
+        uint32_t lb = 0;
+        while ((2u << lb) <= std::min<uint32_t>(64u, SCAN_COLS_BLOCK / cmin)) ++lb;
+        while (lb > 3 && ceil_div(S, 1u << lb) < 128u) --lb;
+        HIPC(c, launch(st, ts, 1, true, true, rx_scan_cols, dim3(ceil_div(S, 1u << lb)),
+                       dim3(SCAN_COLS_BLOCK), 0u, sa, lb));
     } else {
         const uint32_t nc = ceil_div(tiles, SCAN_COL_CHUNK);
         if ((uint64_t)nc * S > c->partial_cap) return -EINVAL;
@@ -623,6 +634,9 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     ScatterArgs xa;
     xa.meta = o->meta_dev;
     xa.base = P.hist;
+    xa.tot = cols ? P.tot : nullptr;
+    xa.lane_off = o->lane_off_dev;
+    xa.total = &P.res->total;
     xa.frames = bt->frames_dev;
     xa.offset = bt->offset_dev;
     xa.port_tab = c->port_tab;
@@ -635,11 +649,13 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     xa.lane_mask = c->lane_mask;
     xa.key_bits = c->key_bits;
     xa.lane_cap = o->lane_cap;
+    xa.dbg = c->dbg;
     if (c->max_fanout <= 1 && S <= SCATTERW_MAX_LANES)
         HIPC(c, launch(st, ts, 2, true, true, rx_scatterw, dim3(tiles), dim3(64 * SCATTER_WAVES),
                        scatterw_lds_bytes(S), xa));
     else
-        HIPC(c, launch(st, ts, 2, true, true, rx_scatter, dim3(tiles), dim3(64), 4u * S, xa));
+        HIPC(c, launch(st, ts, 2, true, true, rx_scatter, dim3(tiles), dim3(SCATTER1_BLOCK),
+                       scatter1_lds_bytes(S), xa));
     return 0;
 }
 
@@ -975,6 +991,7 @@ int udpdk_gpu_rss(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rss_
     sa.partial = c->rss_partial;
     sa.lane_off = o->queue_off_dev;
     sa.total = c->rss_total;
+    sa.tot = nullptr;
     sa.n_elems = tiles * S;
     sa.n_tiles = tiles;
     sa.n_lanes = S;
