@@ -15,7 +15,7 @@ PH = ["prologue", "funnel+fields", "header sums+sweep", "issue next+wait demux",
 L = abi.lib()
 L.udpdk_gpu_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 ctx = abi.GpuContext(0, max_frames=1 << 22, max_lanes=4096)
-dbg = ctx.alloc(16 * 8 * 8192 + 64)
+dbg = ctx.alloc((2 * 8192 + 8192) * 16 * 8)   # classify rows, then rx_scatterw rows from 16384
 L.udpdk_gpu_debug_buffer(ctx.handle, C.c_void_p(dbg.ptr))
 for cfg, n in [(2, 4096), (2, None), (4, 65536), (3, 65536)]:
     w = F.config_batch(cfg, n=n)

@@ -37,7 +37,7 @@ constexpr int TX_BLOCK = 256;
 // round's datagram ends + window sums (frames whose UDP checksum waits for the tail pass);
 // the round's port-table lookups (dst port, dst IPv4).
 constexpr uint32_t RX_ROUND = 1024;               // frames per descriptor-staging / tail round
-constexpr int TP_OFF      = 0;                    // [CLS_WAVES][3][64] chunk start, offset, dge
+constexpr int TP_OFF      = 0;                    // [CLS_WAVES][3][64] chunk base, datagram left, mark
 constexpr int CNT_OFF     = TP_OFF + CLS_WAVES * 3 * 64 * 4;     // [CLS_WAVES][16] counter rows
 constexpr int DSC_OFF     = CNT_OFF + CLS_WAVES * 16 * 4;
 

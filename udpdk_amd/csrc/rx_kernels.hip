@@ -77,6 +77,13 @@ __device__ __forceinline__ uint32_t dword_window(int a, int e, int i)
 
 __device__ __forceinline__ uint32_t sum16(uint32_t v) { return (v & 0xFFFFu) + (v >> 16); }
 
+// acc + both 16-bit halves of v in ONE instruction: v_sad_u16(v, 0, acc) = |v.lo - 0| + |v.hi - 0|
+// + acc. The RFC 1071 sums below are chains of these (the and/shift/add3 form of sum16 is three).
+__device__ __forceinline__ uint32_t sad16(uint32_t v, uint32_t acc)
+{
+    return __builtin_amdgcn_sad_u16(v, 0u, acc);
+}
+
 // One's-complement fold of a 32-bit sum of 16-bit words to [0, 0xffff] (0xffff is -0: a valid
 // RFC 1071 sum folds to 0xffff; only an all-zero input folds to 0).
 __device__ __forceinline__ uint32_t fold32(uint32_t x)
@@ -189,6 +196,18 @@ __device__ __forceinline__ uint32_t scan_dpp(uint32_t v)
     return v;
 }
 
+// Inclusive wave64 prefix maximum on the DPP network (same shifts as scan_dpp).
+__device__ __forceinline__ uint32_t max_scan_dpp(uint32_t v)
+{
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+
 // Frame bytes [12, 64) of one frame, loaded straight from frame byte 12 (byte-aligned buffer
 // loads: 3 x 16 B + 4 B; unaligned dwordx4 buffer loads cost the same as aligned ones here,
 // tools/probe/stream_probe.hip k_unal): g[i] = frame bytes 12 + 4i .. 15 + 4i, no funnel shift.
@@ -199,7 +218,8 @@ struct Win {
 
 // 4 waves per SIMD (<= 128 VGPRs, the tail pass's two groups in flight): one tile of 1024 frames
 // per workgroup puts 4 workgroups on each CU at 1 M frames. (A 96-VGPR budget spills and runs
-// 19 % slower at 64 B.)
+// 19 % slower at 64 B. Four tail groups in flight, at 148 VGPRs and 3 waves per SIMD, measured
+// no faster at 1500 B and slower at IMIX and 106 B: the tail is not bound by its round trips.)
 __global__ void __launch_bounds__(CLS_BLOCK) __attribute__((amdgpu_waves_per_eu(UDPDK_CLS_WPE, 8)))
 rx_classify(RxArgs a)
 {
@@ -305,13 +325,23 @@ rx_classify(RxArgs a)
     // per round of four steps re-fetched the line shared by a frame's header window and its
     // first tail chunk from HBM). The step's pending frames (state 3): frame bytes [64, dge) as
     // 64-byte super-chunks, chunk j = frame bytes [64 + 64 j, 128 + 64 j) loaded as 4
-    // byte-aligned 16-byte pieces (so the words are frame-relative whatever the frame's offset,
-    // and only a frame's last chunk needs byte masks), swept across the wave's lanes: lane i of a
-    // group takes chunk k0 + i of the step's chunk space (its frame found by binary search over
-    // the per-frame chunk starts in LDS), so a group is 4 KiB of dense frame bytes. Per-frame sums
-    // are segment sums of a DPP prefix scan; two groups in flight.
-    uint32_t *l_cs = reinterpret_cast<uint32_t *>(smem + TP_OFF) + w * 192;  // [64] chunk starts
-    uint32_t *l_off = l_cs + 64, *l_dge = l_cs + 128;                       // [64] offset, dge
+    // byte-aligned 16-byte pieces (so the words are frame-relative whatever the frame's offset),
+    // swept across the wave's lanes: lane i of a group takes chunk k0 + i of the step's chunk
+    // space, so a group is 4 KiB of dense frame bytes. A chunk's frame comes from a prefix
+    // maximum over the group's lanes of the marks the frames starting inside the group leave in
+    // LDS (one LDS round trip; a binary search over the chunk starts took six). Pieces at or past
+    // the datagram end are addressed out of the buffer's range (no memory access, zeros); the
+    // piece holding the end, when it ends inside it, has its bytes past the end subtracted from
+    // the chunk sum, so every chunk is summed the same way (v_sad_u16 chains, no masked re-sum).
+    // Per-frame sums are segment sums of a DPP prefix scan; two groups in flight.
+    // per frame q of the step: chunk k of q starts at frame byte B_q + 64 k and holds D_q - 64 k
+    // bytes of the datagram (B_q = offset + 64 - 64 cs_q, D_q = dge - 64 + 64 cs_q, cs_q = the
+    // frame's first chunk index in the step), so a chunk needs two LDS words of its frame
+    uint32_t *l_B = reinterpret_cast<uint32_t *>(smem + TP_OFF) + w * 192;   // [64]
+    uint32_t *l_D = l_B + 64;                                               // [64]
+    uint32_t *l_own = l_B + 128;            // [64] frame + 1 whose chunks start at k0 + slot, else 0
+    l_own[lane] = 0;
+    constexpr uint32_t OOR = 0xFFFFFFF0u;   // past any batch's range (< 4 GiB - 16)
     auto tail_step = [&](uint32_t s2) {
             const uint32_t i = s2 * 64 + lane;
             const uint32_t m = mstage[i];
@@ -325,55 +355,67 @@ rx_classify(RxArgs a)
             const uint32_t inc = scan_dpp(my_nt);
             const uint32_t my_cs = inc - my_nt;
             const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-            l_cs[lane] = my_cs;
-            l_off[lane] = fo;
-            l_dge[lane] = de;
-            wave_sync();
-            uint32_t tsum = 0;
-            auto issue = [&](uint32_t k0, uint32_t &q, uint4 (&R)[4]) {
+            l_B[lane] = fo + 64u - 64u * my_cs;
+            l_D[lane] = de - 64u + 64u * my_cs;
+            uint32_t tsum = 0, carry = 0;
+            // group k0: each lane's frame (q), the chunk's bytes in the datagram (left) and its
+            // four pieces in flight
+            auto issue = [&](uint32_t k0, uint32_t &q, int &left, uint4 (&R)[4]) {
                 const uint32_t k = k0 + lane;
-                q = 0;
+                if (my_nt != 0u && my_cs >= k0 && my_cs < k0 + 64u) l_own[my_cs - k0] = lane + 1u;
+                wave_sync();
+                const uint32_t mark = l_own[lane];
+                l_own[lane] = 0u;                       // cleared for the next group (in order)
+                const uint32_t own = max(max_scan_dpp(mark), carry);
+                carry = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
+                q = (own - 1u) & 63u;
+                left = k < total ? (int)(l_D[q] - 64u * k) : 0;
+                const uint32_t base = l_B[q] + 64u * k;
 #pragma unroll
-                for (int sft = 32; sft >= 1; sft >>= 1)
-                    if (l_cs[q + sft] <= k) q += sft;
-                const uint32_t base = k < total ? l_off[q] + 64u + 64u * (k - l_cs[q]) : 0u;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) R[c] = load16(fr, base + 16u * c);
+                for (int c = 0; c < 4; ++c) R[c] = load16(fr, 16 * c < left ? base + 16u * c : OOR);
             };
             // The full-chunk sum reads every loaded register unconditionally, so the compiler's
-            // wait for this group is placed here on every path (a first use only inside a lane
-            // branch leaves the loads "pending" at the loop header, where it then waits for
-            // every load in flight, the next group's included).
-            auto consume = [&](uint32_t k0, uint32_t q, const uint4 (&R)[4]) {
-                const uint32_t k = k0 + lane;
-                uint32_t part = 0;
+            // wait for this group is placed here on every path.
+            auto consume = [&](uint32_t k0, int left, const uint4 (&R)[4]) {
+                uint32_t pa = 0, pb = 0;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) part += sum16(R[c].x) + sum16(R[c].y) + sum16(R[c].z) + sum16(R[c].w);
-                const int left = (int)l_dge[q] - 64 - 64 * (int)(k - l_cs[q]);   // chunk bytes in the datagram
-                if (left < 64) {                                       // the frame's last chunk
-                    part = 0;
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) part += chunk_sum(R[c], 0, left - 16 * c);
+                for (int c = 0; c < 4; ++c) {
+                    pa = sad16(R[c].x, pa);
+                    pb = sad16(R[c].y, pb);
+                    pa = sad16(R[c].z, pa);
+                    pb = sad16(R[c].w, pb);
                 }
-                part = k < total ? part : 0u;
-                const uint32_t P = scan_dpp(part);
+                // the piece holding the datagram end, if the end falls inside it: its bytes
+                // [r, 16) are the next frame's (or padding) and come off again
+                const int r = left & 15;
+                const uint32_t pc = (uint32_t)left >> 4;
+                const uint4 P = pc == 0u ? R[0] : pc == 1u ? R[1] : pc == 2u ? R[2] : R[3];
+                const uint32_t pv[4] = {P.x, P.y, P.z, P.w};
+                uint32_t ex = 0;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int keep = min(max(r - 4 * d, 0), 4);
+                    ex = sad16(pv[d] & (keep >= 4 ? 0u : 0xFFFFFFFFu << (8 * keep)), ex);
+                }
+                const uint32_t part = pa + pb - (left > 0 && left < 64 && r != 0 ? ex : 0u);
+                const uint32_t Pp = scan_dpp(part);
                 const uint32_t lo = max(my_cs, k0), hi = min(my_cs + my_nt, k0 + 64u);
-                const uint32_t ph = __shfl(P, (int)((hi > k0 ? hi - 1u - k0 : 0u) & 63u), 64);
-                const uint32_t pl = __shfl(P, (int)((lo > k0 ? lo - 1u - k0 : 0u) & 63u), 64);
+                const uint32_t ph = __shfl(Pp, (int)((hi > k0 ? hi - 1u - k0 : 0u) & 63u), 64);
+                const uint32_t pl = __shfl(Pp, (int)((lo > k0 ? lo - 1u - k0 : 0u) & 63u), 64);
                 if (lo < hi) tsum += ph - (lo > k0 ? pl : 0u);
             };
             // Two groups in flight; one back edge, after the second group is consumed (a loop
             // exit between the two halves leaves the second group's loads pending at the
-            // header, which then waits for everything). Groups past the end load from offset 0
-            // and contribute nothing.
+            // header, which then waits for everything). Groups past the end load nothing.
             uint32_t qa, qb;
+            int la, lb;
             uint4 Ra[4], Rb[4];
-            issue(0, qa, Ra);
+            issue(0, qa, la, Ra);
             for (uint32_t k0 = 0;; k0 += 128) {
-                issue(k0 + 64, qb, Rb);
-                consume(k0, qa, Ra);
-                issue(k0 + 128, qa, Ra);
-                consume(k0 + 64, qb, Rb);
+                issue(k0 + 64, qb, lb, Rb);
+                consume(k0, la, Ra);
+                issue(k0 + 128, qa, la, Ra);
+                consume(k0 + 64, lb, Rb);
                 if (k0 + 128 >= total) break;
             }
             wave_sync();
@@ -411,8 +453,8 @@ rx_classify(RxArgs a)
 
             // ---- everything the header window gives ----
             // IPv4 header checksum over the fixed 20 bytes at offset 14 (RFC 1071)
-            const uint32_t ipraw = (g[0] >> 16) + sum16(g[1]) + sum16(g[2]) + sum16(g[3]) +
-                                   sum16(g[4]) + (g[5] & 0xFFFFu);
+            const uint32_t ipraw = sad16(g[4], sad16(g[3], sad16(g[2], sad16(g[1],
+                                   (g[0] >> 16) + (g[5] & 0xFFFFu)))));
             const bool ip_ok = fold32(ipraw) == 0xFFFFu;
             const bool ihl_ne5 = ((g[0] >> 16) & 0x0Fu) != 5u;
             const uint32_t dip = (g[4] >> 16) | (g[5] << 16);         // poller.c:373
@@ -428,13 +470,16 @@ rx_classify(RxArgs a)
             const bool need_cs = is_udp && ucks != 0u && !len_bad;
             const uint32_t dge = 34u + ulen;                          // datagram end (<= len)
             const bool pend = need_cs && dge > 64u;
-            uint32_t ws = 0;
+            uint32_t ws = 0, ws2 = 0;
 #pragma unroll
-            for (int i = 6; i < 13; ++i) ws += sum16(g[i]);
+            for (int i = 6; i < 13; i += 2) ws = sad16(g[i], ws);
+#pragma unroll
+            for (int i = 7; i < 13; i += 2) ws2 = sad16(g[i], ws2);
+            ws += ws2;
             if (__ballot(need_cs && dge < 64u)) {                     // short or padded frames
                 uint32_t wm = 0;
 #pragma unroll
-                for (int i = 6; i < 13; ++i) wm += sum16(g[i] & byte_mask(34, (int)dge, 12 + 4 * i));
+                for (int i = 6; i < 13; ++i) wm = sad16(g[i] & byte_mask(34, (int)dge, 12 + 4 * i), wm);
                 ws = dge < 64u ? wm : ws;
             }
             const uint32_t us = ws + (g[5] >> 16) + (g[3] >> 16) + (g[4] & 0xFFFFu) + (dip & 0xFFFFu) +
@@ -620,6 +665,7 @@ rx_classify(RxArgs a)
     }
     if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = tile_counter(tid);
 }
+
 
 // ------------------------------------------------------------------------------------------
 // rx_compact1: the single-lane batch's lane (no fan-out: every delivery is a whole frame).
@@ -1041,7 +1087,7 @@ rx_scatterw(ScatterArgs a)
     sacc[14] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
                ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
     sacc[15] = tile;
-    if (a.dbg && w == 0 && lane < 16) a.dbg[(size_t)(RX_TILE_MAX * 2 + tile) * 16 + lane] = sacc[lane];
+    if (a.dbg && w == 0 && lane < 16 && tile < RX_TILE_MAX) a.dbg[(size_t)(RX_TILE_MAX * 2 + tile) * 16 + lane] = sacc[lane];
 #endif
 #undef SSTAMP
 }

@@ -576,7 +576,7 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
 
     if (ts) for (int k = 0; k < TIMED_KERNELS; ++k) ts->used[k] = false;
     HIPC(c, launch(st, ts, 0, true, true, rx_classify, dim3(tiles), dim3(CLS_BLOCK),
-                   classify_lds_bytes(S, T), ra));
+                       classify_lds_bytes(S, T), ra));
     if (one_lane) {
         Compact1Args ca;
         ca.meta = o->meta_dev;
