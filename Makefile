@@ -17,7 +17,9 @@ C_OBJ     := $(patsubst udpdk_amd/csrc/host/%.c,$(OBJDIR)/host/%.o,$(C_SRC))
 HDRS      := include/udpdk_gpu.h include/udpdk_api.h udpdk_amd/csrc/rx_common.h \
              $(wildcard udpdk_amd/csrc/host/*.h)
 
-all: $(LIB) oracle
+TOOLS     := tools/bin/bench_sock
+
+all: $(LIB) oracle $(TOOLS)
 
 $(OBJDIR)/%.o: udpdk_amd/csrc/%.hip $(HDRS)
 	@mkdir -p $(dir $@)
@@ -32,6 +34,11 @@ $(LIB): $(HIP_OBJ) $(C_OBJ)
 
 oracle:
 	$(MAKE) -C oracle
+
+# the reference-API path end to end, written against udpdk_api.h like a reference app (bench.py)
+tools/bin/bench_sock: tools/bench_sock.c include/udpdk_api.h include/udpdk_gpu.h $(LIB)
+	@mkdir -p tools/bin
+	$(CC) -O2 -std=gnu11 -Wall -Wextra -Werror -Iinclude $< -o $@ -Ludpdk_amd -ludpdk_amd -Wl,-rpath,'$$ORIGIN/../../udpdk_amd'
 
 # diagnostic library with per-phase s_memtime stamps (tools/stamps.py); never used by tests/bench
 STAMP_LIB := tools/diag/libudpdk_amd.so
@@ -50,7 +57,7 @@ asm: udpdk_amd/csrc/rx_kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(INC) -c -Rpass-analysis=kernel-resource-usage $< -o /dev/null 2> build/asm/rx_resource.txt || true
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(TOOLS)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean asm stamps

@@ -546,6 +546,36 @@ def end_to_end(ctx, cfg: int, reps: int):
             "path": "pinned host frames -> H2D -> rx pipeline -> D2H meta+lanes, synchronous"}
 
 
+def socket_path_lines(specs=((1 << 20, 64, 1024, 5), (1 << 20, 0, 1024, 3), (1 << 20, 1500, 1024, 3))):
+    """The reference-API path end to end: tools/bin/bench_sock, a C program
+    written against include/udpdk_api.h like the reference's apps, times udpdk_poll_rx (frames in
+    pinned host memory -> H2D -> GPU classify/demux -> GPU payload gather -> D2H -> ring
+    admission) and the recvfrom loop that empties every ring, per 1 M-frame batch over 1024
+    sockets (frame size 0 = IMIX). Runs as its own process on the same GPU."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "bin", "bench_sock")
+    if not os.path.exists(exe):
+        return [{"error": "tools/bin/bench_sock not built"}]
+    import tempfile
+    out = []
+    with tempfile.NamedTemporaryFile("w", suffix=".ini", delete=False) as f:
+        f.write("[port0]\nmac_addr = 68:05:ca:95:f8:ec\nip_addr = 172.31.100.1\n"
+                "[port0_dst]\nmac_addr = 68:05:ca:95:fa:64\n"
+                "[gpu]\ndevice = 0\nmax_frames = 1048576\nmax_lanes = 1024\n")
+        ini = f.name
+    try:
+        for n, fb, socks, reps in specs:
+            r = subprocess.run([exe, ini, str(n), str(fb), str(socks), str(reps)], capture_output=True,
+                               text=True, timeout=300)
+            if r.returncode:
+                out.append({"frames": n, "frame_bytes": fb, "error": r.stderr[-300:]})
+            else:
+                out.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    finally:
+        os.unlink(ini)
+    return out
+
+
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -709,6 +739,10 @@ def main():
             except Exception as e:
                 e2e.append({"config": cfg, "async": True, "error": repr(e)})
         line["end_to_end"] = e2e
+        try:
+            line["socket_path"] = socket_path_lines()
+        except Exception as e:
+            line["socket_path"] = [{"error": repr(e)}]
         tx = []
         for plen in (22, 1458):                  # 64 B and 1500 B frames
             try:

@@ -8,9 +8,10 @@
  * What changed underneath: there is no forked DPDK poller. The per-packet RX work of
  * udpdk_poller.c runs as HIP kernels on an MI355X through udpdk_gpu.h; udpdk_init() creates the
  * GPU context (and fails with ENODEV when no GPU is present), and frame batches enter through
- * udpdk_poll_rx() (the replacement of poller.c:516-545's rte_eth_rx_burst loop). Frames built by
- * udpdk_sendto() leave through udpdk_tx_drain() (the replacement of rte_eth_tx_burst,
- * poller.c:415-425).
+ * udpdk_poll_rx() (the replacement of poller.c:516-545's rte_eth_rx_burst loop). Datagrams queued
+ * by udpdk_sendto() leave as frames built on the GPU through udpdk_tx_drain() (the replacement of
+ * the poller's TX half, poller.c:453-514). A poller thread can drive both against a port
+ * (udpdk_port_attach), as the reference's forked poller drives NIC port 0.
  *
  * Extensions below the reference surface are prefixed udpdk_ too and documented in
  * INTEGRATION.md.
@@ -72,18 +73,56 @@ void udpdk_dump_payload(const char *payload, int len);
 #define UDPDK_MAX_SOCKETS  4096
 #define UDPDK_RX_RING_SIZE 2048
 
-/* RX entry point of the GPU poller: classify a batch of received frames (host memory, as they
- * come off the NIC) on the GPU and append every delivered datagram to its socket's RX ring,
- * all-or-nothing per socket per call like rte_ring_enqueue_bulk (poller.c:287-290).
- * stats may be NULL. Returns 0 or -1 with errno. */
+/* RX entry point of the GPU poller (one turn of poller_body's RX half, udpdk_poller.c:516-545):
+ * classify a batch of received frames (host memory, as they come off the NIC) on the GPU,
+ * reassemble IPv4 fragments on the device, gather every accepted datagram's payload on the GPU
+ * into pinned host slabs and append it to its socket's RX ring in arrival order. A socket's
+ * deliveries are admitted per burst of BURST_SIZE = 128 frames (frame index / 128), each burst
+ * all-or-nothing like the rte_ring_enqueue_bulk of flush_rx_queue (poller.c:274-292): a burst
+ * whose datagrams do not fit the ring is dropped, later bursts may still fit. Reassembled
+ * datagrams count at the index of the fragment that completed them. Safe to call from a poller
+ * thread while application threads call the socket functions. stats may be NULL. Returns 0 or
+ * -1 with errno. */
 int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *offset,
                   const uint16_t *length, const uint32_t *ptype, uint32_t n,
                   udpdk_rx_stats_t *stats);
 
-/* TX exit point: move up to max queued frames (built by udpdk_sendto) into out (packed back to
- * back, out_off/out_len per frame). *n_out = frames moved. Returns 0 or -1 with errno. */
+/* TX exit point (the poller's TX half, udpdk_poller.c:453-514): take queued datagrams in the
+ * poller's order (sockets in index order, each drained while the burst holds fewer than
+ * BURST_SIZE frames), build their frames on the GPU (header build, rte_ipv4_cksum, payload copy,
+ * and the IPv4 fragmentation of frames longer than the MTU, udpdk_gpu_tx_build_mtu) and copy
+ * them into out, back to back (out_off/out_len per frame; a datagram's fragments are
+ * consecutive frames and never split across calls). At most max frames and out_cap bytes.
+ * *n_out = frames written. Needs the GPU context (udpdk_init). Returns 0 or -1 with errno. */
 int udpdk_tx_drain(uint8_t *out, uint64_t out_cap, uint32_t *out_off, uint16_t *out_len,
                    uint32_t max, uint32_t *n_out);
+
+/* Datagrams waiting in the TX rings. */
+uint64_t udpdk_tx_pending(void);
+
+/* ---- the poller thread ----------------------------------------------------------------------
+ * The reference forks a poller process that busy-polls NIC port 0 (udpdk_init.c:293-368,
+ * poller.c:448-546). Here a port is a pair of callbacks; udpdk_port_attach starts a poller
+ * thread that loops: udpdk_tx_drain -> tx_burst, rx_burst -> udpdk_poll_rx, until
+ * udpdk_port_detach or udpdk_cleanup. Applications that do not attach a port drive
+ * udpdk_poll_rx / udpdk_tx_drain themselves, from one thread (the poller role). */
+typedef struct udpdk_port_ops {
+    /* Write up to max received frames back to back into frames (cap bytes; keep
+     * UDPDK_GPU_FRAMES_TAILROOM bytes of it free), offset[i] / length[i] per frame; return the
+     * frame count (0: nothing now). */
+    uint32_t (*rx_burst)(void *user, uint8_t *frames, uint64_t cap, uint32_t *offset,
+                         uint16_t *length, uint32_t max);
+    /* Transmit n frames; the callee copies what it keeps. */
+    void (*tx_burst)(void *user, const uint8_t *frames, const uint32_t *offset,
+                     const uint16_t *length, uint32_t n);
+    void    *user;
+    uint32_t batch_frames;   /* frames per RX batch (0: 4096)                                   */
+} udpdk_port_ops_t;
+
+int udpdk_port_attach(const udpdk_port_ops_t *ops);
+int udpdk_port_detach(void);
+/* A built-in loopback port: frames drained from TX come back on RX (tests and demos). */
+int udpdk_port_loopback(udpdk_port_ops_t *ops);
 
 /* Flatten the bind table into a snapshot in list order (valid until the next call or the next
  * bind/close). compat != 0 keys lanes by the reference's (uint8_t) slot (poller.c:294). */
@@ -95,11 +134,8 @@ udpdk_gpu_ctx *udpdk_gpu_context(void);
 /* TX header configuration (what udpdk_init reads from the .ini). Raw network-order IPv4. */
 int udpdk_config_set(const uint8_t src_mac[6], const uint8_t dst_mac[6], uint32_t src_ip_raw);
 int udpdk_config_get(uint8_t src_mac[6], uint8_t dst_mac[6], uint32_t *src_ip_raw);
-
-/* Build the frame udpdk_sendto would build for sockfd (auto-binding it if unbound) into out
- * (len + 42 bytes) without queueing it. Returns frame length or -1 with errno. */
-ssize_t udpdk_build_frame(int sockfd, const void *buf, size_t len,
-                          const struct sockaddr *dest_addr, socklen_t addrlen, uint8_t *out);
+/* IPv4 MTU of the TX fragmentation (default IPV4_MTU_DEFAULT = 1500; (mtu - 20) % 8 == 0). */
+int udpdk_config_mtu(uint32_t mtu);
 
 /* Socket slot state (exch_slot_info, udpdk_types.h:40-47) for the GPU TX slot table. */
 int udpdk_slot_table(udpdk_slot_t *slots, uint32_t n_slots);

@@ -224,8 +224,9 @@ int udpdk_gpu_join(udpdk_gpu_ctx *ctx);
 int udpdk_gpu_rx_stats(udpdk_gpu_ctx *ctx, udpdk_rx_stats_t *stats);
 
 /* End-to-end variant for host-resident batches (the real poller's situation: frames arrive in
- * host mbufs): pinned staging, H2D, the RX pipeline, D2H of meta and lanes. Synchronous.
- * frames_host etc. follow udpdk_rx_batch_t; outputs are host arrays. */
+ * host mbufs): pinned staging, H2D, the RX pipeline, D2H of meta and lanes (lane_pkt: only the
+ * min(deliveries, lane_cap) entries made). Synchronous. frames_host etc. follow
+ * udpdk_rx_batch_t; outputs are host arrays. */
 int udpdk_gpu_rx_host(udpdk_gpu_ctx *ctx,
                       const uint8_t *frames_host, uint64_t frames_bytes,
                       const uint32_t *offset_host, const uint16_t *length_host,
@@ -233,6 +234,11 @@ int udpdk_gpu_rx_host(udpdk_gpu_ctx *ctx,
                       uint32_t *meta_host, uint32_t *lane_off_host,
                       uint32_t *lane_pkt_host, uint32_t lane_cap,
                       udpdk_rx_stats_t *stats);
+
+/* Device view of the batch the last udpdk_gpu_rx_host call staged (frames, descriptors) and its
+ * verdict words, valid until the next udpdk_gpu_rx_host[_async] call: for udpdk_gpu_rx_gather
+ * and udpdk_gpu_rx_reassemble on frames already on the device (the socket layer's poller). */
+int udpdk_gpu_rx_host_batch(udpdk_gpu_ctx *ctx, udpdk_rx_batch_t *batch, const uint32_t **meta_dev);
 
 /* Asynchronous form of udpdk_gpu_rx_host for a stream of host-resident batches: the staging,
  * H2D, RX pipeline, counter reduction and D2H of meta, lane_off and lane_pkt[0, lane_cap) are

@@ -1,0 +1,242 @@
+"""The reference's socket surface over the GPU datapath (udpdk_api.h, -m gpu):
+
+* TX: udpdk_sendto queues, udpdk_tx_drain builds the frames on the GPU in the poller's order
+  (udpdk_poller.c:453-514) — the §8.G golden vectors V1-V5, the fragmentation of datagrams
+  longer than the MTU against the oracle's restatement, the per-socket burst order, partial drains;
+* RX: udpdk_poll_rx admits each socket's deliveries per burst of 128 frames, all-or-nothing
+  (flush_rx_queue, :274-292), into rings recvfrom reads, with payloads gathered on the GPU;
+* both halves driven by the poller thread against the built-in loopback port, while the test
+  thread calls sendto / recvfrom (SP/SC rings across threads)."""
+import ctypes as C
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import oracle as O
+from udpdk_amd import abi, frames as F
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+SRC_MAC, DST_MAC, SRC_IP = "68:05:ca:95:f8:ec", "68:05:ca:95:fa:64", "172.31.100.2"
+
+
+@pytest.fixture()
+def api(tmp_path, host_api):
+    ini = tmp_path / "udpdk.ini"
+    ini.write_text(f"[port0]\nmac_addr = {SRC_MAC}\nip_addr = {SRC_IP}\n"
+                   f"[port0_dst]\nmac_addr = {DST_MAC}\n"
+                   "[gpu]\ndevice = 0\nmax_frames = 65536\nmax_lanes = 64\n"
+                   "frag_buckets = 64\nfrag_bucket_entries = 16\nfrag_max_dgram = 16384\n")
+    L = abi.lib()
+    argv = (C.c_char_p * 4)(b"prog", b"-c", str(ini).encode(), None)
+    assert L.udpdk_init(3, argv) == 0
+    yield host_api
+    L.udpdk_cleanup()
+
+
+def _payload(n, seed=0):
+    return bytes(np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8))
+
+
+def _tx_expected(slot_ip, slot_port, dst, port, payload, mtu=1500):
+    fr = O.tx_frame(bytes.fromhex(SRC_MAC.replace(":", "")), bytes.fromhex(DST_MAC.replace(":", "")),
+                    abi.raw_ip(SRC_IP), 1, slot_ip, slot_port, abi.raw_ip(dst), abi.raw_port(port), payload)
+    return O.tx_fragment(fr, mtu) if len(fr) > mtu else [fr]
+
+
+def test_tx_golden_vectors_through_sendto(api):
+    """§8.G V1-V5 (the reference's udpdk_sendto output) through sendto -> tx_drain on the GPU."""
+    with open(os.path.join(HERE, "tx_vectors.json")) as f:
+        g = json.load(f)
+    cfg = g["config"]
+    for v in g["vectors"]:
+        api.reset()
+        api.config_set(bytes.fromhex(cfg["src_mac"]), bytes.fromhex(cfg["dst_mac"]), cfg["src_ip"])
+        for step in v["setup"]:
+            if step[0] == "socket":
+                assert api.socket() >= 0
+            elif step[0] == "bind":
+                assert api.bind(step[1], step[2], step[3]) == 0
+            elif step[0] == "autobind":
+                assert api.sendto(step[1], b"x", "172.31.100.1", 10001) == 1
+                assert len(api.tx_drain()) == 1
+        pl = bytes((i * 7 + 3) & 0xFF for i in range(v["send"]["len"]))
+        assert api.sendto(v["send"]["sock"], pl, v["send"]["dst"], v["send"]["port"]) == len(pl)
+        frames = api.tx_drain()
+        assert len(frames) == 1, v["id"]
+        assert len(frames[0]) == v["pkt_len"], v["id"]
+        assert frames[0][:42].hex() == v["hdr"], v["id"]
+        assert frames[0][42:] == pl, v["id"]
+
+
+@pytest.mark.parametrize("mtu", [1500, 1020])
+def test_tx_fragmentation_through_sendto(api, mtu):
+    """Datagrams around and far past the MTU: the poller fragments frames longer than the MTU
+    (pkt_len > IPV4_MTU_DEFAULT, poller.c:461-501); frames equal the oracle's restatement."""
+    assert abi.lib().udpdk_config_mtu(mtu) == 0
+    s = api.socket()
+    assert api.bind(s, "10.1.2.3", 5353) == 0
+    lens = [0, 1, 1458, 1459, 1472, 1473, 2000, 2006, 2007, 8000, 65507]
+    want = []
+    for i, n in enumerate(lens):
+        pl = _payload(n, i)
+        assert api.sendto(s, pl, "172.31.100.1", 10001) == n
+        want += _tx_expected(abi.raw_ip("10.1.2.3"), abi.raw_port(5353), "172.31.100.1", 10001, pl, mtu)
+    got = api.tx_drain(max_frames=4096, cap=1 << 21)
+    assert len(got) == len(want)
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert a == b, i
+    assert api.tx_pending() == 0
+
+
+def _poller_drain(q, max_frames, nfrag):
+    """Model of one udpdk_tx_drain call: the poller's TX loop (udpdk_poller.c:452-507) from
+    socket 0 with an empty burst: sockets in index order, each dequeued while the burst holds
+    < 128 frames, flush at >= 128, repeated until the rings are empty or the next datagram's
+    frames would pass max_frames. Mutates q."""
+    order, burst, frames = [], 0, 0
+    while any(q.values()):
+        for s in sorted(q):
+            while burst < 128 and q[s]:
+                nf = nfrag(q[s][0])
+                if frames + nf > max_frames:
+                    return order
+                order.append((s, q[s].pop(0)))
+                burst += nf
+                frames += nf
+            if burst >= 128:
+                burst = 0
+        burst = 0
+    return order
+
+
+def test_tx_poller_order_and_partial_drains(api):
+    socks = [api.socket() for _ in range(3)]
+    for i, s in enumerate(socks):
+        assert api.bind(s, "0.0.0.0", 20000 + i) == 0
+    queues = {s: [] for s in socks}
+    rng = np.random.default_rng(3)
+    for k in range(600):
+        s = socks[int(rng.integers(0, 3))]
+        n = int(rng.choice([10, 100, 3000]))               # 3000 B -> 3 fragments at MTU 1500
+        pl = bytes([s, k & 0xFF, k >> 8]) + b"\0" * (n - 3)
+        assert api.sendto(s, pl, "172.31.100.1", 10001) == n
+        queues[s].append((k, n))
+    span = abi.lib().udpdk_gpu_tx_span
+
+    def nf(item):
+        c = C.c_uint32()
+        span(item[1], 1500, C.byref(c))
+        return c.value
+    q = {s: list(v) for s, v in queues.items()}
+    want, got = [], []
+    while api.tx_pending():
+        frames = api.tx_drain(max_frames=97, cap=1 << 20)     # partial drains: whole datagrams only
+        assert frames and len(frames) <= 97
+        want += _poller_drain(q, 97, nf)
+        got += frames
+    # first fragment (or the frame) of each datagram names its socket and sequence number
+    firsts = [f for f in got if (int.from_bytes(f[20:22], "big") & 0x1FFF) == 0]
+    seq = [(f[42], f[43] | f[44] << 8) for f in firsts]
+    assert seq == [(s, k) for s, (k, _) in want]
+    assert len(got) == sum(nf(it) for v in queues.values() for it in v)
+
+
+def _rx_batch(ports, size=64, seed=5):
+    b = F.build_frames(np.full(len(ports), size, np.uint32), np.asarray(ports, np.uint32), seed)
+    return b
+
+
+def _poll(b):
+    st = abi.RxStats()
+    rc = abi.lib().udpdk_poll_rx(b.frames.ctypes.data, b.frames_bytes, b.offset.ctypes.data,
+                                 b.length.ctypes.data, None, b.n, C.byref(st))
+    assert rc == 0
+    return st
+
+
+def test_rx_burst_admission_and_payloads(api):
+    """A socket gets more deliveries in one poll than its ring holds, with the ring partly full:
+    each burst of 128 frames is admitted whole or dropped whole (poller.c:287-290); payloads and
+    source addresses come from the GPU gather."""
+    s0, s1 = api.socket(), api.socket()
+    assert api.bind(s0, "0.0.0.0", 10001) == 0 and api.bind(s1, "0.0.0.0", 10002) == 0
+    pre = _rx_batch([10001] * 700, seed=1)
+    _poll(pre)
+    rng = np.random.default_rng(9)
+    ports = np.where(rng.random(6000) < 0.7, 10001, 10002)
+    b = _rx_batch(ports, size=int(rng.integers(60, 200)), seed=2)
+    _poll(b)
+    # model: ring room 2047 - 700; bursts = frame index // 128
+    room, acc0 = 2047 - 700, []
+    idx0 = np.nonzero(ports == 10001)[0]
+    for burst in range(0, 6000, 128):
+        grp = [int(i) for i in idx0 if burst <= i < burst + 128]
+        if len(grp) <= room:
+            acc0 += grp
+            room -= len(grp)
+    idx1 = [int(i) for i in np.nonzero(ports == 10002)[0]]
+    acc1 = []
+    room1 = 2047
+    for burst in range(0, 6000, 128):
+        grp = [i for i in idx1 if burst <= i < burst + 128]
+        if len(grp) <= room1:
+            acc1 += grp
+            room1 -= len(grp)
+
+    def payload(batch, i):
+        o, n = int(batch.offset[i]), int(batch.length[i])
+        return bytes(batch.frames[o + 42:o + n])
+    for i in range(700):
+        n, data, addr = api.recvfrom(s0, 4096)
+        assert data == payload(pre, i) and addr == ("172.31.100.2", 10000)
+    for i in acc0:
+        n, data, _ = api.recvfrom(s0, 4096)
+        assert data == payload(b, i), i
+    for i in acc1:
+        n, data, _ = api.recvfrom(s1, 4096)
+        assert data == payload(b, i), i
+    # nothing else is queued: a non-blocking probe through the interrupt flag
+    L = abi.lib()
+    L.udpdk_interrupt(0)
+    assert api.recvfrom(s0, 64)[0] == -1 and api.recvfrom(s1, 64)[0] == -1
+    assert len(acc0) < len(idx0)                          # the model really dropped bursts
+
+
+def test_two_threads_poller_and_app_over_loopback(api):
+    """udpdk_port_attach starts the poller thread (TX drain -> port -> RX poll); the test thread
+    only calls sendto and recvfrom, as an application on the reference would."""
+    L = abi.lib()
+    ops = abi.PortOps()
+    assert L.udpdk_port_loopback(C.byref(ops)) == 0
+    ops.batch_frames = 512
+    a, b = api.socket(), api.socket()
+    assert api.bind(a, "0.0.0.0", 10000) == 0 and api.bind(b, "0.0.0.0", 10001) == 0
+    assert L.udpdk_port_attach(C.byref(ops)) == 0
+    watchdog = threading.Timer(60.0, L.udpdk_interrupt, [0])   # a hang ends as EINTR
+    watchdog.start()
+    try:
+        sent = []
+        for k in range(3000):
+            pl = _payload(int(k % 1400) + 1, k)
+            while api.sendto(a, pl, SRC_IP, 10001) < 0:      # TX ring full: the poller drains it
+                assert api.errno() == 105                     # ENOBUFS
+            sent.append(pl)
+            if k % 500 == 499:                                # let the consumer keep up
+                for want in sent[k - 499:k + 1]:
+                    n, data, addr = api.recvfrom(b, 2048)
+                    assert n == len(want) and data == want and addr == (SRC_IP, 10000)
+        # fragmented on TX (4 fragments at MTU 1500), reassembled on RX; DPDK's table takes at
+        # most RTE_LIBRTE_IP_FRAG_MAX_FRAG = 4 fragments per datagram, so a larger one would be
+        # dropped there as in the reference
+        big = _payload(5000, 77)
+        assert api.sendto(a, big, SRC_IP, 10001) == 5000
+        n, data, addr = api.recvfrom(b, 16384)
+        assert n == 5000 and data == big and addr == (SRC_IP, 10000)
+    finally:
+        watchdog.cancel()
+        assert L.udpdk_port_detach() == 0

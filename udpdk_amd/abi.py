@@ -116,6 +116,17 @@ class TxBatch(C.Structure):
                 ("dst_port_dev", C.c_void_p), ("n", C.c_uint32)]
 
 
+RX_BURST_FN = C.CFUNCTYPE(C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                          C.c_uint32)
+TX_BURST_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32)
+
+
+class PortOps(C.Structure):
+    """udpdk_port_ops_t (udpdk_api.h): a port for the poller thread."""
+    _fields_ = [("rx_burst", RX_BURST_FN), ("tx_burst", TX_BURST_FN), ("user", C.c_void_p),
+                ("batch_frames", C.c_uint32)]
+
+
 class TxOut(C.Structure):
     _fields_ = [("frames_dev", C.c_void_p), ("frames_bytes", C.c_uint64),
                 ("frame_off_dev", C.c_void_p)]
@@ -149,6 +160,7 @@ _PROTOS = {
     "udpdk_gpu_rx_host_async": (C.c_int, [_P, _P, C.c_uint64, _P, _P, _P, C.c_uint32, _P, _P, _P,
                                           C.c_uint32, C.POINTER(RxStats)]),
     "udpdk_gpu_rx_host_wait": (C.c_int, [_P]),
+    "udpdk_gpu_rx_host_batch": (C.c_int, [_P, C.POINTER(RxBatch), C.POINTER(_P)]),
     "udpdk_gpu_rx_gather": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint32, C.c_uint32,
                                       C.POINTER(RxGather)]),
     "udpdk_gpu_frag_table_create": (C.c_int, [_P, C.POINTER(FragTableCfg)]),
@@ -182,7 +194,11 @@ _PROTOS = {
     "udpdk_gpu_context": (_P, []),
     "udpdk_config_set": (C.c_int, [_P, _P, C.c_uint32]),
     "udpdk_config_get": (C.c_int, [_P, _P, C.POINTER(C.c_uint32)]),
-    "udpdk_build_frame": (C.c_ssize_t, [C.c_int, _P, C.c_size_t, _P, C.c_uint32, _P]),
+    "udpdk_config_mtu": (C.c_int, [C.c_uint32]),
+    "udpdk_tx_pending": (C.c_uint64, []),
+    "udpdk_port_attach": (C.c_int, [C.POINTER(PortOps)]),
+    "udpdk_port_detach": (C.c_int, []),
+    "udpdk_port_loopback": (C.c_int, [C.POINTER(PortOps)]),
     "udpdk_slot_table": (C.c_int, [C.POINTER(Slot), C.c_uint32]),
     "udpdk_host_reset": (None, []),
 }
@@ -589,15 +605,6 @@ class HostApi:
     def close(self, s) -> int:
         return self.L.udpdk_close(s)
 
-    def build_frame(self, s, payload: bytes, ip: str, port_host: int) -> bytes:
-        a = C.create_string_buffer(sockaddr_in(ip, port_host), 16)
-        out = C.create_string_buffer(len(payload) + 64)
-        buf = C.create_string_buffer(payload, max(1, len(payload)))
-        n = self.L.udpdk_build_frame(s, buf, len(payload), a, 16, out)
-        if n < 0:
-            raise UdpdkError(f"udpdk_build_frame errno={self.errno()}")
-        return out.raw[:n]
-
     def sendto(self, s, payload: bytes, ip: str, port_host: int, flags: int = 0) -> int:
         a = C.create_string_buffer(sockaddr_in(ip, port_host), 16)
         buf = C.create_string_buffer(payload, max(1, len(payload)))
@@ -615,12 +622,23 @@ class HostApi:
         return n, buf.raw[:n], (ip, port)
 
     def tx_drain(self, max_frames=4096, cap=1 << 22):
+        """Frames built on the GPU from the queued sends (needs udpdk_init)."""
         out = np.zeros(cap, np.uint8)
         off = np.zeros(max_frames, np.uint32)
         ln = np.zeros(max_frames, np.uint16)
         n = C.c_uint32()
-        _check(self.L.udpdk_tx_drain(_ptr(out), cap, _ptr(off), _ptr(ln), max_frames, C.byref(n)), "tx_drain")
+        rc = self.L.udpdk_tx_drain(_ptr(out), cap, _ptr(off), _ptr(ln), max_frames, C.byref(n))
+        if rc != 0:
+            raise UdpdkError(f"udpdk_tx_drain errno={self.errno()}")
         return [bytes(out[off[i]:off[i] + ln[i]]) for i in range(n.value)]
+
+    def tx_pending(self) -> int:
+        return int(self.L.udpdk_tx_pending())
+
+    def slots(self, n: int = 8):
+        t = (Slot * n)()
+        _check(self.L.udpdk_slot_table(t, n), "udpdk_slot_table")
+        return [(t[i].ip, t[i].udp_port, t[i].bound) for i in range(n)]
 
     def config_set(self, src_mac: bytes, dst_mac: bytes, src_ip: str):
         s = C.create_string_buffer(src_mac, 6)

@@ -3,11 +3,16 @@
  *
  * The reference keeps this state in DPDK memzones shared by the app and the forked poller
  * (exch_zone_desc, exch_slots, sock_bind_table: udpdk_globals.c:9-37, udpdk_init.c:226-279).
- * Here app and poller are the same process, so it is plain static memory.
+ * Here the application and the poller are threads of one process: plain static memory, one lock
+ * for the bind table / socket slots (taken by socket, bind, close and by the poller while it
+ * reads the table and fills rings), one for the TX queues, and lock-free single-producer /
+ * single-consumer RX rings between the poller and recvfrom (rte_ring SP/SC, init.c:270-272).
  */
 #ifndef UDPDK_HOST_STATE_H
 #define UDPDK_HOST_STATE_H
 
+#include <pthread.h>
+#include <stdatomic.h>
 #include <stdint.h>
 #include <sys/types.h>
 
@@ -17,28 +22,60 @@
 #define H_SO_REUSEADDR 2
 #define H_SO_REUSEPORT 15
 
-struct h_dgram {             /* one queued datagram (the mbuf a ring entry would point to)   */
-    uint8_t *data;
-    uint32_t len;            /* payload bytes after Ethernet-padding trim                     */
-    uint32_t src_ip;         /* raw */
-    uint32_t src_port;       /* raw */
+#define H_BURST_SIZE     128     /* BURST_SIZE, udpdk_constants.h:41 */
+#define H_UDP_MAX_PAYLOAD 65507  /* 65535 - 20 - 8: the largest datagram fragmentation can carry */
+
+/* A pinned host slab of gathered payloads: one per rx_gather of a poll. Ring entries point into
+ * it; the last recvfrom of its datagrams returns it to the pool (the mbuf pool's role). */
+struct h_arena {
+    uint8_t  *payload;           /* cap_n slots of slot_bytes                                    */
+    uint32_t *len;               /* [cap_n] payload bytes                                        */
+    uint32_t *src_ip;            /* [cap_n] raw                                                  */
+    uint16_t *src_port;          /* [cap_n] raw                                                  */
+    uint64_t  cap_bytes;
+    uint32_t  cap_n;
+    uint32_t  slot_bytes;
+    atomic_uint refs;            /* queued datagrams still pointing into this slab               */
+    struct h_arena *next;        /* free list                                                    */
 };
 
-struct h_ring {              /* SP/SC ring of EXCH_RING_SIZE entries (udpdk_init.c:268-277)   */
+struct h_dgram {                 /* one queued datagram (the mbuf a ring entry would point to)   */
+    const uint8_t *data;
+    uint32_t len;                /* payload bytes after Ethernet-padding trim                    */
+    uint32_t src_ip;             /* raw */
+    uint32_t src_port;           /* raw */
+    struct h_arena *arena;
+};
+
+struct h_ring {                  /* SP/SC ring of EXCH_RING_SIZE entries (udpdk_init.c:268-277)  */
     struct h_dgram *e;
-    uint32_t head, tail;     /* tail - head = entries */
+    _Atomic uint32_t head;       /* consumer (recvfrom) */
+    _Atomic uint32_t tail;       /* producer (the poller); tail - head = entries */
 };
 
-struct h_slot {              /* exch_slot_info (udpdk_types.h:40-47) + bind list links        */
+struct h_txd {                   /* one sendto waiting for the poller's TX half                  */
+    uint64_t pay;                /* offset of its payload in g_udpdk.txp                         */
+    uint32_t len;
+    uint32_t dst_ip;             /* raw */
+    uint32_t dst_port;           /* raw */
+};
+
+struct h_txq {                   /* per-socket TX ring (exch_slots[s].tx_q, EXCH_RING_SIZE)      */
+    struct h_txd *e;
+    uint32_t head, tail;         /* under tx_lock */
+};
+
+struct h_slot {                  /* exch_slot_info (udpdk_types.h:40-47) + bind list links        */
     int      used;
     int      bound;
-    uint32_t udp_port;       /* raw */
-    uint32_t ip;             /* raw */
+    uint32_t udp_port;           /* raw */
+    uint32_t ip;                 /* raw */
     int      so_options;
     /* binding (at most one per socket): node of its port's list */
     int32_t  prev, next;
     uint8_t  reuse_addr, reuse_port;
     struct h_ring rx;
+    struct h_txq  tx;
 };
 
 struct h_state {
@@ -47,29 +84,53 @@ struct h_state {
     uint16_t port_len[65536];
     uint64_t n_active;
     uint64_t version;
-    volatile int interrupted;
+    atomic_int interrupted;
+    pthread_mutex_t lock;        /* bind table + socket slots + the poller's use of them        */
+    pthread_mutex_t tx_lock;     /* TX rings + payload store                                    */
+    pthread_mutex_t arena_lock;  /* arena free list                                             */
     uint8_t  src_mac[6], dst_mac[6];
     uint32_t src_ip;
+    uint32_t mtu;                /* IPV4_MTU_DEFAULT = RTE_ETHER_MTU (udpdk_constants.h:37)      */
     udpdk_gpu_ctx *gpu;
     int      gpu_device;
     uint32_t gpu_max_frames, gpu_max_lanes;
-    uint64_t snap_version;   /* version uploaded to the GPU (UINT64_MAX = none) */
+    /* bind snapshot as uploaded to the GPU: rebuilt only when the table's version moves */
+    uint64_t snap_version;       /* version uploaded (UINT64_MAX = none)                        */
     int      snap_compat;
+    uint32_t snap_lanes, snap_maxfan;
     /* fragments (udpdk_poller.c:338-361): the device reassembly table, created on the first
      * FRAG frame; geometry from the [gpu] frag_* ini keys (defaults: the poller's table) */
     int      frag_ready;
     uint32_t frag_buckets, frag_entries, frag_max_dgram;
     uint64_t frag_ttl_ms;
-    void    *fd_frames, *fd_offset, *fd_length, *fd_meta;      /* device copies, grow-only */
-    uint64_t fd_frames_cap;
-    uint32_t fd_n_cap;
-    void    *fd_meta2, *fd_loff2, *fd_lpkt2;
-    uint32_t fd_out_cap;
-    /* TX queue of built frames (the tx_q rings + TX half of the poller, poller.c:452-514) */
-    uint8_t *txq;
-    uint64_t txq_bytes, txq_cap;
-    uint32_t *txq_len;
-    uint32_t txq_n, txq_ncap;
+    /* RX work buffers (poller thread only), grow-only */
+    uint32_t *rx_meta, *rx_loff, *rx_lpkt;
+    uint64_t  rx_meta_cap, rx_loff_cap, rx_lpkt_cap;
+    uint32_t *fr_loff, *fr_lpkt, *fr_org;        /* reassembled datagrams: lanes, origins     */
+    uint16_t *fr_len;
+    uint64_t  fr_loff_cap, fr_lpkt_cap, fr_org_cap, fr_len_cap;
+    uint32_t *acc_d, *acc_f;                     /* accepted entries: frame / datagram index   */
+    uint32_t *acc_sock;                          /* per accepted entry: socket | from-frag<<31 */
+    uint64_t  acc_d_cap, acc_f_cap, acc_sock_cap;
+    void     *dv_acc, *dv_pay, *dv_len, *dv_sip, *dv_spt;   /* device: gather list + outputs */
+    uint64_t  dv_acc_cap, dv_pay_cap, dv_len_cap, dv_sip_cap, dv_spt_cap;
+    void     *dv_meta2, *dv_loff2, *dv_lpkt2;              /* device: RX of reassembled batch */
+    uint64_t  dv_meta2_cap, dv_loff2_cap, dv_lpkt2_cap;
+    struct h_arena *arena_free;
+    /* TX: per-socket rings of struct h_txd + the payload store they point into */
+    uint8_t  *txp;
+    uint64_t  txp_bytes, txp_cap;
+    uint64_t  tx_queued;                         /* datagrams in all TX rings                   */
+    /* TX work buffers (tx_drain), grow-only: host pinned staging + device */
+    void     *tx_h, *tx_d, *tx_fr_d;
+    uint64_t  tx_h_cap, tx_d_cap, tx_fr_d_cap;
+    struct h_txsel { int32_t s; uint32_t nf; uint64_t foff; } *tx_sel;
+    uint64_t  tx_sel_cap;
+    /* poller thread (udpdk_port_attach) */
+    pthread_t poller;
+    atomic_int poller_run;
+    int       poller_started;
+    udpdk_port_ops_t port;
 };
 
 extern struct h_state g_udpdk;
@@ -82,8 +143,21 @@ int  h_btable_free_port(void);
 
 /* sock_api.c */
 void h_sockets_reset(void);
-ssize_t h_build_frame(int sockfd, const void *buf, size_t len, uint32_t dst_ip,
-                      uint32_t dst_port, uint8_t *out);
-int  h_ring_push_bulk(struct h_ring *r, struct h_dgram *d, uint32_t n);
+uint32_t h_ring_free(const struct h_ring *r);
+int  h_ring_push_bulk(struct h_ring *r, const struct h_dgram *d, uint32_t n);
+struct h_arena *h_arena_get(uint32_t n, uint32_t slot_bytes);
+void h_arena_put(struct h_arena *a);
+void h_arena_release(struct h_arena *a, uint32_t refs);
+void h_arenas_free_all(void);
+void h_tx_reset(void);
+
+/* rx_poll.c */
+int  h_snapshot_refresh(void);            /* under g_udpdk.lock */
+void h_rx_buffers_free(void);
+int  h_grow_dev(void **p, uint64_t *cap, uint64_t need);
+int  h_grow_host(void **p, uint64_t *cap, uint64_t need);
+
+/* tx_drain.c */
+void h_tx_buffers_free(void);
 
 #endif

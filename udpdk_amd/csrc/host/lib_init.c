@@ -1,16 +1,17 @@
 /*
- * lib_init.c — udpdk_init / udpdk_interrupt / udpdk_cleanup, configuration, and the GPU poller
- * entry point udpdk_poll_rx.
+ * lib_init.c — udpdk_init / udpdk_interrupt / udpdk_cleanup, configuration, and the poller
+ * thread with its ports (udpdk_port_attach, the built-in loopback port).
  *
  * udpdk_init follows udpdk_init.c:282-371 minus the DPDK bring-up: parse the .ini the same way
- * (udpdk_args.c:21-49, 122-163), then create the GPU context instead of forking a poller.
- * udpdk_poll_rx stands in for one turn of poller_body's RX half (udpdk_poller.c:516-545): the
- * frames are classified and demultiplexed on the GPU, then each socket's deliveries are appended
- * to its RX ring in arrival order, all-or-nothing per socket (flush_rx_queue, :274-292).
+ * (udpdk_args.c:21-49, 122-163), then create the GPU context instead of forking a poller. The
+ * poller itself is a thread started by udpdk_port_attach (poller_body, udpdk_poller.c:448-546,
+ * against a port given as callbacks); its RX half is udpdk_poll_rx (rx_poll.c), its TX half
+ * udpdk_tx_drain (tx_drain.c).
  */
 #include <arpa/inet.h>
 #include <ctype.h>
 #include <errno.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -20,6 +21,10 @@
 
 __attribute__((constructor)) static void h_lib_load(void)
 {
+    pthread_mutex_init(&g_udpdk.lock, NULL);
+    pthread_mutex_init(&g_udpdk.tx_lock, NULL);
+    pthread_mutex_init(&g_udpdk.arena_lock, NULL);
+    g_udpdk.mtu = 1500;                /* IPV4_MTU_DEFAULT = RTE_ETHER_MTU */
     h_btable_reset();
     h_sockets_reset();
     g_udpdk.snap_version = UINT64_MAX;
@@ -33,12 +38,16 @@ __attribute__((constructor)) static void h_lib_load(void)
 
 void udpdk_host_reset(void)
 {
+    udpdk_port_detach();
+    pthread_mutex_lock(&g_udpdk.lock);
+    pthread_mutex_lock(&g_udpdk.tx_lock);
     h_btable_reset();
     h_sockets_reset();
-    g_udpdk.interrupted = 0;
-    g_udpdk.txq_bytes = 0;
-    g_udpdk.txq_n = 0;
+    pthread_mutex_unlock(&g_udpdk.tx_lock);
+    atomic_store(&g_udpdk.interrupted, 0);
     g_udpdk.snap_version = UINT64_MAX;
+    g_udpdk.mtu = 1500;
+    pthread_mutex_unlock(&g_udpdk.lock);
 }
 
 static int h_parse_mac(const char *v, uint8_t mac[6])
@@ -87,6 +96,8 @@ static int h_load_ini(const char *path)
             g_udpdk.src_ip = inet_addr(v);
         } else if (!strcmp(section, "port0_dst") && !strcmp(k, "mac_addr")) {
             if (h_parse_mac(v, g_udpdk.dst_mac)) { rc = -1; break; }
+        } else if (!strcmp(section, "port0") && !strcmp(k, "mtu")) {
+            if (udpdk_config_mtu((uint32_t)strtoul(v, NULL, 0))) { rc = -1; break; }
         } else if (!strcmp(section, "gpu") && !strcmp(k, "device")) {
             g_udpdk.gpu_device = atoi(v);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "max_frames")) {
@@ -127,34 +138,32 @@ int udpdk_init(int argc, char *argv[])
 void udpdk_interrupt(int signum)
 {
     (void)signum;
-    g_udpdk.interrupted = 1;
+    atomic_store(&g_udpdk.interrupted, 1);
 }
 
 void udpdk_cleanup(void)
 {
+    udpdk_port_detach();
     for (int s = 0; s < UDPDK_MAX_SOCKETS; s++)
         if (g_udpdk.slots[s].used) udpdk_close(s);
-    void **dev[] = {&g_udpdk.fd_frames, &g_udpdk.fd_offset, &g_udpdk.fd_length, &g_udpdk.fd_meta,
-                    &g_udpdk.fd_meta2, &g_udpdk.fd_loff2, &g_udpdk.fd_lpkt2};
-    for (unsigned k = 0; k < sizeof(dev) / sizeof(dev[0]); k++) {
-        if (*dev[k] && g_udpdk.gpu) udpdk_gpu_free(g_udpdk.gpu, *dev[k]);
-        *dev[k] = NULL;
-    }
-    g_udpdk.fd_frames_cap = 0;
-    g_udpdk.fd_n_cap = 0;
+    h_tx_reset();
+    h_rx_buffers_free();
+    h_tx_buffers_free();
+    h_arenas_free_all();
     g_udpdk.frag_ready = 0;
     udpdk_gpu_ctx_destroy(g_udpdk.gpu);
     g_udpdk.gpu = NULL;
-    free(g_udpdk.txq);
-    free(g_udpdk.txq_len);
-    g_udpdk.txq = NULL;
-    g_udpdk.txq_len = NULL;
-    g_udpdk.txq_bytes = g_udpdk.txq_cap = 0;
-    g_udpdk.txq_n = g_udpdk.txq_ncap = 0;
     g_udpdk.snap_version = UINT64_MAX;
 }
 
 udpdk_gpu_ctx *udpdk_gpu_context(void) { return g_udpdk.gpu; }
+
+int udpdk_config_mtu(uint32_t mtu)
+{
+    if (mtu < 68u || mtu > 9000u || (mtu - 20u) % 8u) { errno = EINVAL; return -1; }
+    g_udpdk.mtu = mtu;
+    return 0;
+}
 
 int udpdk_config_set(const uint8_t src_mac[6], const uint8_t dst_mac[6], uint32_t src_ip)
 {
@@ -188,209 +197,141 @@ void udpdk_dump_payload(const char *payload, int len)
     }
 }
 
-/* recvfrom's payload rule (udpdk_syscall.c:438, :459-466): min(data_len - 42, dgram_len - 8)
- * bytes from frame byte 42 (Ethernet padding trimmed), source address from the headers. */
-static int h_make_dgram(const uint8_t *f, uint32_t flen, struct h_dgram *d)
+/* ---- the poller thread (poller_body, udpdk_poller.c:448-546) ------------------------------- */
+static void *h_poller_main(void *arg)
 {
-    const uint16_t dl = (uint16_t)(((uint32_t)f[38] << 8) | f[39]);
-    const uint16_t pl = (uint16_t)(dl - 8u);
-    uint32_t plen = flen - 42u;
-    if (plen > pl) plen = pl;
-    d->len = plen;
-    d->data = malloc(plen ? plen : 1);
-    if (!d->data) return -1;
-    memcpy(d->data, f + 42, plen);
-    memcpy(&d->src_ip, f + 26, 4);
-    d->src_port = (uint32_t)f[34] | ((uint32_t)f[35] << 8);
-    return 0;
-}
-
-static uint64_t h_now_ms(void)
-{
-    struct timespec ts;
-    clock_gettime(CLOCK_MONOTONIC, &ts);
-    return (uint64_t)ts.tv_sec * 1000u + (uint64_t)ts.tv_nsec / 1000000u;
-}
-
-static int h_grow_dev(void **p, uint64_t *cap, uint64_t need)
-{
-    if (*p && *cap >= need) return 0;
-    if (*p) udpdk_gpu_free(g_udpdk.gpu, *p);
-    *p = NULL;
-    *cap = 0;
-    const int rc = udpdk_gpu_alloc(g_udpdk.gpu, need ? need : 16, p);
-    if (rc) { errno = -rc; return -1; }
-    *cap = need;
-    return 0;
-}
-
-/* The batch's FRAG frames (udpdk_poller.c:338-361) through the device reassembly table, then the
- * completed datagrams through the demux. Out: per-lane delivery ranges f_off[lanes + 1], each
- * delivery's arrival index (that of the fragment that completed its datagram: where the
- * reference delivers it) and its payload. Nothing is allocated when there is no datagram. */
-static int h_frag_pass(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *offset,
-                       const uint16_t *length, const uint32_t *meta, uint32_t n, uint32_t lanes,
-                       uint32_t maxfan, uint32_t **f_off, uint32_t **f_idx, struct h_dgram **f_d)
-{
-    *f_off = NULL; *f_idx = NULL; *f_d = NULL;
-    uint32_t nfrag = 0;
-    for (uint32_t i = 0; i < n; i++) nfrag += (meta[i] & 0xFu) == UDPDK_V_FRAG;
-    if (!nfrag) return 0;
-    udpdk_gpu_ctx *g = g_udpdk.gpu;
-    int rc;
-    if (!g_udpdk.frag_ready) {
-        udpdk_frag_table_cfg_t fc = {g_udpdk.frag_buckets, g_udpdk.frag_entries, g_udpdk.frag_ttl_ms,
-                                     g_udpdk.frag_max_dgram};
-        rc = udpdk_gpu_frag_table_create(g, &fc);
-        if (rc) { errno = -rc; return -1; }
-        g_udpdk.frag_ready = 1;
-    }
-    if (h_grow_dev(&g_udpdk.fd_frames, &g_udpdk.fd_frames_cap, frames_bytes + UDPDK_GPU_FRAMES_TAILROOM)) return -1;
-    if (n > g_udpdk.fd_n_cap) {
-        uint64_t c0 = 0, c1 = 0, c2 = 0;
-        if (h_grow_dev(&g_udpdk.fd_offset, &c0, 4ull * n) || h_grow_dev(&g_udpdk.fd_length, &c1, 2ull * n) ||
-            h_grow_dev(&g_udpdk.fd_meta, &c2, 4ull * n))
-            return -1;
-        g_udpdk.fd_n_cap = n;
-    }
-    if ((rc = udpdk_gpu_h2d(g, g_udpdk.fd_frames, frames, frames_bytes)) ||
-        (rc = udpdk_gpu_h2d(g, g_udpdk.fd_offset, offset, 4ull * n)) ||
-        (rc = udpdk_gpu_h2d(g, g_udpdk.fd_length, length, 2ull * n)) ||
-        (rc = udpdk_gpu_h2d(g, g_udpdk.fd_meta, meta, 4ull * n))) {
-        errno = -rc;
-        return -1;
-    }
-    udpdk_rx_batch_t b = {g_udpdk.fd_frames, frames_bytes, g_udpdk.fd_offset, g_udpdk.fd_length, NULL, n};
-    udpdk_reasm_out_t ro;
-    if ((rc = udpdk_gpu_rx_reassemble(g, &b, g_udpdk.fd_meta, h_now_ms(), &ro))) { errno = -rc; return -1; }
-    const uint32_t C = ro.batch.n;
-    if (!C) return 0;
-    const uint64_t cap64 = (uint64_t)C * maxfan;
-    const uint32_t cap = cap64 > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)cap64;
-    uint64_t m0 = 0, m1 = 0, m2 = 0;
-    if (h_grow_dev(&g_udpdk.fd_meta2, &m0, 4ull * C) || h_grow_dev(&g_udpdk.fd_loff2, &m1, 4ull * (lanes + 1)) ||
-        h_grow_dev(&g_udpdk.fd_lpkt2, &m2, 4ull * cap))
-        return -1;
-    udpdk_rx_out_t o2 = {g_udpdk.fd_meta2, g_udpdk.fd_loff2, g_udpdk.fd_lpkt2, cap};
-    udpdk_rx_stats_t st2;
-    if ((rc = udpdk_gpu_rx(g, &ro.batch, &o2))) { errno = -rc; return -1; }
-    if ((rc = udpdk_gpu_rx_stats(g, &st2))) { errno = -rc; return -1; }
-    const uint32_t D = st2.deliveries;
-    uint32_t *loff = malloc(4ull * (lanes + 1)), *lpkt = malloc(4ull * (D + 1));
-    uint32_t *org = malloc(4ull * C), *roff = malloc(4ull * C);
-    uint16_t *rlen = malloc(2ull * C);
-    uint8_t *rfr = malloc(ro.batch.frames_bytes + 1);
-    uint32_t *idx = malloc(4ull * (D + 1));
-    struct h_dgram *dg = calloc(D + 1, sizeof(*dg));
-    int ret = -1;
-    if (!loff || !lpkt || !org || !roff || !rlen || !rfr || !idx || !dg) { errno = ENOMEM; goto out; }
-    if ((rc = udpdk_gpu_d2h(g, loff, g_udpdk.fd_loff2, 4ull * (lanes + 1))) ||
-        (rc = udpdk_gpu_d2h(g, lpkt, g_udpdk.fd_lpkt2, 4ull * D)) ||
-        (rc = udpdk_gpu_d2h(g, org, ro.origin_dev, 4ull * C)) ||
-        (rc = udpdk_gpu_d2h(g, roff, ro.batch.offset_dev, 4ull * C)) ||
-        (rc = udpdk_gpu_d2h(g, rlen, ro.batch.length_dev, 2ull * C)) ||
-        (rc = udpdk_gpu_d2h(g, rfr, ro.batch.frames_dev, ro.batch.frames_bytes)) ||
-        (rc = udpdk_gpu_sync(g))) {
-        errno = -rc;
-        goto out;
-    }
-    for (uint32_t e = 0; e < D; e++) {
-        const uint32_t r = lpkt[e];
-        idx[e] = org[r];
-        if (h_make_dgram(rfr + roff[r], rlen[r], &dg[e])) {
-            for (uint32_t z = 0; z < e; z++) free(dg[z].data);
-            errno = ENOMEM;
-            goto out;
+    (void)arg;
+    const udpdk_port_ops_t *P = &g_udpdk.port;
+    const uint32_t nb = P->batch_frames ? P->batch_frames : 4096;
+    const uint64_t cap = (uint64_t)nb * 2048 + UDPDK_GPU_FRAMES_TAILROOM;
+    /* the RX buffer is pinned (a NIC's DMA target): udpdk_poll_rx's H2D reads it directly */
+    uint8_t *rx = NULL, *tx = malloc(cap);
+    if (udpdk_gpu_host_alloc(g_udpdk.gpu, cap, (void **)&rx)) rx = NULL;
+    uint32_t *roff = malloc(4ull * nb), *toff = malloc(4ull * nb);
+    uint16_t *rlen = malloc(2ull * nb), *tlen = malloc(2ull * nb);
+    while (rx && tx && roff && toff && rlen && tlen &&
+           atomic_load_explicit(&g_udpdk.poller_run, memory_order_acquire)) {
+        int idle = 1;
+        /* TX half first, as the poller loop does */
+        uint32_t nt = 0;
+        if (P->tx_burst && udpdk_tx_pending() && udpdk_tx_drain(tx, cap, toff, tlen, nb, &nt) == 0 && nt) {
+            P->tx_burst(P->user, tx, toff, tlen, nt);
+            idle = 0;
         }
-    }
-    *f_off = loff; loff = NULL;
-    *f_idx = idx; idx = NULL;
-    *f_d = dg; dg = NULL;
-    ret = 0;
-out:
-    free(loff); free(lpkt); free(org); free(roff); free(rlen); free(rfr); free(idx); free(dg);
-    return ret;
-}
-
-int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *offset,
-                  const uint16_t *length, const uint32_t *ptype, uint32_t n,
-                  udpdk_rx_stats_t *stats_out)
-{
-    if (!g_udpdk.gpu) { errno = ENODEV; return -1; }
-    if (n && (!frames || !offset || !length)) { errno = EINVAL; return -1; }
-    if (g_udpdk.snap_version != g_udpdk.version) {
-        udpdk_bind_snapshot_t snap;
-        if (udpdk_btable_snapshot(&snap, 0)) return -1;
-        const int rc = udpdk_gpu_bind_snapshot_upload(g_udpdk.gpu, &snap);
-        if (rc) { errno = -rc; return -1; }
-        g_udpdk.snap_version = g_udpdk.version;
-    }
-    udpdk_bind_snapshot_t cur;
-    if (udpdk_btable_snapshot(&cur, 0)) return -1;
-    const uint32_t lanes = cur.n_lanes;
-    uint32_t maxfan = 1;
-    for (uint32_t p = 0; p < 65536; p++)
-        if (cur.port_count[p] > maxfan) maxfan = cur.port_count[p];
-    const uint64_t cap64 = (uint64_t)n * maxfan;
-    const uint32_t cap = cap64 > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)cap64;
-    uint32_t *meta = malloc(((size_t)n + 1) * 4);
-    uint32_t *loff = malloc(((size_t)lanes + 1) * 4);
-    uint32_t *lpkt = malloc(((size_t)cap + 1) * 4);
-    uint32_t *f_off = NULL, *f_idx = NULL;
-    struct h_dgram *f_d = NULL;
-    int ret = -1;
-    udpdk_rx_stats_t st;
-    if (!meta || !loff || !lpkt) { errno = ENOMEM; goto out; }
-    int rc = udpdk_gpu_rx_host(g_udpdk.gpu, frames, frames_bytes, offset, length, ptype, n, meta,
-                               loff, lpkt, cap, &st);
-    if (rc) { errno = -rc; goto out; }
-    if (h_frag_pass(frames, frames_bytes, offset, length, meta, n, lanes, maxfan, &f_off, &f_idx, &f_d))
-        goto out;
-    for (uint32_t s = 0; s < lanes && s < UDPDK_MAX_SOCKETS; s++) {
-        const uint32_t a = loff[s], b = loff[s + 1];
-        const uint32_t fa = f_off ? f_off[s] : 0u, fb = f_off ? f_off[s + 1] : 0u;
-        if (a == b && fa == fb) continue;
-        if (!g_udpdk.slots[s].used) {
-            for (uint32_t e = fa; e < fb; e++) { free(f_d[e].data); f_d[e].data = NULL; }
-            continue;
-        }
-        const uint32_t total = (b - a) + (fb - fa);
-        struct h_dgram *d = calloc(total, sizeof(*d));
-        if (!d) { errno = ENOMEM; goto out; }
-        /* direct deliveries (frame index) and reassembled ones (index of the completing
-         * fragment) merged in arrival order: the order the reference's rings receive them */
-        uint32_t k = 0, e = a, q = fa;
-        while (e < b || q < fb) {
-            if (q >= fb || (e < b && lpkt[e] < f_idx[q])) {
-                if (h_make_dgram(frames + offset[lpkt[e]], length[lpkt[e]], &d[k])) {
-                    for (uint32_t z = 0; z < k; z++) free(d[z].data);
-                    free(d);
-                    errno = ENOMEM;
-                    goto out;
-                }
-                e++;
-            } else {
-                d[k] = f_d[q];
-                f_d[q].data = NULL;
-                q++;
+        if (P->rx_burst) {
+            const uint32_t n = P->rx_burst(P->user, rx, cap - UDPDK_GPU_FRAMES_TAILROOM, roff, rlen, nb);
+            if (n) {
+                uint64_t fb = 0;
+                for (uint32_t i = 0; i < n; i++)
+                    if ((uint64_t)roff[i] + rlen[i] > fb) fb = (uint64_t)roff[i] + rlen[i];
+                udpdk_poll_rx(rx, fb, roff, rlen, NULL, n, NULL);
+                idle = 0;
             }
-            k++;
         }
-        if (h_ring_push_bulk(&g_udpdk.slots[s].rx, d, k)) {
-            for (uint32_t z = 0; z < k; z++) free(d[z].data);   /* ring full: drop the batch */
-        }
-        free(d);
+        if (idle) sched_yield();
     }
-    if (stats_out) *stats_out = st;
-    ret = 0;
-out:
-    if (f_d && f_off)
-        for (uint32_t e = 0; e < f_off[lanes]; e++) free(f_d[e].data);
-    free(f_off);
-    free(f_idx);
-    free(f_d);
-    free(meta);
-    free(loff);
-    free(lpkt);
-    return ret;
+    if (rx) udpdk_gpu_host_free(g_udpdk.gpu, rx);
+    free(tx); free(roff); free(toff); free(rlen); free(tlen);
+    return NULL;
+}
+
+int udpdk_port_attach(const udpdk_port_ops_t *ops)
+{
+    if (!ops || (!ops->rx_burst && !ops->tx_burst)) { errno = EINVAL; return -1; }
+    if (!g_udpdk.gpu) { errno = ENODEV; return -1; }
+    if (g_udpdk.poller_started) { errno = EBUSY; return -1; }
+    g_udpdk.port = *ops;
+    atomic_store(&g_udpdk.poller_run, 1);
+    if (pthread_create(&g_udpdk.poller, NULL, h_poller_main, NULL)) {
+        atomic_store(&g_udpdk.poller_run, 0);
+        errno = EAGAIN;
+        return -1;
+    }
+    g_udpdk.poller_started = 1;
+    return 0;
+}
+
+int udpdk_port_detach(void)
+{
+    if (!g_udpdk.poller_started) return 0;
+    atomic_store(&g_udpdk.poller_run, 0);
+    pthread_join(g_udpdk.poller, NULL);
+    g_udpdk.poller_started = 0;
+    return 0;
+}
+
+/* Loopback port: a FIFO of frames; tx_burst appends copies, rx_burst hands them back. */
+static struct {
+    pthread_mutex_t mu;
+    uint8_t *buf;
+    uint64_t bytes, cap, head;
+    uint32_t *len;                /* frame lengths in FIFO order */
+    uint64_t n, ncap, nhead;
+} h_lo = {PTHREAD_MUTEX_INITIALIZER, NULL, 0, 0, 0, NULL, 0, 0, 0};
+
+static void h_lo_tx(void *user, const uint8_t *frames, const uint32_t *off, const uint16_t *len, uint32_t n)
+{
+    (void)user;
+    pthread_mutex_lock(&h_lo.mu);
+    for (uint32_t i = 0; i < n; i++) {
+        if (h_lo.bytes + len[i] > h_lo.cap) {
+            const uint64_t live = h_lo.bytes - h_lo.head;        /* compact, then grow */
+            memmove(h_lo.buf, h_lo.buf + h_lo.head, live);
+            h_lo.bytes = live;
+            h_lo.head = 0;
+            if (h_lo.bytes + len[i] > h_lo.cap) {
+                uint64_t nc = h_lo.cap ? 2 * h_lo.cap : (1u << 20);
+                while (nc < h_lo.bytes + len[i]) nc *= 2;
+                uint8_t *nbuf = realloc(h_lo.buf, nc);
+                if (!nbuf) break;
+                h_lo.buf = nbuf;
+                h_lo.cap = nc;
+            }
+        }
+        if (h_lo.n == h_lo.ncap) {
+            const uint64_t live = h_lo.n - h_lo.nhead;
+            memmove(h_lo.len, h_lo.len + h_lo.nhead, live * sizeof(uint32_t));
+            h_lo.n = live;
+            h_lo.nhead = 0;
+            if (h_lo.n == h_lo.ncap) {
+                const uint64_t nc = h_lo.ncap ? 2 * h_lo.ncap : 4096;
+                uint32_t *nl = realloc(h_lo.len, nc * sizeof(uint32_t));
+                if (!nl) break;
+                h_lo.len = nl;
+                h_lo.ncap = nc;
+            }
+        }
+        memcpy(h_lo.buf + h_lo.bytes, frames + off[i], len[i]);
+        h_lo.bytes += len[i];
+        h_lo.len[h_lo.n++] = len[i];
+    }
+    pthread_mutex_unlock(&h_lo.mu);
+}
+
+static uint32_t h_lo_rx(void *user, uint8_t *frames, uint64_t cap, uint32_t *off, uint16_t *len, uint32_t max)
+{
+    (void)user;
+    pthread_mutex_lock(&h_lo.mu);
+    uint32_t k = 0;
+    uint64_t pos = 0;
+    while (k < max && h_lo.nhead < h_lo.n && pos + h_lo.len[h_lo.nhead] <= cap) {
+        const uint32_t l = h_lo.len[h_lo.nhead++];
+        memcpy(frames + pos, h_lo.buf + h_lo.head, l);
+        h_lo.head += l;
+        off[k] = (uint32_t)pos;
+        len[k] = (uint16_t)l;
+        pos += l;
+        k++;
+    }
+    pthread_mutex_unlock(&h_lo.mu);
+    return k;
+}
+
+int udpdk_port_loopback(udpdk_port_ops_t *ops)
+{
+    if (!ops) { errno = EINVAL; return -1; }
+    memset(ops, 0, sizeof(*ops));
+    ops->rx_burst = h_lo_rx;
+    ops->tx_burst = h_lo_tx;
+    return 0;
 }

@@ -1,14 +1,21 @@
 /*
- * sock_api.c — the socket calls of udpdk_api.h.
+ * sock_api.c — the socket calls of udpdk_api.h, the RX rings and payload slabs, the TX rings.
  *
  * Argument validation, errno values and slot state transitions follow udpdk_syscall.c
  * (socket :23-81, get/setsockopt :83-192, bind :194-245, sendto :247-368, recvfrom :370-488,
  * close :490-521). Deliberate fixes: close decrements the active count (the reference
- * increments it, :519) and sendto refuses payloads that would not fit the
- * reference's 2048-byte mbuf data room unfragmented (EMSGSIZE, §8 Q14).
+ * increments it, :519), and sendto accepts payloads up to 65507 bytes, which
+ * the poller's TX fragmentation carries (the reference writes past its 2048-byte mbuf above
+ * 2006 bytes, §8 Q14); larger ones get EMSGSIZE.
+ *
+ * sendto does what the reference's sendto does short of building the frame: validate, auto-bind,
+ * queue the datagram on the socket's TX ring (ENOBUFS when full, :356-365). The frame is built
+ * on the GPU by the poller's TX half (udpdk_tx_drain). recvfrom pops the socket's RX ring and
+ * copies the payload out of the pinned slab the poller gathered it into on the GPU.
  */
 #include <errno.h>
 #include <netinet/in.h>
+#include <sched.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -16,65 +23,189 @@
 
 struct h_state g_udpdk;
 
-#define H_MAX_PAYLOAD 1458   /* largest datagram sent unfragmented: 1500 - 42 (poller.c:461) */
-
 static int h_valid_fd(int s) { return s >= 0 && s < UDPDK_MAX_SOCKETS; }
 
+/* ---- RX rings: single producer (the poller), single consumer (recvfrom) ------------------- */
 static void h_ring_clear(struct h_ring *r)
 {
     if (r->e) {
-        for (uint32_t i = r->head; i != r->tail; i++) free(r->e[i % UDPDK_RX_RING_SIZE].data);
+        const uint32_t t = atomic_load_explicit(&r->tail, memory_order_acquire);
+        for (uint32_t i = atomic_load_explicit(&r->head, memory_order_relaxed); i != t; i++)
+            h_arena_release(r->e[i % UDPDK_RX_RING_SIZE].arena, 1);
         free(r->e);
     }
     r->e = NULL;
-    r->head = r->tail = 0;
+    atomic_store_explicit(&r->head, 0, memory_order_relaxed);
+    atomic_store_explicit(&r->tail, 0, memory_order_relaxed);
+}
+
+/* Entries the producer may still add (usable size = size - 1, as rte_ring). */
+uint32_t h_ring_free(const struct h_ring *r)
+{
+    const uint32_t h = atomic_load_explicit(&r->head, memory_order_acquire);
+    const uint32_t t = atomic_load_explicit(&r->tail, memory_order_relaxed);
+    return (UDPDK_RX_RING_SIZE - 1) - (t - h);
+}
+
+/* All-or-nothing append of n datagrams (rte_ring_enqueue_bulk, poller.c:287-290): the entries
+ * are written first, then published by a release store of tail that recvfrom acquires. */
+int h_ring_push_bulk(struct h_ring *r, const struct h_dgram *d, uint32_t n)
+{
+    if (!r->e) {
+        r->e = calloc(UDPDK_RX_RING_SIZE, sizeof(*r->e));
+        if (!r->e) return -1;
+    }
+    if (n > h_ring_free(r)) return -1;
+    const uint32_t t = atomic_load_explicit(&r->tail, memory_order_relaxed);
+    for (uint32_t i = 0; i < n; i++) r->e[(t + i) % UDPDK_RX_RING_SIZE] = d[i];
+    atomic_store_explicit(&r->tail, t + n, memory_order_release);
+    return 0;
+}
+
+/* ---- payload slabs ------------------------------------------------------------------------ */
+static void h_arena_destroy(struct h_arena *a)
+{
+    if (!a) return;
+    void *p[] = {a->payload, a->len, a->src_ip, a->src_port};
+    for (unsigned k = 0; k < 4; k++)
+        if (p[k]) {
+            if (g_udpdk.gpu) udpdk_gpu_host_free(g_udpdk.gpu, p[k]);
+        }
+    free(a);
+}
+
+/* A slab for n datagrams of slot_bytes: the first free one that is large enough, else a new one
+ * (pinned, so the gather's D2H is a straight DMA). */
+struct h_arena *h_arena_get(uint32_t n, uint32_t slot_bytes)
+{
+    const uint64_t need = (uint64_t)n * slot_bytes;
+    pthread_mutex_lock(&g_udpdk.arena_lock);
+    struct h_arena **pp = &g_udpdk.arena_free, *a = NULL;
+    for (; *pp; pp = &(*pp)->next)
+        if ((*pp)->cap_bytes >= need && (*pp)->cap_n >= n) {
+            a = *pp;
+            *pp = a->next;
+            break;
+        }
+    pthread_mutex_unlock(&g_udpdk.arena_lock);
+    if (!a) {
+        a = calloc(1, sizeof(*a));
+        if (!a) return NULL;
+        const uint32_t cn = n < 4096 ? 4096 : n;
+        const uint64_t cb = need < ((uint64_t)cn * 64) ? (uint64_t)cn * 64 : need;
+        if (udpdk_gpu_host_alloc(g_udpdk.gpu, cb, (void **)&a->payload) ||
+            udpdk_gpu_host_alloc(g_udpdk.gpu, 4ull * cn, (void **)&a->len) ||
+            udpdk_gpu_host_alloc(g_udpdk.gpu, 4ull * cn, (void **)&a->src_ip) ||
+            udpdk_gpu_host_alloc(g_udpdk.gpu, 2ull * cn, (void **)&a->src_port)) {
+            h_arena_destroy(a);
+            return NULL;
+        }
+        a->cap_bytes = cb;
+        a->cap_n = cn;
+    }
+    a->slot_bytes = slot_bytes;
+    a->next = NULL;
+    atomic_store_explicit(&a->refs, 0, memory_order_relaxed);
+    return a;
+}
+
+void h_arena_put(struct h_arena *a)
+{
+    pthread_mutex_lock(&g_udpdk.arena_lock);
+    a->next = g_udpdk.arena_free;
+    g_udpdk.arena_free = a;
+    pthread_mutex_unlock(&g_udpdk.arena_lock);
+}
+
+/* Drop refs references (recvfrom of one datagram, or a ring cleared by close); the last one
+ * returns the slab to the pool. */
+void h_arena_release(struct h_arena *a, uint32_t refs)
+{
+    if (a && refs && atomic_fetch_sub_explicit(&a->refs, refs, memory_order_acq_rel) == refs)
+        h_arena_put(a);
+}
+
+void h_arenas_free_all(void)
+{
+    pthread_mutex_lock(&g_udpdk.arena_lock);
+    struct h_arena *a = g_udpdk.arena_free;
+    g_udpdk.arena_free = NULL;
+    pthread_mutex_unlock(&g_udpdk.arena_lock);
+    while (a) {
+        struct h_arena *n = a->next;
+        h_arena_destroy(a);
+        a = n;
+    }
+}
+
+/* ---- TX rings ----------------------------------------------------------------------------- */
+void h_tx_reset(void)
+{
+    pthread_mutex_lock(&g_udpdk.tx_lock);
+    for (int s = 0; s < UDPDK_MAX_SOCKETS; s++) {
+        free(g_udpdk.slots[s].tx.e);
+        g_udpdk.slots[s].tx.e = NULL;
+        g_udpdk.slots[s].tx.head = g_udpdk.slots[s].tx.tail = 0;
+    }
+    free(g_udpdk.txp);
+    g_udpdk.txp = NULL;
+    g_udpdk.txp_bytes = g_udpdk.txp_cap = 0;
+    g_udpdk.tx_queued = 0;
+    pthread_mutex_unlock(&g_udpdk.tx_lock);
+}
+
+uint64_t udpdk_tx_pending(void)
+{
+    pthread_mutex_lock(&g_udpdk.tx_lock);
+    const uint64_t q = g_udpdk.tx_queued;
+    pthread_mutex_unlock(&g_udpdk.tx_lock);
+    return q;
 }
 
 void h_sockets_reset(void)
 {
     for (int s = 0; s < UDPDK_MAX_SOCKETS; s++) {
         h_ring_clear(&g_udpdk.slots[s].rx);
+        free(g_udpdk.slots[s].tx.e);
         memset(&g_udpdk.slots[s], 0, sizeof(g_udpdk.slots[s]));
         g_udpdk.slots[s].prev = g_udpdk.slots[s].next = -1;
     }
     g_udpdk.n_active = 0;
+    free(g_udpdk.txp);
+    g_udpdk.txp = NULL;
+    g_udpdk.txp_bytes = g_udpdk.txp_cap = 0;
+    g_udpdk.tx_queued = 0;
     g_udpdk.version++;
 }
 
-/* All-or-nothing append of n datagrams (rte_ring_enqueue_bulk semantics, poller.c:287-290).
- * On refusal the caller frees the datagrams. */
-int h_ring_push_bulk(struct h_ring *r, struct h_dgram *d, uint32_t n)
-{
-    if (!r->e) {
-        r->e = calloc(UDPDK_RX_RING_SIZE, sizeof(*r->e));
-        if (!r->e) return -1;
-    }
-    if (r->tail - r->head + n > UDPDK_RX_RING_SIZE - 1) return -1;   /* usable size = size - 1 */
-    for (uint32_t i = 0; i < n; i++) r->e[(r->tail + i) % UDPDK_RX_RING_SIZE] = d[i];
-    r->tail += n;
-    return 0;
-}
-
+/* ---- socket calls ------------------------------------------------------------------------- */
 int udpdk_socket(int domain, int type, int protocol)
 {
     if (domain != AF_INET) { errno = EAFNOSUPPORT; return -1; }
     if (type != SOCK_DGRAM) { errno = EPROTONOSUPPORT; return -1; }
     if (protocol != 0 && protocol != IPPROTO_UDP) { errno = EINVAL; return -1; }
-    if (g_udpdk.n_active >= UDPDK_MAX_SOCKETS) { errno = ENOBUFS; return -1; }
-    for (int s = 0; s < UDPDK_MAX_SOCKETS; s++) {   /* lowest free slot */
-        struct h_slot *sl = &g_udpdk.slots[s];
-        if (sl->used) continue;
-        sl->used = 1;
-        sl->bound = 0;
-        sl->so_options = 0;
-        sl->ip = 0;
-        sl->udp_port = 0;
-        sl->prev = sl->next = -1;
-        g_udpdk.n_active++;
-        return s;
+    pthread_mutex_lock(&g_udpdk.lock);
+    int ret = -1;
+    if (g_udpdk.n_active >= UDPDK_MAX_SOCKETS) {
+        errno = ENOBUFS;
+    } else {
+        for (int s = 0; s < UDPDK_MAX_SOCKETS; s++) {   /* lowest free slot */
+            struct h_slot *sl = &g_udpdk.slots[s];
+            if (sl->used) continue;
+            sl->used = 1;
+            sl->bound = 0;
+            sl->so_options = 0;
+            sl->ip = 0;
+            sl->udp_port = 0;
+            sl->prev = sl->next = -1;
+            g_udpdk.n_active++;
+            ret = s;
+            break;
+        }
+        if (ret < 0) errno = ENOBUFS;
     }
-    errno = ENOBUFS;
-    return -1;
+    pthread_mutex_unlock(&g_udpdk.lock);
+    return ret;
 }
 
 static int h_sockopt_check(int s, int level, int optname, const void *optval, const void *optlen)
@@ -106,7 +237,7 @@ int udpdk_setsockopt(int s, int level, int optname, const void *optval, socklen_
     return 0;
 }
 
-int udpdk_bind(int s, const struct sockaddr *addr, socklen_t addrlen)
+static int h_bind_locked(int s, const struct sockaddr *addr, socklen_t addrlen)
 {
     if (!h_valid_fd(s) || !g_udpdk.slots[s].used) { errno = EBADF; return -1; }
     if (g_udpdk.slots[s].bound) { errno = EINVAL; return -1; }
@@ -122,21 +253,44 @@ int udpdk_bind(int s, const struct sockaddr *addr, socklen_t addrlen)
     return 0;
 }
 
+int udpdk_bind(int s, const struct sockaddr *addr, socklen_t addrlen)
+{
+    pthread_mutex_lock(&g_udpdk.lock);
+    const int rc = h_bind_locked(s, addr, addrlen);
+    pthread_mutex_unlock(&g_udpdk.lock);
+    return rc;
+}
+
 int udpdk_close(int s)
 {
-    if (!h_valid_fd(s) || !g_udpdk.slots[s].used) { errno = EBADF; return -1; }
+    pthread_mutex_lock(&g_udpdk.lock);
+    if (!h_valid_fd(s) || !g_udpdk.slots[s].used) {
+        pthread_mutex_unlock(&g_udpdk.lock);
+        errno = EBADF;
+        return -1;
+    }
     struct h_slot *sl = &g_udpdk.slots[s];
     if (sl->bound) h_btable_del(s, sl->udp_port);
     h_ring_clear(&sl->rx);
+    pthread_mutex_lock(&g_udpdk.tx_lock);
+    if (sl->tx.e) {
+        g_udpdk.tx_queued -= sl->tx.tail - sl->tx.head;   /* queued sends die with the socket */
+        free(sl->tx.e);
+    }
+    sl->tx.e = NULL;
+    sl->tx.head = sl->tx.tail = 0;
+    pthread_mutex_unlock(&g_udpdk.tx_lock);
     sl->bound = 0;
     sl->used = 0;
     sl->so_options = 0;
     g_udpdk.n_active--;
+    g_udpdk.version++;
+    pthread_mutex_unlock(&g_udpdk.lock);
     return 0;
 }
 
 /* Auto-bind an unbound socket to ANY on the lowest free raw port (udpdk_syscall.c:294-304). */
-static int h_autobind(int s)
+static int h_autobind_locked(int s)
 {
     if (g_udpdk.slots[s].bound) return 0;
     struct sockaddr_in a;
@@ -146,116 +300,54 @@ static int h_autobind(int s)
     const int p = h_btable_free_port();
     if (p < 0) { errno = EADDRINUSE; return -1; }
     a.sin_port = (uint16_t)p;
-    return udpdk_bind(s, (const struct sockaddr *)&a, sizeof(a));
-}
-
-static uint16_t h_ipv4_cksum(const uint8_t *ip)
-{
-    /* rte_raw_cksum + rte_ipv4_cksum, DPDK 20.05: raw 0xffff kept as is */
-    uint32_t s = 0;
-    for (int i = 0; i < 20; i += 2) s += (uint32_t)ip[i] | ((uint32_t)ip[i + 1] << 8);
-    s = (s >> 16) + (s & 0xFFFFu);
-    s = (s >> 16) + (s & 0xFFFFu);
-    const uint16_t raw = (uint16_t)s;
-    return raw == 0xFFFFu ? raw : (uint16_t)~raw;
-}
-
-ssize_t h_build_frame(int s, const void *buf, size_t len, uint32_t dst_ip, uint32_t dst_port,
-                      uint8_t *f)
-{
-    const struct h_slot *sl = &g_udpdk.slots[s];
-    memcpy(f, g_udpdk.dst_mac, 6);
-    memcpy(f + 6, g_udpdk.src_mac, 6);
-    f[12] = 0x08; f[13] = 0x00;
-    uint8_t *ip = f + 14;
-    memset(ip, 0, 20);
-    ip[0] = 0x45;
-    ip[8] = 64;
-    ip[9] = 17;
-    const uint32_t src = (sl->bound && sl->ip != 0) ? sl->ip : g_udpdk.src_ip;
-    memcpy(ip + 12, &src, 4);
-    memcpy(ip + 16, &dst_ip, 4);
-    const uint32_t tl = (uint32_t)len + 28;
-    ip[2] = (uint8_t)(tl >> 8); ip[3] = (uint8_t)tl;
-    const uint16_t ck = h_ipv4_cksum(ip);
-    memcpy(ip + 10, &ck, 2);
-    uint8_t *u = f + 34;
-    u[0] = (uint8_t)sl->udp_port; u[1] = (uint8_t)(sl->udp_port >> 8);
-    u[2] = (uint8_t)dst_port; u[3] = (uint8_t)(dst_port >> 8);
-    const uint32_t ul = (uint32_t)len + 8;
-    u[4] = (uint8_t)(ul >> 8); u[5] = (uint8_t)ul;
-    u[6] = u[7] = 0;
-    if (len) memcpy(f + 42, buf, len);
-    return (ssize_t)len + 42;
-}
-
-static int h_sendto_check(int s, size_t len, int flags, const struct sockaddr *dest, socklen_t addrlen)
-{
-    if (s < 0 || s >= UDPDK_MAX_SOCKETS) { errno = ENOTSOCK; return -1; }
-    if (!g_udpdk.slots[s].used) { errno = EBADF; return -1; }
-    if (flags != 0) { errno = EINVAL; return -1; }
-    if (!dest || addrlen == 0) { errno = EINVAL; return -1; }
-    if (len > H_MAX_PAYLOAD) { errno = EMSGSIZE; return -1; }
-    return 0;
-}
-
-ssize_t udpdk_build_frame(int s, const void *buf, size_t len, const struct sockaddr *dest,
-                          socklen_t addrlen, uint8_t *out)
-{
-    if (h_sendto_check(s, len, 0, dest, addrlen)) return -1;
-    if (h_autobind(s)) return -1;
-    const struct sockaddr_in *d = (const struct sockaddr_in *)dest;
-    return h_build_frame(s, buf, len, d->sin_addr.s_addr, d->sin_port, out);
+    return h_bind_locked(s, (const struct sockaddr *)&a, sizeof(a));
 }
 
 ssize_t udpdk_sendto(int s, const void *buf, size_t len, int flags,
                      const struct sockaddr *dest, socklen_t addrlen)
 {
-    if (h_sendto_check(s, len, flags, dest, addrlen)) return -1;
-    if (h_autobind(s)) return -1;
-    const uint64_t need = g_udpdk.txq_bytes + len + 42;
-    if (need > g_udpdk.txq_cap) {
-        uint64_t nc = g_udpdk.txq_cap ? g_udpdk.txq_cap * 2 : (1u << 20);
-        while (nc < need) nc *= 2;
-        uint8_t *nq = realloc(g_udpdk.txq, nc);
-        if (!nq) { errno = ENOMEM; return -1; }
-        g_udpdk.txq = nq;
-        g_udpdk.txq_cap = nc;
-    }
-    if (g_udpdk.txq_n == g_udpdk.txq_ncap) {
-        uint32_t nc = g_udpdk.txq_ncap ? g_udpdk.txq_ncap * 2 : 1024;
-        uint32_t *nl = realloc(g_udpdk.txq_len, (size_t)nc * sizeof(uint32_t));
-        if (!nl) { errno = ENOMEM; return -1; }
-        g_udpdk.txq_len = nl;
-        g_udpdk.txq_ncap = nc;
-    }
+    if (s < 0 || s >= UDPDK_MAX_SOCKETS) { errno = ENOTSOCK; return -1; }
+    if (!g_udpdk.slots[s].used) { errno = EBADF; return -1; }
+    if (flags != 0) { errno = EINVAL; return -1; }
+    if (!dest || addrlen == 0) { errno = EINVAL; return -1; }
+    if (len > H_UDP_MAX_PAYLOAD) { errno = EMSGSIZE; return -1; }
+    if (len && !buf) { errno = EFAULT; return -1; }
+    pthread_mutex_lock(&g_udpdk.lock);
+    const int rc = h_autobind_locked(s);
+    pthread_mutex_unlock(&g_udpdk.lock);
+    if (rc) return -1;
     const struct sockaddr_in *d = (const struct sockaddr_in *)dest;
-    const ssize_t fl = h_build_frame(s, buf, len, d->sin_addr.s_addr, d->sin_port,
-                                     g_udpdk.txq + g_udpdk.txq_bytes);
-    g_udpdk.txq_len[g_udpdk.txq_n++] = (uint32_t)fl;
-    g_udpdk.txq_bytes += (uint64_t)fl;
-    return (ssize_t)len;
-}
-
-int udpdk_tx_drain(uint8_t *out, uint64_t out_cap, uint32_t *out_off, uint16_t *out_len,
-                   uint32_t max, uint32_t *n_out)
-{
-    if (!n_out || (max && (!out || !out_off || !out_len))) { errno = EINVAL; return -1; }
-    uint32_t k = 0;
-    uint64_t pos = 0;
-    while (k < max && k < g_udpdk.txq_n && pos + g_udpdk.txq_len[k] <= out_cap) {
-        out_off[k] = (uint32_t)pos;
-        out_len[k] = (uint16_t)g_udpdk.txq_len[k];
-        pos += g_udpdk.txq_len[k];
-        k++;
+    pthread_mutex_lock(&g_udpdk.tx_lock);
+    struct h_txq *q = &g_udpdk.slots[s].tx;
+    ssize_t ret = -1;
+    if (!q->e && !(q->e = malloc(UDPDK_RX_RING_SIZE * sizeof(*q->e)))) {
+        errno = ENOMEM;
+    } else if (q->tail - q->head >= UDPDK_RX_RING_SIZE - 1) {
+        errno = ENOBUFS;                           /* rte_ring_enqueue failed (:356-365) */
+    } else {
+        const uint64_t need = g_udpdk.txp_bytes + len;
+        if (need > g_udpdk.txp_cap) {
+            uint64_t nc = g_udpdk.txp_cap ? g_udpdk.txp_cap * 2 : (1u << 20);
+            while (nc < need) nc *= 2;
+            uint8_t *np = realloc(g_udpdk.txp, nc);
+            if (!np) { errno = ENOMEM; goto out; }
+            g_udpdk.txp = np;
+            g_udpdk.txp_cap = nc;
+        }
+        struct h_txd *t = &q->e[q->tail % UDPDK_RX_RING_SIZE];
+        t->pay = g_udpdk.txp_bytes;
+        t->len = (uint32_t)len;
+        t->dst_ip = d->sin_addr.s_addr;
+        t->dst_port = d->sin_port;
+        if (len) memcpy(g_udpdk.txp + g_udpdk.txp_bytes, buf, len);
+        g_udpdk.txp_bytes += len;
+        q->tail++;
+        g_udpdk.tx_queued++;
+        ret = (ssize_t)len;
     }
-    if (pos) memcpy(out, g_udpdk.txq, pos);
-    memmove(g_udpdk.txq, g_udpdk.txq + pos, g_udpdk.txq_bytes - pos);
-    memmove(g_udpdk.txq_len, g_udpdk.txq_len + k, (size_t)(g_udpdk.txq_n - k) * sizeof(uint32_t));
-    g_udpdk.txq_bytes -= pos;
-    g_udpdk.txq_n -= k;
-    *n_out = k;
-    return 0;
+out:
+    pthread_mutex_unlock(&g_udpdk.tx_lock);
+    return ret;
 }
 
 ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
@@ -266,12 +358,16 @@ ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
     if (flags != 0) { errno = EINVAL; return -1; }
     if (buf == NULL && addrlen != NULL) { errno = EINVAL; return -1; }
     struct h_ring *r = &g_udpdk.slots[s].rx;
-    while (r->head == r->tail && !g_udpdk.interrupted) {
-        /* busy wait like udpdk_syscall.c:424-426; datagrams arrive via udpdk_poll_rx */
+    const uint32_t h = atomic_load_explicit(&r->head, memory_order_relaxed);
+    /* busy wait like udpdk_syscall.c:424-426; datagrams arrive from the poller (udpdk_poll_rx) */
+    while (atomic_load_explicit(&r->tail, memory_order_acquire) == h) {
+        if (atomic_load_explicit(&g_udpdk.interrupted, memory_order_relaxed)) {
+            errno = EINTR;
+            return -1;
+        }
+        sched_yield();
     }
-    if (g_udpdk.interrupted) { errno = EINTR; return -1; }
-    struct h_dgram d = r->e[r->head % UDPDK_RX_RING_SIZE];
-    r->head++;
+    const struct h_dgram d = r->e[h % UDPDK_RX_RING_SIZE];
     if (src_addr && addrlen) {
         struct sockaddr_in a;
         memset(&a, 0, sizeof(a));
@@ -284,7 +380,8 @@ ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
     }
     const size_t n = d.len < len ? d.len : len;
     if (n) memcpy(buf, d.data, n);
-    free(d.data);
+    atomic_store_explicit(&r->head, h + 1, memory_order_release);
+    h_arena_release(d.arena, 1);
     return (ssize_t)n;
 }
 

@@ -62,6 +62,8 @@ struct Pipe {
     uint8_t *st_desc_h = nullptr; size_t st_desc_hcap = 0;
     uint8_t *st_out_d = nullptr; size_t st_out_cap = 0;
     udpdk_rx_stats_t *host_stats = nullptr;   // outstanding async host call: where its stats go
+    udpdk_rx_batch_t staged{};                // device view of the last host batch staged here
+    const uint32_t *staged_meta = nullptr;    // and its verdict words
 };
 constexpr int MAX_PIPES = 4;
 
@@ -727,7 +729,7 @@ int enqueue_host(udpdk_gpu_ctx *c, int pipe, const uint8_t *frames_host, uint64_
                  const uint32_t *offset_host, const uint16_t *length_host,
                  const uint32_t *ptype_host, uint32_t n, uint32_t *meta_host,
                  uint32_t *lane_off_host, uint32_t *lane_pkt_host, uint32_t lane_cap,
-                 udpdk_rx_stats_t *stats)
+                 udpdk_rx_stats_t *stats, bool copy_lanes = true)
 {
     if (!stats || !lane_off_host || n > c->max_frames) return -EINVAL;
     if (n && (!frames_host || !offset_host || !length_host || !meta_host)) return -EINVAL;
@@ -776,8 +778,11 @@ int enqueue_host(udpdk_gpu_ctx *c, int pipe, const uint8_t *frames_host, uint64_
     if ((rc = enqueue_result(c, P))) return rc;
     if (n) HIPC(c, hipMemcpyAsync(meta_host, meta_d, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     HIPC(c, hipMemcpyAsync(lane_off_host, off_d, (size_t)(c->n_lanes + 1) * 4, hipMemcpyDeviceToHost, s));
-    if (lane_cap) HIPC(c, hipMemcpyAsync(lane_pkt_host, pkt_d, (size_t)lane_cap * 4, hipMemcpyDeviceToHost, s));
+    if (lane_cap && copy_lanes)
+        HIPC(c, hipMemcpyAsync(lane_pkt_host, pkt_d, (size_t)lane_cap * 4, hipMemcpyDeviceToHost, s));
     P.host_stats = stats;
+    P.staged = b;
+    P.staged_meta = meta_d;
     return 0;
 }
 
@@ -806,9 +811,29 @@ int udpdk_gpu_rx_host(udpdk_gpu_ctx *c, const uint8_t *frames_host, uint64_t fra
     int rc = finish_all_host(c);
     if (rc && rc != -ENOSPC) return rc;
     if (c->depth > 1) { int r = join_pipes(c); if (r) return r; }
+    // synchronous: the lane entries come back after the counters, only as many as were made
     if ((rc = enqueue_host(c, 0, frames_host, frames_bytes, offset_host, length_host, ptype_host, n,
-                           meta_host, lane_off_host, lane_pkt_host, lane_cap, stats))) return rc;
-    return finish_host(c, c->pipes[0]);
+                           meta_host, lane_off_host, lane_pkt_host, lane_cap, stats, false))) return rc;
+    Pipe &P = c->pipes[0];
+    rc = finish_host(c, P);
+    if (rc && rc != -ENOSPC) return rc;
+    const uint32_t d = std::min(stats->deliveries, lane_cap);
+    if (d) {
+        const uint32_t *pkt_d = P.staged_meta + n + c->n_lanes + 1;
+        HIPC(c, hipMemcpyAsync(lane_pkt_host, pkt_d, (size_t)d * 4, hipMemcpyDeviceToHost, P.stream));
+        HIPC(c, hipStreamSynchronize(P.stream));
+    }
+    return rc;
+}
+
+int udpdk_gpu_rx_host_batch(udpdk_gpu_ctx *c, udpdk_rx_batch_t *batch, const uint32_t **meta_dev)
+{
+    if (!c || !batch) return -EINVAL;
+    const Pipe &P = c->pipes[0];
+    if (!P.staged_meta) return -ENOENT;
+    *batch = P.staged;
+    if (meta_dev) *meta_dev = P.staged_meta;
+    return 0;
 }
 
 int udpdk_gpu_rx_host_async(udpdk_gpu_ctx *c, const uint8_t *frames_host, uint64_t frames_bytes,
