@@ -304,7 +304,10 @@ enum udpdk_rs_stat {
     UDPDK_RS_EXPIRED    = 6, /* flows freed on timeout                                           */
     UDPDK_RS_DONE       = 7, /* datagrams reassembled                                             */
     UDPDK_RS_STORED     = 8, /* fragments of this batch held by the table for later batches      */
-    UDPDK_RS_N          = 9
+    UDPDK_RS_SERIAL     = 9, /* diagnostic: fragments that went through the table one at a time
+                                in arrival order (flows that share buckets with an overlapping
+                                flow, stay pending, or meet an existing or expired entry)       */
+    UDPDK_RS_N          = 10
 };
 
 typedef struct {
@@ -321,8 +324,9 @@ typedef struct {
 int udpdk_gpu_frag_table_create(udpdk_gpu_ctx *ctx, const udpdk_frag_table_cfg_t *cfg);
 /* Reassembly step for one batch whose udpdk_gpu_rx verdicts are in meta_dev (FRAG frames are
  * consumed; state persists across calls). tms is the batch's timestamp (the poller's cur_tsc).
- * Synchronous. Equals one-fragment-at-a-time processing in arrival order unless the batch's
- * flows compete for the last free entries of a bucket pair. */
+ * Synchronous. Every output, count and table entry equals one-fragment-at-a-time processing in
+ * arrival order (rte_ipv4_frag_reassemble_packet per fragment, udpdk_poller.c:338-361): flows
+ * that cannot meet another flow in the table run in parallel, the rest in arrival order. */
 int udpdk_gpu_rx_reassemble(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch,
                             const uint32_t *meta_dev, uint64_t tms, udpdk_reasm_out_t *out);
 
@@ -373,7 +377,9 @@ typedef struct {
 } udpdk_tx_config_t;
 
 typedef struct {
-    const uint8_t  *payload_dev;     /* payload bytes                                          */
+    const uint8_t  *payload_dev;     /* payload bytes, followed by UDPDK_GPU_FRAMES_TAILROOM
+                                        readable bytes (a payload ending at payload_bytes is
+                                        read with dword loads up to 3 bytes past it)           */
     uint64_t        payload_bytes;
     const uint32_t *payload_off_dev; /* [n]                                                    */
     const uint16_t *payload_len_dev; /* [n] sendto len, <= 65507                               */

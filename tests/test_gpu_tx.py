@@ -17,14 +17,18 @@ DST_MAC = bytes.fromhex("6805ca95fa64")
 SRC_IP = abi.raw_ip("172.31.100.2")
 
 
-def _tx_gpu(ctx, slots, sock, dst_ip, dst_port, payloads, frame_off, frames_cap, mtu=None):
+def _tx_gpu(ctx, slots, sock, dst_ip, dst_port, payloads, frame_off, frames_cap, mtu=None, exact=False):
+    """exact: payload_bytes ends at the last payload's last byte and the payload allocation is
+    exactly payload_bytes + UDPDK_GPU_FRAMES_TAILROOM (the contract of udpdk_tx_batch_t)."""
     n = len(payloads)
     pay_off = np.zeros(n, np.uint32)
     pos = 0
     for i, p in enumerate(payloads):
         pay_off[i] = pos
         pos += len(p) + int(i % 3)                       # unaligned payload starts
-    pay = np.zeros(pos + 256, np.uint8)
+    if exact:
+        pos = int(pay_off[-1]) + len(payloads[-1])
+    pay = np.zeros(pos + (abi.FRAMES_TAILROOM if exact else 256), np.uint8)
     for i, p in enumerate(payloads):
         pay[pay_off[i]:pay_off[i] + len(p)] = np.frombuffer(p, np.uint8)
     lens = np.array([len(p) for p in payloads], np.uint16)
@@ -118,6 +122,26 @@ def test_tx_small_frames(gpu_ctx, gap):
         want_buf[fo[i]:fo[i] + len(want)] = np.frombuffer(want, np.uint8)
     bad = np.nonzero(res != want_buf)[0]
     assert bad.size == 0, f"first differing byte {bad[0]} (frame {np.searchsorted(fo, bad[0], 'right') - 1})"
+
+
+@pytest.mark.parametrize("start", [0, 1, 2, 3])
+def test_tx_payload_ends_at_payload_bytes(gpu_ctx, start):
+    """The batch's last payload ends exactly at payload_bytes at every dword alignment, lengths
+    1-40 (so its last bytes come from a dword that ends past payload_bytes), the allocation being
+    exactly payload_bytes + tailroom: every byte is copied (udpdk_tx_drain packs payloads like
+    this; a range rounded to 16 bytes returned those dwords as zeros)."""
+    for last in range(1, 41):
+        payloads = [bytes(range(1, 1 + start))] if start else []
+        payloads += [bytes((7 * k + last) & 0xFF or 1 for k in range(last))]
+        n = len(payloads)
+        fo = np.cumsum([0] + [len(p) + 42 for p in payloads[:-1]]).astype(np.uint32)
+        cap = int(fo[-1]) + len(payloads[-1]) + 42 + 64
+        res = _tx_gpu(gpu_ctx, [(0, 10000, 1)], [0] * n, [abi.raw_ip("10.0.0.9")] * n, [4242] * n,
+                      payloads, fo, cap, exact=True)
+        for i, p in enumerate(payloads):
+            want = O.tx_frame(SRC_MAC, DST_MAC, SRC_IP, 1, 0, 10000, abi.raw_ip("10.0.0.9"), 4242, p)
+            got = res[fo[i]:fo[i] + len(want)].tobytes()
+            assert got == want, (start, last, i)
 
 
 def test_tx_golden_vectors(gpu_ctx):

@@ -5,17 +5,27 @@
 //
 // Semantics: oracle/udpdk_oracle_frag.c restates DPDK 20.05's table (ip_frag_lookup/find/process,
 // ipv4_frag_reassemble) and is the parity checker; this file follows it fragment for fragment.
-// The reference handles one fragment at a time in arrival order; here the batch's fragments are
-// grouped by flow key (two stable radix sorts: (id, index) then src|dst) and each flow's fragments
-// are processed in arrival order by one wavefront, flows in parallel. The result equals the
-// sequential one whenever the flows of a batch do not compete for the last free slot of a
-// bucket pair (then which flow gets it depends on timing, as it would on arrival order).
-//
+// The reference handles one fragment at a time in arrival order. Here the batch's fragments are
+// grouped by flow key (two stable radix sorts: (id, index) then src|dst), and the result is the
+// same as the reference's for every batch:
+//  * flows only interact through the entries of their two buckets, and only at a lookup;
+//  * a flow whose lookups fall in a span [first, last fragment] that no other flow's span
+//    overlaps on a shared bucket, whose buckets hold no expired entry and not its key, that
+//    ends (completes or fails) by its last fragment, and whose buckets are sure to have a free
+//    entry, holds an entry only while no one else looks: it is reassembled in parallel without
+//    the table (reasm_process);
+//  * every other flow's fragments go through the table in arrival order on one wave
+//    (reasm_serial), which is then exactly the reference's sequence of ip_frag_find calls.
 // Launch sequence (udpdk_gpu_rx_reassemble, synchronous):
 //   reasm_collect   FRAG verdicts -> fragment list + (id << ib | index) sort keys
 //   radix sort 1    by (id, index); reasm_keys: src|dst keys in that order; radix sort 2 (stable)
-//   reasm_process   one wave per flow segment: table find (2 x assoc slots scanned by the lanes,
-//                   entry locks), ip_frag_process on lane 0, completion records, store jobs
+//   reasm_prep      per sorted position: frame, key, crc32c signature, length class
+//   reasm_bsum      per bucket: valid entries, any expired
+//   reasm_flows     per flow: span, pending or not, key in the table, overlap records
+//   radix sort 4 + max scan + reasm_overlap: flows whose spans overlap on a shared bucket
+//   reasm_ec        a free entry guaranteed for every parallel flow, else all go serial
+//   reasm_process   parallel flows without the table; the rest -> serial list
+//   radix sort 5    serial list by arrival; reasm_serial (one wave, the table in arrival order)
 //   radix sort 3    completions by origin (the arrival index of the completing fragment: where
 //                   the reference delivers the datagram) + exclusive scan of frame sizes
 //   reasm_emit      one wave per datagram: first fragment's header (total length, DF only, IPv4
@@ -24,8 +34,8 @@
 //                   the flow's entry buffer, after every read of the table buffers
 //
 // Table memory: entries x 80 B of state + entries x stride bytes of fragment data (stride =
-// 34 + max_dgram rounded to 256). All cross-wave state is accessed with agent-scope atomics (the
-// per-XCD L2s are not coherent for plain accesses); entry locks are acquire/release.
+// 34 + max_dgram rounded to 256). Table words are accessed with agent-scope atomics (the per-XCD
+// L2s are not coherent for plain accesses).
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -45,26 +55,32 @@ constexpr uint32_t RS_BLOCK = 256;
 constexpr uint32_t RS_WAVES = RS_BLOCK / 64;
 constexpr uint32_t RS_HELD = 0xFFFFFFFFu;       // fragment data lives in the entry buffer
 constexpr uint32_t RS_NONE = 0xFFFFFFFFu;
-constexpr uint32_t RS_VIRTUAL = 0xFFFFFFFEu;    // flow state only in LDS (no table entry yet)
 constexpr uint32_t RS_MAX_FRAG = 4;             // RTE_LIBRTE_IP_FRAG_MAX_FRAG
-constexpr uint32_t RS_SPIN = 1u << 20;          // bound on lock spins / find retries
+constexpr uint32_t RS_FLOW_CHUNK = 1024;        // sorted positions per reasm_flows block step
 
 // Bits to hold every value in [0, v]
 inline uint32_t bits_for(uint32_t v) { return v ? 32u - (uint32_t)__builtin_clz(v) : 1u; }
 
 // One table entry (struct ip_frag_pkt) as 20 u32 words, every one accessed with agent-scope
-// relaxed atomics; a wave holding the entry's lock owns the words after E_ID.
+// relaxed atomics; only reasm_serial writes them.
 enum : uint32_t {
-    E_LOCK = 0,         // 0 free, else holder tag
+    E_LOCK = 0,         // unused (kept for the layout)
     E_VALID = 1,        // key_len != 0
     E_SRC = 2, E_DST = 3, E_ID = 4,
     E_FSIZE = 5, E_TOTAL = 6, E_LAST = 7,
     E_START = 8,        // u64 start (lo, hi)
     E_FR = 10,          // [4] ofs | len << 16, 0 = empty slot (len > 0 when present)
-    E_WHERE = 14,       // [4] frame index in the current call, or RS_HELD
-    E_USED = 18,
+    E_WHERE = 14,       // [4] frame index in the call E_CALL, or RS_HELD
+    E_CALL = 18,        // the call whose fragments E_WHERE may name (older ones are held)
+    E_USED = 19,
     E_WORDS = 20
 };
+
+// Flags of a flow segment, at its first sorted position (pflag).
+constexpr uint32_t PF_TOUCH = 1;      // has a fragment that reaches ip_frag_find
+constexpr uint32_t PF_COMPLEX = 2;    // pending after its last fragment, key in the table, or an
+                                      // expired entry in one of its buckets
+constexpr uint32_t PF_SHARED = 4;     // its span overlaps another flow's on a shared bucket
 
 struct ReasmDone {            // one reassembled datagram
     uint32_t origin, total, n, entry;
@@ -99,7 +115,15 @@ struct ReasmArgs {
     uint32_t *dk;                      // [F] origin of the completion there, or ~0
     uint32_t *dv;                      // [F] 0..F-1
     ReasmJob *jobs;                    // [F] at the stored fragment's position (frame ~0: none)
-    uint32_t tag_base;
+    // flow analysis (per first sorted position of a flow) and the serial path
+    uint32_t assoc_log2, nbuckets;
+    uint32_t *pflag, *sb1, *sb2, *tf, *tl;   // [F] flags, bucket pair, span
+    unsigned long long *rk;            // [2F] overlap records: bucket << ib | tf
+    uint32_t *rv;                      // [2F] their flow's first position
+    uint32_t *bsum, *cplx;             // [buckets] valid | stale << 31; complex flows
+    uint32_t *sl_k, *sl_v;             // [F] serial list: arrival index, sorted position
+    uint32_t *tpos;                    // [entries][4] sorted position of a slot's fragment (this call)
+    uint32_t call;                     // this call's number (E_CALL), from 1
 };
 
 template <typename T>
@@ -216,10 +240,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_collect(ReasmArgs a)
     for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
     if (lane == 0 && c) atomicAdd(&s_n, c);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        s_base = s_n ? atomicAdd(&a.counts[0], s_n) : 0u;
-        if (s_n) atomicAdd(&a.stats[UDPDK_RS_FRAGS], (unsigned long long)s_n);
-    }
+    if (threadIdx.x == 0) s_base = s_n ? atomicAdd(&a.counts[0], s_n) : 0u;
     __syncthreads();
     if (!s_n) return;
     for (uint32_t i0 = b0 + (threadIdx.x & ~63u); i0 < b1; i0 += RS_BLOCK) {
@@ -291,8 +312,22 @@ __device__ __forceinline__ void wave_sync_rs()
 // Every store this wave issued has completed (CDNA counts stores in vmcnt).
 __device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Fresh flow state (ip_frag_reset) for lane 0.
-__device__ void state_reset(const ReasmArgs &a, uint32_t *st, uint32_t src, uint32_t dst, uint32_t id)
+// Exclusive prefix sum of v over the wave's lanes; *total gets the wave's sum. Wave-uniform.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total)
+{
+    const uint32_t lane = __lane_id();
+    uint32_t x = v;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    *total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+// Fresh flow state (ip_frag_reset / ip_frag_tbl_add) for the key.
+__device__ __forceinline__ void state_reset(uint32_t *st, uint32_t src, uint32_t dst, uint32_t id,
+                                            unsigned long long tms, uint32_t call)
 {
     st[E_VALID] = 1;
     st[E_SRC] = src;
@@ -301,116 +336,10 @@ __device__ void state_reset(const ReasmArgs &a, uint32_t *st, uint32_t src, uint
     st[E_FSIZE] = 0;
     st[E_TOTAL] = 0xFFFFFFFFu;
     st[E_LAST] = 2;
-    st[E_START] = (uint32_t)a.tms;
-    st[E_START + 1] = (uint32_t)(a.tms >> 32);
+    st[E_START] = (uint32_t)tms;
+    st[E_START + 1] = (uint32_t)(tms >> 32);
     for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) { st[E_FR + k] = 0; st[E_WHERE + k] = RS_HELD; }
-}
-
-// ip_frag_find: returns the entry for the key, locked by this wave with its words in st[], or
-// RS_NONE (no space). With allow_virtual, a key that is not in the table while its buckets
-// have a free slot (and no expired one to reclaim) gets RS_VIRTUAL: the flow starts in LDS and
-// only takes a table entry if it is still pending when the wave leaves it (a flow that
-// completes or fails inside one batch never touches the table). Wave-uniform.
-__device__ uint32_t table_find(const ReasmArgs &a, uint32_t src, uint32_t dst, uint32_t id,
-                               uint32_t sig, uint32_t tag, uint32_t *st, unsigned long long *cnt,
-                               bool allow_virtual)
-{
-    const uint32_t lane = __lane_id();
-    const uint32_t p1 = sig & a.mask, p2 = ((sig << 7) + (sig >> 14)) & a.mask;
-    for (uint32_t tries = 0; tries < RS_SPIN; ++tries) {
-        // lanes scan p1[0], p2[0], p1[1], p2[1], ... (ip_frag_lookup's order)
-        const uint32_t slot = (lane & 1u ? p2 : p1) + (lane >> 1);
-        bool match = false, empty = false, stale = false;
-        if (lane < 2u * a.assoc) {
-            const uint32_t *e = a.tab + (size_t)slot * E_WORDS;
-            const uint32_t val = ld_a(e + E_VALID), es = ld_a(e + E_SRC), ed = ld_a(e + E_DST);
-            const uint32_t ei = ld_a(e + E_ID), lo = ld_a(e + E_START), hi = ld_a(e + E_START + 1);
-            const unsigned long long start = ((unsigned long long)hi << 32) | lo;
-            match = val && es == src && ed == dst && ei == id;
-            stale = val && !match && a.max_cycles + start < a.tms;
-            empty = !val;
-        }
-        const unsigned long long mm = __ballot(match), ms = __ballot(stale), me = __ballot(empty);
-        uint32_t cand;
-        uint32_t kind;                               // 0 match, 1 stale, 2 empty
-        if (mm) { cand = __shfl(slot, __ffsll((long long)mm) - 1, 64); kind = 0; }
-        else if (ms) { cand = __shfl(slot, __ffsll((long long)ms) - 1, 64); kind = 1; }
-        else if (me) {
-            if (allow_virtual) {
-                if (lane == 0) state_reset(a, st, src, dst, id);
-                wave_sync_rs();
-                return RS_VIRTUAL;
-            }
-            cand = __shfl(slot, __ffsll((long long)me) - 1, 64);
-            kind = 2;
-        } else {
-            return RS_NONE;
-        }
-        uint32_t *e = a.tab + (size_t)cand * E_WORDS;
-        uint32_t got = 0;
-        if (lane == 0) {
-            uint32_t exp = 0;
-            got = __hip_atomic_compare_exchange_strong(e + E_LOCK, &exp, tag, __ATOMIC_RELAXED,
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // a matching entry is only held briefly by a wave testing it as a candidate
-            for (uint32_t k = 0; !got && kind == 0 && k < RS_SPIN; ++k) {
-                __builtin_amdgcn_s_sleep(2);
-                exp = 0;
-                got = __hip_atomic_compare_exchange_strong(e + E_LOCK, &exp, tag, __ATOMIC_RELAXED,
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        if (!__shfl(got, 0, 64)) continue;
-        // under the lock: the entry's words (the previous holder's stores completed before it
-        // released the lock)
-        if (lane < E_USED) st[lane] = lane == E_LOCK ? tag : ld_a(e + lane);
-        wave_sync_rs();
-        uint32_t ok = 0, fresh = 0;
-        if (lane == 0) {
-            const bool val = st[E_VALID] != 0;
-            const bool same = val && st[E_SRC] == src && st[E_DST] == dst && st[E_ID] == id;
-            const unsigned long long start =
-                ((unsigned long long)st[E_START + 1] << 32) | st[E_START];
-            const bool expired = val && a.max_cycles + start < a.tms;
-            if (kind == 0 && same) {
-                ok = 1;
-                if (expired) {                                   // ip_frag_tbl_reuse
-                    atomicAdd(&cnt[UDPDK_RS_EXPIRED], 1ull);
-                    fresh = 1;
-                }
-            } else if (kind == 1 && val && !same && expired) {   // ip_frag_tbl_del + add
-                atomicAdd(&cnt[UDPDK_RS_EXPIRED], 1ull);
-                ok = fresh = 1;
-            } else if (kind == 2 && !val) {                      // ip_frag_tbl_add
-                ok = fresh = 1;
-            }
-            if (fresh) state_reset(a, st, src, dst, id);
-        }
-        wave_sync_rs();
-        ok = __shfl(ok, 0, 64);
-        if (!ok) {
-            if (lane == 0) st_a(e + E_LOCK, 0u);
-            continue;
-        }
-        if (__shfl(fresh, 0, 64) && lane >= E_VALID && lane < E_USED) st_a(e + lane, st[lane]);
-        return cand;
-    }
-    return RS_NONE;
-}
-
-// Write the held entry back (or invalidate it) and release the lock. Wave-uniform.
-__device__ void table_release(const ReasmArgs &a, uint32_t cur, const uint32_t *st, bool invalidate)
-{
-    const uint32_t lane = __lane_id();
-    uint32_t *e = a.tab + (size_t)cur * E_WORDS;
-    wave_sync_rs();
-    if (invalidate) {
-        if (lane == 0) st_a(e + E_VALID, 0u);
-    } else if (lane >= E_FSIZE && lane < E_USED) {
-        st_a(e + lane, st[lane]);
-    }
-    stores_done();
-    if (lane == 0) st_a(e + E_LOCK, 0u);
+    st[E_CALL] = call;
 }
 
 // ipv4_frag_reassemble's backward chain walk over the held fragments.
@@ -433,134 +362,421 @@ __device__ bool chain_ok(const uint32_t *st)
     return ofs == first_len;
 }
 
+// ip_frag_process of one fragment on flow state st: the fragment goes to slot *idx (FA_KEEP,
+// FA_DONE, FA_HOLE, FA_ERR) or to none (FA_NOSLOT: duplicate first/last, more than 4). Every
+// outcome but FA_KEEP ends the flow (the entry is invalidated).
+enum : uint32_t { FA_KEEP = 0, FA_DONE = 1, FA_HOLE = 2, FA_ERR = 3, FA_NOSLOT = 4 };
+
+__device__ uint32_t frag_apply(uint32_t *st, uint32_t len, uint32_t ofs, uint32_t mf, uint32_t where,
+                               uint32_t *idx_out)
+{
+    uint32_t idx;
+    st[E_FSIZE] += len;
+    if (ofs == 0) {
+        idx = st[E_FR + 0] == 0 ? 0u : RS_NONE;
+    } else if (!mf) {
+        st[E_TOTAL] = ofs + len;
+        idx = st[E_FR + 1] == 0 ? 1u : RS_NONE;
+    } else {
+        idx = st[E_LAST];
+        if (idx < RS_MAX_FRAG) st[E_LAST] = idx + 1u;
+    }
+    if (idx >= RS_MAX_FRAG) return FA_NOSLOT;
+    *idx_out = idx;
+    st[E_FR + idx] = ofs | (len << 16);
+    st[E_WHERE + idx] = where;
+    if (st[E_FSIZE] < st[E_TOTAL]) return FA_KEEP;
+    const bool sized = st[E_FSIZE] == st[E_TOTAL] && st[E_FR + 0] != 0;
+    if (sized && chain_ok(st)) return FA_DONE;
+    return sized ? FA_HOLE : FA_ERR;
+}
+
+// Completion record of the flow in st, completed by the fragment at sorted position q (frame i).
+__device__ void write_done(const ReasmArgs &a, const uint32_t *st, uint32_t q, uint32_t i, uint32_t entry)
+{
+    ReasmDone r;
+    r.origin = i;
+    r.total = st[E_TOTAL];
+    r.n = st[E_LAST];
+    r.entry = entry;
+    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
+        r.fr[k] = st[E_FR + k];
+        r.where[k] = st[E_WHERE + k];
+    }
+    a.done[q] = r;
+    a.dk[q] = i;
+}
+
+__device__ __forceinline__ bool same_key(const ReasmArgs &a, uint32_t p, uint32_t q)
+{
+    return a.s_src[p] == a.s_src[q] && a.s_dst[p] == a.s_dst[q] && a.s_id[p] == a.s_id[q];
+}
+
+__device__ __forceinline__ bool seg_start(const ReasmArgs &a, uint32_t p)
+{
+    return p == 0 || !same_key(a, p, p - 1u);
+}
+
+__device__ __forceinline__ uint32_t bucket_of(const ReasmArgs &a, uint32_t sig)
+{
+    return (sig & a.mask) >> a.assoc_log2;
+}
+
+__device__ __forceinline__ uint32_t bucket2_of(const ReasmArgs &a, uint32_t sig)
+{
+    return (((sig << 7) + (sig >> 14)) & a.mask) >> a.assoc_log2;
+}
+
 } // namespace
 
-// One wave per flow segment of the sorted fragment list; lane 0 runs ip_frag_process on the
-// held entry's words in LDS, the other lanes scan buckets and move entry words.
-__global__ void __launch_bounds__(RS_BLOCK) reasm_process(ReasmArgs a, uint32_t F)
+// Per bucket of the table at call start: valid entries | (an expired valid entry) << 31; the
+// bucket's count of complex flows (below) is reset. One lane per entry, assoc lanes per bucket.
+__global__ void __launch_bounds__(RS_BLOCK) reasm_bsum(ReasmArgs a)
 {
-    __shared__ uint32_t s_st[RS_WAVES][E_WORDS];
-    __shared__ uint32_t s_tmp[RS_WAVES][E_WORDS];           // entry words while installing
-    __shared__ uint32_t s_pos[RS_WAVES][RS_MAX_FRAG];      // sorted position of each held slot
-    __shared__ unsigned long long s_cnt[UDPDK_RS_N + 1];    // block totals: stats, out bytes
-    const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
-    uint32_t *st = s_st[w];
-    unsigned long long *cnt = s_cnt;
-    if (threadIdx.x <= UDPDK_RS_N) s_cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t gw = blockIdx.x * RS_WAVES + w, nw = gridDim.x * RS_WAVES;
-    const uint32_t tag = a.tag_base + gw + 1u;
-    for (uint32_t base = gw * 64u; base < F; base += nw * 64u) {
-        const uint32_t p = base + lane;
-        bool start = false;
-        if (p < F) {
-            start = p == 0 || a.s_src[p] != a.s_src[p - 1] || a.s_dst[p] != a.s_dst[p - 1] ||
-                    a.s_id[p] != a.s_id[p - 1];
+    const uint32_t lane = __lane_id();
+    const uint32_t g0 = lane & ~(a.assoc - 1u);                  // the bucket's first lane
+    const unsigned long long gm = (a.assoc == 64u ? ~0ull : ((1ull << a.assoc) - 1ull)) << g0;
+    const uint32_t ne = a.nbuckets * a.assoc;
+    for (uint32_t x0 = blockIdx.x * RS_BLOCK + (threadIdx.x & ~63u); x0 < ne; x0 += gridDim.x * RS_BLOCK) {
+        const uint32_t x = x0 + lane;
+        bool v = false, old = false;
+        if (x < ne) {
+            const uint32_t *e = a.tab + (size_t)x * E_WORDS;
+            v = ld_a(e + E_VALID) != 0;
+            if (v) {
+                const unsigned long long start =
+                    ((unsigned long long)ld_a(e + E_START + 1) << 32) | ld_a(e + E_START);
+                old = a.max_cycles + start < a.tms;
+            }
         }
-        unsigned long long starts = __ballot(start);
-        while (starts) {
-            const uint32_t s = base + (uint32_t)(__ffsll((long long)starts) - 1);
-            starts &= starts - 1ull;
-            const uint32_t ksrc = a.s_src[s], kdst = a.s_dst[s], kid = a.s_id[s], sig = a.s_sig[s];
-            uint32_t cur = RS_NONE;
-            for (uint32_t q = s; q < F; ++q) {
-                const uint32_t i = a.s_i[q], m = a.s_meta[q];
-                if (q != s && (a.s_src[q] != ksrc || a.s_dst[q] != kdst || a.s_id[q] != kid)) break;
-                const uint32_t cls = m >> 30;
-                if (cls) {
-                    if (lane == 0) atomicAdd(&cnt[cls == 1 ? UDPDK_RS_DROP_LEN : UDPDK_RS_DROP_SHORT], 1ull);
-                    continue;
-                }
-                const uint32_t len = m & 0xFFFFu, ofs = ((m >> 16) & 0x1FFFu) * 8u, mf = (m >> 29) & 1u;
-                if (cur == RS_NONE) {
-                    cur = table_find(a, ksrc, kdst, kid, sig, tag, st, cnt, true);
-                    if (cur == RS_NONE) {
-                        if (lane == 0) atomicAdd(&cnt[UDPDK_RS_NO_SPACE], 1ull);
-                        continue;
-                    }
-                }
-                // ip_frag_process (lane 0 owns the state; the outcome is broadcast)
-                uint32_t outcome = 0;                 // 0 keep, 1 invalidate
-                if (lane == 0) {
+        const unsigned long long bv = __ballot(v), bo = __ballot(old);
+        if (x < ne && lane == g0) {
+            const uint32_t b = x >> a.assoc_log2;
+            a.bsum[b] = (uint32_t)__popcll(bv & gm) | ((bo & gm) ? 1u << 31 : 0u);
+            a.cplx[b] = 0;
+        }
+    }
+}
+
+// One thread per flow segment (at its first sorted position p). The flow is walked on its own,
+// as if every ip_frag_find it makes succeeded with a fresh entry: its span [tf, tl] (arrival
+// indices of its first and last fragment that reaches ip_frag_find) and whether it is still
+// pending after its last one. PF_COMPLEX when it is pending, its key is in the table, or one of
+// its buckets holds an expired entry; complex flows are counted per bucket. Each flow adds one
+// (bucket << ib | tf) record per distinct bucket of its pair for the overlap test.
+__global__ void __launch_bounds__(RS_BLOCK) reasm_flows(ReasmArgs a, uint32_t F)
+{
+    constexpr uint32_t PER = RS_FLOW_CHUNK / RS_BLOCK;
+    __shared__ uint32_t s_st[RS_BLOCK][E_WORDS];
+    __shared__ unsigned long long s_rk[2 * RS_FLOW_CHUNK];   // the chunk's records, reserved at once
+    __shared__ uint32_t s_rv[2 * RS_FLOW_CHUNK];
+    __shared__ uint32_t s_nr, s_base;
+    uint32_t *st = s_st[threadIdx.x];
+    for (uint32_t c0 = blockIdx.x * RS_FLOW_CHUNK; c0 < F; c0 += gridDim.x * RS_FLOW_CHUNK) {
+        if (threadIdx.x == 0) s_nr = 0;
+        __syncthreads();
+        for (uint32_t j = 0; j < PER; ++j) {
+            const uint32_t p = c0 + j * RS_BLOCK + threadIdx.x;
+            uint32_t flag = 0, nrec = 0, bk1 = 0, bk2 = 0, tfirst = RS_NONE;
+            if (p < F && seg_start(a, p)) {
+                uint32_t tlast = 0;
+                bool live = false;
+                for (uint32_t q = p; q < F && (q == p || same_key(a, p, q)); ++q) {
+                    const uint32_t m = a.s_meta[q];
+                    if (m >> 30) continue;
+                    const uint32_t i = a.s_i[q];
+                    if (tfirst == RS_NONE) tfirst = i;
+                    tlast = i;
+                    if (!live) state_reset(st, 0, 0, 0, 0, 0);
                     uint32_t idx;
-                    st[E_FSIZE] += len;
-                    if (ofs == 0) {
-                        idx = st[E_FR + 0] == 0 ? 0u : RS_NONE;
-                    } else if (!mf) {
-                        st[E_TOTAL] = ofs + len;
-                        idx = st[E_FR + 1] == 0 ? 1u : RS_NONE;
-                    } else {
-                        idx = st[E_LAST];
-                        if (idx < RS_MAX_FRAG) st[E_LAST] = idx + 1u;
-                    }
-                    if (idx >= RS_MAX_FRAG) {
-                        atomicAdd(&cnt[UDPDK_RS_ERRORS], 1ull);
-                        outcome = 1;
-                    } else {
-                        st[E_FR + idx] = ofs | (len << 16);
-                        st[E_WHERE + idx] = i;
-                        s_pos[w][idx] = q;
-                        if (st[E_FSIZE] >= st[E_TOTAL]) {
-                            const bool sized = st[E_FSIZE] == st[E_TOTAL] && st[E_FR + 0] != 0;
-                            if (sized && chain_ok(st)) {
-                                ReasmDone r;
-                                r.origin = i;
-                                r.total = st[E_TOTAL];
-                                r.n = st[E_LAST];
-                                r.entry = cur;
-                                for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
-                                    r.fr[k] = st[E_FR + k];
-                                    r.where[k] = st[E_WHERE + k];
-                                }
-                                a.done[q] = r;
-                                a.dk[q] = i;
-                                atomicAdd(&cnt[UDPDK_RS_N], (unsigned long long)((34u + st[E_TOTAL] + 15u) & ~15u));
-                                atomicAdd(&cnt[UDPDK_RS_DONE], 1ull);
-                            } else {
-                                atomicAdd(&cnt[sized ? UDPDK_RS_HOLES : UDPDK_RS_ERRORS], 1ull);
-                            }
-                            outcome = 1;
+                    live = frag_apply(st, m & 0xFFFFu, ((m >> 16) & 0x1FFFu) * 8u, (m >> 29) & 1u, i, &idx) == FA_KEEP;
+                }
+                if (tfirst != RS_NONE) {
+                    flag = PF_TOUCH | (live ? PF_COMPLEX : 0u);
+                    const uint32_t sig = a.s_sig[p];
+                    bk1 = bucket_of(a, sig);
+                    bk2 = bucket2_of(a, sig);
+                    const uint32_t s1 = a.bsum[bk1], s2 = a.bsum[bk2];
+                    if ((s1 | s2) >> 31) {
+                        flag |= PF_COMPLEX;                       // an expired entry to reclaim
+                    } else if ((s1 | s2) & 0xFFFFu) {             // is the key in the table?
+                        const uint32_t src = a.s_src[p], dst = a.s_dst[p], id = a.s_id[p];
+                        for (uint32_t h = 0; h < 2; ++h) {
+                            const uint32_t *e = a.tab + (size_t)(h ? bk2 : bk1) * a.assoc * E_WORDS;
+                            for (uint32_t k = 0; k < a.assoc; ++k, e += E_WORDS)
+                                if (ld_a(e + E_VALID) && ld_a(e + E_SRC) == src && ld_a(e + E_DST) == dst &&
+                                    ld_a(e + E_ID) == id)
+                                    flag |= PF_COMPLEX;
                         }
                     }
-                }
-                if (__shfl(outcome, 0, 64)) {
-                    if (cur != RS_VIRTUAL) table_release(a, cur, st, true);
-                    cur = RS_NONE;
-                }
-            }
-            if (cur == RS_VIRTUAL) {
-                // still pending: the flow takes a table entry now (its key is not in the table:
-                // no other wave handles it), or is dropped if its buckets have filled meanwhile
-                cur = table_find(a, ksrc, kdst, kid, sig, tag, s_tmp[w], cnt, false);
-                if (cur == RS_NONE) {
-                    if (lane == 0) atomicAdd(&cnt[UDPDK_RS_NO_SPACE], 1ull);
-                } else if (lane >= E_VALID && lane < E_USED) {
-                    st_a(a.tab + (size_t)cur * E_WORDS + lane, st[lane]);
-                }
-            }
-            if (cur != RS_NONE) {
-                if (lane == 0) {
-                    // still pending: this call's fragments move into the entry buffer (reasm_store)
-                    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
-                        if (st[E_FR + k] && st[E_WHERE + k] != RS_HELD) {
-                            ReasmJob jb;
-                            jb.frame = st[E_WHERE + k];
-                            jb.entry = cur;
-                            jb.fr = st[E_FR + k];
-                            jb.pad = 0;
-                            a.jobs[s_pos[w][k]] = jb;
-                            st[E_WHERE + k] = RS_HELD;
-                            atomicAdd(&cnt[UDPDK_RS_STORED], 1ull);
-                        }
+                    a.sb1[p] = bk1;
+                    a.sb2[p] = bk2;
+                    a.tf[p] = tfirst;
+                    a.tl[p] = tlast;
+                    nrec = bk1 != bk2 ? 2u : 1u;
+                    if (flag & PF_COMPLEX) {
+                        atomicAdd(&a.cplx[bk1], 1u);
+                        if (bk2 != bk1) atomicAdd(&a.cplx[bk2], 1u);
                     }
                 }
-                table_release(a, cur, st, false);
+            }
+            if (p < F) a.pflag[p] = flag;
+            uint32_t total;
+            const uint32_t off = wave_excl_scan(nrec, &total);
+            uint32_t base = 0;
+            if (__lane_id() == 0 && total) base = atomicAdd(&s_nr, total);     // LDS
+            base = __shfl(base, 0, 64) + off;
+            if (nrec) {
+                s_rk[base] = ((unsigned long long)bk1 << a.ib) | tfirst;
+                s_rv[base] = p;
+                if (nrec == 2) {
+                    s_rk[base + 1] = ((unsigned long long)bk2 << a.ib) | tfirst;
+                    s_rv[base + 1] = p;
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t nr = s_nr;
+        if (threadIdx.x == 0) s_base = nr ? atomicAdd(&a.counts[1], nr) : 0u;
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nr; k += RS_BLOCK) {
+            a.rk[s_base + k] = s_rk[k];
+            a.rv[s_base + k] = s_rv[k];
+        }
+        __syncthreads();
+    }
+}
+
+// Records sorted by (bucket, tf): x = bucket << 32 | tl, whose running maximum gives, per
+// record, the latest end among the flows of its bucket that start before it.
+__global__ void __launch_bounds__(RS_BLOCK) reasm_rec(ReasmArgs a, const unsigned long long *rks,
+                                                      const uint32_t *rvs, unsigned long long *x, uint32_t R)
+{
+    for (uint32_t k = blockIdx.x * RS_BLOCK + threadIdx.x; k < R; k += gridDim.x * RS_BLOCK)
+        x[k] = ((rks[k] >> a.ib) << 32) | a.tl[rvs[k]];
+}
+
+// A flow whose span overlaps the span of another flow on a bucket they share is PF_SHARED
+// (counted as complex in both its buckets the first time it becomes complex).
+__global__ void __launch_bounds__(RS_BLOCK) reasm_overlap(ReasmArgs a, const unsigned long long *rks,
+                                                          const uint32_t *rvs, const unsigned long long *xs,
+                                                          uint32_t R)
+{
+    const unsigned long long tmask = (1ull << a.ib) - 1ull;
+    for (uint32_t k = blockIdx.x * RS_BLOCK + threadIdx.x; k < R; k += gridDim.x * RS_BLOCK) {
+        const unsigned long long key = rks[k];
+        const unsigned long long b = key >> a.ib;
+        const uint32_t t1 = (uint32_t)(key & tmask), p = rvs[k], t2 = a.tl[p];
+        bool ov = k > 0 && (xs[k - 1] >> 32) == b && (uint32_t)xs[k - 1] >= t1;
+        ov = ov || (k + 1 < R && (rks[k + 1] >> a.ib) == b && (uint32_t)(rks[k + 1] & tmask) <= t2);
+        if (ov) {
+            const uint32_t old = atomicOr(&a.pflag[p], PF_SHARED);
+            if (!(old & (PF_COMPLEX | PF_SHARED))) {
+                atomicAdd(&a.cplx[a.sb1[p]], 1u);
+                if (a.sb2[p] != a.sb1[p]) atomicAdd(&a.cplx[a.sb2[p]], 1u);
             }
         }
     }
+}
+
+// A flow that is neither complex nor shared runs without the table only if its ip_frag_find is
+// sure to find a free entry: its buckets' free entries at call start minus the complex flows
+// that could hold one of them. Otherwise every flow of the batch takes the serial path.
+__global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
+{
+    for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
+        const uint32_t f = a.pflag[p];
+        if (!(f & PF_TOUCH) || (f & (PF_COMPLEX | PF_SHARED))) continue;
+        const uint32_t b1 = a.sb1[p], b2 = a.sb2[p];
+        int32_t fr = (int32_t)a.assoc - (int32_t)(a.bsum[b1] & 0xFFFFu) - (int32_t)a.cplx[b1];
+        if (b2 != b1) fr += (int32_t)a.assoc - (int32_t)(a.bsum[b2] & 0xFFFFu) - (int32_t)a.cplx[b2];
+        if (fr < 1) a.counts[3] = 1u;
+    }
+}
+
+// One thread per flow segment. A flow that cannot see or be seen by another flow (not complex,
+// not shared, and no fallback) is reassembled here on its own state, never touching the table:
+// a reference that processes the batch one fragment at a time gives it a free entry at its
+// first fragment and frees it at its last, with no other lookup in its buckets in between.
+// Every other flow's fragments that reach ip_frag_find go to the serial list (arrival index,
+// sorted position). Length-class drops are counted for every flow.
+__global__ void __launch_bounds__(RS_BLOCK) reasm_process(ReasmArgs a, uint32_t F)
+{
+    __shared__ uint32_t s_st[RS_BLOCK][E_WORDS];
+    __shared__ unsigned long long s_cnt[UDPDK_RS_N + 1];    // block totals: stats, out bytes
+    uint32_t *st = s_st[threadIdx.x];
+    if (threadIdx.x <= UDPDK_RS_N) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const bool fallback = a.counts[3] != 0;
+    const uint32_t step = gridDim.x * RS_BLOCK;
+    unsigned long long c_len = 0, c_short = 0, c_done = 0, c_holes = 0, c_err = 0, c_bytes = 0;
+    for (uint32_t p0 = blockIdx.x * RS_BLOCK + (threadIdx.x & ~63u); p0 < F; p0 += step) {
+        const uint32_t p = p0 + __lane_id();
+        uint32_t nser = 0;
+        bool serial = false;
+        if (p < F && seg_start(a, p)) {
+            const uint32_t f = a.pflag[p];
+            serial = (f & PF_TOUCH) && (fallback || (f & (PF_COMPLEX | PF_SHARED)));
+            bool live = false;
+            for (uint32_t q = p; q < F && (q == p || same_key(a, p, q)); ++q) {
+                const uint32_t m = a.s_meta[q], cls = m >> 30;
+                if (cls) {
+                    if (cls == 1) ++c_len;
+                    else ++c_short;
+                    continue;
+                }
+                if (serial) { ++nser; continue; }
+                const uint32_t i = a.s_i[q];
+                if (!live) state_reset(st, 0, 0, 0, 0, 0);
+                uint32_t idx;
+                const uint32_t r = frag_apply(st, m & 0xFFFFu, ((m >> 16) & 0x1FFFu) * 8u, (m >> 29) & 1u, i, &idx);
+                live = r == FA_KEEP;
+                if (r == FA_DONE) {
+                    write_done(a, st, q, i, RS_NONE);
+                    ++c_done;
+                    c_bytes += (34u + st[E_TOTAL] + 15u) & ~15u;
+                } else if (r == FA_HOLE) {
+                    ++c_holes;
+                } else if (r != FA_KEEP) {
+                    ++c_err;
+                }
+            }
+        }
+        uint32_t total;
+        const uint32_t off = wave_excl_scan(nser, &total);
+        uint32_t base = 0;
+        if (__lane_id() == 0 && total) base = atomicAdd(&a.counts[2], total);
+        base = __shfl(base, 0, 64) + off;
+        if (nser) {
+            for (uint32_t q = p; q < F && (q == p || same_key(a, p, q)); ++q) {
+                if (a.s_meta[q] >> 30) continue;
+                a.sl_k[base] = a.s_i[q];
+                a.sl_v[base] = q;
+                ++base;
+            }
+        }
+    }
+    if (c_len) atomicAdd(&s_cnt[UDPDK_RS_DROP_LEN], c_len);
+    if (c_short) atomicAdd(&s_cnt[UDPDK_RS_DROP_SHORT], c_short);
+    if (c_done) atomicAdd(&s_cnt[UDPDK_RS_DONE], c_done);
+    if (c_holes) atomicAdd(&s_cnt[UDPDK_RS_HOLES], c_holes);
+    if (c_err) atomicAdd(&s_cnt[UDPDK_RS_ERRORS], c_err);
+    if (c_bytes) atomicAdd(&s_cnt[UDPDK_RS_N], c_bytes);
     __syncthreads();
     if (threadIdx.x < UDPDK_RS_N && s_cnt[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], s_cnt[threadIdx.x]);
     if (threadIdx.x == UDPDK_RS_N && s_cnt[UDPDK_RS_N]) atomicAdd(a.out_bytes, s_cnt[UDPDK_RS_N]);
+}
+
+// The serial path: one wave takes the listed fragments in arrival order, exactly as the
+// reference's per-fragment rte_ipv4_frag_reassemble_packet does: ip_frag_find (the lanes load the
+// key's 2 x assoc candidate entries at once; match, else the first expired, else the first free
+// entry in ip_frag_lookup's order), ip_frag_process on the entry's words in LDS, write-back or
+// invalidation. It is the only writer of the table while it runs. A fragment that stays in a
+// pending entry gets a store job; a flow that ends later in the call cancels its jobs.
+__global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *list, uint32_t K)
+{
+    __shared__ uint32_t st[E_WORDS];
+    const uint32_t lane = __lane_id();
+    unsigned long long c_ns = 0, c_err = 0, c_holes = 0, c_exp = 0, c_done = 0, c_bytes = 0;
+    long long c_stored = 0;
+    const uint32_t nslot = 2u * a.assoc;
+    for (uint32_t k = 0; k < K; ++k) {
+        const uint32_t q = list[k];
+        const uint32_t i = a.s_i[q], m = a.s_meta[q];
+        const uint32_t src = a.s_src[q], dst = a.s_dst[q], id = a.s_id[q], sig = a.s_sig[q];
+        const uint32_t p1 = sig & a.mask, p2 = ((sig << 7) + (sig >> 14)) & a.mask;
+        // lanes scan p1[0], p2[0], p1[1], p2[1], ... (ip_frag_lookup's order), whole entries
+        const uint32_t slot = (lane & 1u ? p2 : p1) + (lane >> 1);
+        uint32_t w[E_USED];
+        bool match = false, empty = false, stale = false;
+        if (lane < nslot) {
+            const uint32_t *e = a.tab + (size_t)slot * E_WORDS;
+#pragma unroll
+            for (uint32_t j = 1; j < E_USED; ++j) w[j] = ld_a(e + j);
+            const unsigned long long start = ((unsigned long long)w[E_START + 1] << 32) | w[E_START];
+            match = w[E_VALID] && w[E_SRC] == src && w[E_DST] == dst && w[E_ID] == id;
+            stale = w[E_VALID] && !match && a.max_cycles + start < a.tms;
+            empty = !w[E_VALID];
+        }
+        const unsigned long long mm = __ballot(match), ms = __ballot(stale), me = __ballot(empty);
+        const unsigned long long pick = mm ? mm : ms ? ms : me;
+        if (!pick) {
+            ++c_ns;                                          // ip_frag_find: no space
+            continue;
+        }
+        const uint32_t cl = (uint32_t)__ffsll((long long)pick) - 1u;
+        const uint32_t cand = __shfl(slot, cl, 64);
+        if (lane == cl) {
+#pragma unroll
+            for (uint32_t j = 1; j < E_USED; ++j) st[j] = w[j];
+        }
+        wave_sync_rs();
+        uint32_t inval = 0;
+        if (lane == 0) {
+            bool fresh = !mm;                                // ip_frag_tbl_add (after del if stale)
+            if (ms && !mm) ++c_exp;
+            if (mm && a.max_cycles + (((unsigned long long)st[E_START + 1] << 32) | st[E_START]) < a.tms) {
+                ++c_exp;                                     // ip_frag_tbl_reuse
+                fresh = true;
+            }
+            if (fresh) {
+                state_reset(st, src, dst, id, a.tms, a.call);
+            } else if (st[E_CALL] != a.call) {               // fragments of earlier calls are held
+                for (uint32_t j = 0; j < RS_MAX_FRAG; ++j) st[E_WHERE + j] = RS_HELD;
+                st[E_CALL] = a.call;
+            }
+            uint32_t idx = RS_NONE;
+            const uint32_t r = frag_apply(st, m & 0xFFFFu, ((m >> 16) & 0x1FFFu) * 8u, (m >> 29) & 1u, i, &idx);
+            uint32_t *tp = a.tpos + (size_t)cand * RS_MAX_FRAG;
+            if (r == FA_KEEP) {
+                tp[idx] = q;
+                ReasmJob jb;
+                jb.frame = i;
+                jb.entry = cand;
+                jb.fr = st[E_FR + idx];
+                jb.pad = 0;
+                a.jobs[q] = jb;
+                ++c_stored;
+            } else {
+                if (r == FA_DONE) {
+                    write_done(a, st, q, i, cand);
+                    ++c_done;
+                    c_bytes += (34u + st[E_TOTAL] + 15u) & ~15u;
+                } else if (r == FA_HOLE) {
+                    ++c_holes;
+                } else {
+                    ++c_err;
+                }
+                // the flow ends: this call's fragments it held no longer go to the table
+                for (uint32_t j = 0; j < RS_MAX_FRAG; ++j) {
+                    if (j == idx || !st[E_FR + j] || st[E_WHERE + j] == RS_HELD) continue;
+                    a.jobs[tp[j]].frame = RS_NONE;
+                    --c_stored;
+                }
+                inval = 1;
+            }
+        }
+        wave_sync_rs();
+        inval = __shfl(inval, 0, 64);
+        uint32_t *e = a.tab + (size_t)cand * E_WORDS;
+        if (inval) {
+            if (lane == 0) st_a(e + E_VALID, 0u);
+        } else if (lane >= E_VALID && lane < E_USED) {
+            st_a(e + lane, st[lane]);
+        }
+        stores_done();
+        wave_sync_rs();
+    }
+    if (lane == 0) {
+        unsigned long long *s = a.stats;
+        if (c_ns) atomicAdd(&s[UDPDK_RS_NO_SPACE], c_ns);
+        if (c_err) atomicAdd(&s[UDPDK_RS_ERRORS], c_err);
+        if (c_holes) atomicAdd(&s[UDPDK_RS_HOLES], c_holes);
+        if (c_exp) atomicAdd(&s[UDPDK_RS_EXPIRED], c_exp);
+        if (c_done) atomicAdd(&s[UDPDK_RS_DONE], c_done);
+        if (c_stored) atomicAdd(&s[UDPDK_RS_STORED], (unsigned long long)c_stored);
+        if (c_bytes) atomicAdd(a.out_bytes, c_bytes);
+    }
 }
 
 // Frame sizes of the completions in origin order (for the offset scan).
@@ -675,18 +891,22 @@ struct Reasm {
     int device = 0;
     uint32_t *tab = nullptr;                 // [entries][E_WORDS]
     uint8_t *ebuf = nullptr;
-    uint32_t entries = 0, assoc = 0, mask = 0, max_dgram = 0, stride = 0;
+    uint32_t entries = 0, assoc = 0, mask = 0, max_dgram = 0, stride = 0, assoc_log2 = 0, nbuckets = 0;
     uint64_t max_cycles = 0;
     uint32_t cap = 0;                        // fragments per call (= context max_frames)
     uint32_t *frag_list = nullptr, *v1 = nullptr, *v1s = nullptr, *v2s = nullptr;
     unsigned long long *k1 = nullptr, *k1s = nullptr, *k2 = nullptr, *k2s = nullptr;
-    uint32_t *counts = nullptr;              // device [4]
+    uint32_t *counts = nullptr;              // device [4]: F, records, serial list, fallback
     unsigned long long *stats = nullptr;     // device [UDPDK_RS_N]
     unsigned long long *out_bytes = nullptr;
     ReasmDone *done = nullptr;
     ReasmJob *jobs = nullptr;
     uint32_t *dk = nullptr, *dks = nullptr;
     uint32_t *dv = nullptr, *perm = nullptr, *sizes = nullptr, *offs = nullptr;
+    uint32_t *pflag = nullptr, *sb1 = nullptr, *sb2 = nullptr, *tf = nullptr, *tl = nullptr;
+    unsigned long long *rk = nullptr, *rks = nullptr, *rx = nullptr;
+    uint32_t *rv = nullptr, *rvs = nullptr, *bsum = nullptr, *cplx = nullptr, *tpos = nullptr;
+    uint32_t *sl_k = nullptr, *sl_ks = nullptr, *sl_v = nullptr, *sl_vs = nullptr;
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
     uint32_t *host = nullptr;                // pinned readback: counts + out_bytes + stats
@@ -719,7 +939,8 @@ void reasm_destroy(Reasm *r)
     void *dev[] = {r->tab, r->ebuf, r->frag_list, r->v1, r->v1s, r->v2s, r->k1, r->k1s, r->k2,
                    r->k2s, r->counts, r->stats, r->out_bytes, r->done, r->jobs, r->dk, r->dks,
                    r->dv, r->perm, r->sizes, r->offs, r->tmp, r->out, r->out_off, r->out_ptype,
-                   r->out_origin, r->out_len};
+                   r->out_origin, r->out_len, r->pflag, r->sb1, r->sb2, r->tf, r->tl, r->rk, r->rks,
+                   r->rx, r->rv, r->rvs, r->bsum, r->cplx, r->tpos, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (r->host) (void)hipHostFree(r->host);
@@ -740,6 +961,8 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
     r->device = device;
     r->entries = (uint32_t)entries;
     r->assoc = cfg->bucket_entries;
+    r->assoc_log2 = (uint32_t)__builtin_ctz(r->assoc);
+    r->nbuckets = r->entries / r->assoc;
     r->mask = (r->entries - 1u) & ~(r->assoc - 1u);
     r->max_cycles = cfg->max_cycles;
     r->max_dgram = cfg->max_dgram;
@@ -748,7 +971,7 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
     int rc = 0;
     auto fail = [&](hipError_t e) { *hip_err = (int)e; rc = e == hipErrorOutOfMemory ? -ENOMEM : -EIO; };
     hipError_t e = hipSuccess;
-    const size_t C = r->cap;
+    const size_t C = r->cap, C2 = 2 * (size_t)r->cap;
     if ((e = dalloc(&r->tab, (size_t)r->entries * E_WORDS)) != hipSuccess ||
         (e = hipMemset(r->tab, 0, (size_t)r->entries * E_WORDS * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void **)&r->ebuf, (size_t)r->entries * r->stride)) != hipSuccess ||
@@ -763,22 +986,38 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
         (e = dalloc(&r->sizes, C)) != hipSuccess || (e = dalloc(&r->offs, C)) != hipSuccess ||
         (e = dalloc(&r->out_off, C)) != hipSuccess || (e = dalloc(&r->out_len, C)) != hipSuccess ||
         (e = dalloc(&r->out_ptype, C)) != hipSuccess || (e = dalloc(&r->out_origin, C)) != hipSuccess ||
+        (e = dalloc(&r->pflag, C)) != hipSuccess || (e = dalloc(&r->sb1, C)) != hipSuccess ||
+        (e = dalloc(&r->sb2, C)) != hipSuccess || (e = dalloc(&r->tf, C)) != hipSuccess ||
+        (e = dalloc(&r->tl, C)) != hipSuccess || (e = dalloc(&r->rk, C2)) != hipSuccess ||
+        (e = dalloc(&r->rks, C2)) != hipSuccess || (e = dalloc(&r->rx, C2)) != hipSuccess ||
+        (e = dalloc(&r->rv, C2)) != hipSuccess || (e = dalloc(&r->rvs, C2)) != hipSuccess ||
+        (e = dalloc(&r->bsum, r->nbuckets)) != hipSuccess || (e = dalloc(&r->cplx, r->nbuckets)) != hipSuccess ||
+        (e = dalloc(&r->tpos, (size_t)r->entries * RS_MAX_FRAG)) != hipSuccess ||
+        (e = dalloc(&r->sl_k, C)) != hipSuccess || (e = dalloc(&r->sl_ks, C)) != hipSuccess ||
+        (e = dalloc(&r->sl_v, C)) != hipSuccess || (e = dalloc(&r->sl_vs, C)) != hipSuccess ||
         (e = hipHostMalloc((void **)&r->host, 4096)) != hipSuccess) {
         fail(e);
         reasm_destroy(r);
         return rc;
     }
-    // rocPRIM temporary storage for the largest call (sorts of u64 keys / u32 values, u32 scan)
-    size_t t1 = 0, t2 = 0, t3 = 0;
-    if ((e = rocprim::radix_sort_pairs(nullptr, t1, r->k1, r->k1s, r->v1s, r->v2s, (size_t)C, 0, 64)) != hipSuccess ||
-        (e = rocprim::radix_sort_pairs(nullptr, t3, r->dk, r->dks, r->v1s, r->v2s, (size_t)C, 0, 32)) != hipSuccess ||
-        (e = rocprim::exclusive_scan(nullptr, t2, r->sizes, r->offs, 0u, (size_t)C, rocprim::plus<uint32_t>())) != hipSuccess ||
-        (e = hipMalloc(&r->tmp, std::max<size_t>(std::max(std::max(t1, t2), t3), 256))) != hipSuccess) {
+    // rocPRIM temporary storage for the largest call (sorts of u64 keys / u32 values, u32 scan,
+    // u64 max scan)
+    size_t t[5] = {0, 0, 0, 0, 0};
+    if ((e = rocprim::radix_sort_pairs(nullptr, t[0], r->k1, r->k1s, r->v1s, r->v2s, C, 0, 64)) != hipSuccess ||
+        (e = rocprim::radix_sort_pairs(nullptr, t[1], r->dk, r->dks, r->v1s, r->v2s, C, 0, 32)) != hipSuccess ||
+        (e = rocprim::exclusive_scan(nullptr, t[2], r->sizes, r->offs, 0u, C, rocprim::plus<uint32_t>())) != hipSuccess ||
+        (e = rocprim::radix_sort_pairs(nullptr, t[3], r->rk, r->rks, r->rv, r->rvs, C2, 0, 64)) != hipSuccess ||
+        (e = rocprim::inclusive_scan(nullptr, t[4], r->rk, r->rx, C2, rocprim::maximum<unsigned long long>())) != hipSuccess) {
         fail(e);
         reasm_destroy(r);
         return rc;
     }
-    r->tmp_bytes = std::max<size_t>(std::max(std::max(t1, t2), t3), 256);
+    r->tmp_bytes = std::max<size_t>(*std::max_element(t, t + 5), 256);
+    if ((e = hipMalloc(&r->tmp, r->tmp_bytes)) != hipSuccess) {
+        fail(e);
+        reasm_destroy(r);
+        return rc;
+    }
     *out = r;
     return 0;
 }
@@ -815,17 +1054,33 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     a.dk = r->dk;
     a.dv = r->dv;
     a.jobs = r->jobs;
-    a.tag_base = 0;
+    a.assoc_log2 = r->assoc_log2;
+    a.nbuckets = r->nbuckets;
+    a.pflag = r->pflag;
+    a.sb1 = r->sb1;
+    a.sb2 = r->sb2;
+    a.tf = r->tf;
+    a.tl = r->tl;
+    a.rk = r->rk;
+    a.rv = r->rv;
+    a.bsum = r->bsum;
+    a.cplx = r->cplx;
+    a.sl_k = r->sl_k;
+    a.sl_v = r->sl_v;
+    a.tpos = r->tpos;
+    if (++r->calls == 0) r->calls = 1;          // 0 marks entries never touched
+    a.call = r->calls;
     a.ib = bits_for(n - 1u);
     RS_HIP(hipMemsetAsync(r->counts, 0, 4 * sizeof(uint32_t), st));
     RS_HIP(hipMemsetAsync(r->stats, 0, UDPDK_RS_N * sizeof(unsigned long long), st));
     RS_HIP(hipMemsetAsync(r->out_bytes, 0, sizeof(unsigned long long), st));
-    const uint32_t g1 = std::max<uint32_t>(1, std::min<uint32_t>((n + 2047) / 2048, 1024));
+    const uint32_t g1 = std::max<uint32_t>(1, std::min<uint32_t>((n + 1023) / 1024, 2048));
     hipLaunchKernelGGL(reasm_collect, dim3(g1), dim3(RS_BLOCK), 0, st, a);
     RS_HIP(hipGetLastError());
     RS_HIP(hipMemcpyAsync(r->host, r->counts, 4, hipMemcpyDeviceToHost, st));
     RS_HIP(hipStreamSynchronize(st));
     const uint32_t F = r->host[0];
+    uint32_t K = 0;                          // fragments on the serial path
     memset(o, 0, sizeof(*o));
     if (F) {
         size_t tb = r->tmp_bytes;
@@ -847,11 +1102,46 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         RS_HIP(hipGetLastError());
         RS_HIP(hipMemsetAsync(r->dk, 0xFF, (size_t)F * sizeof(uint32_t), st));
         RS_HIP(hipMemsetAsync(r->jobs, 0xFF, (size_t)F * sizeof(ReasmJob), st));
-        a.tag_base = (r->calls++ & 0x3FFu) << 20;
-        const uint32_t waves = (F + 63u) / 64u;
-        const uint32_t gp = std::max<uint32_t>(1, std::min<uint32_t>((waves + RS_WAVES - 1) / RS_WAVES, 2048));
-        hipLaunchKernelGGL(reasm_process, dim3(gp), dim3(RS_BLOCK), 0, st, a, F);
+        // flow analysis: which flows can run without the table (see the top of this file)
+        const uint32_t gb = std::max<uint32_t>(1, std::min<uint32_t>((r->entries + RS_BLOCK - 1) / RS_BLOCK, 4096));
+        hipLaunchKernelGGL(reasm_bsum, dim3(gb), dim3(RS_BLOCK), 0, st, a);
         RS_HIP(hipGetLastError());
+        const uint32_t gfl = std::max<uint32_t>(1, std::min<uint32_t>((F + RS_FLOW_CHUNK - 1) / RS_FLOW_CHUNK, 2048));
+        hipLaunchKernelGGL(reasm_flows, dim3(gfl), dim3(RS_BLOCK), 0, st, a, F);
+        RS_HIP(hipGetLastError());
+        RS_HIP(hipMemcpyAsync(r->host, r->counts, 8, hipMemcpyDeviceToHost, st));
+        RS_HIP(hipStreamSynchronize(st));
+        const uint32_t R = r->host[1];
+        if (R) {
+            tb = r->tmp_bytes;
+            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->rk, r->rks, r->rv, r->rvs, (size_t)R, 0,
+                                             a.ib + bits_for(r->nbuckets - 1u), st));
+            const uint32_t gR = std::max<uint32_t>(1, std::min<uint32_t>((R + RS_BLOCK - 1) / RS_BLOCK, 4096));
+            hipLaunchKernelGGL(reasm_rec, dim3(gR), dim3(RS_BLOCK), 0, st, a,
+                               (const unsigned long long *)r->rks, (const uint32_t *)r->rvs, r->rk, R);
+            RS_HIP(hipGetLastError());
+            tb = r->tmp_bytes;
+            RS_HIP(rocprim::inclusive_scan(r->tmp, tb, r->rk, r->rx, (size_t)R,
+                                           rocprim::maximum<unsigned long long>(), st));
+            hipLaunchKernelGGL(reasm_overlap, dim3(gR), dim3(RS_BLOCK), 0, st, a,
+                               (const unsigned long long *)r->rks, (const uint32_t *)r->rvs,
+                               (const unsigned long long *)r->rx, R);
+            RS_HIP(hipGetLastError());
+        }
+        hipLaunchKernelGGL(reasm_ec, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
+        RS_HIP(hipGetLastError());
+        hipLaunchKernelGGL(reasm_process, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
+        RS_HIP(hipGetLastError());
+        RS_HIP(hipMemcpyAsync(r->host, r->counts, 16, hipMemcpyDeviceToHost, st));
+        RS_HIP(hipStreamSynchronize(st));
+        K = r->host[2];
+        if (K) {
+            tb = r->tmp_bytes;
+            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs, (size_t)K, 0,
+                                             bits_for(n - 1u), st));
+            hipLaunchKernelGGL(reasm_serial, dim3(1), dim3(64), 0, st, a, (const uint32_t *)r->sl_vs, K);
+            RS_HIP(hipGetLastError());
+        }
     }
     RS_HIP(hipMemcpyAsync(r->host + 4, r->out_bytes, 8, hipMemcpyDeviceToHost, st));
     RS_HIP(hipMemcpyAsync(r->host + 8, r->stats, UDPDK_RS_N * 8, hipMemcpyDeviceToHost, st));
@@ -859,6 +1149,8 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     uint64_t ob;
     memcpy(&ob, r->host + 4, 8);
     memcpy(o->stats, r->host + 8, UDPDK_RS_N * 8);
+    o->stats[UDPDK_RS_FRAGS] = F;
+    o->stats[UDPDK_RS_SERIAL] = K;
     const uint32_t Cn = (uint32_t)o->stats[UDPDK_RS_DONE], J = (uint32_t)o->stats[UDPDK_RS_STORED];
     if (Cn) {
         if (ob + UDPDK_GPU_FRAMES_TAILROOM > r->out_cap) {

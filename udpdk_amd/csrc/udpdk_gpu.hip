@@ -1103,7 +1103,10 @@ int udpdk_gpu_tx_build_mtu(udpdk_gpu_ctx *c, const udpdk_tx_config_t *cfg,
     ta.n = bt->n;
     ta.n_slots = c->n_slots;
     ta.payload_bytes = (uint32_t)bt->payload_bytes;
-    ta.payload_rsrc = (uint32_t)std::min<uint64_t>((bt->payload_bytes + 15) & ~15ull, 0xFFFFFFFFull);
+    // a dword comes back from a buffer load only if it ends inside the range: a
+    // payload's last bytes are read by a byte-aligned load whose last dword may end up to 3
+    // bytes past payload_bytes, inside the caller's UDPDK_GPU_FRAMES_TAILROOM
+    ta.payload_rsrc = (uint32_t)std::min<uint64_t>((bt->payload_bytes + 3 + 3) & ~3ull, 0xFFFFFFFCull);
     ta.frames_bytes = (uint32_t)o->frames_bytes;
     ta.src_ip = cfg->src_ip;
     ta.mtu = mtu;
