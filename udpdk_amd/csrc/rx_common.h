@@ -9,7 +9,10 @@ namespace udpdk {
 constexpr int RX_BLOCK  = 256;              // rx_classify workgroup (4 waves)
 constexpr int RX_WAVES  = RX_BLOCK / 64;
 constexpr int RX_UNROLL = 4;                // 16-byte chunk loads in flight per lane
-constexpr uint32_t RX_TILE_MIN = 1024;      // frames per tile (histogram granularity)
+#ifndef UDPDK_RX_ROUND
+#define UDPDK_RX_ROUND 1024
+#endif
+constexpr uint32_t RX_TILE_MIN = UDPDK_RX_ROUND;   // frames per tile (histogram granularity)
 constexpr uint32_t RX_TILE_MAX = 8192;   // classify LDS: <= 143 KiB at 16384 lanes
 constexpr uint32_t RX_HIST_CAP = 1u << 21;  // target bound on lanes x tiles
 #ifndef UDPDK_CLS_BLOCK
@@ -36,7 +39,7 @@ constexpr int TX_BLOCK = 256;
 // length | ptype bit); the tile's per-lane delivery histogram; the tile's verdict words; the
 // round's datagram ends + window sums (frames whose UDP checksum waits for the tail pass);
 // the round's port-table lookups (dst port, dst IPv4).
-constexpr uint32_t RX_ROUND = 1024;               // frames per descriptor-staging / tail round
+constexpr uint32_t RX_ROUND = UDPDK_RX_ROUND;     // frames per descriptor-staging / tail round
 constexpr int TP_OFF      = 0;                    // [CLS_WAVES][3][64] chunk base, datagram left, mark
 constexpr int CNT_OFF     = TP_OFF + CLS_WAVES * 3 * 64 * 4;     // [CLS_WAVES][16] counter rows
 constexpr int DSC_OFF     = CNT_OFF + CLS_WAVES * 16 * 4;

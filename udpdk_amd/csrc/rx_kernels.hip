@@ -226,7 +226,8 @@ rx_classify(RxArgs a)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t steps = a.tile_frames / 64;
-    constexpr uint32_t SPR = (RX_ROUND / 64) / CLS_WAVES;   // steps per wave per staging round
+    constexpr uint32_t RSTEPS = RX_ROUND / 64;              // steps per staging round
+    constexpr uint32_t SPR = RSTEPS / CLS_WAVES;            // steps per wave per staging round
     static_assert(SPR >= 2, "round staging needs two steps per wave per round");
 #ifdef UDPDK_STAMPS
     unsigned long long st_acc[16] = {0}, st_last = __builtin_amdgcn_s_memtime();
@@ -428,7 +429,7 @@ rx_classify(RxArgs a)
 
     // rounds of RX_ROUND frames: SPR steps per wave (each followed by its tail pass when a frame
     // of the step is pending), then the round's demux pass
-    for (uint32_t rnd = 0; rnd < steps / 16u; ++rnd) {
+    for (uint32_t rnd = 0; rnd < steps / RSTEPS; ++rnd) {
 #pragma unroll 1
         for (uint32_t jstep = 0; jstep < SPR; ++jstep) {
             const uint32_t p = t0 + st * 64 + lane;
@@ -522,8 +523,8 @@ rx_classify(RxArgs a)
             // buffer were before the previous round's barrier, and the next round is first read at
             // j = SPR - 1.
             // Uniform across the workgroup (every wave has steps / 4 steps).
-            if ((st / CLS_WAVES) % SPR == SPR - 2u && (st >> 4) + 1u < steps / 16u) {
-                stage((st >> 4) + 1u);
+            if ((st / CLS_WAVES) % SPR == SPR - 2u && st / RSTEPS + 1u < steps / RSTEPS) {
+                stage(st / RSTEPS + 1u);
                 __syncthreads();
             }
             W = NW;
@@ -539,12 +540,12 @@ rx_classify(RxArgs a)
             uint4 E[SPR];
             uint2 S[SPR];
 #pragma unroll
-            for (uint32_t j = 0; j < SPR; ++j) S[j] = dstash[((st - 16u + CLS_WAVES * j) * 64 + lane) & (RX_ROUND - 1u)];
+            for (uint32_t j = 0; j < SPR; ++j) S[j] = dstash[((st - RSTEPS + CLS_WAVES * j) * 64 + lane) & (RX_ROUND - 1u)];
 #pragma unroll
             for (uint32_t j = 0; j < SPR; ++j) E[j] = a.port_tab[S[j].x & 0xFFFFu];
 #pragma unroll
             for (uint32_t j = 0; j < SPR; ++j) {
-                const uint32_t i = (st - 16u + CLS_WAVES * j) * 64 + lane;
+                const uint32_t i = (st - RSTEPS + CLS_WAVES * j) * 64 + lane;
                 const uint32_t m = mstage[i];
                 const bool valid = t0 + i < t1;
                 const uint4 e = (S[j].x >> 16) ? E[j] : make_uint4(0, 0, 0, 0);
@@ -698,6 +699,7 @@ rx_compact1(Compact1Args a)
         for (int u = 0; u < 4; ++u) mv[u] = a.meta[min(wb + (s0 + u) * 64 + lane, plast)];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
+            if (s0 + u >= steps) break;                     // fewer than 4 steps per wave
             const uint32_t p = wb + (s0 + u) * 64 + lane;
             const unsigned long long m = __ballot(p < t1 && (mv[u] & 0xFu) == UDPDK_V_DELIVERED);
             if (lane == 0) msk[w][s0 + u] = m;
