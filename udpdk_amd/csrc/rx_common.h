@@ -50,10 +50,18 @@ __host__ __device__ constexpr uint32_t classify_dsc_bufs(uint32_t tile_frames)
     return tile_frames > RX_ROUND ? 2u : 1u;
 }
 
+// verdict words staged in LDS: the whole tile when it is one round (stored once at the tile end,
+// 16 B per lane), else one round (each round stored at the end of its demux pass)
+__host__ __device__ constexpr uint32_t classify_stage_frames(uint32_t tile_frames)
+{
+    return tile_frames > RX_ROUND ? RX_ROUND : tile_frames;
+}
+
 __host__ __device__ constexpr uint32_t classify_lds_bytes(uint32_t n_lanes, uint32_t tile_frames)
 {
     return (uint32_t)DSC_OFF + 8u * RX_ROUND * classify_dsc_bufs(tile_frames) +
-           4u * ((n_lanes + 3u) & ~3u) + 4u * tile_frames + 4u * RX_ROUND + 8u * RX_ROUND;
+           4u * ((n_lanes + 3u) & ~3u) + 4u * classify_stage_frames(tile_frames) + 4u * RX_ROUND +
+           8u * RX_ROUND;
 }
 
 // Port table entry (16 B per raw port): x = bindings on the port, y = index of the first in the

@@ -245,10 +245,10 @@ rx_classify(RxArgs a)
     // The tile's verdict words are staged in LDS and stored once per tile (16 B per lane): no
     // global store inside the step loop, so no s_waitcnt there ever waits for a store (on gfx9
     // stores count in vmcnt, in order with the loads).
-    uint32_t *mstage = hist + ((a.n_lanes + 3u) & ~3u);              // [tile_frames]
+    uint32_t *mstage = hist + ((a.n_lanes + 3u) & ~3u);              // [stage frames], index & SMASK
     // datagram end (34 + UDP length) of the frames whose checksum the tail pass completes
     // pending frames' datagram end | folded window part of the UDP sum << 16
-    uint32_t *dgl = mstage + a.tile_frames;                          // [RX_ROUND]
+    uint32_t *dgl = mstage + classify_stage_frames(a.tile_frames);   // [RX_ROUND]
     // the round's port-table lookups: raw dst port | is-UDP << 16, raw dst IPv4
     uint2 *dstash = reinterpret_cast<uint2 *>(dgl + RX_ROUND);       // [RX_ROUND]
 
@@ -345,7 +345,7 @@ rx_classify(RxArgs a)
     constexpr uint32_t OOR = 0xFFFFFFF0u;   // past any batch's range (< 4 GiB - 16)
     auto tail_step = [&](uint32_t s2) {
             const uint32_t i = s2 * 64 + lane;
-            const uint32_t m = mstage[i];
+            const uint32_t m = mstage[i & (RX_ROUND - 1u)];
             const bool pd = t0 + i < t1 && ((m >> 5) & 3u) == 3u;
             if (!__ballot(pd)) return;
             // the frame's offset: the staged descriptor of a single-round tile, else global
@@ -422,7 +422,7 @@ rx_classify(RxArgs a)
             wave_sync();
             if (pd) {
                 const bool ok = fold32(fold32(tsum) + (dw >> 16)) == 0xFFFFu;
-                mstage[i] = (m & ~0x60u) | ((ok ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD) << 5);
+                mstage[i & (RX_ROUND - 1u)] = (m & ~0x60u) | ((ok ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD) << 5);
                 acc_f0 += ok ? 0x10000u : 0x1000000u;
             }
     };
@@ -514,7 +514,7 @@ rx_classify(RxArgs a)
             if (good) lane_bytes += len;
 
             // the port-table lookup waits for the round's demux pass: verdict field 0xF until then
-            mstage[st * 64 + lane] = (pre == 0xFFu ? 0xFu : pre) | l3f | udpf;
+            mstage[(st * 64 + lane) & (RX_ROUND - 1u)] = (pre == 0xFFu ? 0xFu : pre) | l3f | udpf;
             dstash[(st * 64 + lane) & (RX_ROUND - 1u)] = make_uint2(dport | (is_udp ? 0x10000u : 0u), dip);
             if (__ballot(pend)) tail_step(st);
             STAMP(6);
@@ -546,7 +546,7 @@ rx_classify(RxArgs a)
 #pragma unroll
             for (uint32_t j = 0; j < SPR; ++j) {
                 const uint32_t i = (st - RSTEPS + CLS_WAVES * j) * 64 + lane;
-                const uint32_t m = mstage[i];
+                const uint32_t m = mstage[i & (RX_ROUND - 1u)];
                 const bool valid = t0 + i < t1;
                 const uint4 e = (S[j].x >> 16) ? E[j] : make_uint4(0, 0, 0, 0);
                 const uint32_t dip = S[j].y;
@@ -573,7 +573,11 @@ rx_classify(RxArgs a)
                 const uint32_t verdict = pre != 0xFu ? pre
                                        : e.x == 0u ? UDPDK_V_NO_BIND
                                        : fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
-                mstage[i] = (m & ~0xFu) | verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
+                const uint32_t fin = (m & ~0xFu) | verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
+                mstage[i & (RX_ROUND - 1u)] = fin;
+                // a tile of several rounds stores each round's verdict words here (its LDS holds
+                // one round, so three workgroups fit a CU at 4096 lanes instead of two)
+                if (nbuf > 1u && valid) a.meta[t0 + i] = fin;
                 // per-lane packed counters (8-bit fields; a lane sees <= 64 frames per tile)
                 const uint32_t vinc = valid ? 1u << (8u * (verdict & 3u)) : 0u;
                 acc_v0 += verdict < 4u ? vinc : 0u;
@@ -643,7 +647,7 @@ rx_classify(RxArgs a)
         for (int i = 0; i < CLS_WAVES; ++i) v += cntw[i * 16 + c];
         return v;
     };
-    {
+    if (nbuf == 1u) {
         const uint32_t nv = t1 - t0;
         uint32_t *dst = a.meta + t0;
         if (nv == a.tile_frames && ((uintptr_t)dst & 15u) == 0) {
