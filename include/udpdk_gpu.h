@@ -307,7 +307,10 @@ enum udpdk_rs_stat {
     UDPDK_RS_SERIAL     = 9, /* diagnostic: fragments that went through the table one at a time
                                 in arrival order (flows that share buckets with an overlapping
                                 flow, stay pending, or meet an existing or expired entry)       */
-    UDPDK_RS_N          = 10
+    UDPDK_RS_SORTED     = 10, /* diagnostic: 1 if the batch's flow keys needed the sorts (a key
+                                 with fragments in several runs of the batch), 0 if every key's
+                                 fragments were already one run in arrival order                */
+    UDPDK_RS_N          = 11
 };
 
 typedef struct {

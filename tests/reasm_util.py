@@ -72,12 +72,14 @@ def raw_ip(s):
 
 
 def scenario(seed, n_batches=6, flows_per_batch=120, normal_per_batch=200, ports=(10000, 10001, 10002, 10003),
-             dt=10):
+             dt=10, grouped=False):
     """Seeded multi-batch fragment workload: [(frames list, tms)]. Datagrams are cut into 2..4
     fragments (some into 5: too many), fragments arrive shuffled within a window that spans
     batch boundaries; some are lost (their flows expire later), duplicated (first/last
     duplicates error a flow) or overlapping; keys are sometimes reused after completion;
-    unfragmented UDP frames to the same ports are interleaved."""
+    unfragmented UDP frames to the same ports are interleaved. grouped: each datagram's
+    fragments arrive back to back (in order, duplicates after them) and keys are not reused, so
+    every key is one run of the batch's fragments (batch boundaries still cut flows)."""
     rng = np.random.default_rng(seed)
     src_pool = [raw_ip(f"10.0.{k}.{j}") for k in range(4) for j in range(1, 5)]
     dst = raw_ip("172.31.100.1")
@@ -87,7 +89,7 @@ def scenario(seed, n_batches=6, flows_per_batch=120, normal_per_batch=200, ports
     for b in range(n_batches):
         for k in range(flows_per_batch):
             src = int(rng.choice(src_pool))
-            if used_keys and rng.random() < 0.05:
+            if used_keys and rng.random() < 0.05 and not grouped:
                 src, pid = used_keys[int(rng.integers(len(used_keys)))]
             else:
                 pid = int(rng.integers(0, 65536))
@@ -116,14 +118,17 @@ def scenario(seed, n_batches=6, flows_per_batch=120, normal_per_batch=200, ports
             elif r < 0.16 and len(sizes) >= 2:            # overlapping rewrite of fragment 0
                 frs = frs + [ip_frame(src, dst, pid, 0, d[:sizes[0] + 8], True)]
             t0 = pos + rng.random() * 0.6
-            for f in frs:
-                events.append((t0 + rng.random() * 1.4, f))
+            for j, f in enumerate(frs):
+                events.append((pos + 1e-6 * j if grouped else t0 + rng.random() * 1.4, f))
             pos += 1.0 / flows_per_batch
         for k in range(normal_per_batch):
             port = int(rng.choice(ports))
             d = udp_datagram(0x1027, int.from_bytes(port.to_bytes(2, "big"), "little"),
                              rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8).tobytes())
-            events.append((b + rng.random(), ip_frame(int(rng.choice(src_pool)), dst, 0, 0, d, False)))
+            tn = b + rng.random()
+            if grouped:                                   # between two datagrams' fragments
+                tn = int(tn * flows_per_batch) / flows_per_batch + 0.5 / flows_per_batch
+            events.append((tn, ip_frame(int(rng.choice(src_pool)), dst, 0, 0, d, False)))
     events.sort(key=lambda e: e[0])
     out = []
     for b in range(n_batches + 2):

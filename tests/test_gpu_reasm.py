@@ -47,6 +47,7 @@ def _check_scenario(gpu_ctx, frames_tms, geometry):
         rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, out.meta, tms)
         wout, woo, wol, wog, wst = t.reassemble(buf, off, ln, wm, tms)
         serial = gst.pop("serial")
+        tot["sorted"] = tot.get("sorted", 0) + gst.pop("sorted")
         assert gst == wst, f"batch {b}: stats {gst} vs {wst}"
         assert rb.n == len(woo)
         for k, v in gst.items():
@@ -82,6 +83,19 @@ def test_reassembly_matches_oracle(gpu_ctx, seed):
     for k in ("errors", "holes", "expired", "done", "stored"):
         assert tot[k] > 0, (k, tot)
     assert 0 < tot["serial"] < tot["frags"], tot          # both paths ran
+    assert tot["sorted"] > 0, tot                         # shuffled arrival: the sorted path
+
+
+@pytest.mark.parametrize("seed,buckets,entries", [(21, 256, 16), (22, 4, 4), (23, 1, 8)])
+def test_reassembly_grouped_batches_exact(gpu_ctx, seed, buckets, entries):
+    """Fragments of each datagram back to back (the grouped path: no key sorts, no overlap test,
+    completions by a select) with flows cut by batch boundaries, lost fragments, duplicates and
+    flow expiry; tables from roomy to far too small: every outcome equals the oracle's."""
+    tot = _check_scenario(gpu_ctx, scenario(seed, n_batches=5, flows_per_batch=90, dt=12, grouped=True),
+                          dict(bucket_num=buckets, bucket_entries=entries, max_cycles=20))
+    for k in ("done", "stored", "expired"):
+        assert tot[k] > 0, (k, tot)
+    assert tot["sorted"] == 0, tot                        # every batch took the grouped path
 
 
 @pytest.mark.parametrize("seed,buckets,entries", [(11, 4, 4), (12, 8, 2), (13, 16, 4), (14, 1, 8)])
@@ -107,7 +121,7 @@ def test_reassembly_in_order_is_parallel(gpu_ctx):
     out = abi.rx_alloc_out(gpu_ctx, b.n, 1, b.n)
     assert abi.rx_run(gpu_ctx, db, out)[4] == 0
     rb, _, st = abi.rx_reassemble(gpu_ctx, db, out.meta, 0)
-    assert st["done"] == 4096 and st["serial"] == 0, st
+    assert st["done"] == 4096 and st["serial"] == 0 and st["sorted"] == 0, st
 
 
 def test_no_space_and_table_reuse(gpu_ctx):
@@ -129,6 +143,7 @@ def test_no_space_and_table_reuse(gpu_ctx):
         rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, mb, tms)
         _, woo, _, _, wst = t.reassemble(buf, off, ln, meta, tms)
         gst.pop("serial")
+        gst.pop("sorted")
         assert gst == wst and rb.n == len(woo), (tms, gst, wst)
         for bb in (db.frames, db.offset, db.length, mb):
             bb.free()

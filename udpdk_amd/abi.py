@@ -82,9 +82,9 @@ class RxGather(C.Structure):
                 ("src_ip_dev", C.c_void_p), ("src_port_dev", C.c_void_p)]
 
 
-RS_N = 10                 # udpdk_rs_stat
+RS_N = 11                 # udpdk_rs_stat
 RS_STATS = ("frags", "drop_len", "drop_short", "no_space", "errors", "holes", "expired", "done",
-            "stored", "serial")
+            "stored", "serial", "sorted")
 
 
 class FragTableCfg(C.Structure):

@@ -14,7 +14,10 @@ constexpr int RX_UNROLL = 4;                // 16-byte chunk loads in flight per
 #endif
 constexpr uint32_t RX_TILE_MIN = UDPDK_RX_ROUND;   // frames per tile (histogram granularity)
 constexpr uint32_t RX_TILE_MAX = 8192;   // classify LDS: <= 143 KiB at 16384 lanes
-constexpr uint32_t RX_HIST_CAP = 1u << 21;  // target bound on lanes x tiles
+#ifndef UDPDK_RX_HIST_CAP
+#define UDPDK_RX_HIST_CAP (1u << 21)
+#endif
+constexpr uint32_t RX_HIST_CAP = UDPDK_RX_HIST_CAP;  // target bound on lanes x tiles
 #ifndef UDPDK_CLS_BLOCK
 #define UDPDK_CLS_BLOCK 256
 #endif

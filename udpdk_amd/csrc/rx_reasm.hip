@@ -17,17 +17,21 @@
 //  * every other flow's fragments go through the table in arrival order on one wave
 //    (reasm_serial), which is then exactly the reference's sequence of ip_frag_find calls.
 // Launch sequence (udpdk_gpu_rx_reassemble, synchronous):
-//   reasm_collect   FRAG verdicts -> fragment list + (id << ib | index) sort keys
-//   radix sort 1    by (id, index); reasm_keys: src|dst keys in that order; radix sort 2 (stable)
+//   select          FRAG verdicts -> fragment list in arrival order
+//   reasm_runs      (id << ib | index) sort keys; does every flow key form one run? (grouped)
+//   [not grouped]   radix sort 1 by (id, index); reasm_keys: src|dst keys in that order; radix
+//                   sort 2 (stable). Grouped batches skip both: the list is already grouped
 //   reasm_prep      per sorted position: frame, key, crc32c signature, length class
 //   reasm_bsum      per bucket: valid entries, any expired
 //   reasm_flows     per flow: span, pending or not, key in the table, overlap records
-//   radix sort 4 + max scan + reasm_overlap: flows whose spans overlap on a shared bucket
+//   [not grouped]   radix sort 4 + max scan + reasm_overlap: flows whose spans overlap on a
+//                   shared bucket (grouped: no two spans overlap)
 //   reasm_ec        a free entry guaranteed for every parallel flow, else all go serial
 //   reasm_process   parallel flows without the table; the rest -> serial list
 //   radix sort 5    serial list by arrival; reasm_serial (one wave, the table in arrival order)
 //   radix sort 3    completions by origin (the arrival index of the completing fragment: where
-//                   the reference delivers the datagram) + exclusive scan of frame sizes
+//                   the reference delivers the datagram; grouped: a select of the positions
+//                   holding one) + exclusive scan of frame sizes
 //   reasm_emit      one wave per datagram: first fragment's header (total length, DF only, IPv4
 //                   checksum) + every fragment's data at its offset, from the batch or the table
 //   reasm_store     one wave per fragment left pending: its data (and header, for offset 0) into
@@ -39,6 +43,8 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 #include <stdint.h>
 
 #include <algorithm>
@@ -124,6 +130,7 @@ struct ReasmArgs {
     uint32_t *sl_k, *sl_v;             // [F] serial list: arrival index, sorted position
     uint32_t *tpos;                    // [entries][4] sorted position of a slot's fragment (this call)
     uint32_t call;                     // this call's number (E_CALL), from 1
+    uint32_t grouped;                  // every key one run in arrival order: no span overlaps
 };
 
 template <typename T>
@@ -223,39 +230,46 @@ __device__ void wave_copy16(uint8_t *dst, __amdgpu_buffer_rsrc_t r, uint32_t src
 
 } // namespace
 
-// FRAG verdicts -> fragment list and sort keys (order within the list does not matter: the
-// keys carry the arrival index). Each workgroup takes a contiguous range of frames, counts its
-// fragments, reserves their slots with one atomic, then writes them.
-__global__ void __launch_bounds__(RS_BLOCK) reasm_collect(ReasmArgs a)
+// rocPRIM select predicates: FRAG verdicts (the fragment list in arrival order) and positions
+// holding a completion (the completions in arrival order on the grouped path).
+struct IsFrag {
+    const uint32_t *meta;
+    __device__ bool operator()(uint32_t i) const { return (meta[i] & 0xFu) == UDPDK_V_FRAG; }
+};
+struct HasDone {
+    const uint32_t *dk;
+    __device__ bool operator()(uint32_t q) const { return dk[q] != RS_NONE; }
+};
+
+// Over the fragment list (arrival order; F = counts[0], from the select): the (id << ib | index)
+// sort keys, and whether every flow key forms a single run. A run's first fragment inserts a
+// 64-bit fingerprint of its key into an open-addressing set; meeting it again (the key has
+// another run, or two keys share a fingerprint) sets counts[4] and the batch takes the sorts.
+__global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned long long *hset, uint32_t hmask)
 {
-    __shared__ uint32_t s_n, s_base, s_off;
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
-    const uint32_t lane = __lane_id();
-    const uint32_t per = ((a.n + gridDim.x - 1) / gridDim.x + RS_BLOCK - 1) / RS_BLOCK * RS_BLOCK;
-    const uint32_t b0 = blockIdx.x * per, b1 = min(a.n, b0 + per);
-    if (threadIdx.x == 0) { s_n = 0; s_off = 0; }
-    __syncthreads();
-    uint32_t c = 0;
-    for (uint32_t i = b0 + threadIdx.x; i < b1; i += RS_BLOCK) c += (a.meta[i] & 0xFu) == UDPDK_V_FRAG;
-    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
-    if (lane == 0 && c) atomicAdd(&s_n, c);
-    __syncthreads();
-    if (threadIdx.x == 0) s_base = s_n ? atomicAdd(&a.counts[0], s_n) : 0u;
-    __syncthreads();
-    if (!s_n) return;
-    for (uint32_t i0 = b0 + (threadIdx.x & ~63u); i0 < b1; i0 += RS_BLOCK) {
-        const uint32_t i = i0 + lane;
-        const bool f = i < b1 && (a.meta[i] & 0xFu) == UDPDK_V_FRAG;
-        const unsigned long long m = __ballot(f);
-        if (!m) continue;
-        uint32_t off = 0;
-        if (lane == 0) off = atomicAdd(&s_off, (uint32_t)__popcll(m));
-        off = __shfl(off, 0, 64);
-        if (f) {
-            const uint32_t j = s_base + off + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            const uint32_t id = ld32(fr, a.offset[i] + 16) >> 16;
-            a.frag_list[j] = i;
-            a.k1[j] = ((unsigned long long)id << a.ib) | i;
+    const uint32_t F = a.counts[0];
+    for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
+        const uint32_t i = a.frag_list[p], o = a.offset[i];
+        const uint32_t id = ld32(fr, o + 16) >> 16, src = ld32(fr, o + 26), dst = ld32(fr, o + 30);
+        a.k1[p] = ((unsigned long long)id << a.ib) | i;
+        bool start = p == 0;
+        if (!start) {
+            const uint32_t op = a.offset[a.frag_list[p - 1]];
+            start = (ld32(fr, op + 16) >> 16) != id || ld32(fr, op + 26) != src || ld32(fr, op + 30) != dst;
+        }
+        if (!start) continue;
+        unsigned long long fp = ((unsigned long long)dst << 32 | src) * 0x9E3779B97F4A7C15ull;
+        fp ^= (unsigned long long)(id + 1u) * 0xC2B2AE3D27D4EB4Full;
+        fp ^= fp >> 29;
+        fp |= 1ull;                                     // 0 marks a free slot
+        for (uint32_t slot = (uint32_t)fp & hmask, k = 0; k <= hmask; ++k, slot = (slot + 1u) & hmask) {
+            const unsigned long long old = atomicCAS(&hset[slot], 0ull, fp);
+            if (old == 0ull) break;
+            if (old == fp) {
+                a.counts[4] = 1u;
+                break;
+            }
         }
     }
 }
@@ -513,7 +527,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_flows(ReasmArgs a, uint32_t F)
                     a.sb2[p] = bk2;
                     a.tf[p] = tfirst;
                     a.tl[p] = tlast;
-                    nrec = bk1 != bk2 ? 2u : 1u;
+                    nrec = a.grouped ? 0u : bk1 != bk2 ? 2u : 1u;
                     if (flag & PF_COMPLEX) {
                         atomicAdd(&a.cplx[bk1], 1u);
                         if (bk2 != bk1) atomicAdd(&a.cplx[bk2], 1u);
@@ -896,7 +910,9 @@ struct Reasm {
     uint32_t cap = 0;                        // fragments per call (= context max_frames)
     uint32_t *frag_list = nullptr, *v1 = nullptr, *v1s = nullptr, *v2s = nullptr;
     unsigned long long *k1 = nullptr, *k1s = nullptr, *k2 = nullptr, *k2s = nullptr;
-    uint32_t *counts = nullptr;              // device [4]: F, records, serial list, fallback
+    uint32_t *counts = nullptr;              // device [8]: F, records, serial list, fallback, not grouped
+    unsigned long long *hset = nullptr;      // [hcap] run-key fingerprints (reasm_runs)
+    uint32_t hcap = 0;
     unsigned long long *stats = nullptr;     // device [UDPDK_RS_N]
     unsigned long long *out_bytes = nullptr;
     ReasmDone *done = nullptr;
@@ -940,7 +956,7 @@ void reasm_destroy(Reasm *r)
                    r->k2s, r->counts, r->stats, r->out_bytes, r->done, r->jobs, r->dk, r->dks,
                    r->dv, r->perm, r->sizes, r->offs, r->tmp, r->out, r->out_off, r->out_ptype,
                    r->out_origin, r->out_len, r->pflag, r->sb1, r->sb2, r->tf, r->tl, r->rk, r->rks,
-                   r->rx, r->rv, r->rvs, r->bsum, r->cplx, r->tpos, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs};
+                   r->rx, r->rv, r->rvs, r->bsum, r->cplx, r->tpos, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs, r->hset};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (r->host) (void)hipHostFree(r->host);
@@ -978,7 +994,7 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
         (e = dalloc(&r->frag_list, C)) != hipSuccess || (e = dalloc(&r->v1s, C)) != hipSuccess ||
         (e = dalloc(&r->v2s, C)) != hipSuccess || (e = dalloc(&r->k1, C)) != hipSuccess ||
         (e = dalloc(&r->k1s, C)) != hipSuccess || (e = dalloc(&r->k2, C)) != hipSuccess ||
-        (e = dalloc(&r->k2s, C)) != hipSuccess || (e = dalloc(&r->counts, 4)) != hipSuccess ||
+        (e = dalloc(&r->k2s, C)) != hipSuccess || (e = dalloc(&r->counts, 8)) != hipSuccess ||
         (e = dalloc(&r->stats, UDPDK_RS_N)) != hipSuccess || (e = dalloc(&r->out_bytes, 1)) != hipSuccess ||
         (e = dalloc(&r->done, C)) != hipSuccess || (e = dalloc(&r->jobs, C)) != hipSuccess ||
         (e = dalloc(&r->dk, C)) != hipSuccess || (e = dalloc(&r->dks, C)) != hipSuccess ||
@@ -1002,17 +1018,28 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
     }
     // rocPRIM temporary storage for the largest call (sorts of u64 keys / u32 values, u32 scan,
     // u64 max scan)
-    size_t t[5] = {0, 0, 0, 0, 0};
+    size_t t[7] = {0, 0, 0, 0, 0, 0, 0};
     if ((e = rocprim::radix_sort_pairs(nullptr, t[0], r->k1, r->k1s, r->v1s, r->v2s, C, 0, 64)) != hipSuccess ||
         (e = rocprim::radix_sort_pairs(nullptr, t[1], r->dk, r->dks, r->v1s, r->v2s, C, 0, 32)) != hipSuccess ||
         (e = rocprim::exclusive_scan(nullptr, t[2], r->sizes, r->offs, 0u, C, rocprim::plus<uint32_t>())) != hipSuccess ||
         (e = rocprim::radix_sort_pairs(nullptr, t[3], r->rk, r->rks, r->rv, r->rvs, C2, 0, 64)) != hipSuccess ||
-        (e = rocprim::inclusive_scan(nullptr, t[4], r->rk, r->rx, C2, rocprim::maximum<unsigned long long>())) != hipSuccess) {
+        (e = rocprim::inclusive_scan(nullptr, t[4], r->rk, r->rx, C2, rocprim::maximum<unsigned long long>())) != hipSuccess ||
+        (e = rocprim::select(nullptr, t[5], rocprim::counting_iterator<uint32_t>(0u), r->frag_list, r->counts, C,
+                             IsFrag{nullptr})) != hipSuccess ||
+        (e = rocprim::select(nullptr, t[6], rocprim::counting_iterator<uint32_t>(0u), r->perm, r->counts, C,
+                             HasDone{nullptr})) != hipSuccess) {
         fail(e);
         reasm_destroy(r);
         return rc;
     }
-    r->tmp_bytes = std::max<size_t>(*std::max_element(t, t + 5), 256);
+    r->tmp_bytes = std::max<size_t>(*std::max_element(t, t + 7), 256);
+    r->hcap = 1024;                                         // >= 2 x fragments per call, power of 2
+    while (r->hcap < 2u * r->cap) r->hcap <<= 1;
+    if ((e = dalloc(&r->hset, r->hcap)) != hipSuccess) {
+        fail(e);
+        reasm_destroy(r);
+        return rc;
+    }
     if ((e = hipMalloc(&r->tmp, r->tmp_bytes)) != hipSuccess) {
         fail(e);
         reasm_destroy(r);
@@ -1071,26 +1098,44 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     if (++r->calls == 0) r->calls = 1;          // 0 marks entries never touched
     a.call = r->calls;
     a.ib = bits_for(n - 1u);
-    RS_HIP(hipMemsetAsync(r->counts, 0, 4 * sizeof(uint32_t), st));
+    RS_HIP(hipMemsetAsync(r->counts, 0, 8 * sizeof(uint32_t), st));
     RS_HIP(hipMemsetAsync(r->stats, 0, UDPDK_RS_N * sizeof(unsigned long long), st));
     RS_HIP(hipMemsetAsync(r->out_bytes, 0, sizeof(unsigned long long), st));
-    const uint32_t g1 = std::max<uint32_t>(1, std::min<uint32_t>((n + 1023) / 1024, 2048));
-    hipLaunchKernelGGL(reasm_collect, dim3(g1), dim3(RS_BLOCK), 0, st, a);
-    RS_HIP(hipGetLastError());
-    RS_HIP(hipMemcpyAsync(r->host, r->counts, 4, hipMemcpyDeviceToHost, st));
+    uint32_t hsize = 1024;                   // the run-key set: >= 2 x fragments, power of 2
+    while (hsize < 2u * n && hsize < r->hcap) hsize <<= 1;
+    // the fragment list in arrival order (F to counts[0]), then its sort keys and the run test
+    size_t tb = r->tmp_bytes;
+    if (n) {
+        RS_HIP(rocprim::select(r->tmp, tb, rocprim::counting_iterator<uint32_t>(0u), r->frag_list, r->counts,
+                               (size_t)n, IsFrag{meta_dev}, st));
+        RS_HIP(hipMemsetAsync(r->hset, 0, (size_t)hsize * sizeof(unsigned long long), st));
+        const uint32_t g1 = std::max<uint32_t>(1, std::min<uint32_t>((n + RS_BLOCK - 1) / RS_BLOCK, 4096));
+        hipLaunchKernelGGL(reasm_runs, dim3(g1), dim3(RS_BLOCK), 0, st, a, r->hset, hsize - 1u);
+        RS_HIP(hipGetLastError());
+    }
+    RS_HIP(hipMemcpyAsync(r->host, r->counts, 32, hipMemcpyDeviceToHost, st));
     RS_HIP(hipStreamSynchronize(st));
-    const uint32_t F = r->host[0];
+    const uint32_t F = n ? r->host[0] : 0u;
+    // every key one run in arrival order: the list is already grouped, and no flow's span can
+    // overlap another's (each span holds only its own fragments)
+    const bool grouped = r->host[4] == 0u;
+    a.grouped = grouped ? 1u : 0u;
     uint32_t K = 0;                          // fragments on the serial path
     memset(o, 0, sizeof(*o));
     if (F) {
-        size_t tb = r->tmp_bytes;
-        RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k1, r->k1s, r->frag_list, r->v1s, (size_t)F, 0,
-                                                  16 + a.ib, st));
         const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((F + RS_BLOCK - 1) / RS_BLOCK, 4096));
-        hipLaunchKernelGGL(reasm_keys, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
-        RS_HIP(hipGetLastError());
-        tb = r->tmp_bytes;
-        RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k2, r->k2s, r->v1s, r->v2s, (size_t)F, 0, 64, st));
+        if (grouped) {
+            a.order = r->frag_list;
+        } else {
+            // group by key keeping arrival order: stable sorts by (id, index), then src|dst
+            tb = r->tmp_bytes;
+            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k1, r->k1s, r->frag_list, r->v1s, (size_t)F, 0,
+                                             16 + a.ib, st));
+            hipLaunchKernelGGL(reasm_keys, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
+            RS_HIP(hipGetLastError());
+            tb = r->tmp_bytes;
+            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k2, r->k2s, r->v1s, r->v2s, (size_t)F, 0, 64, st));
+        }
         // the sort keys are dead now: their buffers hold the per-position records
         a.s_i = reinterpret_cast<uint32_t *>(r->k1);
         a.s_src = a.s_i + F;
@@ -1109,9 +1154,12 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         const uint32_t gfl = std::max<uint32_t>(1, std::min<uint32_t>((F + RS_FLOW_CHUNK - 1) / RS_FLOW_CHUNK, 2048));
         hipLaunchKernelGGL(reasm_flows, dim3(gfl), dim3(RS_BLOCK), 0, st, a, F);
         RS_HIP(hipGetLastError());
-        RS_HIP(hipMemcpyAsync(r->host, r->counts, 8, hipMemcpyDeviceToHost, st));
-        RS_HIP(hipStreamSynchronize(st));
-        const uint32_t R = r->host[1];
+        uint32_t R = 0;                      // overlap records (none when grouped)
+        if (!grouped) {
+            RS_HIP(hipMemcpyAsync(r->host, r->counts, 8, hipMemcpyDeviceToHost, st));
+            RS_HIP(hipStreamSynchronize(st));
+            R = r->host[1];
+        }
         if (R) {
             tb = r->tmp_bytes;
             RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->rk, r->rks, r->rv, r->rvs, (size_t)R, 0,
@@ -1151,6 +1199,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     memcpy(o->stats, r->host + 8, UDPDK_RS_N * 8);
     o->stats[UDPDK_RS_FRAGS] = F;
     o->stats[UDPDK_RS_SERIAL] = K;
+    o->stats[UDPDK_RS_SORTED] = F && !grouped ? 1u : 0u;
     const uint32_t Cn = (uint32_t)o->stats[UDPDK_RS_DONE], J = (uint32_t)o->stats[UDPDK_RS_STORED];
     if (Cn) {
         if (ob + UDPDK_GPU_FRAMES_TAILROOM > r->out_cap) {
@@ -1161,13 +1210,18 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
             RS_HIP(hipMalloc((void **)&r->out, nc));
             r->out_cap = nc;
         }
-        // completions in origin (arrival) order (positions without one sort last), then their
-        // frame offsets
+        // completions in origin (arrival) order, then their frame offsets. Grouped: positions are
+        // in arrival order, so the positions holding one, in order; else a sort by origin
+        // (positions without one have all-ones keys and sort last)
         const uint32_t gC = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_BLOCK - 1) / RS_BLOCK, 4096));
-        size_t tb = r->tmp_bytes;
-        // (origins are < n < 2^bits_for(n); the all-ones keys of positions without one stay last)
-        RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->dk, r->dks, r->dv, r->perm, (size_t)F, 0,
-                                                  bits_for(n), st));
+        tb = r->tmp_bytes;
+        if (grouped) {
+            RS_HIP(rocprim::select(r->tmp, tb, rocprim::counting_iterator<uint32_t>(0u), r->perm, r->counts + 5,
+                                   (size_t)F, HasDone{r->dk}, st));
+        } else {
+            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->dk, r->dks, r->dv, r->perm, (size_t)F, 0,
+                                             bits_for(n), st));
+        }
         hipLaunchKernelGGL(reasm_sizes, dim3(gC), dim3(RS_BLOCK), 0, st, (const ReasmDone *)r->done,
                            (const uint32_t *)r->perm, r->sizes, Cn);
         RS_HIP(hipGetLastError());

@@ -109,9 +109,13 @@ __device__ __forceinline__ void tx_small(const TxArgs &a, uint32_t i, uint32_t f
     uint32_t P[4 * TX_SMALL_LOADS + 1];
 #pragma unroll
     for (uint32_t m = 0; m < TX_SMALL_LOADS; ++m) {
-        const uint32_t off = ok && 16u * m < L ? po + 16u * m : 0x80000000u;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)off, 0, 0);
-        P[4 * m] = v[0]; P[4 * m + 1] = v[1]; P[4 * m + 2] = v[2]; P[4 * m + 3] = v[3];
+        // (a piece no lane needs is not issued: its lanes would still cost address-unit cycles)
+        const bool need = ok && 16u * m < L;
+        P[4 * m] = P[4 * m + 1] = P[4 * m + 2] = P[4 * m + 3] = 0u;
+        if (__ballot(need)) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)(need ? po + 16u * m : 0x80000000u), 0, 0);
+            P[4 * m] = v[0]; P[4 * m + 1] = v[1]; P[4 * m + 2] = v[2]; P[4 * m + 3] = v[3];
+        }
     }
     P[4 * TX_SMALL_LOADS] = 0u;
     if (!ok) return;
@@ -157,7 +161,7 @@ __device__ __forceinline__ void tx_small(const TxArgs &a, uint32_t i, uint32_t f
 
 } // namespace
 
-__global__ void __launch_bounds__(TX_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8)))
+__global__ void __launch_bounds__(TX_BLOCK) __attribute__((amdgpu_waves_per_eu(6, 8)))
 tx_build(TxArgs a)
 {
     __shared__ __attribute__((aligned(16))) uint32_t win[TXW][64][TX_WIN / 4];
