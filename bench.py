@@ -2,9 +2,10 @@
 
 A step = one udpdk_gpu_rx call over one batch of frames already resident in HBM (single-lane
 batches: rx_classify + rx_compact1; otherwise rx_classify + rx_scan + rx_scatter). The timed
-region's GPU time comes from two events on the library stream around all K steps; per-kernel
-durations from events carried by the kernel dispatches themselves (hipExtLaunchKernelGGL), so
-they agree with rocprofv3's kernel trace. Default workload at N = 1: BASELINE.json configs[1], 1 M synthetic 64 B Eth/IPv4/UDP frames, 1 bound
+region is exactly K steps between a barrier + hipDeviceSynchronize on each side (host wall
+clock: `value`); an untimed pass of K steps before it gives the GPU time (two events on the
+library stream) and the per-kernel durations (events carried by the kernel dispatches
+themselves, hipExtLaunchKernelGGL, so they agree with rocprofv3's kernel trace). Default workload at N = 1: BASELINE.json configs[1], 1 M synthetic 64 B Eth/IPv4/UDP frames, 1 bound
 port. At N > 1 the default is the scaling workload BASELINE.json configs[4] (config 5): every rank
 processes its own independent 4 M x 64 B shard over 4096 ports, Zipf-0.99 (ports seeded 1000 +
 rank, frames 0x5EED ^ rank) with no data-path collective: weak scaling.
@@ -164,36 +165,58 @@ class HipEvents:
             self.hip.hipEventDestroy(e)
 
 
+_HIP = None
+
+
+def device_sync():
+    """hipDeviceSynchronize (what torch.cuda.synchronize does): the timed region's brackets.
+    The library's own ctx.sync() waits on each pipe's stream in turn and costs ~1 us per step
+    more at 20 steps (profiles/r02g_sync_cost.json)."""
+    global _HIP
+    if _HIP is None:
+        _HIP = C.CDLL("libamdhip64.so")
+    rc = _HIP.hipDeviceSynchronize()
+    if rc:
+        raise RuntimeError(f"hipDeviceSynchronize failed: {rc}")
+
+
 def time_loop(rx: Rx, steps: int, warmup: int, barrier, timing_every: int):
-    """Timed region: `steps` back-to-back udpdk_gpu_rx calls between a barrier + sync on each
-    side (host wall clock) and two events on the library stream (GPU time). Per-kernel
-    durations come from the library's timing mode, whose events ride on the kernel dispatches
-    themselves (no marker packets between kernels), on every `timing_every`-th call."""
+    """`warmup` untimed calls; then, also untimed, the `steps` calls once between two events on
+    the library stream (GPU time, with a join so that the other pipes' calls are inside) and with
+    the library's per-kernel timing mode (events riding on the kernel dispatches themselves, on
+    every `timing_every`-th call). Then the timed region (value): the same number of calls
+    between a barrier + device synchronisation on each side (host wall clock) and nothing else
+    inside: the join and the event records cost ~30 us per region (profiles/r02g_sync_cost.json)."""
     ctx = rx.ctx
-    ev = HipEvents(ctx)
     for i in range(warmup):
         rx.step(i)
     rx.check()
+    ev = HipEvents(ctx)
     ctx.timing(timing_every)
     ctx.timing_read()                    # reset accumulators
-    barrier()
     ctx.sync()
-    t0 = time.perf_counter()
     ev.record(0)
     for i in range(steps):
         rx.step(warmup + i)
-    ctx.join()                           # the second pipe's calls before the closing event
+    ctx.join()                           # the other pipes' calls before the closing event
     ev.record(1)
     ctx.sync()
-    t1 = time.perf_counter()
-    barrier()
     gpu_ms = ev.elapsed_ms()
     ev.close()
-    st = rx.check()
     ms, n = ctx.timing_read() if timing_every else ([0.0] * abi.N_KERNEL_IDS, [0] * abi.N_KERNEL_IDS)
     ctx.timing(0)
     kt = {name: 1e3 * ms[k] / n[k] for k, name in
           enumerate(("rx_classify", "rx_scan", "rx_scatter")) if n[k]}
+    # the timed region
+    barrier()
+    device_sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        rx.step(warmup + steps + i)
+    device_sync()
+    t1 = time.perf_counter()
+    barrier()
+    st = rx.check()
     return (t1 - t0), gpu_ms / steps, kt, st
 
 
