@@ -29,8 +29,9 @@ $(OBJDIR)/host/%.o: udpdk_amd/csrc/host/%.c $(HDRS)
 	@mkdir -p $(dir $@)
 	$(CC) $(CFLAGS_H) $(INC) -c $< -o $@
 
-$(LIB): $(HIP_OBJ) $(C_OBJ)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -Wl,--no-undefined -Wl,-soname,libudpdk_amd.so
+$(LIB): $(HIP_OBJ) $(C_OBJ) udpdk_amd/csrc/libudpdk_amd.map
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(HIP_OBJ) $(C_OBJ) -Wl,--no-undefined \
+	    -Wl,-soname,libudpdk_amd.so -Wl,--version-script=udpdk_amd/csrc/libudpdk_amd.map
 
 oracle:
 	$(MAKE) -C oracle

@@ -279,6 +279,13 @@ typedef struct {
 int udpdk_gpu_rx_gather(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch,
                         const uint32_t *lane_pkt_dev, uint32_t first, uint32_t count,
                         const udpdk_rx_gather_t *out);
+/* The same with packed slots: entry k's buffer is payload_dev + slot_off_dev[k], of
+ * slot_off_dev[k + 1] - slot_off_dev[k] bytes (multiples of 16, ascending, count + 1 offsets);
+ * out->slot_bytes is not used. A poller sizing each slot to its frame (data_len - 42, rounded up
+ * to 16) hands the application every payload with one copy of only the bytes that exist. */
+int udpdk_gpu_rx_gather_packed(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch,
+                               const uint32_t *lane_pkt_dev, uint32_t first, uint32_t count,
+                               const uint32_t *slot_off_dev, const udpdk_rx_gather_t *out);
 
 /* ---------------------------------------------------------------------------------------------
  * RX reassembly of IPv4 fragments (udpdk_poller.c:338-361: FRAG frames go through

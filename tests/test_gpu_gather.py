@@ -84,3 +84,41 @@ def test_gather_configs(gpu_ctx, cfg, n):
     for want, got in res:
         _assert_same(want, got, w.name)
         assert int(want[1].sum()) == int(got[1].sum()) > 0
+
+
+@pytest.mark.parametrize("caps", ["frame", "random"])
+def test_gather_packed_slots(gpu_ctx, caps):
+    """udpdk_gpu_rx_gather_packed (the slabs udpdk_poll_rx fills): entry k lands at slot_off[k]
+    with slot_off[k + 1] - slot_off[k] bytes of room. Caps sized to each frame (data_len - 42
+    rounded up to 16: nothing truncated) or random multiples of 16 (recvfrom truncation per
+    entry); lengths, addresses and bytes vs the oracle's untruncated recvfrom cut to the cap."""
+    w = F.config_batch(4, n=20000)
+    b = w.batch
+    ctx = gpu_ctx
+    ctx.upload_snapshot(abi.snapshot_from_lists(w.port_lists(), w.n_sockets))
+    db = abi.rx_upload(ctx, b.frames, b.offset, b.length)
+    db.frames_bytes = b.frames_bytes
+    out = abi.rx_alloc_out(ctx, b.n, w.n_sockets, b.n)
+    _, loff, pkt, _, rc = abi.rx_run(ctx, db, out)
+    assert rc == 0
+    d = int(loff[-1])
+    assert d == b.n
+    rng = np.random.default_rng(3 if caps == "frame" else 4)
+    if caps == "frame":
+        cap = (np.maximum(b.length[pkt[:d]].astype(np.int64) - 42, 1) + 15) // 16 * 16
+    else:
+        cap = rng.integers(1, 100, d) * 16
+    so = np.concatenate([[0], np.cumsum(cap)]).astype(np.uint32)
+    gp, gl, gi, gs = abi.rx_gather_packed_run(ctx, db, out.lane_pkt, 0, so)
+    wp, wl, wi, ws = O.recv_gather(b.frames, b.offset, b.length, pkt, 0, d, 2048)   # IMIX <= 1476 B
+    want_len = np.minimum(wl, cap)
+    assert np.array_equal(gl, want_len) and np.array_equal(gi, wi) and np.array_equal(gs, ws)
+    if caps == "frame":
+        assert np.array_equal(want_len, wl)                      # nothing truncated
+    else:
+        assert np.any(want_len < wl)
+    for k in range(d):
+        n = int(want_len[k])
+        assert gp[so[k]:so[k] + n].tobytes() == wp[k, :n].tobytes(), k
+    for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt):
+        x.free()

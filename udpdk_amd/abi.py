@@ -163,6 +163,8 @@ _PROTOS = {
     "udpdk_gpu_rx_host_batch": (C.c_int, [_P, C.POINTER(RxBatch), C.POINTER(_P)]),
     "udpdk_gpu_rx_gather": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint32, C.c_uint32,
                                       C.POINTER(RxGather)]),
+    "udpdk_gpu_rx_gather_packed": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint32, C.c_uint32, _P,
+                                             C.POINTER(RxGather)]),
     "udpdk_gpu_frag_table_create": (C.c_int, [_P, C.POINTER(FragTableCfg)]),
     "udpdk_gpu_rx_reassemble": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint64, C.POINTER(ReasmOut)]),
     "udpdk_gpu_rss_default_conf": (C.c_int, [C.POINTER(RssConf), C.c_uint32]),
@@ -473,6 +475,29 @@ def rx_gather_run(ctx: GpuContext, b: RxDeviceBatch, lane_pkt: DeviceBuffer, fir
     pay = ctx.download(g.payload, np.uint8, g.count * g.slot_bytes).reshape(g.count, g.slot_bytes)
     return (pay, ctx.download(g.length, np.uint32, g.count), ctx.download(g.src_ip, np.uint32, g.count),
             ctx.download(g.src_port, np.uint16, g.count))
+
+
+def rx_gather_packed_run(ctx: GpuContext, b: RxDeviceBatch, lane_pkt: DeviceBuffer, first: int,
+                         slot_off: np.ndarray):
+    """udpdk_gpu_rx_gather_packed over lane entries [first, first + len(slot_off) - 1): entry k's
+    buffer is bytes [slot_off[k], slot_off[k + 1]) of one payload area. Returns (payload area
+    u8, len, src_ip, src_port)."""
+    count = len(slot_off) - 1
+    so = ctx.upload(np.asarray(slot_off, np.uint32))
+    total = int(slot_off[-1])
+    pay = ctx.alloc(max(16, total))
+    ln, ip, pt = ctx.alloc(4 * max(1, count)), ctx.alloc(4 * max(1, count)), ctx.alloc(2 * max(1, count))
+    bt = RxBatch(b.frames.ptr, b.frames_bytes, b.offset.ptr, b.length.ptr,
+                 b.ptype.ptr if b.ptype is not None else None, b.n)
+    gt = RxGather(pay.ptr, 16, ln.ptr, ip.ptr, pt.ptr)
+    _check(lib().udpdk_gpu_rx_gather_packed(ctx.handle, C.byref(bt), C.c_void_p(lane_pkt.ptr), first, count,
+                                            C.c_void_p(so.ptr), C.byref(gt)), "udpdk_gpu_rx_gather_packed")
+    ctx.sync()
+    out = (ctx.download(pay, np.uint8, total), ctx.download(ln, np.uint32, count),
+           ctx.download(ip, np.uint32, count), ctx.download(pt, np.uint16, count))
+    for x in (so, pay, ln, ip, pt):
+        x.free()
+    return out
 
 
 @dataclass

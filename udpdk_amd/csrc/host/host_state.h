@@ -28,13 +28,12 @@
 /* A pinned host slab of gathered payloads: one per rx_gather of a poll. Ring entries point into
  * it; the last recvfrom of its datagrams returns it to the pool (the mbuf pool's role). */
 struct h_arena {
-    uint8_t  *payload;           /* cap_n slots of slot_bytes                                    */
+    uint8_t  *payload;           /* cap_bytes: the datagrams' packed slots (16-byte aligned)     */
     uint32_t *len;               /* [cap_n] payload bytes                                        */
     uint32_t *src_ip;            /* [cap_n] raw                                                  */
     uint16_t *src_port;          /* [cap_n] raw                                                  */
     uint64_t  cap_bytes;
     uint32_t  cap_n;
-    uint32_t  slot_bytes;
     atomic_uint refs;            /* queued datagrams still pointing into this slab               */
     struct h_arena *next;        /* free list                                                    */
 };
@@ -110,8 +109,9 @@ struct h_state {
     uint16_t *fr_len;
     uint64_t  fr_loff_cap, fr_lpkt_cap, fr_org_cap, fr_len_cap;
     uint32_t *acc_d, *acc_f;                     /* accepted entries: frame / datagram index   */
+    uint32_t *acc_do, *acc_fo;                   /* their packed slot offsets (+ the total)    */
     uint32_t *acc_sock;                          /* per accepted entry: socket | from-frag<<31 */
-    uint64_t  acc_d_cap, acc_f_cap, acc_sock_cap;
+    uint64_t  acc_d_cap, acc_f_cap, acc_do_cap, acc_fo_cap, acc_sock_cap;
     void     *dv_acc, *dv_pay, *dv_len, *dv_sip, *dv_spt;   /* device: gather list + outputs */
     uint64_t  dv_acc_cap, dv_pay_cap, dv_len_cap, dv_sip_cap, dv_spt_cap;
     void     *dv_meta2, *dv_loff2, *dv_lpkt2;              /* device: RX of reassembled batch */
@@ -145,7 +145,7 @@ int  h_btable_free_port(void);
 void h_sockets_reset(void);
 uint32_t h_ring_free(const struct h_ring *r);
 int  h_ring_push_bulk(struct h_ring *r, const struct h_dgram *d, uint32_t n);
-struct h_arena *h_arena_get(uint32_t n, uint32_t slot_bytes);
+struct h_arena *h_arena_get(uint32_t n, uint64_t bytes);
 void h_arena_put(struct h_arena *a);
 void h_arena_release(struct h_arena *a, uint32_t refs);
 void h_arenas_free_all(void);
@@ -154,6 +154,7 @@ void h_tx_reset(void);
 /* rx_poll.c */
 int  h_snapshot_refresh(void);            /* under g_udpdk.lock */
 void h_rx_buffers_free(void);
+void udpdk_poll_profile_dump(void);   /* -DUDPDK_POLL_PROFILE builds: phase times to stderr */
 int  h_grow_dev(void **p, uint64_t *cap, uint64_t need);
 int  h_grow_host(void **p, uint64_t *cap, uint64_t need);
 

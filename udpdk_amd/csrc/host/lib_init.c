@@ -144,6 +144,7 @@ void udpdk_interrupt(int signum)
 void udpdk_cleanup(void)
 {
     udpdk_port_detach();
+    udpdk_poll_profile_dump();
     for (int s = 0; s < UDPDK_MAX_SOCKETS; s++)
         if (g_udpdk.slots[s].used) udpdk_close(s);
     h_tx_reset();

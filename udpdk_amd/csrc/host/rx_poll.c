@@ -21,6 +21,34 @@
 
 #include "host_state.h"
 
+/* Diagnostic build (-DUDPDK_POLL_PROFILE): wall time per phase of udpdk_poll_rx, summed over the
+ * calls and printed to stderr by udpdk_poll_profile_dump (called from udpdk_cleanup). */
+#ifdef UDPDK_POLL_PROFILE
+#include <stdio.h>
+static double g_prof[8];
+static const char *g_prof_name[8] = {"snapshot", "gpu_rx_host", "frag_pass", "admission", "gather",
+                                     "gather_sync", "publish", "calls"};
+static double h_prof_now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+#define PROF_T(v) const double v = h_prof_now()
+#define PROF_ADD(k, a, b) (g_prof[k] += (b) - (a))
+__attribute__((visibility("hidden"))) void udpdk_poll_profile_dump(void)
+{
+    if (!g_prof[7]) return;
+    fprintf(stderr, "{\"udpdk_poll_profile_ms_per_call\": {");
+    for (int k = 0; k < 7; k++) fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", g_prof_name[k], g_prof[k] / g_prof[7]);
+    fprintf(stderr, "}, \"calls\": %.0f}\n", g_prof[7]);
+}
+#else
+#define PROF_T(v) do {} while (0)
+#define PROF_ADD(k, a, b) do {} while (0)
+void udpdk_poll_profile_dump(void) {}
+#endif
+
 int h_grow_dev(void **p, uint64_t *cap, uint64_t need)
 {
     if (*p && *cap >= need) return 0;
@@ -50,11 +78,11 @@ void h_rx_buffers_free(void)
     void **host[] = {(void **)&g_udpdk.rx_meta, (void **)&g_udpdk.rx_loff, (void **)&g_udpdk.rx_lpkt,
                      (void **)&g_udpdk.fr_loff, (void **)&g_udpdk.fr_lpkt, (void **)&g_udpdk.fr_org,
                      (void **)&g_udpdk.fr_len, (void **)&g_udpdk.acc_d, (void **)&g_udpdk.acc_f,
-                     (void **)&g_udpdk.acc_sock};
+                     (void **)&g_udpdk.acc_do, (void **)&g_udpdk.acc_fo, (void **)&g_udpdk.acc_sock};
     uint64_t *hcap[] = {&g_udpdk.rx_meta_cap, &g_udpdk.rx_loff_cap, &g_udpdk.rx_lpkt_cap,
                         &g_udpdk.fr_loff_cap, &g_udpdk.fr_lpkt_cap, &g_udpdk.fr_org_cap,
                         &g_udpdk.fr_len_cap, &g_udpdk.acc_d_cap, &g_udpdk.acc_f_cap,
-                        &g_udpdk.acc_sock_cap};
+                        &g_udpdk.acc_do_cap, &g_udpdk.acc_fo_cap, &g_udpdk.acc_sock_cap};
     for (unsigned k = 0; k < sizeof(host) / sizeof(host[0]); k++) {
         free(*host[k]);
         *host[k] = NULL;
@@ -101,13 +129,11 @@ static uint64_t h_now_ms(void)
  * datagrams through the demux. Out: *rb = the reassembled batch (device, valid until the next
  * reassembly call), fr_loff[lanes + 1] / fr_lpkt[] its lanes (host), fr_org[] each datagram's
  * completing fragment index, fr_len[] its frame length. *nf = 0 when nothing completed. */
-static int h_frag_pass(const udpdk_rx_batch_t *staged, const uint32_t *meta_dev, const uint32_t *meta,
-                       uint32_t n, uint32_t lanes, uint32_t maxfan, udpdk_rx_batch_t *rb, uint32_t *nd)
+static int h_frag_pass(const udpdk_rx_batch_t *staged, const uint32_t *meta_dev, uint64_t nfrag,
+                       uint32_t lanes, uint32_t maxfan, udpdk_rx_batch_t *rb, uint32_t *nd)
 {
     *nd = 0;
-    uint32_t nfrag = 0;
-    for (uint32_t i = 0; i < n; i++) nfrag += (meta[i] & 0xFu) == UDPDK_V_FRAG;
-    if (!nfrag) return 0;
+    if (!nfrag) return 0;                   /* the batch's FRAG verdict count (RX counters) */
     udpdk_gpu_ctx *g = g_udpdk.gpu;
     int rc;
     if (!g_udpdk.frag_ready) {
@@ -148,29 +174,33 @@ static int h_frag_pass(const udpdk_rx_batch_t *staged, const uint32_t *meta_dev,
 }
 
 /* Gather the payloads of the count entries listed in acc (frame indices of batch b) into a new
- * slab: one gather launch, one D2H of each output. slot_bytes covers the longest. */
-static int h_gather(const udpdk_rx_batch_t *b, const uint32_t *acc, uint32_t count, uint32_t maxlen,
+ * slab of packed slots (entry k at offs[k], offs[count] bytes in all, each slot its frame's
+ * payload room rounded up to 16): one gather launch, one D2H of each output, and only the
+ * bytes that exist cross PCIe (a slot per longest datagram moved 4.6x the IMIX payload). */
+static int h_gather(const udpdk_rx_batch_t *b, const uint32_t *acc, const uint32_t *offs, uint32_t count,
                     struct h_arena **out)
 {
     *out = NULL;
     if (!count) return 0;
     udpdk_gpu_ctx *g = g_udpdk.gpu;
-    const uint32_t slot = ((maxlen ? maxlen : 1) + 15u) & ~15u;
-    struct h_arena *a = h_arena_get(count, slot);
+    const uint64_t bytes = offs[count] ? offs[count] : 16u;
+    struct h_arena *a = h_arena_get(count, bytes);
     if (!a) { errno = ENOMEM; return -1; }
     int rc;
-    if (h_grow_dev(&g_udpdk.dv_acc, &g_udpdk.dv_acc_cap, 4ull * count) ||
-        h_grow_dev(&g_udpdk.dv_pay, &g_udpdk.dv_pay_cap, (uint64_t)count * slot) ||
+    if (h_grow_dev(&g_udpdk.dv_acc, &g_udpdk.dv_acc_cap, 8ull * count + 4) ||
+        h_grow_dev(&g_udpdk.dv_pay, &g_udpdk.dv_pay_cap, bytes) ||
         h_grow_dev(&g_udpdk.dv_len, &g_udpdk.dv_len_cap, 4ull * count) ||
         h_grow_dev(&g_udpdk.dv_sip, &g_udpdk.dv_sip_cap, 4ull * count) ||
         h_grow_dev(&g_udpdk.dv_spt, &g_udpdk.dv_spt_cap, 2ull * count)) {
         h_arena_put(a);
         return -1;
     }
-    udpdk_rx_gather_t go = {g_udpdk.dv_pay, slot, g_udpdk.dv_len, g_udpdk.dv_sip, g_udpdk.dv_spt};
-    if ((rc = udpdk_gpu_h2d(g, g_udpdk.dv_acc, acc, 4ull * count)) ||
-        (rc = udpdk_gpu_rx_gather(g, b, g_udpdk.dv_acc, 0, count, &go)) ||
-        (rc = udpdk_gpu_d2h(g, a->payload, g_udpdk.dv_pay, (uint64_t)count * slot)) ||
+    udpdk_rx_gather_t go = {g_udpdk.dv_pay, 16u, g_udpdk.dv_len, g_udpdk.dv_sip, g_udpdk.dv_spt};
+    uint32_t *dacc = g_udpdk.dv_acc, *doff = dacc + count;
+    if ((rc = udpdk_gpu_h2d(g, dacc, acc, 4ull * count)) ||
+        (rc = udpdk_gpu_h2d(g, doff, offs, 4ull * count + 4)) ||
+        (rc = udpdk_gpu_rx_gather_packed(g, b, dacc, 0, count, doff, &go)) ||
+        (rc = udpdk_gpu_d2h(g, a->payload, g_udpdk.dv_pay, bytes)) ||
         (rc = udpdk_gpu_d2h(g, a->len, g_udpdk.dv_len, 4ull * count)) ||
         (rc = udpdk_gpu_d2h(g, a->src_ip, g_udpdk.dv_sip, 4ull * count)) ||
         (rc = udpdk_gpu_d2h(g, a->src_port, g_udpdk.dv_spt, 2ull * count))) {
@@ -192,7 +222,9 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
     pthread_mutex_lock(&g_udpdk.lock);
     int ret = -1, rc;
     struct h_arena *ad = NULL, *af = NULL;
+    PROF_T(p0);
     if (h_snapshot_refresh()) goto out;
+    PROF_T(p1);
     const uint32_t lanes = g_udpdk.snap_lanes, maxfan = g_udpdk.snap_maxfan;
     const uint64_t cap64 = (uint64_t)n * maxfan;
     const uint32_t cap = cap64 > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)cap64;
@@ -204,21 +236,26 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
     udpdk_rx_stats_t st;
     if ((rc = udpdk_gpu_rx_host(g, frames, frames_bytes, offset, length, ptype, n, meta, loff, lpkt,
                                 cap, &st))) { errno = -rc; goto out; }
+    PROF_T(p2);
     udpdk_rx_batch_t staged;
     const uint32_t *meta_dev = NULL;
     if ((rc = udpdk_gpu_rx_host_batch(g, &staged, &meta_dev))) { errno = -rc; goto out; }
     udpdk_rx_batch_t rb;
     uint32_t nd = 0;
-    if (h_frag_pass(&staged, meta_dev, meta, n, lanes, maxfan, &rb, &nd)) goto out;
+    if (h_frag_pass(&staged, meta_dev, st.counters[UDPDK_V_FRAG], lanes, maxfan, &rb, &nd)) goto out;
+    PROF_T(p3);
     const uint32_t *floff = nd ? g_udpdk.fr_loff : NULL, *flpkt = g_udpdk.fr_lpkt, *forg = g_udpdk.fr_org;
 
     /* admission: per socket, arrival-ordered merge, one all-or-nothing decision per burst */
     const uint32_t D = loff[lanes], DF = nd ? floff[lanes] : 0u;
     if (h_grow_host((void **)&g_udpdk.acc_d, &g_udpdk.acc_d_cap, 4ull * D + 4) ||
         h_grow_host((void **)&g_udpdk.acc_f, &g_udpdk.acc_f_cap, 4ull * DF + 4) ||
+        h_grow_host((void **)&g_udpdk.acc_do, &g_udpdk.acc_do_cap, 4ull * D + 8) ||
+        h_grow_host((void **)&g_udpdk.acc_fo, &g_udpdk.acc_fo_cap, 4ull * DF + 8) ||
         h_grow_host((void **)&g_udpdk.acc_sock, &g_udpdk.acc_sock_cap, 4ull * (D + DF) + 4))
         goto out;
-    uint32_t nad = 0, naf = 0, nacc = 0, maxd = 0, maxf = 0;
+    uint32_t nad = 0, naf = 0, nacc = 0;
+    uint64_t offd = 0, offf = 0;                    /* packed slot offsets (payload room / 16) */
     for (uint32_t s = 0; s < lanes && s < UDPDK_MAX_SOCKETS; s++) {
         const uint32_t a0 = loff[s], a1 = loff[s + 1];
         const uint32_t b0 = nd ? floff[s] : 0u, b1 = nd ? floff[s + 1] : 0u;
@@ -240,13 +277,15 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
                     if (q >= cq || (e < ce && lpkt[e] < forg[flpkt[q]])) {
                         const uint32_t fi = lpkt[e++];
                         const uint32_t pl = length[fi] > 42u ? length[fi] - 42u : 0u;
-                        if (pl > maxd) maxd = pl;
+                        g_udpdk.acc_do[nad] = (uint32_t)offd;
+                        offd += (pl + 15u) & ~15u;
                         g_udpdk.acc_d[nad++] = fi;
                         g_udpdk.acc_sock[nacc++] = s;
                     } else {
                         const uint32_t di = flpkt[q++];
                         const uint32_t pl = g_udpdk.fr_len[di] > 42u ? g_udpdk.fr_len[di] - 42u : 0u;
-                        if (pl > maxf) maxf = pl;
+                        g_udpdk.acc_fo[naf] = (uint32_t)offf;
+                        offf += (pl + 15u) & ~15u;
                         g_udpdk.acc_f[naf++] = di;
                         g_udpdk.acc_sock[nacc++] = s | 0x80000000u;
                     }
@@ -258,9 +297,15 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
         }
     }
     /* payloads of the admitted datagrams, gathered on the GPU into pinned slabs */
-    if (h_gather(&staged, g_udpdk.acc_d, nad, maxd, &ad)) goto out;
-    if (naf && h_gather(&rb, g_udpdk.acc_f, naf, maxf, &af)) goto out;
+    PROF_T(p4);
+    if (offd > 0xFFFFFFF0ull || offf > 0xFFFFFFF0ull) { errno = ENOBUFS; goto out; }
+    g_udpdk.acc_do[nad] = (uint32_t)offd;
+    g_udpdk.acc_fo[naf] = (uint32_t)offf;
+    if (h_gather(&staged, g_udpdk.acc_d, g_udpdk.acc_do, nad, &ad)) goto out;
+    if (naf && h_gather(&rb, g_udpdk.acc_f, g_udpdk.acc_fo, naf, &af)) goto out;
+    PROF_T(p5);
     if ((rc = udpdk_gpu_sync(g))) { errno = -rc; goto out; }
+    PROF_T(p6);
     if (ad) atomic_store_explicit(&ad->refs, nad, memory_order_relaxed);
     if (af) atomic_store_explicit(&af->refs, naf, memory_order_relaxed);
     /* publish: consecutive entries of one socket go to its ring in one bulk enqueue */
@@ -274,14 +319,14 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
                 struct h_dgram *d = &buf[nb++];
                 if (g_udpdk.acc_sock[k] >> 31) {
                     d->arena = af;
-                    d->data = af->payload + (uint64_t)kf * af->slot_bytes;
+                    d->data = af->payload + g_udpdk.acc_fo[kf];
                     d->len = af->len[kf];
                     d->src_ip = af->src_ip[kf];
                     d->src_port = af->src_port[kf];
                     kf++;
                 } else {
                     d->arena = ad;
-                    d->data = ad->payload + (uint64_t)kd * ad->slot_bytes;
+                    d->data = ad->payload + g_udpdk.acc_do[kd];
                     d->len = ad->len[kd];
                     d->src_ip = ad->src_ip[kd];
                     d->src_port = ad->src_port[kd];
@@ -297,6 +342,18 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
     ad = af = NULL;
     if (stats_out) *stats_out = st;
     ret = 0;
+#ifdef UDPDK_POLL_PROFILE
+    {   /* the first call (allocations, snapshot upload) is left out */
+        static int first = 1;
+        PROF_T(p7);
+        if (!first) {
+            PROF_ADD(0, p0, p1); PROF_ADD(1, p1, p2); PROF_ADD(2, p2, p3); PROF_ADD(3, p3, p4);
+            PROF_ADD(4, p4, p5); PROF_ADD(5, p5, p6); PROF_ADD(6, p6, p7);
+            g_prof[7] += 1;
+        }
+        first = 0;
+    }
+#endif
 out:
     if (ad) h_arena_put(ad);
     if (af) h_arena_put(af);

@@ -74,11 +74,10 @@ static void h_arena_destroy(struct h_arena *a)
     free(a);
 }
 
-/* A slab for n datagrams of slot_bytes: the first free one that is large enough, else a new one
- * (pinned, so the gather's D2H is a straight DMA). */
-struct h_arena *h_arena_get(uint32_t n, uint32_t slot_bytes)
+/* A slab for n datagrams in `need` bytes of packed slots: the first free one that is large
+ * enough, else a new one (pinned, so the gather's D2H is a straight DMA). */
+struct h_arena *h_arena_get(uint32_t n, uint64_t need)
 {
-    const uint64_t need = (uint64_t)n * slot_bytes;
     pthread_mutex_lock(&g_udpdk.arena_lock);
     struct h_arena **pp = &g_udpdk.arena_free, *a = NULL;
     for (; *pp; pp = &(*pp)->next)
@@ -103,7 +102,6 @@ struct h_arena *h_arena_get(uint32_t n, uint32_t slot_bytes)
         a->cap_bytes = cb;
         a->cap_n = cn;
     }
-    a->slot_bytes = slot_bytes;
     a->next = NULL;
     atomic_store_explicit(&a->refs, 0, memory_order_relaxed);
     return a;

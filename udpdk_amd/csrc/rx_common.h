@@ -181,6 +181,7 @@ struct GatherArgs {
     uint32_t slot_bytes;
     uint32_t rsrc_bytes;
     uint32_t n;
+    const uint32_t *slot_off;   // [count + 1] packed slots (udpdk_gpu_rx_gather_packed), or null
 };
 
 __global__ void rx_classify(RxArgs a);

@@ -3,7 +3,8 @@
 //
 // Lane entry k (frame i = lane_pkt[first + k]): payload = frame bytes
 // [42, 42 + min(data_len - 42, dgram_len - 8)) (Ethernet padding trimmed, :459-466), truncated
-// to slot_bytes (recvfrom's len, :467-472), copied to payload + k * slot_bytes; len[k] = bytes
+// to slot_bytes (recvfrom's len, :467-472), copied to payload + k * slot_bytes (packed slots, as
+// the poll uses them: payload + slot_off[k], slot_off[k + 1] - slot_off[k] bytes); len[k] = bytes
 // copied (recvfrom's return, :487); src_ip[k] / src_port[k] = ip_hdr->src_addr /
 // udp_hdr->src_port, raw (:446-447).
 //
@@ -47,7 +48,10 @@ __global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
         const uint32_t dl = ((dlr & 0xFFu) << 8) | (dlr >> 8);
         const uint32_t pl = (dl - 8u) & 0xFFFFu;                 // uint16_t dgram_payl_len (:436)
         const uint32_t seg = len >= 42u ? len - 42u : 0u;        // data_len - offset_payload (:458)
-        const uint32_t n = valid ? min(min(seg, pl), a.slot_bytes) : 0u;
+        const uint32_t so32 = valid && a.slot_off ? a.slot_off[k] : 0u;
+        const uint64_t so = !valid ? 0ull : a.slot_off ? (uint64_t)so32 : (uint64_t)k * a.slot_bytes;
+        const uint32_t cap = !valid ? 0u : a.slot_off ? a.slot_off[k + 1] - so32 : a.slot_bytes;
+        const uint32_t n = valid ? min(min(seg, pl), cap) : 0u;
         if (valid) {
             a.len_out[k] = n;
             a.src_ip[k] = h[0];
@@ -56,7 +60,7 @@ __global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
         const uint32_t kw = k - lane;                            // the wave's first entry
         if (!__ballot(n > 128u)) {
             // short payloads: each lane copies its own, 16-byte pieces, four loads in flight
-            uint8_t *dst = a.payload + (size_t)k * a.slot_bytes;
+            uint8_t *dst = a.payload + so;
             for (uint32_t c = 0; c < n; c += 64u) {
                 uint4 v[4];
                 if (c == 0u && fseg <= 64u) {
@@ -78,10 +82,13 @@ __global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
             // contiguous KiB of one payload (lane i: bytes 16 i .. 16 i + 15 of each KiB)
             for (uint32_t j = 0; j < 64u; j += 2u) {
                 uint32_t nj[2], oj[2];
+                uint64_t dj[2];
 #pragma unroll
                 for (uint32_t u = 0; u < 2; ++u) {
                     nj[u] = (uint32_t)__builtin_amdgcn_readlane((int)n, (int)(j + u));
                     oj[u] = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)(j + u));
+                    dj[u] = a.slot_off ? (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)so32, (int)(j + u))
+                                       : (uint64_t)(kw + j + u) * a.slot_bytes;
                 }
                 const uint32_t m = max(nj[0], nj[1]);
                 for (uint32_t c = 0; c < m; c += 2048u) {
@@ -101,7 +108,7 @@ __global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
                         for (uint32_t h2 = 0; h2 < 2; ++h2) {
                             const uint32_t b = c + 1024u * h2 + 16u * lane;
                             if (b < nj[u])
-                                *reinterpret_cast<uint4 *>(a.payload + (size_t)(kw + j + u) * a.slot_bytes + b) = v[u][h2];
+                                *reinterpret_cast<uint4 *>(a.payload + dj[u] + b) = v[u][h2];
                         }
                 }
             }

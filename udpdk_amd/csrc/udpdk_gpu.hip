@@ -861,14 +861,18 @@ int udpdk_gpu_rx_host_wait(udpdk_gpu_ctx *c)
     return finish_all_host(c);
 }
 
-int udpdk_gpu_rx_gather(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint32_t *lane_pkt_dev,
-                        uint32_t first, uint32_t count, const udpdk_rx_gather_t *o)
+namespace {
+
+static int rx_gather_launch(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint32_t *lane_pkt_dev,
+                     uint32_t first, uint32_t count, const uint32_t *slot_off_dev,
+                     const udpdk_rx_gather_t *o)
 {
     if (!c || !bt || !o) return -EINVAL;
     if (!count) return 0;
     if (!bt->n || !bt->frames_dev || !bt->offset_dev || !bt->length_dev || !lane_pkt_dev ||
         !o->payload_dev || !o->len_dev || !o->src_ip_dev || !o->src_port_dev) return -EINVAL;
-    if (o->slot_bytes < 16u || (o->slot_bytes & 15u) || ((uintptr_t)o->payload_dev & 15u)) return -EINVAL;
+    if (!slot_off_dev && (o->slot_bytes < 16u || (o->slot_bytes & 15u))) return -EINVAL;
+    if ((uintptr_t)o->payload_dev & 15u) return -EINVAL;
     if (bt->frames_bytes >= (1ull << 32) || (uint64_t)first + count > 0xFFFFFFFFull) return -EINVAL;
     HIPC(c, hipSetDevice(c->device));
     if (c->depth > 1) { int r = join_pipes(c); if (r) return r; }
@@ -886,6 +890,7 @@ int udpdk_gpu_rx_gather(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint
     ga.slot_bytes = o->slot_bytes;
     ga.rsrc_bytes = frames_rsrc_bytes(bt->frames_bytes);
     ga.n = bt->n;
+    ga.slot_off = slot_off_dev;
     const uint32_t grid = std::min<uint32_t>(ceil_div(count, GATHER_BLOCK), 16384);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing_every) {
@@ -906,6 +911,22 @@ int udpdk_gpu_rx_gather(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint
         (void)hipEventDestroy(e1);
     }
     return 0;
+}
+
+} // namespace
+
+int udpdk_gpu_rx_gather(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint32_t *lane_pkt_dev,
+                        uint32_t first, uint32_t count, const udpdk_rx_gather_t *o)
+{
+    return rx_gather_launch(c, bt, lane_pkt_dev, first, count, nullptr, o);
+}
+
+int udpdk_gpu_rx_gather_packed(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint32_t *lane_pkt_dev,
+                               uint32_t first, uint32_t count, const uint32_t *slot_off_dev,
+                               const udpdk_rx_gather_t *o)
+{
+    if (count && !slot_off_dev) return -EINVAL;
+    return rx_gather_launch(c, bt, lane_pkt_dev, first, count, slot_off_dev, o);
 }
 
 int udpdk_gpu_rss_default_conf(udpdk_rss_conf_t *conf, uint32_t n_queues)
