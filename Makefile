@@ -52,6 +52,17 @@ $(STAMP_LIB): $(STAMP_OBJ) $(C_OBJ)
 	@mkdir -p tools/diag
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -Wl,--no-undefined
 
+# diagnostic library with per-phase wall-clock timing inside udpdk_poll_rx (tools/sock_prof.sh)
+PROF_LIB := tools/diag/pollprof/libudpdk_amd.so
+PROF_OBJ := $(patsubst udpdk_amd/csrc/host/%.c,build/pollprof/%.o,$(C_SRC))
+pollprof: $(PROF_LIB)
+build/pollprof/%.o: udpdk_amd/csrc/host/%.c $(HDRS)
+	@mkdir -p build/pollprof
+	$(CC) $(CFLAGS_H) -DUDPDK_POLL_PROFILE $(INC) -c $< -o $@
+$(PROF_LIB): $(HIP_OBJ) $(PROF_OBJ)
+	@mkdir -p tools/diag/pollprof
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -Wl,--no-undefined -Wl,-soname,libudpdk_amd.so
+
 asm: udpdk_amd/csrc/rx_kernels.hip $(HDRS)
 	@mkdir -p build/asm
 	$(HIPCC) $(HIPFLAGS) -Wno-unused-command-line-argument $(INC) -S --cuda-device-only -o build/asm/rx_kernels.s $<
@@ -61,4 +72,4 @@ clean:
 	rm -rf build $(LIB) $(TOOLS)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean asm stamps
+.PHONY: all oracle clean asm stamps pollprof

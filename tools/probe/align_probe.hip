@@ -1,0 +1,147 @@
+// How fast does the vector memory path move 16-byte buffer loads at each alignment? 1 GiB read
+// once per launch (more than the 256 MiB Infinity Cache), every wave streaming its own 128 KiB
+// span in 4 KiB groups (two groups in flight), one u32 written per lane. Patterns:
+//   chunk  lane i reads the 64-byte chunk i of a group as 4 pieces (rx_classify's tail pass)
+//   coal   instruction c reads 1 KiB contiguous, lane i at 16 i
+// Loaders:
+//   b128   byte-addressed 16-byte loads at the shifted address (what the tail pass issues)
+//   al     16-byte loads at the aligned-down address (5 per 64-byte chunk for chunk, 17 per
+//          1 KiB... coal keeps 4 and adds one) + v_alignbyte funnel to the shifted words
+//   b32    four 4-byte loads per piece
+// Usage: align_probe [reps]; prints GB/s per (pattern, loader, shift).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 ld128(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ uint4 ld4x32(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    return make_uint4(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0),
+                      __builtin_amdgcn_raw_buffer_load_b32(r, (int)off + 4, 0, 0),
+                      __builtin_amdgcn_raw_buffer_load_b32(r, (int)off + 8, 0, 0),
+                      __builtin_amdgcn_raw_buffer_load_b32(r, (int)off + 12, 0, 0));
+}
+__device__ __forceinline__ uint32_t s4(uint4 v) { return v.x + v.y + v.z + v.w; }
+
+// 16 words starting at byte sh (0-15) of the 20 aligned words D
+__device__ __forceinline__ uint32_t funnel_sum(const uint32_t (&D)[20], uint32_t sh)
+{
+    const uint32_t q = sh >> 2, b = (sh & 3u) * 8u;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t lo = q == 0 ? D[i] : q == 1 ? D[i + 1] : q == 2 ? D[i + 2] : D[i + 3];
+        const uint32_t hi = q == 0 ? D[i + 1] : q == 1 ? D[i + 2] : q == 2 ? D[i + 3] : D[i + 4];
+        acc += (uint32_t)(((((uint64_t)hi) << 32) | lo) >> b);
+    }
+    return acc;
+}
+
+template <int PAT, int LD>
+__global__ void __launch_bounds__(256) k_probe(const uint8_t *buf, uint32_t bytes, uint32_t shift,
+                                               uint32_t span, uint32_t *out)
+{
+    const __amdgpu_buffer_rsrc_t r = rsrc(buf, bytes);
+    const uint32_t lane = threadIdx.x & 63, g = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t base = g * span + shift;
+    uint32_t acc = 0;
+#pragma unroll 2
+    for (uint32_t k = 0; k < span; k += 4096) {
+        const uint32_t o = base + k;
+        if (LD == 1) {
+            uint32_t D[20];
+            if (PAT == 0) {
+                const uint32_t a = (o + 64 * lane) & ~15u, sh = (o + 64 * lane) & 15u;
+#pragma unroll
+                for (int c = 0; c < 5; ++c) {
+                    const uint4 v = ld128(r, a + 16 * c);
+                    D[4 * c] = v.x; D[4 * c + 1] = v.y; D[4 * c + 2] = v.z; D[4 * c + 3] = v.w;
+                }
+                acc += funnel_sum(D, sh);
+            } else {
+                // contiguous: lane i's aligned piece and its right neighbour's first word
+                const uint32_t sh = o & 15u;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint32_t a = ((o + 1024 * c) & ~15u) + 16 * lane;
+                    const uint4 v = ld128(r, a);
+                    const uint32_t nx = __shfl_down(v.x, 1, 64);
+                    const uint32_t tail = lane == 63 ? __builtin_amdgcn_raw_buffer_load_b32(r, (int)(a + 16), 0, 0) : nx;
+                    const uint32_t w[5] = {v.x, v.y, v.z, v.w, tail};
+                    const uint32_t q = sh >> 2, b = (sh & 3u) * 8u;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t lo = q == 0 ? w[i] : q == 1 ? w[min(i + 1, 4)] : q == 2 ? w[min(i + 2, 4)] : w[min(i + 3, 4)];
+                        const uint32_t hi = q == 0 ? w[i + 1] : q == 1 ? w[min(i + 2, 4)] : q == 2 ? w[min(i + 3, 4)] : w[4];
+                        acc += (uint32_t)(((((uint64_t)hi) << 32) | lo) >> b);
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t off = PAT == 0 ? o + 64 * lane + 16 * c : o + 1024 * c + 16 * lane;
+                acc += s4(LD == 0 ? ld128(r, off) : ld4x32(r, off));
+            }
+        }
+    }
+    out[g * 64 + lane] = acc;
+}
+
+template <int PAT, int LD>
+static float run(const uint8_t *buf, uint32_t bytes, uint32_t shift, uint32_t span, uint32_t *out, int reps)
+{
+    const uint32_t waves = (bytes - 64) / span, blocks = waves / 4;
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    hipLaunchKernelGGL((k_probe<PAT, LD>), dim3(blocks), dim3(256), 0, 0, buf, bytes, shift, span, out);
+    CHECK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL((k_probe<PAT, LD>), dim3(blocks), dim3(256), 0, 0, buf, bytes, shift, span, out);
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    CHECK(hipEventDestroy(e0));
+    CHECK(hipEventDestroy(e1));
+    return (float)((double)blocks * 4 * span * reps / (ms * 1e-3) / 1e9);
+}
+
+int main(int argc, char **argv)
+{
+    const int reps = argc > 1 ? atoi(argv[1]) : 20;
+    const uint32_t span = 128u << 10, bytes = (1u << 30) + 4096;
+    uint8_t *buf;
+    uint32_t *out;
+    CHECK(hipMalloc(&buf, bytes));
+    CHECK(hipMemset(buf, 1, bytes));
+    CHECK(hipMalloc(&out, (bytes / span + 1) * 64 * 4));
+    const uint32_t shifts[] = {0, 4, 8, 1, 2, 3};
+    printf("{");
+    const char *sep = "";
+    for (uint32_t s : shifts) {
+        printf("%s\"chunk b128 +%u\": %.0f", sep, s, run<0, 0>(buf, bytes, s, span, out, reps)); sep = ", ";
+        printf(", \"chunk b32 +%u\": %.0f", s, run<0, 2>(buf, bytes, s, span, out, reps));
+        printf(", \"chunk al +%u\": %.0f", s, run<0, 1>(buf, bytes, s, span, out, reps));
+        printf(", \"coal b128 +%u\": %.0f", s, run<1, 0>(buf, bytes, s, span, out, reps));
+        printf(", \"coal al +%u\": %.0f", s, run<1, 1>(buf, bytes, s, span, out, reps));
+        fflush(stdout);
+    }
+    printf("}\n");
+    CHECK(hipFree(buf));
+    CHECK(hipFree(out));
+    return 0;
+}

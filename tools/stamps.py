@@ -10,14 +10,17 @@ sys.path.insert(0, ROOT)
 import numpy as np
 from udpdk_amd import abi, frames as F
 
-PH = ["prologue", "funnel+fields", "header sums+sweep", "issue next+wait demux", "udp state",
-      "demux+verdict", "meta/ctr/hist", "tile ctr"]
+PH = ["prologue", "window wait+fields (+demux)", "header sums", "-", "-", "-",
+      "state+stash+tail+next window", "counters+tile end"]
 L = abi.lib()
 L.udpdk_gpu_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 ctx = abi.GpuContext(0, max_frames=1 << 22, max_lanes=4096)
 dbg = ctx.alloc((2 * 8192 + 8192) * 16 * 8)   # classify rows, then rx_scatterw rows from 16384
 L.udpdk_gpu_debug_buffer(ctx.handle, C.c_void_p(dbg.ptr))
-for cfg, n in [(2, 4096), (2, None), (4, 65536), (3, 65536)]:
+CASES = [(2, 4096), (2, None), (4, 65536), (3, 65536)]
+if os.environ.get("STAMPS_CASES"):      # e.g. "4:0,3:0" (0 = the config's full size)
+    CASES = [(int(c), int(m) or None) for c, m in (x.split(":") for x in os.environ["STAMPS_CASES"].split(","))]
+for cfg, n in CASES:
     w = F.config_batch(cfg, n=n)
     ctx.upload_snapshot(abi.snapshot_from_lists(w.port_lists(), w.n_sockets))
     # enough device copies that the 256 MiB Infinity Cache cannot hold them (as bench.py), so
@@ -58,6 +61,17 @@ for cfg, n in [(2, 4096), (2, None), (4, 65536), (3, 65536)]:
     simd = (hw >> 4) & 3
     print(f"   CUs used {len(ucu)}; WGs per CU min/median/max {per.min()}/{int(np.median(per))}/"
           f"{per.max()}; wave0 SIMD histogram {np.bincount(simd, minlength=4).tolist()}")
+    # is a slow workgroup slow because of its CU (all its CU's workgroups slow) or on its own?
+    cu_mean = np.bincount(inv, weights=dur) / per
+    within = dur - cu_mean[inv]
+    print(f"   duration std us: all {dur.std() / 100:.2f}, between CUs {cu_mean.std() / 100:.2f}, "
+          f"within a CU {within.std() / 100:.2f}; CU mean p10/50/90 "
+          f"{' '.join(f'{np.percentile(cu_mean, q) / 100:.2f}' for q in (10, 50, 90))}")
+    se = (hw >> 13) & 7
+    for x in np.unique(xcc)[:2]:
+        m = xcc == x
+        print(f"     xcc {x}: per-SE mean duration us "
+              f"{[round(float(dur[m & (se == e)].mean()) / 100, 1) for e in np.unique(se[m])]}")
     late = st0 > 500                                   # started > 5 us after the first
     if late.any():
         print(f"   late WGs {late.sum()}: on CUs holding {np.bincount(per[inv[late]]).nonzero()[0].tolist()} WGs")

@@ -213,7 +213,7 @@ __device__ __forceinline__ uint32_t max_scan_dpp(uint32_t v)
 // tools/probe/stream_probe.hip k_unal): g[i] = frame bytes 12 + 4i .. 15 + 4i, no funnel shift.
 struct Win {
     uint4 a, b, c;
-    uint32_t d;
+    uint2 d;
 };
 
 // 4 waves per SIMD (<= 128 VGPRs, the tail pass's two groups in flight): one tile of 1024 frames
@@ -298,17 +298,21 @@ rx_classify(RxArgs a)
         lp = d_lp[b];
     };
     // The frame's header window, frame bytes [12, 64) (bytes 0-11, the MAC addresses, are never
-    // read). One lane per frame. Bytes past the frame are never used (parse and sums mask by
-    // length); lanes without a frame read the buffer's first bytes (cached, never used).
+    // read). One lane per frame, 14 dwords from the dword-aligned buffer offset at or below
+    // offset + 12 (byte-aligned 16-byte loads cost the vector memory path ~25 %); the step
+    // funnels them to frame-relative words by offset & 3. Bytes past the frame are never used
+    // (parse and sums mask by length); lanes without a frame read the buffer's first bytes
+    // (cached, never used).
     auto load_win = [&](uint32_t s, uint32_t o, uint32_t l) -> Win {
         const uint32_t p = t0 + s * 64 + lane;
         const bool ok = s < steps && p < t1 && l >= 14u && l <= a.frames_bytes && o <= a.frames_bytes - l;
-        const uint32_t b = ok ? o + 12u : 0u;
+        const uint32_t b = ok ? (o + 12u) & ~3u : 0u;
         Win r;
         r.a = load16(fr, b);
         r.b = load16(fr, b + 16u);
         r.c = load16(fr, b + 32u);
-        r.d = __builtin_amdgcn_raw_buffer_load_b32(fr, (int)(b + 48u), 0, 0);
+        const auto d = __builtin_amdgcn_raw_buffer_load_b64(fr, (int)(b + 48u), 0, 0);
+        r.d = make_uint2(d[0], d[1]);
         return r;
     };
 
@@ -324,20 +328,25 @@ rx_classify(RxArgs a)
     // ---- tail pass: UDP checksums of the datagrams that extend past the header window ----
     // Run for each step right after it (while the frames' first lines are still in L2: a pass
     // per round of four steps re-fetched the line shared by a frame's header window and its
-    // first tail chunk from HBM). The step's pending frames (state 3): frame bytes [64, dge) as
-    // 64-byte super-chunks, chunk j = frame bytes [64 + 64 j, 128 + 64 j) loaded as 4
-    // byte-aligned 16-byte pieces (so the words are frame-relative whatever the frame's offset),
-    // swept across the wave's lanes: lane i of a group takes chunk k0 + i of the step's chunk
-    // space, so a group is 4 KiB of dense frame bytes. A chunk's frame comes from a prefix
+    // first tail chunk from HBM). The step's pending frames (state 3): the tail's bytes, frame
+    // bytes [64, dge) at buffer offsets [S, E) = [offset + 64, offset + dge), as 64-byte
+    // super-chunks from the dword-aligned Sa = S & ~3 (chunk j = [Sa + 64 j, Sa + 64 j + 64), 4
+    // dword-aligned 16-byte pieces; byte-aligned pieces ran the vector memory path at 4.45
+    // instead of 5.9 TB/s, tools/probe/align_probe.hip). The words are then buffer-aligned, not
+    // frame-aligned: a frame at an odd offset has its tail sum byte-swapped (RFC 1071 sums are
+    // byte-order independent up to that swap), and the first chunk's S - Sa lead bytes (the
+    // window's) come off again. The chunks are swept across the wave's lanes: lane i of a group
+    // takes chunk k0 + i of the step's chunk space, so a group is 4 KiB of dense frame bytes. A chunk's frame comes from a prefix
     // maximum over the group's lanes of the marks the frames starting inside the group leave in
     // LDS (one LDS round trip; a binary search over the chunk starts took six). Pieces at or past
     // the datagram end are addressed out of the buffer's range (no memory access, zeros); the
     // piece holding the end, when it ends inside it, has its bytes past the end subtracted from
     // the chunk sum, so every chunk is summed the same way (v_sad_u16 chains, no masked re-sum).
     // Per-frame sums are segment sums of a DPP prefix scan; two groups in flight.
-    // per frame q of the step: chunk k of q starts at frame byte B_q + 64 k and holds D_q - 64 k
-    // bytes of the datagram (B_q = offset + 64 - 64 cs_q, D_q = dge - 64 + 64 cs_q, cs_q = the
-    // frame's first chunk index in the step), so a chunk needs two LDS words of its frame
+    // per frame q of the step: chunk k of q starts at buffer offset B_q + 64 k and holds D_q - 64 k
+    // bytes up to the datagram end (B_q = Sa - 64 cs_q, D_q = E - Sa + 64 cs_q, cs_q = the frame's
+    // first chunk index in the step), so a chunk needs two LDS words of its frame (B_q's low two
+    // bits carry the lead S - Sa)
     uint32_t *l_B = reinterpret_cast<uint32_t *>(smem + TP_OFF) + w * 192;   // [64]
     uint32_t *l_D = l_B + 64;                                               // [64]
     uint32_t *l_own = l_B + 128;            // [64] frame + 1 whose chunks start at k0 + slot, else 0
@@ -352,16 +361,17 @@ rx_classify(RxArgs a)
             const uint32_t fo = nbuf == 1u ? d_off[i] : a.offset[min(t0 + i, plast)];
             const uint32_t dw = dgl[i & (RX_ROUND - 1u)];
             const uint32_t de = pd ? dw & 0xFFFFu : 64u;
-            const uint32_t my_nt = (de - 64u + 63u) >> 6;
+            const uint32_t lead = (fo + 64u) & 3u;
+            const uint32_t my_nt = pd ? (de - 64u + lead + 63u) >> 6 : 0u;
             const uint32_t inc = scan_dpp(my_nt);
             const uint32_t my_cs = inc - my_nt;
             const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-            l_B[lane] = fo + 64u - 64u * my_cs;
-            l_D[lane] = de - 64u + 64u * my_cs;
+            l_B[lane] = (fo + 64u - lead - 64u * my_cs) | lead;
+            l_D[lane] = de - 64u + lead + 64u * my_cs;
             uint32_t tsum = 0, carry = 0;
             // group k0: each lane's frame (q), the chunk's bytes in the datagram (left) and its
             // four pieces in flight
-            auto issue = [&](uint32_t k0, uint32_t &q, int &left, uint4 (&R)[4]) {
+            auto issue = [&](uint32_t k0, uint32_t &q, int &left, uint32_t &lead_b, uint4 (&R)[4]) {
                 const uint32_t k = k0 + lane;
                 if (my_nt != 0u && my_cs >= k0 && my_cs < k0 + 64u) l_own[my_cs - k0] = lane + 1u;
                 wave_sync();
@@ -371,13 +381,15 @@ rx_classify(RxArgs a)
                 carry = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
                 q = (own - 1u) & 63u;
                 left = k < total ? (int)(l_D[q] - 64u * k) : 0;
-                const uint32_t base = l_B[q] + 64u * k;
+                const uint32_t bq = l_B[q];
+                lead_b = mark != 0u ? bq & 3u : 0u;     // a frame's first chunk: its lead bytes
+                const uint32_t base = (bq & ~3u) + 64u * k;
 #pragma unroll
                 for (int c = 0; c < 4; ++c) R[c] = load16(fr, 16 * c < left ? base + 16u * c : OOR);
             };
             // The full-chunk sum reads every loaded register unconditionally, so the compiler's
             // wait for this group is placed here on every path.
-            auto consume = [&](uint32_t k0, int left, const uint4 (&R)[4]) {
+            auto consume = [&](uint32_t k0, int left, uint32_t lead_b, const uint4 (&R)[4]) {
                 uint32_t pa = 0, pb = 0;
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
@@ -398,7 +410,9 @@ rx_classify(RxArgs a)
                     const int keep = min(max(r - 4 * d, 0), 4);
                     ex = sad16(pv[d] & (keep >= 4 ? 0u : 0xFFFFFFFFu << (8 * keep)), ex);
                 }
-                const uint32_t part = pa + pb - (left > 0 && left < 64 && r != 0 ? ex : 0u);
+                // and the first chunk's lead bytes [0, lead_b) (<= 3: in the first dword)
+                ex = sad16(R[0].x & ((1u << (8u * lead_b)) - 1u), ex & (left > 0 && left < 64 && r != 0 ? ~0u : 0u));
+                const uint32_t part = pa + pb - ex;
                 const uint32_t Pp = scan_dpp(part);
                 const uint32_t lo = max(my_cs, k0), hi = min(my_cs + my_nt, k0 + 64u);
                 const uint32_t ph = __shfl(Pp, (int)((hi > k0 ? hi - 1u - k0 : 0u) & 63u), 64);
@@ -408,20 +422,22 @@ rx_classify(RxArgs a)
             // Two groups in flight; one back edge, after the second group is consumed (a loop
             // exit between the two halves leaves the second group's loads pending at the
             // header, which then waits for everything). Groups past the end load nothing.
-            uint32_t qa, qb;
+            uint32_t qa, qb, ea, eb;
             int la, lb;
             uint4 Ra[4], Rb[4];
-            issue(0, qa, la, Ra);
+            issue(0, qa, la, ea, Ra);
             for (uint32_t k0 = 0;; k0 += 128) {
-                issue(k0 + 64, qb, lb, Rb);
-                consume(k0, la, Ra);
-                issue(k0 + 128, qa, la, Ra);
-                consume(k0 + 64, lb, Rb);
+                issue(k0 + 64, qb, lb, eb, Rb);
+                consume(k0, la, ea, Ra);
+                issue(k0 + 128, qa, la, ea, Ra);
+                consume(k0 + 64, lb, eb, Rb);
                 if (k0 + 128 >= total) break;
             }
             wave_sync();
             if (pd) {
-                const bool ok = fold32(fold32(tsum) + (dw >> 16)) == 0xFFFFu;
+                uint32_t t = fold32(tsum);
+                if (fo & 1u) t = ((t & 0xFFu) << 8) | (t >> 8);   // buffer-aligned words: swap back
+                const bool ok = fold32(t + (dw >> 16)) == 0xFFFFu;
                 mstage[i & (RX_ROUND - 1u)] = (m & ~0x60u) | ((ok ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD) << 5);
                 acc_f0 += ok ? 0x10000u : 0x1000000u;
             }
@@ -438,8 +454,12 @@ rx_classify(RxArgs a)
             const bool good = valid && len <= a.frames_bytes && off <= a.frames_bytes - len;
 
             // ---- header fields from the window registers (lane = frame) ----
-            const uint32_t g[13] = {W.a.x, W.a.y, W.a.z, W.a.w, W.b.x, W.b.y, W.b.z, W.b.w,
-                                    W.c.x, W.c.y, W.c.z, W.c.w, W.d};  // g[i] = frame bytes 12+4i ..
+            const uint32_t D[14] = {W.a.x, W.a.y, W.a.z, W.a.w, W.b.x, W.b.y, W.b.z, W.b.w,
+                                    W.c.x, W.c.y, W.c.z, W.c.w, W.d.x, W.d.y};
+            const uint32_t sh = off & 3u;     // lanes whose window was not loaded: unused words
+            uint32_t g[13];                   // g[i] = frame bytes 12+4i ..
+#pragma unroll
+            for (int i = 0; i < 13; ++i) g[i] = __builtin_amdgcn_alignbyte(D[i + 1], D[i], sh);
             // IPv4 gate (udpdk_poller.c:334): the ptype array's L3_IPV4 bit when given, else derived
             // from ether_type (frames shorter than an Ethernet header are not IPv4)
             const uint32_t eth_ip = (len >= 14u && (g[0] & 0xFFFFu) == 0x0008u) ? 0x10u : 0u;
@@ -488,11 +508,17 @@ rx_classify(RxArgs a)
             dgl[(st * 64 + lane) & (RX_ROUND - 1u)] = dge | fold32(us) << 16;
             STAMP(2);
 
-            // ---- next step of this wave: window loads stay in flight across the rest of this step
+            // ---- next step of this wave: window loads stay in flight across the rest of this step.
+            // A step with pending frames issues them after its tail pass instead: a window's lines
+            // (the one it shares with the frame's first tail chunk, and the one the previous
+            // frame's tail ends in) are then still in L2 when that step's tail reads them, where a
+            // window loaded a whole step earlier had left L2 by then (IMIX fetched 1.29x its bytes).
             const uint32_t nst = st + CLS_WAVES;
             uint32_t n_off, n_lp;
             read_desc(nst, n_off, n_lp);      // in range of the buffers for any s (unused past the tile)
-            const Win NW = load_win(nst, n_off, n_lp & 0xFFFFu);
+            const bool tail_now = __ballot(pend) != 0ull;
+            Win NW;
+            if (!tail_now) NW = load_win(nst, n_off, n_lp & 0xFFFFu);
 
             // ---- what does not need the port entry: UDP state, flags, flag counters ----
             const uint32_t state = ucks == 0u ? UDPDK_UDP_CSUM_NONE
@@ -516,7 +542,10 @@ rx_classify(RxArgs a)
             // the port-table lookup waits for the round's demux pass: verdict field 0xF until then
             mstage[(st * 64 + lane) & (RX_ROUND - 1u)] = (pre == 0xFFu ? 0xFu : pre) | l3f | udpf;
             dstash[(st * 64 + lane) & (RX_ROUND - 1u)] = make_uint2(dport | (is_udp ? 0x10000u : 0u), dip);
-            if (__ballot(pend)) tail_step(st);
+            if (tail_now) {
+                tail_step(st);
+                NW = load_win(nst, n_off, n_lp & 0xFFFFu);
+            }
             STAMP(6);
             // next round's descriptors into the other buffer at the wave's next-to-last step of a
             // round (its steps of round r are 16 r + w + CLS_WAVES j, j < SPR): the last reads of that
@@ -603,14 +632,6 @@ rx_classify(RxArgs a)
                 }
             }
         }
-        // ---- tail pass: UDP checksums of the datagrams that extend past the header window ----
-        // The wave's pending frames of the round (state 3), one step (64 frames) at a time: frame
-        // bytes [64, dge) as 64-byte super-chunks, chunk j = frame bytes [64 + 64 j, 128 + 64 j)
-        // loaded as 4 byte-aligned 16-byte pieces (so the words are frame-relative whatever the
-        // frame's offset, and only a frame's last chunk needs byte masks), swept across the wave's
-        // lanes: lane i of a group takes chunk k0 + i of the step's chunk space (its frame found by
-        // binary search over the per-frame chunk starts in LDS), so a group is 4 KiB of dense frame
-        // bytes. Per-frame sums are segment sums of a DPP prefix scan; two groups in flight.
     }
 
     // ---- tile counters: one row per wave (lanes 0-15), summed by the readers ----
