@@ -124,6 +124,41 @@ def test_zipf_4096_full(gpu_ctx):
     assert np.all(d[mask] > 0)
 
 
+@pytest.mark.parametrize("seed", [21, 22])
+def test_tail_checksums_every_alignment(gpu_ctx, seed):
+    """rx_classify sums a datagram's tail (frame bytes [64, end)) from the dword-aligned buffer
+    offset at or below offset + 64, subtracting the lead bytes and byte-swapping the sum for odd
+    offsets: long datagrams at every offset residue, one byte corrupted in a third of them (in
+    the lead bytes 64-67, anywhere in the tail, or the last byte). Exact against the oracle,
+    and every corrupted datagram is flagged UDP_BAD, every intact one UDP_OK."""
+    rng = np.random.default_rng(seed)
+    n = 6000
+    sizes = rng.integers(65, 1515, n).astype(np.uint32)
+    sizes[:8] = [65, 66, 67, 68, 69, 127, 128, 129]
+    src = F.build_frames(sizes, np.full(n, 10001, np.uint32), seed)
+    gaps = rng.integers(0, 4, n)
+    off = np.zeros(n, np.int64)
+    pos = 1
+    for i in range(n):
+        off[i] = pos
+        pos += int(sizes[i]) + int(gaps[i])
+    fr = np.zeros(pos + 256, np.uint8)
+    for i in range(n):
+        fr[off[i]:off[i] + sizes[i]] = src.frames[int(src.offset[i]):int(src.offset[i]) + int(sizes[i])]
+    bad = rng.random(n) < 1 / 3
+    where = rng.integers(0, 3, n)
+    for i in np.nonzero(bad)[0]:
+        L = int(sizes[i])
+        k = {0: 64 + int(rng.integers(0, min(4, L - 64))), 1: int(rng.integers(64, L)), 2: L - 1}[int(where[i])]
+        fr[off[i] + k] ^= 0x5A
+    b = F.Batch(fr, off.astype(np.uint32), sizes.astype(np.uint16), pos)
+    want, got = _rx_both(gpu_ctx, b, {abi.raw_port(10001): [(0, 0, 0)]}, 1)
+    _assert_same(want, got, f"seed={seed}")
+    assert set(np.unique(off % 4)) == {0, 1, 2, 3}
+    udp = abi.meta_udp(got[0])
+    assert np.all(udp[bad] == abi.UDP_BAD) and np.all(udp[~bad] == abi.UDP_OK)
+
+
 def test_edge_sizes(gpu_ctx):
     lists = {abi.raw_port(10001): [(0, 0, 0)]}
     for n in [1, 63, 64, 65, 1023, 1024, 1025, 4097]:
