@@ -100,6 +100,45 @@ __global__ void __launch_bounds__(256) k_probe(const uint8_t *buf, uint32_t byte
     out[g * 64 + lane] = acc;
 }
 
+// copy: wave-contiguous 1 KiB per instruction, source at +rs and destination at +ws bytes
+__global__ void __launch_bounds__(256) k_copy(const uint8_t *src, uint8_t *dst, uint32_t bytes,
+                                              uint32_t rs, uint32_t ws, uint32_t span)
+{
+    const __amdgpu_buffer_rsrc_t r = rsrc(src, bytes), w = rsrc(dst, bytes);
+    const uint32_t lane = threadIdx.x & 63, g = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t base = g * span;
+    for (uint32_t k = 0; k < span; k += 4096) {
+        uint4 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = ld128(r, base + k + 1024 * c + 16 * lane + rs);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            __attribute__((ext_vector_type(4))) uint32_t x = {v[c].x, v[c].y, v[c].z, v[c].w};
+            __builtin_amdgcn_raw_buffer_store_b128(x, w, (int)(base + k + 1024 * c + 16 * lane + ws), 0, 0);
+        }
+    }
+}
+
+static float run_copy(const uint8_t *src, uint8_t *dst, uint32_t bytes, uint32_t rs, uint32_t ws,
+                      uint32_t span, int reps)
+{
+    const uint32_t blocks = (bytes - 64) / span / 4;
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(256), 0, 0, src, dst, bytes, rs, ws, span);
+    CHECK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(256), 0, 0, src, dst, bytes, rs, ws, span);
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    CHECK(hipEventDestroy(e0));
+    CHECK(hipEventDestroy(e1));
+    return (float)(2.0 * blocks * 4 * span * reps / (ms * 1e-3) / 1e9);   // read + written
+}
+
 template <int PAT, int LD>
 static float run(const uint8_t *buf, uint32_t bytes, uint32_t shift, uint32_t span, uint32_t *out, int reps)
 {
@@ -129,6 +168,18 @@ int main(int argc, char **argv)
     CHECK(hipMalloc(&buf, bytes));
     CHECK(hipMemset(buf, 1, bytes));
     CHECK(hipMalloc(&out, (bytes / span + 1) * 64 * 4));
+    if (argc > 2) {                      // copy mode: GB/s (read + written) per (src, dst) shift
+        uint8_t *dst;
+        CHECK(hipMalloc(&dst, bytes));
+        const uint32_t cs[][2] = {{0, 0}, {2, 0}, {0, 2}, {2, 2}, {0, 4}, {1, 3}};
+        printf("{");
+        for (int i = 0; i < 6; ++i)
+            printf("%s\"copy src+%u dst+%u\": %.0f", i ? ", " : "", cs[i][0], cs[i][1],
+                   run_copy(buf, dst, bytes, cs[i][0], cs[i][1], span, reps));
+        printf("}\n");
+        CHECK(hipFree(dst));
+        return 0;
+    }
     const uint32_t shifts[] = {0, 4, 8, 1, 2, 3};
     printf("{");
     const char *sep = "";

@@ -91,24 +91,44 @@ __global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
                                        : (uint64_t)(kw + j + u) * a.slot_bytes;
                 }
                 const uint32_t m = max(nj[0], nj[1]);
+                // Sources are read from the dword-aligned offset at or below each piece (byte-
+                // aligned 16-byte loads run the vector memory path ~15-25 % slower,
+                // tools/probe/align_probe.hip) and funnelled by the payload's offset & 3 with the
+                // next lane's first dword; lane 63 loads its own next dword. Shift 0: identity.
+                uint32_t sh[2];
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u) sh[u] = (oj[u] + 42u) & 3u;
                 for (uint32_t c = 0; c < m; c += 2048u) {
                     uint4 v[2][2];
+                    uint32_t e[2][2];
 #pragma unroll
                     for (uint32_t u = 0; u < 2; ++u)
 #pragma unroll
                         for (uint32_t h2 = 0; h2 < 2; ++h2) {
                             const uint32_t b = c + 1024u * h2 + 16u * lane;
+                            const uint32_t sa = (oj[u] + 42u + b) & ~3u;
+                            // (a piece just past the payload still loads when the piece before
+                            // it needs its first dword)
                             const auto x = __builtin_amdgcn_raw_buffer_load_b128(
-                                fr, (int)(b < nj[u] ? oj[u] + 42u + b : 0u), 0, 0);
+                                fr, (int)(b < nj[u] + (sh[u] != 0u ? 16u : 0u) ? sa : 0x80000000u), 0, 0);
                             v[u][h2] = make_uint4(x[0], x[1], x[2], x[3]);
+                            e[u][h2] = __builtin_amdgcn_raw_buffer_load_b32(
+                                fr, (int)(lane == 63u && sh[u] != 0u && b < nj[u] ? sa + 16u : 0x80000000u), 0, 0);
                         }
 #pragma unroll
                     for (uint32_t u = 0; u < 2; ++u)
 #pragma unroll
                         for (uint32_t h2 = 0; h2 < 2; ++h2) {
                             const uint32_t b = c + 1024u * h2 + 16u * lane;
+                            const uint4 x = v[u][h2];
+                            const uint32_t nx = __shfl_down(x.x, 1, 64);
+                            const uint32_t hi = lane == 63u ? e[u][h2] : nx;
+                            const uint4 y = make_uint4(__builtin_amdgcn_alignbyte(x.y, x.x, sh[u]),
+                                                       __builtin_amdgcn_alignbyte(x.z, x.y, sh[u]),
+                                                       __builtin_amdgcn_alignbyte(x.w, x.z, sh[u]),
+                                                       __builtin_amdgcn_alignbyte(hi, x.w, sh[u]));
                             if (b < nj[u])
-                                *reinterpret_cast<uint4 *>(a.payload + dj[u] + b) = v[u][h2];
+                                *reinterpret_cast<uint4 *>(a.payload + dj[u] + b) = y;
                         }
                 }
             }
