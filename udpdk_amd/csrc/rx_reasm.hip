@@ -61,6 +61,8 @@ constexpr uint32_t RS_BLOCK = 256;
 constexpr uint32_t RS_WAVES = RS_BLOCK / 64;
 constexpr uint32_t RS_HELD = 0xFFFFFFFFu;       // fragment data lives in the entry buffer
 constexpr uint32_t RS_NONE = 0xFFFFFFFFu;
+// per-call device block: stats [UDPDK_RS_N], out_bytes [1], counts [8 x u32] (u64 words)
+constexpr uint32_t RS_ZERO_WORDS = UDPDK_RS_N + 1 + 4;
 constexpr uint32_t RS_MAX_FRAG = 4;             // RTE_LIBRTE_IP_FRAG_MAX_FRAG
 constexpr uint32_t RS_FLOW_CHUNK = 1024;        // sorted positions per reasm_flows block step
 
@@ -311,6 +313,8 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
         a.s_sig[p] = v;
         a.s_meta[p] = (cls ? 0u : len) | ((h.ff & 0x1FFFu) << 16) | ((h.ff & 0x2000u) << 16) | (cls << 30);
         a.dv[p] = p;
+        a.dk[p] = RS_NONE;                                           // no completion / store job yet
+        a.jobs[p] = ReasmJob{RS_NONE, RS_NONE, RS_NONE, RS_NONE};
     }
 }
 
@@ -953,7 +957,7 @@ void reasm_destroy(Reasm *r)
 {
     if (!r) return;
     void *dev[] = {r->tab, r->ebuf, r->frag_list, r->v1, r->v1s, r->v2s, r->k1, r->k1s, r->k2,
-                   r->k2s, r->counts, r->stats, r->out_bytes, r->done, r->jobs, r->dk, r->dks,
+                   r->k2s, r->stats, r->done, r->jobs, r->dk, r->dks,
                    r->dv, r->perm, r->sizes, r->offs, r->tmp, r->out, r->out_off, r->out_ptype,
                    r->out_origin, r->out_len, r->pflag, r->sb1, r->sb2, r->tf, r->tl, r->rk, r->rks,
                    r->rx, r->rv, r->rvs, r->bsum, r->cplx, r->tpos, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs, r->hset};
@@ -994,8 +998,7 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
         (e = dalloc(&r->frag_list, C)) != hipSuccess || (e = dalloc(&r->v1s, C)) != hipSuccess ||
         (e = dalloc(&r->v2s, C)) != hipSuccess || (e = dalloc(&r->k1, C)) != hipSuccess ||
         (e = dalloc(&r->k1s, C)) != hipSuccess || (e = dalloc(&r->k2, C)) != hipSuccess ||
-        (e = dalloc(&r->k2s, C)) != hipSuccess || (e = dalloc(&r->counts, 8)) != hipSuccess ||
-        (e = dalloc(&r->stats, UDPDK_RS_N)) != hipSuccess || (e = dalloc(&r->out_bytes, 1)) != hipSuccess ||
+        (e = dalloc(&r->k2s, C)) != hipSuccess || (e = dalloc(&r->stats, RS_ZERO_WORDS)) != hipSuccess ||
         (e = dalloc(&r->done, C)) != hipSuccess || (e = dalloc(&r->jobs, C)) != hipSuccess ||
         (e = dalloc(&r->dk, C)) != hipSuccess || (e = dalloc(&r->dks, C)) != hipSuccess ||
         (e = dalloc(&r->dv, C)) != hipSuccess || (e = dalloc(&r->perm, C)) != hipSuccess ||
@@ -1016,6 +1019,9 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
         reasm_destroy(r);
         return rc;
     }
+    // stats, out_bytes and counts share one block, zeroed by one memset per call
+    r->out_bytes = r->stats + UDPDK_RS_N;
+    r->counts = reinterpret_cast<uint32_t *>(r->stats + UDPDK_RS_N + 1);
     // rocPRIM temporary storage for the largest call (sorts of u64 keys / u32 values, u32 scan,
     // u64 max scan)
     size_t t[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -1098,9 +1104,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     if (++r->calls == 0) r->calls = 1;          // 0 marks entries never touched
     a.call = r->calls;
     a.ib = bits_for(n - 1u);
-    RS_HIP(hipMemsetAsync(r->counts, 0, 8 * sizeof(uint32_t), st));
-    RS_HIP(hipMemsetAsync(r->stats, 0, UDPDK_RS_N * sizeof(unsigned long long), st));
-    RS_HIP(hipMemsetAsync(r->out_bytes, 0, sizeof(unsigned long long), st));
+    RS_HIP(hipMemsetAsync(r->stats, 0, RS_ZERO_WORDS * sizeof(unsigned long long), st));
     uint32_t hsize = 1024;                   // the run-key set: >= 2 x fragments, power of 2
     while (hsize < 2u * n && hsize < r->hcap) hsize <<= 1;
     // the fragment list in arrival order (F to counts[0]), then its sort keys and the run test
@@ -1121,6 +1125,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     const bool grouped = r->host[4] == 0u;
     a.grouped = grouped ? 1u : 0u;
     uint32_t K = 0;                          // fragments on the serial path
+    bool read_back = true;                   // the stats block still to be read back
     memset(o, 0, sizeof(*o));
     if (F) {
         const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((F + RS_BLOCK - 1) / RS_BLOCK, 4096));
@@ -1145,8 +1150,6 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         a.s_meta = a.s_sig + F;
         hipLaunchKernelGGL(reasm_prep, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
         RS_HIP(hipGetLastError());
-        RS_HIP(hipMemsetAsync(r->dk, 0xFF, (size_t)F * sizeof(uint32_t), st));
-        RS_HIP(hipMemsetAsync(r->jobs, 0xFF, (size_t)F * sizeof(ReasmJob), st));
         // flow analysis: which flows can run without the table (see the top of this file)
         const uint32_t gb = std::max<uint32_t>(1, std::min<uint32_t>((r->entries + RS_BLOCK - 1) / RS_BLOCK, 4096));
         hipLaunchKernelGGL(reasm_bsum, dim3(gb), dim3(RS_BLOCK), 0, st, a);
@@ -1180,9 +1183,12 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         RS_HIP(hipGetLastError());
         hipLaunchKernelGGL(reasm_process, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
         RS_HIP(hipGetLastError());
-        RS_HIP(hipMemcpyAsync(r->host, r->counts, 16, hipMemcpyDeviceToHost, st));
+        // the serial list's size comes back with the stats (one round trip; a second one only
+        // when the serial path runs and adds to them)
+        RS_HIP(hipMemcpyAsync(r->host, r->stats, RS_ZERO_WORDS * 8, hipMemcpyDeviceToHost, st));
         RS_HIP(hipStreamSynchronize(st));
-        K = r->host[2];
+        K = reinterpret_cast<const uint32_t *>(r->host + 2 * (UDPDK_RS_N + 1))[2];
+        read_back = K != 0;
         if (K) {
             tb = r->tmp_bytes;
             RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs, (size_t)K, 0,
@@ -1191,12 +1197,13 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
             RS_HIP(hipGetLastError());
         }
     }
-    RS_HIP(hipMemcpyAsync(r->host + 4, r->out_bytes, 8, hipMemcpyDeviceToHost, st));
-    RS_HIP(hipMemcpyAsync(r->host + 8, r->stats, UDPDK_RS_N * 8, hipMemcpyDeviceToHost, st));
-    RS_HIP(hipStreamSynchronize(st));
+    if (read_back) {
+        RS_HIP(hipMemcpyAsync(r->host, r->stats, RS_ZERO_WORDS * 8, hipMemcpyDeviceToHost, st));
+        RS_HIP(hipStreamSynchronize(st));
+    }
     uint64_t ob;
-    memcpy(&ob, r->host + 4, 8);
-    memcpy(o->stats, r->host + 8, UDPDK_RS_N * 8);
+    memcpy(&ob, r->host + 2 * UDPDK_RS_N, 8);
+    memcpy(o->stats, r->host, UDPDK_RS_N * 8);
     o->stats[UDPDK_RS_FRAGS] = F;
     o->stats[UDPDK_RS_SERIAL] = K;
     o->stats[UDPDK_RS_SORTED] = F && !grouped ? 1u : 0u;
