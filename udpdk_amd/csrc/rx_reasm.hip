@@ -156,6 +156,18 @@ __device__ __forceinline__ uint32_t ld32(__amdgpu_buffer_rsrc_t r, uint32_t off)
     return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
 }
 
+__device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v)
+{
+    __attribute__((ext_vector_type(4))) uint32_t x = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, 0);
+}
+
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
 __device__ __forceinline__ uint32_t crc32c_u32(uint32_t crc, uint32_t v)
@@ -824,7 +836,9 @@ struct EmitArgs {
 
 __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
 {
-    const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+    // the wave index as a scalar: the datagram record and everything derived from it are
+    // wave-uniform scalar loads and SGPRs, not per-lane copies
+    const uint32_t lane = __lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
     for (uint32_t k = blockIdx.x * RS_WAVES + w; k < a.C; k += gridDim.x * RS_WAVES) {
         const ReasmDone r = a.done[a.perm[k]];
@@ -863,11 +877,40 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
         if (lane == 6) hw |= ck;
         if (lane < 8) reinterpret_cast<uint32_t *>(o)[lane] = hw;      // o is 16-byte aligned
         if (lane == 8) { o[32] = (uint8_t)hw; o[33] = (uint8_t)(hw >> 8); }
-        for (uint32_t q = 0; q < r.n && q < RS_MAX_FRAG; ++q) {
-            if (!r.fr[q]) continue;
-            const uint32_t ofs = r.fr[q] & 0xFFFFu, len = r.fr[q] >> 16;
-            if (r.where[q] == RS_HELD) wave_copy16(o + 34 + ofs, er, 34u + ofs, len);
-            else wave_copy16(o + 34 + ofs, fr, a.offset[r.where[q]] + 34u, len);
+        // Payload: each fragment as 16-byte pieces, lane j taking fragment bytes [16 j, 16 j + 16)
+        // and the last piece moved back to end at the fragment's end (it overlaps the piece
+        // before it, whose bytes it rewrites with the same values), so a fragment of >= 16 bytes
+        // needs no byte stores; every fragment's loads of a round are issued before its stores.
+        // (Per fragment, head and tail byte stores around 16-byte body stores took twice the
+        // memory instructions.) Stores are byte-aligned 16-byte buffer stores into the datagram.
+        const __amdgpu_buffer_rsrc_t orr = rsrc(o, 34u + r.total);
+        uint32_t sb[RS_MAX_FRAG], ln[RS_MAX_FRAG], np[RS_MAX_FRAG], rounds = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < RS_MAX_FRAG; ++q) {
+            const bool use = q < r.n && r.fr[q] != 0u;
+            ln[q] = use ? r.fr[q] >> 16 : 0u;
+            sb[q] = r.where[q] == RS_HELD ? 34u + (r.fr[q] & 0xFFFFu) : use ? a.offset[r.where[q]] + 34u : 0u;
+            np[q] = ln[q] >= 16u ? (ln[q] + 15u) >> 4 : 0u;
+            rounds = max(rounds, (np[q] + 63u) >> 6);
+        }
+        for (uint32_t c0 = 0; c0 < rounds; ++c0) {
+            uint4 v[RS_MAX_FRAG];
+            const uint32_t j = 64u * c0 + lane;
+#pragma unroll
+            for (uint32_t q = 0; q < RS_MAX_FRAG; ++q) {
+                const __amdgpu_buffer_rsrc_t sr = r.where[q] == RS_HELD ? er : fr;
+                v[q] = load16(sr, j < np[q] ? sb[q] + min(16u * j, ln[q] - 16u) : 0x80000000u);
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < RS_MAX_FRAG; ++q)
+                if (j < np[q]) store16(orr, 34u + (r.fr[q] & 0xFFFFu) + min(16u * j, ln[q] - 16u), v[q]);
+        }
+        // fragments shorter than 16 bytes, byte by byte
+#pragma unroll
+        for (uint32_t q = 0; q < RS_MAX_FRAG; ++q) {
+            if (ln[q] == 0u || ln[q] >= 16u) continue;
+            const __amdgpu_buffer_rsrc_t sr = r.where[q] == RS_HELD ? er : fr;
+            if (lane < ln[q]) o[34u + (r.fr[q] & 0xFFFFu) + lane] = (uint8_t)ld32(sr, sb[q] + lane);
         }
         if (lane == 0) {
             a.out_off[k] = oo;
