@@ -53,6 +53,7 @@ struct Pipe {
     DevResult *res = nullptr;                 // counters, total (device)
     DevResult *h_res = nullptr;               // pinned mirror, filled by udpdk_gpu_rx_stats
     hipEvent_t tail = nullptr;                // join point for udpdk_gpu_join
+    bool dirty = false;                       // work enqueued since the last join
     uint32_t last_tiles = 0;                  // tiles of this pipe's last call (counter rows)
     uint32_t last_lane_cap = 0;
     // host-resident batches (udpdk_gpu_rx_host[_async]): staging, lazily sized
@@ -186,9 +187,12 @@ int join_pipes(udpdk_gpu_ctx *c)
 {
     for (int i = 1; i < MAX_PIPES; ++i) {
         Pipe &P = c->pipes[i];
-        if (!P.stream) continue;
+        // an event record + stream wait costs host and GPU time even on an idle stream: only
+        // pipes with work since their last join
+        if (!P.stream || !P.dirty) continue;
         HIPC(c, hipEventRecord(P.tail, P.stream));
         HIPC(c, hipStreamWaitEvent(c->stream, P.tail, 0));
+        P.dirty = false;
     }
     return 0;
 }
@@ -528,6 +532,7 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     HIPC(c, hipSetDevice(c->device));
     Pipe &P = c->pipes[pipe];
     const hipStream_t st = P.stream;
+    P.dirty = true;
     c->last_pipe = pipe;
     const uint32_t S = c->n_lanes;
     TimingSet *ts = nullptr;
@@ -695,6 +700,7 @@ namespace {
 // into its pinned mirror, on the pipe's stream.
 int enqueue_result(udpdk_gpu_ctx *c, Pipe &P)
 {
+    P.dirty = true;
     if (P.last_tiles) {
         hipLaunchKernelGGL(rx_counters, dim3(1), dim3(256), 0, P.stream, (const uint32_t *)P.tile_cnt,
                            P.last_tiles, P.res->counters);
@@ -737,6 +743,7 @@ int enqueue_host(udpdk_gpu_ctx *c, int pipe, const uint8_t *frames_host, uint64_
     if (frames_bytes >= (1ull << 32)) return -EINVAL;
     Pipe &P = c->pipes[pipe];
     const hipStream_t s = P.stream;
+    P.dirty = true;
     // frames + the tailroom the kernels may read past them (UDPDK_GPU_FRAMES_TAILROOM)
     const size_t fb = (((size_t)frames_bytes + 255) & ~(size_t)255) + UDPDK_GPU_FRAMES_TAILROOM;
     const size_t desc = (size_t)n * 10 + 64;
