@@ -76,6 +76,17 @@ def test_rss_full_size_config5(gpu_ctx, nq):
     assert go[-1] == w.batch.n
 
 
+@pytest.mark.parametrize("nq,n", [(8, None), (7, None), (3, 700001)])
+def test_rss_config4(gpu_ctx, nq, n):
+    """1 M IMIX frames over 1024 ports (uniform destination ports, so every queue gets frames):
+    the one-workgroup base scan over 1024 tiles x 8 queues; 7 queues and a ragged 700001-frame
+    batch put queue rows across its threads' 32-entry boundaries."""
+    w = F.config_batch(4, n=n)
+    (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, w.batch, abi.rss_conf(nq))
+    assert np.array_equal(wh, gh) and np.array_equal(wo, go) and np.array_equal(wp, gp)
+    assert go[-1] == w.batch.n and np.all(np.diff(go.astype(np.int64)) > 0)
+
+
 def test_rss_edges(gpu_ctx):
     """Empty batch, bad configurations, a single frame; the RSS call needs a configuration."""
     import ctypes as C
