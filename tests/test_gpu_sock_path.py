@@ -25,12 +25,15 @@ SRC_MAC, DST_MAC, SRC_IP = "68:05:ca:95:f8:ec", "68:05:ca:95:fa:64", "172.31.100
 
 
 @pytest.fixture()
-def api(tmp_path, host_api):
+def api(tmp_path, host_api, request):
+    """udpdk_init over a test ini; indirect parametrization sets [gpu] poll_threads."""
+    threads = getattr(request, "param", None)
     ini = tmp_path / "udpdk.ini"
     ini.write_text(f"[port0]\nmac_addr = {SRC_MAC}\nip_addr = {SRC_IP}\n"
                    f"[port0_dst]\nmac_addr = {DST_MAC}\n"
                    "[gpu]\ndevice = 0\nmax_frames = 65536\nmax_lanes = 64\n"
-                   "frag_buckets = 64\nfrag_bucket_entries = 16\nfrag_max_dgram = 16384\n")
+                   "frag_buckets = 64\nfrag_bucket_entries = 16\nfrag_max_dgram = 16384\n"
+                   + (f"poll_threads = {threads}\n" if threads else ""))
     L = abi.lib()
     argv = (C.c_char_p * 4)(b"prog", b"-c", str(ini).encode(), None)
     assert L.udpdk_init(3, argv) == 0
@@ -159,6 +162,48 @@ def _poll(b):
     return st
 
 
+def _admitted(idx, room):
+    """flush_rx_queue's model: per burst of 128 frame indices, all-or-nothing into the ring."""
+    acc = []
+    for burst in range(0, (max(idx) if idx else 0) + 128, 128):
+        grp = [i for i in idx if burst <= i < burst + 128]
+        if grp and len(grp) <= room:
+            acc += grp
+            room -= len(grp)
+    return acc
+
+
+@pytest.mark.parametrize("api", [1, 3, 8], indirect=True)
+def test_rx_many_sockets_over_poll_threads(api):
+    """40 sockets, Zipf-skewed destination ports, some rings partly full before the poll: the
+    admission and ring publication split the sockets over 1, 3 or 8 threads (sockets straddle
+    the parts' boundaries) and every socket still gets exactly its admitted bursts, in order."""
+    ns = 40
+    socks = [api.socket() for _ in range(ns)]
+    for k, s in enumerate(socks):
+        assert api.bind(s, "0.0.0.0", 11000 + k) == 0
+    pre = {0: 1500, 3: 2000, 7: 300}
+    for k, m in pre.items():
+        _poll(_rx_batch([11000 + k] * m, seed=10 + k))
+    rng = np.random.default_rng(21)
+    ports = 11000 + np.minimum(rng.zipf(1.3, 30000) - 1, ns - 1)
+    b = _rx_batch(ports, size=int(rng.integers(60, 300)), seed=3)
+    _poll(b)
+    L = abi.lib()
+    for k, s in enumerate(socks):
+        idx = [int(i) for i in np.nonzero(ports == 11000 + k)[0]]
+        want = _admitted(idx, 2047 - pre.get(k, 0))
+        for _ in range(pre.get(k, 0)):
+            assert api.recvfrom(s, 4096)[0] > 0
+        for i in want:
+            n, data, _ = api.recvfrom(s, 4096)
+            o, ln = int(b.offset[i]), int(b.length[i])
+            assert data == bytes(b.frames[o + 42:o + ln]), (k, i)
+    L.udpdk_interrupt(0)
+    assert all(api.recvfrom(s, 64)[0] == -1 for s in socks)
+
+
+@pytest.mark.parametrize("api", [None, 3], indirect=True)
 def test_rx_burst_admission_and_payloads(api):
     """A socket gets more deliveries in one poll than its ring holds, with the ring partly full:
     each burst of 128 frames is admitted whole or dropped whole (poller.c:287-290); payloads and

@@ -23,6 +23,8 @@
 #define H_SO_REUSEPORT 15
 
 #define H_BURST_SIZE     128     /* BURST_SIZE, udpdk_constants.h:41 */
+#define H_MAX_WORKERS    31      /* poll worker threads beyond the caller's ([gpu] poll_threads) */
+#define H_POLL_THREADS_DEFAULT 8
 #define H_UDP_MAX_PAYLOAD 65507  /* 65535 - 20 - 8: the largest datagram fragmentation can carry */
 
 /* A pinned host slab of gathered payloads: one per rx_gather of a poll. Ring entries point into
@@ -102,6 +104,7 @@ struct h_state {
     int      frag_ready;
     uint32_t frag_buckets, frag_entries, frag_max_dgram;
     uint64_t frag_ttl_ms;
+    uint32_t poll_threads;       /* [gpu] poll_threads: threads of udpdk_poll_rx's socket loops  */
     /* RX work buffers (poller thread only), grow-only */
     uint32_t *rx_meta, *rx_loff, *rx_lpkt;
     uint64_t  rx_meta_cap, rx_loff_cap, rx_lpkt_cap;
@@ -150,6 +153,13 @@ void h_arena_put(struct h_arena *a);
 void h_arena_release(struct h_arena *a, uint32_t refs);
 void h_arenas_free_all(void);
 void h_tx_reset(void);
+
+/* h_pool.c: fork-join workers; h_pool_run calls fn(ctx, part, parts) for every part < parts
+ * (part 0 on the caller) and returns when all have returned */
+typedef void (*h_job_fn)(void *ctx, uint32_t part, uint32_t parts);
+uint32_t h_pool_parts(void);
+void h_pool_run(h_job_fn fn, void *ctx);
+void h_pool_stop(void);
 
 /* rx_poll.c */
 int  h_snapshot_refresh(void);            /* under g_udpdk.lock */

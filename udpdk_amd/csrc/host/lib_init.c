@@ -104,6 +104,8 @@ static int h_load_ini(const char *path)
             g_udpdk.gpu_max_frames = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "max_lanes")) {
             g_udpdk.gpu_max_lanes = (uint32_t)strtoul(v, NULL, 0);
+        } else if (!strcmp(section, "gpu") && !strcmp(k, "poll_threads")) {
+            g_udpdk.poll_threads = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "frag_buckets")) {
             g_udpdk.frag_buckets = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "frag_bucket_entries")) {
@@ -145,6 +147,7 @@ void udpdk_cleanup(void)
 {
     udpdk_port_detach();
     udpdk_poll_profile_dump();
+    h_pool_stop();
     for (int s = 0; s < UDPDK_MAX_SOCKETS; s++)
         if (g_udpdk.slots[s].used) udpdk_close(s);
     h_tx_reset();

@@ -212,6 +212,160 @@ static int h_gather(const udpdk_rx_batch_t *b, const uint32_t *acc, const uint32
     return 0;
 }
 
+/* Per-socket admission (two passes over the same sockets, split over the pool's parts): pass 1
+ * records the ring room each socket had and what it admits (entries and slab bytes, direct and
+ * reassembled); pass 2, after a prefix over the sockets, writes the accepted lists at those
+ * bases. Both passes make the same decisions: they read the room once, in pass 1. */
+static uint32_t s_room[UDPDK_MAX_SOCKETS], s_nd[UDPDK_MAX_SOCKETS], s_nf[UDPDK_MAX_SOCKETS];
+static uint64_t s_bd[UDPDK_MAX_SOCKETS], s_bf[UDPDK_MAX_SOCKETS];
+static uint32_t s_kd[UDPDK_MAX_SOCKETS], s_kf[UDPDK_MAX_SOCKETS];
+static uint64_t s_od[UDPDK_MAX_SOCKETS], s_of[UDPDK_MAX_SOCKETS];
+
+struct h_adm {
+    const uint32_t *loff, *lpkt, *floff, *flpkt, *forg;
+    const uint16_t *length;
+    uint32_t lanes;
+    int fill;
+    uint32_t sb[H_MAX_WORKERS + 3];   /* part p takes sockets [sb[p], sb[p + 1]) */
+};
+
+/* socket ranges of about equal delivery counts */
+static void h_adm_split(struct h_adm *A, uint32_t parts)
+{
+    const uint32_t L = A->lanes, D = A->loff[L] + (A->floff ? A->floff[L] : 0u);
+    uint32_t s = 0;
+    A->sb[0] = 0;
+    for (uint32_t p = 1; p < parts; p++) {
+        const uint64_t want = (uint64_t)D * p / parts;
+        while (s < L && (uint64_t)A->loff[s] + (A->floff ? A->floff[s] : 0u) < want) s++;
+        A->sb[p] = s;
+    }
+    A->sb[parts] = L;
+}
+
+static void h_adm_socket(const struct h_adm *A, uint32_t s)
+{
+    const uint32_t *lpkt = A->lpkt, *flpkt = A->flpkt, *forg = A->forg;
+    const uint32_t a0 = A->loff[s], a1 = A->loff[s + 1];
+    const uint32_t b0 = A->floff ? A->floff[s] : 0u, b1 = A->floff ? A->floff[s + 1] : 0u;
+    if (!A->fill) {
+        s_nd[s] = s_nf[s] = 0;
+        s_bd[s] = s_bf[s] = 0;
+        if ((a0 == a1 && b0 == b1) || !g_udpdk.slots[s].used) return;   /* closed: dropped */
+        s_room[s] = h_ring_free(&g_udpdk.slots[s].rx);
+    } else if (!s_nd[s] && !s_nf[s]) {
+        return;
+    }
+    uint32_t room = s_room[s], nd = 0, nf = 0;
+    uint64_t bd = 0, bf = 0;
+    uint32_t kd = s_kd[s], kf = s_kf[s], ka = s_kd[s] + s_kf[s];
+    uint64_t od = s_od[s], of = s_of[s];
+    uint32_t e = a0, q = b0;
+    while (e < a1 || q < b1) {
+        /* the burst of the next delivery in arrival order, and its deliveries */
+        const uint32_t ie = e < a1 ? lpkt[e] : UINT32_MAX, iq = q < b1 ? forg[flpkt[q]] : UINT32_MAX;
+        const uint32_t burst = (ie < iq ? ie : iq) / H_BURST_SIZE;
+        uint32_t ce = e, cq = q;
+        while (ce < a1 && lpkt[ce] / H_BURST_SIZE == burst) ce++;
+        while (cq < b1 && forg[flpkt[cq]] / H_BURST_SIZE == burst) cq++;
+        const uint32_t k = (ce - e) + (cq - q);
+        if (k > room) {                            /* ring full: the burst is dropped */
+            e = ce;
+            q = cq;
+            continue;
+        }
+        room -= k;
+        while (e < ce || q < cq) {
+            if (q >= cq || (e < ce && lpkt[e] < forg[flpkt[q]])) {
+                const uint32_t fi = lpkt[e++];
+                const uint32_t pl = A->length[fi] > 42u ? A->length[fi] - 42u : 0u;
+                const uint32_t sz = (pl + 15u) & ~15u;
+                if (A->fill) {
+                    g_udpdk.acc_do[kd] = (uint32_t)od;
+                    g_udpdk.acc_d[kd++] = fi;
+                    g_udpdk.acc_sock[ka++] = s;
+                    od += sz;
+                } else {
+                    nd++;
+                    bd += sz;
+                }
+            } else {
+                const uint32_t di = flpkt[q++];
+                const uint32_t pl = g_udpdk.fr_len[di] > 42u ? g_udpdk.fr_len[di] - 42u : 0u;
+                const uint32_t sz = (pl + 15u) & ~15u;
+                if (A->fill) {
+                    g_udpdk.acc_fo[kf] = (uint32_t)of;
+                    g_udpdk.acc_f[kf++] = di;
+                    g_udpdk.acc_sock[ka++] = s | 0x80000000u;
+                    of += sz;
+                } else {
+                    nf++;
+                    bf += sz;
+                }
+            }
+        }
+    }
+    if (!A->fill) {
+        s_nd[s] = nd;
+        s_nf[s] = nf;
+        s_bd[s] = bd;
+        s_bf[s] = bf;
+    }
+}
+
+static void h_adm_job(void *ctx, uint32_t part, uint32_t parts)
+{
+    const struct h_adm *A = ctx;
+    (void)parts;
+    for (uint32_t s = A->sb[part]; s < A->sb[part + 1]; s++) h_adm_socket(A, s);
+}
+
+/* Ring publication of the admitted entries: socket s's are acc_sock[s_kd + s_kf ...] in arrival
+ * order, its direct and reassembled ones consumed from acc_d / acc_f at s_kd[s] / s_kf[s]. */
+struct h_pub {
+    const struct h_adm *A;
+    struct h_arena *ad, *af;
+};
+
+static void h_pub_job(void *ctx, uint32_t part, uint32_t parts)
+{
+    const struct h_pub *P = ctx;
+    (void)parts;
+    struct h_dgram buf[H_BURST_SIZE];
+    for (uint32_t s = P->A->sb[part]; s < P->A->sb[part + 1]; s++) {
+        const uint32_t n = s_nd[s] + s_nf[s];
+        uint32_t kd = s_kd[s], kf = s_kf[s], k = s_kd[s] + s_kf[s];
+        const uint32_t kend = k + n;
+        while (k < kend) {
+            uint32_t nb = 0;
+            while (k < kend && nb < H_BURST_SIZE) {
+                struct h_dgram *d = &buf[nb++];
+                if (g_udpdk.acc_sock[k] >> 31) {
+                    struct h_arena *af = P->af;
+                    d->arena = af;
+                    d->data = af->payload + g_udpdk.acc_fo[kf];
+                    d->len = af->len[kf];
+                    d->src_ip = af->src_ip[kf];
+                    d->src_port = af->src_port[kf];
+                    kf++;
+                } else {
+                    struct h_arena *ad = P->ad;
+                    d->arena = ad;
+                    d->data = ad->payload + g_udpdk.acc_do[kd];
+                    d->len = ad->len[kd];
+                    d->src_ip = ad->src_ip[kd];
+                    d->src_port = ad->src_port[kd];
+                    kd++;
+                }
+                k++;
+            }
+            if (h_ring_push_bulk(&g_udpdk.slots[s].rx, buf, nb)) {   /* admitted: cannot fail */
+                for (uint32_t z = 0; z < nb; z++) h_arena_release(buf[z].arena, 1);
+            }
+        }
+    }
+}
+
 int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *offset,
                   const uint16_t *length, const uint32_t *ptype, uint32_t n,
                   udpdk_rx_stats_t *stats_out)
@@ -246,7 +400,8 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
     PROF_T(p3);
     const uint32_t *floff = nd ? g_udpdk.fr_loff : NULL, *flpkt = g_udpdk.fr_lpkt, *forg = g_udpdk.fr_org;
 
-    /* admission: per socket, arrival-ordered merge, one all-or-nothing decision per burst */
+    /* admission: per socket, arrival-ordered merge, one all-or-nothing decision per burst; the
+     * sockets split over the pool's parts, counted first, then filled at their prefix bases */
     const uint32_t D = loff[lanes], DF = nd ? floff[lanes] : 0u;
     if (h_grow_host((void **)&g_udpdk.acc_d, &g_udpdk.acc_d_cap, 4ull * D + 4) ||
         h_grow_host((void **)&g_udpdk.acc_f, &g_udpdk.acc_f_cap, 4ull * DF + 4) ||
@@ -254,51 +409,26 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
         h_grow_host((void **)&g_udpdk.acc_fo, &g_udpdk.acc_fo_cap, 4ull * DF + 8) ||
         h_grow_host((void **)&g_udpdk.acc_sock, &g_udpdk.acc_sock_cap, 4ull * (D + DF) + 4))
         goto out;
-    uint32_t nad = 0, naf = 0, nacc = 0;
+    struct h_adm A = {loff, lpkt, floff, flpkt, forg, length, lanes < UDPDK_MAX_SOCKETS ? lanes : UDPDK_MAX_SOCKETS, 0, {0}};
+    h_adm_split(&A, h_pool_parts());
+    h_pool_run(h_adm_job, &A);                       /* pass 1: what each socket admits */
+    uint32_t nad = 0, naf = 0;
     uint64_t offd = 0, offf = 0;                    /* packed slot offsets (payload room / 16) */
-    for (uint32_t s = 0; s < lanes && s < UDPDK_MAX_SOCKETS; s++) {
-        const uint32_t a0 = loff[s], a1 = loff[s + 1];
-        const uint32_t b0 = nd ? floff[s] : 0u, b1 = nd ? floff[s + 1] : 0u;
-        if (a0 == a1 && b0 == b1) continue;
-        if (!g_udpdk.slots[s].used) continue;          /* closed since the snapshot: dropped */
-        uint32_t room = h_ring_free(&g_udpdk.slots[s].rx);
-        uint32_t e = a0, q = b0;
-        while (e < a1 || q < b1) {
-            /* the burst of the next delivery in arrival order, and its deliveries */
-            const uint32_t ie = e < a1 ? lpkt[e] : UINT32_MAX, iq = q < b1 ? forg[flpkt[q]] : UINT32_MAX;
-            const uint32_t burst = (ie < iq ? ie : iq) / H_BURST_SIZE;
-            uint32_t ce = e, cq = q;
-            while (ce < a1 && lpkt[ce] / H_BURST_SIZE == burst) ce++;
-            while (cq < b1 && forg[flpkt[cq]] / H_BURST_SIZE == burst) cq++;
-            const uint32_t k = (ce - e) + (cq - q);
-            if (k <= room) {
-                room -= k;
-                while (e < ce || q < cq) {
-                    if (q >= cq || (e < ce && lpkt[e] < forg[flpkt[q]])) {
-                        const uint32_t fi = lpkt[e++];
-                        const uint32_t pl = length[fi] > 42u ? length[fi] - 42u : 0u;
-                        g_udpdk.acc_do[nad] = (uint32_t)offd;
-                        offd += (pl + 15u) & ~15u;
-                        g_udpdk.acc_d[nad++] = fi;
-                        g_udpdk.acc_sock[nacc++] = s;
-                    } else {
-                        const uint32_t di = flpkt[q++];
-                        const uint32_t pl = g_udpdk.fr_len[di] > 42u ? g_udpdk.fr_len[di] - 42u : 0u;
-                        g_udpdk.acc_fo[naf] = (uint32_t)offf;
-                        offf += (pl + 15u) & ~15u;
-                        g_udpdk.acc_f[naf++] = di;
-                        g_udpdk.acc_sock[nacc++] = s | 0x80000000u;
-                    }
-                }
-            } else {
-                e = ce;                                /* ring full: the burst is dropped */
-                q = cq;
-            }
-        }
+    for (uint32_t s = 0; s < A.lanes; s++) {
+        s_kd[s] = nad;
+        s_kf[s] = naf;
+        s_od[s] = offd;
+        s_of[s] = offf;
+        nad += s_nd[s];
+        naf += s_nf[s];
+        offd += s_bd[s];
+        offf += s_bf[s];
     }
+    if (offd > 0xFFFFFFF0ull || offf > 0xFFFFFFF0ull) { errno = ENOBUFS; goto out; }
+    A.fill = 1;
+    h_pool_run(h_adm_job, &A);                       /* pass 2: the accepted lists */
     /* payloads of the admitted datagrams, gathered on the GPU into pinned slabs */
     PROF_T(p4);
-    if (offd > 0xFFFFFFF0ull || offf > 0xFFFFFFF0ull) { errno = ENOBUFS; goto out; }
     g_udpdk.acc_do[nad] = (uint32_t)offd;
     g_udpdk.acc_fo[naf] = (uint32_t)offf;
     if (h_gather(&staged, g_udpdk.acc_d, g_udpdk.acc_do, nad, &ad)) goto out;
@@ -308,36 +438,10 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
     PROF_T(p6);
     if (ad) atomic_store_explicit(&ad->refs, nad, memory_order_relaxed);
     if (af) atomic_store_explicit(&af->refs, naf, memory_order_relaxed);
-    /* publish: consecutive entries of one socket go to its ring in one bulk enqueue */
+    /* publish: each socket's entries go to its ring in bulk enqueues, sockets over the pool */
     {
-        struct h_dgram buf[H_BURST_SIZE];
-        uint32_t kd = 0, kf = 0, k = 0;
-        while (k < nacc) {
-            const uint32_t s = g_udpdk.acc_sock[k] & 0x7FFFFFFFu;
-            uint32_t nb = 0;
-            while (k < nacc && (g_udpdk.acc_sock[k] & 0x7FFFFFFFu) == s && nb < H_BURST_SIZE) {
-                struct h_dgram *d = &buf[nb++];
-                if (g_udpdk.acc_sock[k] >> 31) {
-                    d->arena = af;
-                    d->data = af->payload + g_udpdk.acc_fo[kf];
-                    d->len = af->len[kf];
-                    d->src_ip = af->src_ip[kf];
-                    d->src_port = af->src_port[kf];
-                    kf++;
-                } else {
-                    d->arena = ad;
-                    d->data = ad->payload + g_udpdk.acc_do[kd];
-                    d->len = ad->len[kd];
-                    d->src_ip = ad->src_ip[kd];
-                    d->src_port = ad->src_port[kd];
-                    kd++;
-                }
-                k++;
-            }
-            if (h_ring_push_bulk(&g_udpdk.slots[s].rx, buf, nb)) {   /* admitted: cannot fail */
-                for (uint32_t z = 0; z < nb; z++) h_arena_release(buf[z].arena, 1);
-            }
-        }
+        struct h_pub P = {&A, ad, af};
+        h_pool_run(h_pub_job, &P);
     }
     ad = af = NULL;
     if (stats_out) *stats_out = st;
