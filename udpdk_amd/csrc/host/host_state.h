@@ -52,6 +52,10 @@ struct h_ring {                  /* SP/SC ring of EXCH_RING_SIZE entries (udpdk_
     struct h_dgram *e;
     _Atomic uint32_t head;       /* consumer (recvfrom) */
     _Atomic uint32_t tail;       /* producer (the poller); tail - head = entries */
+    /* consumer only: entries of one slab consumed and not yet released to it (one atomic release
+     * per run of a slab's entries instead of one per recvfrom) */
+    struct h_arena *rel_arena;
+    uint32_t rel_n;
 };
 
 struct h_txd {                   /* one sendto waiting for the poller's TX half                  */

@@ -28,6 +28,9 @@ static int h_valid_fd(int s) { return s >= 0 && s < UDPDK_MAX_SOCKETS; }
 /* ---- RX rings: single producer (the poller), single consumer (recvfrom) ------------------- */
 static void h_ring_clear(struct h_ring *r)
 {
+    h_arena_release(r->rel_arena, r->rel_n);
+    r->rel_arena = NULL;
+    r->rel_n = 0;
     if (r->e) {
         const uint32_t t = atomic_load_explicit(&r->tail, memory_order_acquire);
         for (uint32_t i = atomic_load_explicit(&r->head, memory_order_relaxed); i != t; i++)
@@ -378,8 +381,23 @@ ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
     }
     const size_t n = d.len < len ? d.len : len;
     if (n) memcpy(buf, d.data, n);
+    /* the slab reference goes back once per run of one slab's entries: when the next entry is
+     * another slab's or the ring is drained (a consumed entry never holds its slab longer than an
+     * unconsumed one would) */
+    if (d.arena != r->rel_arena) {
+        h_arena_release(r->rel_arena, r->rel_n);
+        r->rel_arena = d.arena;
+        r->rel_n = 0;
+    }
+    r->rel_n++;
+    const uint32_t t = atomic_load_explicit(&r->tail, memory_order_acquire);
+    const bool run_ends = t == h + 1 || r->e[(h + 1) % UDPDK_RX_RING_SIZE].arena != d.arena;
     atomic_store_explicit(&r->head, h + 1, memory_order_release);
-    h_arena_release(d.arena, 1);
+    if (run_ends) {
+        h_arena_release(r->rel_arena, r->rel_n);
+        r->rel_arena = NULL;
+        r->rel_n = 0;
+    }
     return (ssize_t)n;
 }
 
