@@ -119,6 +119,52 @@ __global__ void __launch_bounds__(256) k_copy(const uint8_t *src, uint8_t *dst, 
     }
 }
 
+// copy in tasks of `task` bytes (a wave per task, grid-stride over tasks, loads of a task issued
+// before its stores), the shape of reasm_emit's per-datagram copies
+__global__ void __launch_bounds__(256) k_copy_tasks(const uint8_t *src, uint8_t *dst, uint32_t bytes,
+                                                    uint32_t task, uint32_t ntask)
+{
+    const __amdgpu_buffer_rsrc_t r = rsrc(src, bytes), w = rsrc(dst, bytes);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t t = wv; t < ntask; t += nw) {
+        const uint32_t base = t * task;
+        uint4 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t o = 1024 * c + 16 * lane;
+            v[c] = ld128(r, o < task ? base + o + 2 : 0x80000000u);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t o = 1024 * c + 16 * lane;
+            __attribute__((ext_vector_type(4))) uint32_t x = {v[c].x, v[c].y, v[c].z, v[c].w};
+            if (o < task) __builtin_amdgcn_raw_buffer_store_b128(x, w, (int)(base + o + 2), 0, 0);
+        }
+    }
+}
+
+static float run_copy_tasks(const uint8_t *src, uint8_t *dst, uint32_t task, uint32_t ntask,
+                            uint32_t blocks, int reps)
+{
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    const uint32_t bytes = task * ntask + 64;
+    hipLaunchKernelGGL(k_copy_tasks, dim3(blocks), dim3(256), 0, 0, src, dst, bytes, task, ntask);
+    CHECK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL(k_copy_tasks, dim3(blocks), dim3(256), 0, 0, src, dst, bytes, task, ntask);
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    CHECK(hipEventDestroy(e0));
+    CHECK(hipEventDestroy(e1));
+    return (float)(2.0 * task * ntask * reps / (ms * 1e-3) / 1e9);
+}
+
 static float run_copy(const uint8_t *src, uint8_t *dst, uint32_t bytes, uint32_t rs, uint32_t ws,
                       uint32_t span, int reps)
 {
@@ -171,6 +217,11 @@ int main(int argc, char **argv)
     if (argc > 2) {                      // copy mode: GB/s (read + written) per (src, dst) shift
         uint8_t *dst;
         CHECK(hipMalloc(&dst, bytes));
+        // emit-shaped: 256 K tasks of 2992 B (776 MB each way), grids of 2048 / 8192 blocks
+        printf("{\"tasks 2992 B x 256K, 2048 blocks\": %.0f, \"tasks 2992 B x 256K, 8192 blocks\": %.0f, "
+               "\"tasks 4096 B x 192K, 8192 blocks\": %.0f}\n",
+               run_copy_tasks(buf, dst, 2992, 262144, 2048, reps), run_copy_tasks(buf, dst, 2992, 262144, 8192, reps),
+               run_copy_tasks(buf, dst, 4096, 196608, 8192, reps));
         const uint32_t cs[][2] = {{0, 0}, {2, 0}, {0, 2}, {2, 2}, {0, 4}, {1, 3}};
         printf("{");
         for (int i = 0; i < 6; ++i)

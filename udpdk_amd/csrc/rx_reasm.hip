@@ -840,18 +840,71 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
     // wave-uniform scalar loads and SGPRs, not per-lane copies
     const uint32_t lane = __lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
-    for (uint32_t k = blockIdx.x * RS_WAVES + w; k < a.C; k += gridDim.x * RS_WAVES) {
-        const ReasmDone r = a.done[a.perm[k]];
-        const uint32_t oo = a.out_off_in[k];
+    // The next datagram's record and output offset are loaded while this one is copied, and a
+    // datagram's header dwords and payload pieces are all loaded before any of its stores (the
+    // compiler cannot move the frame loads above the output stores, which may alias them).
+    const uint32_t stride = gridDim.x * RS_WAVES;
+    uint32_t k = blockIdx.x * RS_WAVES + w;
+    ReasmDone rn{};
+    uint32_t oon = 0;
+    if (k < a.C) {
+        rn = a.done[a.perm[k]];
+        oon = a.out_off_in[k];
+    }
+    for (; k < a.C; k += stride) {
+        const ReasmDone r = rn;
+        const uint32_t oo = oon;
+        if (k + stride < a.C) {
+            rn = a.done[a.perm[k + stride]];
+            oon = a.out_off_in[k + stride];
+        }
         uint8_t *o = a.out + oo;
         const uint8_t *eb = a.ebuf + (size_t)r.entry * a.stride;
         const __amdgpu_buffer_rsrc_t er = rsrc(eb, a.stride);
+        // Payload: each fragment as 16-byte pieces, lane j taking fragment bytes [16 j, 16 j + 16)
+        // and the last piece moved back to end at the fragment's end (it overlaps the piece
+        // before it, whose bytes it rewrites with the same values), so a fragment of >= 16 bytes
+        // needs no byte stores. (Per fragment, head and tail byte stores around 16-byte body
+        // stores took twice the memory instructions.) Stores are byte-aligned 16-byte buffer
+        // stores into the datagram; 128 pieces (2 KiB) per fragment and round.
+        const __amdgpu_buffer_rsrc_t orr = rsrc(o, 34u + r.total);
+        uint32_t sb[RS_MAX_FRAG], ln[RS_MAX_FRAG], np[RS_MAX_FRAG], rounds = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < RS_MAX_FRAG; ++q) {
+            const bool use = q < r.n && r.fr[q] != 0u;
+            ln[q] = use ? r.fr[q] >> 16 : 0u;
+            sb[q] = r.where[q] == RS_HELD ? 34u + (r.fr[q] & 0xFFFFu) : use ? a.offset[r.where[q]] + 34u : 0u;
+            np[q] = ln[q] >= 16u ? (ln[q] + 15u) >> 4 : 0u;
+            rounds = max(rounds, (np[q] + 127u) >> 7);
+        }
+        uint4 v[RS_MAX_FRAG][2];
+        auto load_round = [&](uint32_t c0) {
+#pragma unroll
+            for (uint32_t q = 0; q < RS_MAX_FRAG; ++q) {
+                const __amdgpu_buffer_rsrc_t sr = r.where[q] == RS_HELD ? er : fr;
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u) {
+                    const uint32_t j = 128u * c0 + 64u * u + lane;
+                    v[q][u] = load16(sr, j < np[q] ? sb[q] + min(16u * j, ln[q] - 16u) : 0x80000000u);
+                }
+            }
+        };
+        auto store_round = [&](uint32_t c0) {
+#pragma unroll
+            for (uint32_t q = 0; q < RS_MAX_FRAG; ++q)
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u) {
+                    const uint32_t j = 128u * c0 + 64u * u + lane;
+                    if (j < np[q]) store16(orr, 34u + (r.fr[q] & 0xFFFFu) + min(16u * j, ln[q] - 16u), v[q][u]);
+                }
+        };
         // header: the first fragment's 34 bytes (ipv4_frag_reassemble keeps the first mbuf's)
         const bool hh = r.where[0] == RS_HELD;
         const __amdgpu_buffer_rsrc_t hr = hh ? er : fr;
         const uint32_t hb = hh ? 0u : a.offset[r.where[0]];
         uint32_t hw = 0;
         if (lane < 9) hw = ld32(hr, hb + 4u * lane);      // bytes 0..35 (34, 35 dropped)
+        if (rounds) load_round(0);
         // dword 4: bytes 16-17 total length, 18-19 id; dword 5: 20-21 fragment field, 22-23;
         // dword 6: 24-25 checksum, 26-27 src
         const uint32_t tl = r.total + 20u;
@@ -877,33 +930,10 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
         if (lane == 6) hw |= ck;
         if (lane < 8) reinterpret_cast<uint32_t *>(o)[lane] = hw;      // o is 16-byte aligned
         if (lane == 8) { o[32] = (uint8_t)hw; o[33] = (uint8_t)(hw >> 8); }
-        // Payload: each fragment as 16-byte pieces, lane j taking fragment bytes [16 j, 16 j + 16)
-        // and the last piece moved back to end at the fragment's end (it overlaps the piece
-        // before it, whose bytes it rewrites with the same values), so a fragment of >= 16 bytes
-        // needs no byte stores; every fragment's loads of a round are issued before its stores.
-        // (Per fragment, head and tail byte stores around 16-byte body stores took twice the
-        // memory instructions.) Stores are byte-aligned 16-byte buffer stores into the datagram.
-        const __amdgpu_buffer_rsrc_t orr = rsrc(o, 34u + r.total);
-        uint32_t sb[RS_MAX_FRAG], ln[RS_MAX_FRAG], np[RS_MAX_FRAG], rounds = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < RS_MAX_FRAG; ++q) {
-            const bool use = q < r.n && r.fr[q] != 0u;
-            ln[q] = use ? r.fr[q] >> 16 : 0u;
-            sb[q] = r.where[q] == RS_HELD ? 34u + (r.fr[q] & 0xFFFFu) : use ? a.offset[r.where[q]] + 34u : 0u;
-            np[q] = ln[q] >= 16u ? (ln[q] + 15u) >> 4 : 0u;
-            rounds = max(rounds, (np[q] + 63u) >> 6);
-        }
-        for (uint32_t c0 = 0; c0 < rounds; ++c0) {
-            uint4 v[RS_MAX_FRAG];
-            const uint32_t j = 64u * c0 + lane;
-#pragma unroll
-            for (uint32_t q = 0; q < RS_MAX_FRAG; ++q) {
-                const __amdgpu_buffer_rsrc_t sr = r.where[q] == RS_HELD ? er : fr;
-                v[q] = load16(sr, j < np[q] ? sb[q] + min(16u * j, ln[q] - 16u) : 0x80000000u);
-            }
-#pragma unroll
-            for (uint32_t q = 0; q < RS_MAX_FRAG; ++q)
-                if (j < np[q]) store16(orr, 34u + (r.fr[q] & 0xFFFFu) + min(16u * j, ln[q] - 16u), v[q]);
+        if (rounds) store_round(0);
+        for (uint32_t c0 = 1; c0 < rounds; ++c0) {   // fragments over 2 KiB
+            load_round(c0);
+            store_round(c0);
         }
         // fragments shorter than 16 bytes, byte by byte
 #pragma unroll
