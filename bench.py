@@ -453,7 +453,9 @@ def gather_line(ctx, cfg: int, steps: int, slot: int = 2048):
     """udpdk_gpu_rx_gather (f1, the batch form of recvfrom) over every delivery of one RX batch
     of config `cfg`: payload slots of `slot` bytes + length + source address per datagram, GPU
     time from events around `steps` back-to-back launches. Bytes per datagram: payload read +
-    payload written + 16 header + 4 lane entry + 6 descriptor + 10 outputs."""
+    payload written + 16 header + 4 lane entry + 6 descriptor + 10 outputs. slot=0: packed
+    slots, each its frame's payload rounded up to 16 bytes (udpdk_gpu_rx_gather_packed, the
+    layout udpdk_poll_rx gathers into), + 4 bytes of slot offset per datagram."""
     w = F.config_batch(cfg)
     b = w.batch
     ctx.upload_snapshot(abi.snapshot_from_lists(w.port_lists(), w.n_sockets))
@@ -462,24 +464,39 @@ def gather_line(ctx, cfg: int, steps: int, slot: int = 2048):
     out = abi.rx_alloc_out(ctx, b.n, w.n_sockets, b.n)
     _, loff, pkt, _, rc = abi.rx_run(ctx, db, out)
     d = int(loff[-1])
-    g = abi.rx_alloc_gather(ctx, d, slot)
+    so = None
+    if slot:
+        g = abi.rx_alloc_gather(ctx, d, slot)
+        call = lambda: abi.rx_gather_enqueue(ctx, db, out.lane_pkt, 0, g)
+    else:
+        pl = b.length[pkt[:d]].astype(np.int64) - 42
+        offs = np.concatenate([[0], np.cumsum((np.maximum(pl, 0) + 15) // 16 * 16)])
+        so = ctx.upload(offs.astype(np.uint32))
+        g = abi.rx_alloc_gather(ctx, d, 16)
+        g.payload.free()
+        g.payload = ctx.alloc(int(offs[-1]) + 16)
+        bt = abi.RxBatch(db.frames.ptr, db.frames_bytes, db.offset.ptr, db.length.ptr, None, b.n)
+        gt = abi.RxGather(g.payload.ptr, 16, g.length.ptr, g.src_ip.ptr, g.src_port.ptr)
+        call = lambda: abi.lib().udpdk_gpu_rx_gather_packed(ctx.handle, C.byref(bt), C.c_void_p(out.lane_pkt.ptr),
+                                                           0, d, C.c_void_p(so.ptr), C.byref(gt))
     for _ in range(3):
-        abi._check(abi.rx_gather_enqueue(ctx, db, out.lane_pkt, 0, g), "udpdk_gpu_rx_gather")
+        abi._check(call(), "udpdk_gpu_rx_gather")
     ev = HipEvents(ctx)
     ctx.sync()
     ev.record(0)
     for _ in range(steps):
-        abi.rx_gather_enqueue(ctx, db, out.lane_pkt, 0, g)
+        call()
     ev.record(1)
     ctx.sync()
     us = 1e3 * ev.elapsed_ms() / steps
     ev.close()
     lens = ctx.download(g.length, np.uint32, d)
-    nbytes = 2 * int(lens.astype(np.int64).sum()) + 36 * d
+    nbytes = 2 * int(lens.astype(np.int64).sum()) + (36 if slot else 40) * d
     for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt, g.payload,
-              g.length, g.src_ip, g.src_port):
+              g.length, g.src_ip, g.src_port) + ((so,) if so is not None else ()):
         x.free()
-    return {"workload": f"gather {w.name}, {slot} B slots", "mdgram_s": round(d / us, 1),
+    return {"workload": f"gather {w.name}, " + (f"{slot} B slots" if slot else "packed slots (udpdk_poll_rx layout)"),
+            "mdgram_s": round(d / us, 1),
             "us_per_launch": round(us, 2), "gbps": round(nbytes / us / 1e3, 1),
             "frac_hbm": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4)}
 
@@ -792,6 +809,8 @@ def main():
         for cfg in (2, 3):
             try:
                 ga.append(gather_line(ctx, cfg, 50))
+                if cfg == 2:
+                    ga.append(gather_line(ctx, cfg, 50, slot=0))
             except Exception as e:
                 ga.append({"config": cfg, "error": repr(e)})
         line["gather"] = ga
