@@ -56,8 +56,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1500 B / IMIX side lines")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU time per baseline leg")
-    p.add_argument("--pipeline", type=int, default=3, choices=(1, 2, 3, 4),
-                   help="udpdk_gpu_pipeline_depth: d > 1 overlaps consecutive batches on d streams")
+    p.add_argument("--pipeline", type=int, default=None, choices=(1, 2, 3, 4),
+                   help="udpdk_gpu_pipeline_depth: d > 1 overlaps consecutive batches on d streams "
+                        "(default: 3 for one socket, 4 when the batch takes the multi-lane path)")
     p.add_argument("--timing-every", type=int, default=16,
                    help="per-kernel timing on every Nth call (dispatch-carried events)")
     p.add_argument("--dry-run", action="store_true",
@@ -302,10 +303,17 @@ def config1_line(target_s: float):
             "gbps_all_cores": round(res[(cores, True)][0] * 106 / 1e3, 2)}
 
 
+def auto_depth(w) -> int:
+    """Batches in flight for a workload: the single-lane path (classify + compaction) is fastest
+    at 3 streams, the multi-lane path (classify + scan + scatter, whose short kernels fill the
+    gaps of other batches' classify) at 4 (profiles/r02j_pipeline_depth.json)."""
+    return 3 if w.n_sockets <= 1 else 4
+
+
 def side_config(ctx, cfg: int, steps: int, rotate: int):
     w = F.config_batch(cfg)
     rx = Rx(ctx, w, rotate)
-    ctx.pipeline(3)
+    ctx.pipeline(auto_depth(w))
     wall, gpu_step, _, st = time_loop(rx, steps, 5, lambda: None, 0)
     ctx.pipeline(1)
     wall1, gpu_step1, kt, _ = time_loop(rx, steps, 5, lambda: None, 4)
@@ -659,7 +667,9 @@ def main():
     w = F.config_batch(args.config, n=frames, shard=rank)
     ctx = abi.GpuContext(device, max_frames=max(w.batch.n, 1 << 22), max_lanes=4096)
     rx = Rx(ctx, w, args.rotate_mib << 20)
-    # the timed region (value): consecutive batches pipelined over two streams, no events inside
+    # the timed region (value): consecutive batches pipelined over several streams, no events inside
+    if args.pipeline is None:
+        args.pipeline = auto_depth(w)
     ctx.pipeline(args.pipeline)
     wall, gpu_step, _, st = time_loop(rx, args.steps, args.warmup, barrier, 0)
     # kernel durations for the roofline: the same calls one at a time (depth 1), every
