@@ -17,12 +17,16 @@ def _port(p):
     return int.from_bytes(p.to_bytes(2, "big"), "little")
 
 
-def test_poll_rx_delivers_reassembled_datagrams_in_order(tmp_path, host_api):
+@pytest.mark.parametrize("threads", [None, 2])
+def test_poll_rx_delivers_reassembled_datagrams_in_order(tmp_path, host_api, threads):
+    """(threads = 2: each socket's admission, with its reassembled datagrams merged in, runs on
+    its own thread of the poll pool)"""
     ini = tmp_path / "udpdk.ini"
     ini.write_text("[port0]\nmac_addr = 68:05:ca:95:f8:ec\nip_addr = 172.31.100.1\n"
                    "[port0_dst]\nmac_addr = 68:05:ca:95:fa:64\n"
                    "[gpu]\ndevice = 0\nmax_frames = 65536\nmax_lanes = 16\n"
-                   "frag_buckets = 16\nfrag_bucket_entries = 16\nfrag_max_dgram = 16384\n")
+                   "frag_buckets = 16\nfrag_bucket_entries = 16\nfrag_max_dgram = 16384\n"
+                   + (f"poll_threads = {threads}\n" if threads else ""))
     L = abi.lib()
     argv = (C.c_char_p * 4)(b"prog", b"-c", str(ini).encode(), None)
     assert L.udpdk_init(3, argv) == 0
