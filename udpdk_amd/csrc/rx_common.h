@@ -105,6 +105,11 @@ struct ScanArgs {
 // rx_scan_cols: one launch, workgroup = a block of 2^lb lanes x every tile; each thread keeps up
 // to SCAN_COLS_TPT tiles of one lane in registers, so tiles <= SCAN_COLS_TPT * (256 >> lb).
 constexpr int SCAN_COLS_BLOCK = 256;
+// lanes from which rx_lane_off scans lane_off once instead of every scatter workgroup
+#ifndef UDPDK_LANE_ONCE_MIN
+#define UDPDK_LANE_ONCE_MIN 2048
+#endif
+constexpr uint32_t LANE_ONCE_MIN = UDPDK_LANE_ONCE_MIN;
 constexpr uint32_t SCAN_COLS_TPT = 64;
 constexpr uint32_t SCAN_COLS_MAX_TILES = SCAN_COLS_TPT * SCAN_COLS_BLOCK;
 
@@ -113,6 +118,7 @@ struct ScatterArgs {
     const uint32_t *base;  // scanned hist: per-lane exclusive prefix over the earlier tiles
     const uint32_t *tot;   // lane totals (rx_scan_cols); null: base already includes lane_off
     uint32_t *lane_off;    // written by the workgroup of tile 0 when tot is given
+    const uint32_t *lane_base;  // lane_off computed by rx_lane_off: cursor = lane_base + base
     uint32_t *total;
     const uint8_t  *frames;
     const uint32_t *offset;
@@ -192,6 +198,7 @@ __global__ void rx_scan_top(ScanArgs a, uint32_t n_part);
 __global__ void rx_scan_down(ScanArgs a);
 __global__ void rx_scatter(ScatterArgs a);
 __global__ void rx_scatterw(ScatterArgs a);
+__global__ void rx_lane_off(const uint32_t *tot, uint32_t n_lanes, uint32_t *lane_off, uint32_t *total);
 constexpr uint32_t SCATTER_WAVES = 8;           // rx_scatterw workgroup: 8 waves per tile
 constexpr uint32_t SCATTERW_MAX_LANES = 4096;   // rx_scatterw LDS: (4 + 2 x 8) x lanes bytes
 __host__ __device__ constexpr uint32_t scatterw_lds_bytes(uint32_t n_lanes)

@@ -948,6 +948,15 @@ rx_scan_down(ScanArgs a)
     }
 }
 
+// lane_off = exclusive scan of the lane totals rx_scan_cols left, once per batch (one
+// workgroup), instead of in every scatter workgroup's prologue.
+__global__ void __launch_bounds__(1024)
+rx_lane_off(const uint32_t *tot, uint32_t n_lanes, uint32_t *lane_off, uint32_t *total)
+{
+    __shared__ uint32_t lds16[16];
+    scan_lane_totals(tot, n_lanes, lane_off, total, lds16);
+}
+
 // Tile of workgroup b out of n so that each XCD walks a contiguous run of tiles (blocks are dealt
 // round-robin over the 8 XCDs, MI355X_MICROARCH.md §Workgroup dispatch; b % 8 labels the blocks
 // sharing one). Bijective for any n. A lane's entries from consecutive tiles are adjacent in
@@ -970,6 +979,11 @@ __device__ void lane_cursors(const ScatterArgs &a, uint32_t tile, uint32_t *cur,
 {
     const uint32_t tid = threadIdx.x, NT = blockDim.x, S = a.n_lanes;
     const uint32_t *base = a.base + (size_t)tile * S;
+    if (a.lane_base) {                                  // lane_off scanned once (rx_lane_off)
+        for (uint32_t k = tid; k < S; k += NT) cur[k] = a.lane_base[k] + base[k];
+        __syncthreads();
+        return;
+    }
     if (!a.tot) {
         for (uint32_t k = tid; k < S; k += NT) cur[k] = base[k];
         __syncthreads();

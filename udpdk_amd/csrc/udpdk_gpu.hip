@@ -620,6 +620,9 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     // one-launch column scan while each thread's tile chunk fits its registers; beyond (very
     // large batches over few lanes) the reduce / top / down chain, which also writes lane_off
     const bool cols = tiles <= SCAN_COLS_MAX_TILES;
+    // with many lanes, lane_off is scanned once by rx_lane_off rather than by every scatter
+    // workgroup
+    const bool lane_once = cols && S >= LANE_ONCE_MIN;
     if (cols) {
         // lanes per workgroup: as many as the chunking allows (<= 64, 256 B rows), then fewer
         // until the grid has >= 128 workgroups, never under 8 lanes (32 B row segments)
@@ -627,8 +630,11 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
         uint32_t lb = 0;
         while ((2u << lb) <= std::min<uint32_t>(64u, SCAN_COLS_BLOCK / cmin)) ++lb;
         while (lb > 3 && ceil_div(S, 1u << lb) < 128u) --lb;
-        HIPC(c, launch(st, ts, 1, true, true, rx_scan_cols, dim3(ceil_div(S, 1u << lb)),
+        HIPC(c, launch(st, ts, 1, true, !lane_once, rx_scan_cols, dim3(ceil_div(S, 1u << lb)),
                        dim3(SCAN_COLS_BLOCK), 0u, sa, lb));
+        if (lane_once)
+            HIPC(c, launch(st, ts, 1, false, true, rx_lane_off, dim3(1), dim3(1024), 0u,
+                           (const uint32_t *)P.tot, S, o->lane_off_dev, &P.res->total));
     } else {
         const uint32_t nc = ceil_div(tiles, SCAN_COL_CHUNK);
         if ((uint64_t)nc * S > c->partial_cap) return -EINVAL;
@@ -641,7 +647,8 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     ScatterArgs xa;
     xa.meta = o->meta_dev;
     xa.base = P.hist;
-    xa.tot = cols ? P.tot : nullptr;
+    xa.tot = cols && !lane_once ? P.tot : nullptr;
+    xa.lane_base = lane_once ? o->lane_off_dev : nullptr;
     xa.lane_off = o->lane_off_dev;
     xa.total = &P.res->total;
     xa.frames = bt->frames_dev;
