@@ -27,11 +27,6 @@ namespace udpdk {
 
 namespace {
 
-__device__ __forceinline__ uint32_t ld32(__amdgpu_buffer_rsrc_t r, uint32_t off)
-{
-    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
-}
-
 // Orders a wave's LDS accesses across lanes (its DS instructions execute in order).
 __device__ __forceinline__ void wsync()
 {
@@ -65,7 +60,8 @@ __global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
     const uint32_t t0 = tile * RSS_TILE, t1 = min(a.n, t0 + RSS_TILE);
     constexpr uint32_t STEPS = RSS_TILE / RSS_BLOCK;
     // all of the thread's frames' loads first (descriptors, then header words), then the work
-    uint32_t o[STEPS], len[STEPS], w12[STEPS], w20[STEPS], src[STEPS], dst[STEPS], ports[STEPS];
+    uint32_t o[STEPS], len[STEPS];
+    uint4 h0[STEPS], h1[STEPS];        // frame bytes [12, 38) from the dword at or below offset + 12
 #pragma unroll
     for (uint32_t s = 0; s < STEPS; ++s) {
         const uint32_t i = t0 + s * RSS_BLOCK + (tid & ~63u) + lane;
@@ -81,15 +77,15 @@ __global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
     const uint4 *ksrc = reinterpret_cast<const uint4 *>(a.ktab);
 #pragma unroll
     for (uint32_t e = 0; e < KV; ++e) kv[e] = ksrc[e * RSS_BLOCK + tid];
+    // two dword-aligned 16-byte loads per frame instead of five 4-byte loads, three of them at
+    // byte offsets (26, 30, 34: byte-aligned loads run the vector memory path ~25 % slower,
+    // tools/probe/align_probe.hip); the words are funnelled by offset & 3 below
 #pragma unroll
     for (uint32_t s = 0; s < STEPS; ++s) {
         const bool ok = (uint64_t)o[s] + len[s] <= a.frames_bytes && len[s] >= 34u;
-        const uint32_t b0 = ok ? o[s] : 0u;
-        w12[s] = ok ? ld32(fr, b0 + 12) : 0u;
-        w20[s] = ok ? ld32(fr, b0 + 20) : 0u;
-        src[s] = ok ? ld32(fr, b0 + 26) : 0u;
-        dst[s] = ok ? ld32(fr, b0 + 30) : 0u;
-        ports[s] = ok && len[s] >= 38u ? ld32(fr, b0 + 34) : 0u;
+        const uint32_t A = ok ? (o[s] + 12u) & ~3u : 0u;
+        h0[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(fr, (int)A, 0, 0));
+        h1[s] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(fr, (int)(A + 16u), 0, 0));
     }
     {
         uint4 *dst = reinterpret_cast<uint4 *>(&tab[0][0]);
@@ -105,13 +101,22 @@ __global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
         const bool in = i < t1;
         uint32_t hash = 0;
         const bool ok = in && (uint64_t)o[s] + len[s] <= a.frames_bytes && len[s] >= 34u;
-        const uint32_t pt = ok ? (a.ptype ? a.ptype[i] : ((w12[s] & 0xFFFFu) == 0x0008u ? 0x211u : 0x1u)) : 0u;
+        // frame-relative words g[i] = frame bytes [12 + 4 i, 16 + 4 i)
+        const uint32_t D[8] = {h0[s].x, h0[s].y, h0[s].z, h0[s].w, h1[s].x, h1[s].y, h1[s].z, h1[s].w};
+        const uint32_t sh = o[s] & 3u;
+        uint32_t g[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) g[k] = __builtin_amdgcn_alignbyte(D[k + 1], D[k], sh);
+        const uint32_t w12 = g[0], w20 = g[2];
+        const uint32_t src = (g[3] >> 16) | (g[4] << 16), dst = (g[4] >> 16) | (g[5] << 16);
+        const uint32_t ports = (g[5] >> 16) | (g[6] << 16);       // used only when len >= 38
+        const uint32_t pt = ok ? (a.ptype ? a.ptype[i] : ((w12 & 0xFFFFu) == 0x0008u ? 0x211u : 0x1u)) : 0u;
         if (ok && (pt & 0x10u)) {
-            const uint32_t ff = ((w20[s] & 0xFFu) << 8) | ((w20[s] >> 8) & 0xFFu);
+            const uint32_t ff = ((w20 & 0xFFu) << 8) | ((w20 >> 8) & 0xFFu);
             const bool frag = (ff & 0x3FFFu) != 0u;
-            const bool udp4 = !frag && ((w20[s] >> 24) & 0xFFu) == 17u && len[s] >= 38u && (a.hash_types & 2u);
+            const bool udp4 = !frag && ((w20 >> 24) & 0xFFu) == 17u && len[s] >= 38u && (a.hash_types & 2u);
             if (udp4 || (a.hash_types & 1u)) {
-                const uint32_t sa = src[s], da = dst[s], pp = ports[s];
+                const uint32_t sa = src, da = dst, pp = ports;
                 hash = tab[0][sa & 255u] ^ tab[1][(sa >> 8) & 255u] ^ tab[2][(sa >> 16) & 255u] ^
                        tab[3][sa >> 24] ^ tab[4][da & 255u] ^ tab[5][(da >> 8) & 255u] ^
                        tab[6][(da >> 16) & 255u] ^ tab[7][da >> 24];
