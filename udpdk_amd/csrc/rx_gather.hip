@@ -33,17 +33,28 @@ __global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
         const uint32_t i = valid ? min(a.lane_pkt[a.first + k], a.n - 1u) : 0u;
         const uint32_t o = a.offset[i];
         const uint32_t len = a.length[i];
-        const auto h = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)(o + 26u), 0, 0);  // bytes 26..41
-        // a short frame's first 64 payload bytes go out with the header load (the frame length
-        // bounds them; pieces past it are addressed out of range: no memory access)
+        // Frame bytes [26, 42) (source address and port, dgram_len) and, for a short frame, its
+        // first 64 payload bytes [42, 106), as up to six dword-aligned 16-byte loads from the
+        // dword at or below offset + 26, funnelled by offset & 3 (byte-aligned 16-byte loads run
+        // the vector memory path ~25 % slower, tools/probe/align_probe.hip). The frame length
+        // bounds the payload part; pieces past it are addressed out of range (no memory access).
         const uint32_t fseg = len >= 42u ? len - 42u : 0u;
+        const uint32_t X = o + 26u, sh = X & 3u;
+        const uint32_t need = 16u + (valid && fseg <= 64u ? fseg : 0u) + sh;
+        uint32_t D[24];
+#pragma unroll
+        for (uint32_t u = 0; u < 6; ++u) {
+            const uint32_t off = 16u * u < need ? (X & ~3u) + 16u * u : 0x80000000u;
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)off, 0, 0);
+            D[4 * u] = x[0]; D[4 * u + 1] = x[1]; D[4 * u + 2] = x[2]; D[4 * u + 3] = x[3];
+        }
+        uint32_t W[20];                                          // W[m] = frame bytes 26 + 4m ..
+#pragma unroll
+        for (int m = 0; m < 20; ++m) W[m] = __builtin_amdgcn_alignbyte(D[m + 1], D[m], sh);
+        const uint32_t h[4] = {W[0], W[1], W[2], W[3]};
         uint4 v0[4];
 #pragma unroll
-        for (uint32_t u = 0; u < 4; ++u) {
-            const uint32_t off = valid && fseg <= 64u && 16u * u < fseg ? o + 42u + 16u * u : 0x80000000u;
-            const auto x = __builtin_amdgcn_raw_buffer_load_b128(fr, (int)off, 0, 0);
-            v0[u] = make_uint4(x[0], x[1], x[2], x[3]);
-        }
+        for (uint32_t u = 0; u < 4; ++u) v0[u] = make_uint4(W[4 + 4 * u], W[5 + 4 * u], W[6 + 4 * u], W[7 + 4 * u]);
         const uint32_t dlr = h[3] & 0xFFFFu;                                           // dgram_len, BE
         const uint32_t dl = ((dlr & 0xFFu) << 8) | (dlr >> 8);
         const uint32_t pl = (dl - 8u) & 0xFFFFu;                 // uint16_t dgram_payl_len (:436)
