@@ -263,16 +263,24 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned lon
 {
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
     const uint32_t F = a.counts[0];
-    for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
-        const uint32_t i = a.frag_list[p], o = a.offset[i];
+    const uint32_t lane = __lane_id();
+    // wave-uniform loop: lane l holds position p = wave base + l, so the previous position's key
+    // comes from lane l - 1 by a shuffle (each frame header read once), lane 0 reads its own
+    for (uint32_t pb = blockIdx.x * RS_BLOCK + (threadIdx.x & ~63u); pb < F; pb += gridDim.x * RS_BLOCK) {
+        const uint32_t p = pb + lane;
+        const bool valid = p < F;
+        const uint32_t i = valid ? a.frag_list[p] : 0u, o = valid ? a.offset[i] : 0u;
         const uint32_t id = ld32(fr, o + 16) >> 16, src = ld32(fr, o + 26), dst = ld32(fr, o + 30);
-        a.k1[p] = ((unsigned long long)id << a.ib) | i;
-        bool start = p == 0;
-        if (!start) {
+        if (valid) a.k1[p] = ((unsigned long long)id << a.ib) | i;
+        uint32_t pid = __shfl_up(id, 1, 64), psrc = __shfl_up(src, 1, 64), pdst = __shfl_up(dst, 1, 64);
+        if (lane == 0u && valid && p > 0u) {
             const uint32_t op = a.offset[a.frag_list[p - 1]];
-            start = (ld32(fr, op + 16) >> 16) != id || ld32(fr, op + 26) != src || ld32(fr, op + 30) != dst;
+            pid = ld32(fr, op + 16) >> 16;
+            psrc = ld32(fr, op + 26);
+            pdst = ld32(fr, op + 30);
         }
-        if (!start) continue;
+        const bool start = p == 0u || pid != id || psrc != src || pdst != dst;
+        if (!valid || !start) continue;
         unsigned long long fp = ((unsigned long long)dst << 32 | src) * 0x9E3779B97F4A7C15ull;
         fp ^= (unsigned long long)(id + 1u) * 0xC2B2AE3D27D4EB4Full;
         fp ^= fp >> 29;
