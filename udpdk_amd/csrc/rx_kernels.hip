@@ -426,12 +426,17 @@ rx_classify(RxArgs a)
             int la, lb;
             uint4 Ra[4], Rb[4];
             issue(0, qa, la, ea, Ra);
-            for (uint32_t k0 = 0;; k0 += 128) {
-                issue(k0 + 64, qb, lb, eb, Rb);
-                consume(k0, la, ea, Ra);
-                issue(k0 + 128, qa, la, ea, Ra);
-                consume(k0 + 64, lb, eb, Rb);
-                if (k0 + 128 >= total) break;
+            if (total <= 64u) {
+                // one group (e.g. every frame's tail one chunk): no groups issued past the end
+                consume(0, la, ea, Ra);
+            } else {
+                for (uint32_t k0 = 0;; k0 += 128) {
+                    issue(k0 + 64, qb, lb, eb, Rb);
+                    consume(k0, la, ea, Ra);
+                    issue(k0 + 128, qa, la, ea, Ra);
+                    consume(k0 + 64, lb, eb, Rb);
+                    if (k0 + 128 >= total) break;
+                }
             }
             wave_sync();
             if (pd) {
