@@ -41,7 +41,9 @@
 extern "C" {
 #endif
 
-#define UDPDK_GPU_ABI_VERSION 1
+/* 2: udpdk_reasm_out_t stats grew to UDPDK_RS_N = 11 (RS_SERIAL, RS_SORTED);
+ *    udpdk_gpu_rx_gather_packed; TX payloads need UDPDK_GPU_FRAMES_TAILROOM readable bytes */
+#define UDPDK_GPU_ABI_VERSION 2
 
 /* ---------------------------------------------------------------------------------------------
  * Per-frame verdict word (one uint32 per frame, written by udpdk_gpu_rx)
