@@ -173,11 +173,13 @@ def _admitted(idx, room):
     return acc
 
 
-@pytest.mark.parametrize("api", [1, 3, 8], indirect=True)
+@pytest.mark.parametrize("api", [1, 3, 8, 32], indirect=True)
 def test_rx_many_sockets_over_poll_threads(api):
     """40 sockets, Zipf-skewed destination ports, some rings partly full before the poll: the
-    admission and ring publication split the sockets over 1, 3 or 8 threads (sockets straddle
-    the parts' boundaries) and every socket still gets exactly its admitted bursts, in order."""
+    admission and ring publication split the sockets over 1, 3, 8 or 32 threads (sockets
+    straddle the parts' boundaries; at 32 most parts hold one socket or none, the Zipf head
+    filling several parts' share alone) and every socket still gets exactly its admitted
+    bursts, in order."""
     ns = 40
     socks = [api.socket() for _ in range(ns)]
     for k, s in enumerate(socks):
