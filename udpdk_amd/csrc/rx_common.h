@@ -168,6 +168,7 @@ struct TxArgs {
     uint32_t src_ip;
     uint32_t mtu;              // 0: no fragmentation; else IPv4 MTU ((mtu - 20) % 8 == 0)
     uint32_t mac_lo[3];        // 12 MAC bytes: dst(6) src(6) as three LE dwords
+    uint32_t parts;            // waves sharing one group of 64 datagrams' chunk sweep (>= 1)
 };
 
 // Payload delivery (rx_gather): lane entries [first, first + count) -> payload slots + source

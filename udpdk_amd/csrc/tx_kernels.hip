@@ -174,7 +174,12 @@ tx_build(TxArgs a)
     const uint32_t waves_total = gridDim.x * TXW;
     const uint32_t fpl = a.mtu ? a.mtu - 20u : 0u;      // IP payload bytes per full fragment
 
-    for (uint32_t g = blockIdx.x * TXW + w; g * 64 < a.n; g += waves_total) {
+    // a.parts waves share each group of 64 datagrams: every one builds the group's headers and
+    // takes every a.parts-th 64 chunks of its sweep (few large datagrams, e.g. 256 K datagrams
+    // of 2952 B, are 4096 groups: one wave per group left 4 waves per SIMD, each a long sweep)
+    const uint32_t groups = (a.n + 63u) / 64u;
+    for (uint32_t gp = blockIdx.x * TXW + w; gp < groups * a.parts; gp += waves_total) {
+        const uint32_t g = gp / a.parts, part = gp % a.parts;
         const uint32_t i = g * 64 + lane;
         uint32_t nf = 0, fo = 0, L = 0, po = 0, src = 0, dst = 0, pt = 0;
         int32_t sock = -1;
@@ -186,7 +191,7 @@ tx_build(TxArgs a)
         }
         // a wave of small unfragmented frames: one lane builds and stores its own frame
         if (!__ballot(i < a.n && (L + 42u > TX_SMALL_SPAN || (a.mtu && L + 42u > a.mtu)))) {
-            tx_small(a, i, fo, L, po, sock);
+            if (part == 0u) tx_small(a, i, fo, L, po, sock);
             continue;
         }
         if (i < a.n) {
@@ -295,7 +300,7 @@ tx_build(TxArgs a)
             l_po[w][lane] = ppo;
             wave_sync_tx();
 
-            for (uint32_t k = lane; k < total; k += 64) {
+            for (uint32_t k = lane + 64u * part; k < total; k += 64u * a.parts) {
                 uint32_t q = 0;
 #pragma unroll
                 for (int sft = 32; sft >= 1; sft >>= 1)

@@ -1150,7 +1150,10 @@ int udpdk_gpu_tx_build_mtu(udpdk_gpu_ctx *c, const udpdk_tx_config_t *cfg,
     memcpy(mac + 6, cfg->src_mac, 6);
     memcpy(ta.mac_lo, mac, 12);
     const uint32_t groups = ceil_div(bt->n, 64);
-    const uint32_t grid = std::min<uint32_t>(ceil_div(groups, TX_BLOCK / 64), 4096);
+    // waves per group of 64 datagrams: up to 4 while groups alone would leave the chip under
+    // ~16 K waves (their chunk sweeps split between them)
+    ta.parts = std::max<uint32_t>(1u, std::min<uint32_t>(4u, 16384u / std::max<uint32_t>(groups, 1u)));
+    const uint32_t grid = std::min<uint32_t>(ceil_div(groups * ta.parts, TX_BLOCK / 64), 4096);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing_every) {
         HIPC(c, hipEventCreate(&e0));
