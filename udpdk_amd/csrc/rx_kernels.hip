@@ -208,18 +208,19 @@ __device__ __forceinline__ uint32_t max_scan_dpp(uint32_t v)
     return v;
 }
 
-// Frame bytes [12, 64) of one frame, loaded straight from frame byte 12 (byte-aligned buffer
-// loads: 3 x 16 B + 4 B; unaligned dwordx4 buffer loads cost the same as aligned ones here,
-// tools/probe/stream_probe.hip k_unal): g[i] = frame bytes 12 + 4i .. 15 + 4i, no funnel shift.
+// Frame bytes [12, 64) of one frame: 14 dwords from the dword at or below frame byte 12 (3 x 16 B
+// + 8 B; at 64 B frame strides a dword-aligned start costs the same as an aligned one, a byte-
+// aligned one ~25 % more, tools/probe/align_probe.hip), funnelled to g[i] = frame bytes 12 + 4i ..
 struct Win {
     uint4 a, b, c;
     uint2 d;
 };
 
 // 4 waves per SIMD (<= 128 VGPRs, the tail pass's two groups in flight): one tile of 1024 frames
-// per workgroup puts 4 workgroups on each CU at 1 M frames. (A 96-VGPR budget spills and runs
-// 19 % slower at 64 B. Four tail groups in flight, at 148 VGPRs and 3 waves per SIMD, measured
-// no faster at 1500 B and slower at IMIX and 106 B: the tail is not bound by its round trips.)
+// per workgroup puts 4 workgroups on each CU at 1 M frames. (Round 1: a 96-VGPR budget spilled
+// and ran 19 % slower at 64 B; four tail groups in flight at 148 VGPRs and 3 waves per SIMD were
+// no faster at 1500 B and slower at IMIX and 106 B. Round 2: three groups at 127 VGPRs, DESIGN.md
+// §4.)
 __global__ void __launch_bounds__(CLS_BLOCK) __attribute__((amdgpu_waves_per_eu(UDPDK_CLS_WPE, 8)))
 rx_classify(RxArgs a)
 {
