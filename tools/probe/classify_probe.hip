@@ -124,7 +124,7 @@ int main()
     (void)hipMemcpy(port_tab, pt.data(), 65536 * 16, hipMemcpyHostToDevice);
     (void)hipMalloc(&binds, 8);
     (void)hipMemset(binds, 0, 8);
-    const uint32_t T = 1024, tiles = N / T;
+    const uint32_t T = getenv("TILE") ? (uint32_t)atoi(getenv("TILE")) : 1024u, tiles = N / T;
     uint32_t *meta, *hist, *tcnt;
     (void)hipMalloc(&meta, (size_t)N * 4);
     (void)hipMalloc(&hist, tiles * 4);
