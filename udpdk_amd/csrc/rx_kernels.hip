@@ -26,6 +26,7 @@
 // (verdict word), + 4 per (lane, tile) histogram entry.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "udpdk_gpu.h"
 #include "rx_common.h"
@@ -833,11 +834,35 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds16,
 
 // Lane totals tot[] (LDS, n_lanes words) -> lane_off[] exclusive scan + total. Thread j takes the
 // contiguous lanes [j * L, (j + 1) * L).
-__device__ void scan_lane_totals(const uint32_t *tot, uint32_t n_lanes, uint32_t *lane_off,
+__device__ __forceinline__ void scan_lane_totals(const uint32_t *tot, uint32_t n_lanes, uint32_t *lane_off,
                                  uint32_t *total_out, uint32_t *lds16)
 {
     const uint32_t tid = threadIdx.x, L = (n_lanes + blockDim.x - 1) / blockDim.x;
     const uint32_t l0 = min(n_lanes, tid * L), l1 = min(n_lanes, l0 + L);
+    // the thread's lanes in registers, loaded at once with clamped indices (a loop with a
+    // data-dependent trip count waited for every load in turn); LR = 4, 8 or 16 lanes per thread
+    // covers UDPDK_GPU_MAX_LANES at 1024 threads
+    auto regs = [&](auto lr) {
+        constexpr uint32_t LR = decltype(lr)::value;
+        uint32_t v[LR], s = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < LR; ++i) {
+            const uint32_t x = tot[min(l0 + i, n_lanes - 1u)];
+            v[i] = l0 + i < l1 ? x : 0u;
+            s += v[i];
+        }
+        uint32_t total;
+        uint32_t run = block_excl_scan(s, lds16, &total);
+#pragma unroll
+        for (uint32_t i = 0; i < LR; ++i) {
+            if (l0 + i < l1) lane_off[l0 + i] = run;
+            run += v[i];
+        }
+        if (tid == 0) { lane_off[n_lanes] = total; *total_out = total; }
+    };
+    if (L <= 4u) return regs(std::integral_constant<uint32_t, 4>{});
+    if (L <= 8u) return regs(std::integral_constant<uint32_t, 8>{});
+    if (L <= 16u) return regs(std::integral_constant<uint32_t, 16>{});
     uint32_t s = 0;
     for (uint32_t l = l0; l < l1; ++l) s += tot[l];
     uint32_t total;
@@ -981,24 +1006,48 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n)
 // scratch (no static LDS here: rx_scatterw's dynamic carve is sized so two workgroups share a
 // CU, and one more word would halve that). With a.tot == null (the 3-launch scan) base is
 // already absolute.
-__device__ void lane_cursors(const ScatterArgs &a, uint32_t tile, uint32_t *cur, uint32_t *tmp)
+__device__ __forceinline__ void lane_cursors(const ScatterArgs &a, uint32_t tile, uint32_t *cur, uint32_t *tmp)
 {
     const uint32_t tid = threadIdx.x, NT = blockDim.x, S = a.n_lanes;
     const uint32_t *base = a.base + (size_t)tile * S;
+    // x[k] -> d0[k], y[k] -> d1[k] for k < S, CU loads per thread in flight at once (clamped
+    // indices, stores guarded): a plain strided loop waited for each iteration's loads, one L2 /
+    // HBM round trip per NT lanes (8 at 4096 lanes and 512 threads)
+    auto stage2 = [&](const uint32_t *x, const uint32_t *y, uint32_t *d0, uint32_t *d1, bool sum) {
+        constexpr uint32_t CU = 8;
+        for (uint32_t k0 = tid; k0 < S; k0 += NT * CU) {
+            uint32_t vx[CU], vy[CU];
+#pragma unroll
+            for (uint32_t u = 0; u < CU; ++u) {
+                const uint32_t k = min(k0 + u * NT, S - 1u);
+                vx[u] = x ? x[k] : 0u;
+                vy[u] = y[k];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < CU; ++u) {
+                const uint32_t k = k0 + u * NT;
+                if (k < S) {
+                    if (sum) {
+                        d0[k] = vx[u] + vy[u];
+                    } else {
+                        d0[k] = vx[u];
+                        d1[k] = vy[u];
+                    }
+                }
+            }
+        }
+    };
     if (a.lane_base) {                                  // lane_off scanned once (rx_lane_off)
-        for (uint32_t k = tid; k < S; k += NT) cur[k] = a.lane_base[k] + base[k];
+        stage2(a.lane_base, base, cur, nullptr, true);
         __syncthreads();
         return;
     }
     if (!a.tot) {
-        for (uint32_t k = tid; k < S; k += NT) cur[k] = base[k];
+        stage2(nullptr, base, cur, nullptr, true);
         __syncthreads();
         return;
     }
-    for (uint32_t k = tid; k < S; k += NT) {
-        cur[k] = a.tot[k];
-        tmp[k] = base[k];
-    }
+    stage2(a.tot, base, cur, tmp, false);
     __syncthreads();
     const uint32_t L = (S + NT - 1u) / NT, l0 = min(S, tid * L), l1 = min(S, l0 + L);
     uint32_t s = 0;
