@@ -869,43 +869,75 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
         uint8_t *o = a.out + oo;
         const uint8_t *eb = a.ebuf + (size_t)r.entry * a.stride;
         const __amdgpu_buffer_rsrc_t er = rsrc(eb, a.stride);
-        // Payload: each fragment as 16-byte pieces, lane j taking fragment bytes [16 j, 16 j + 16)
-        // and the last piece moved back to end at the fragment's end (it overlaps the piece
-        // before it, whose bytes it rewrites with the same values), so a fragment of >= 16 bytes
-        // needs no byte stores. (Per fragment, head and tail byte stores around 16-byte body
-        // stores took twice the memory instructions.) Stores are byte-aligned 16-byte buffer
-        // stores into the datagram; 128 pieces (2 KiB) per fragment and round.
+        // Payload: each fragment as 16-byte pieces (piece j = fragment bytes [16 j, 16 j + 16), the
+        // last piece moved back to end at the fragment's end: it overlaps the piece before it,
+        // whose bytes it rewrites with the same values, so a fragment of >= 16 bytes needs no byte
+        // stores). The datagram's pieces are numbered across its fragments (fragment q's pieces
+        // are [pb[q], pb[q + 1])) and lane = piece, so a 2-fragment datagram of 2 x 1480 bytes
+        // takes 3 loads and 3 stores per wave instead of one pair of instructions per fragment
+        // and 64 pieces (8 loads, half of them past every fragment, and 4 stores). Stores are
+        // byte-aligned 16-byte buffer stores into the datagram; 128 pieces (2 KiB) per round.
         const __amdgpu_buffer_rsrc_t orr = rsrc(o, 34u + r.total);
-        uint32_t sb[RS_MAX_FRAG], ln[RS_MAX_FRAG], np[RS_MAX_FRAG], rounds = 0;
+        uint32_t sb[RS_MAX_FRAG], ln[RS_MAX_FRAG], db[RS_MAX_FRAG], pb[RS_MAX_FRAG + 1];
+        bool any_held = false, any_frame = false;
+        pb[0] = 0;
 #pragma unroll
         for (uint32_t q = 0; q < RS_MAX_FRAG; ++q) {
             const bool use = q < r.n && r.fr[q] != 0u;
+            const bool held = r.where[q] == RS_HELD;
             ln[q] = use ? r.fr[q] >> 16 : 0u;
-            sb[q] = r.where[q] == RS_HELD ? 34u + (r.fr[q] & 0xFFFFu) : use ? a.offset[r.where[q]] + 34u : 0u;
-            np[q] = ln[q] >= 16u ? (ln[q] + 15u) >> 4 : 0u;
-            rounds = max(rounds, (np[q] + 127u) >> 7);
+            sb[q] = held ? 34u + (r.fr[q] & 0xFFFFu) : use ? a.offset[r.where[q]] + 34u : 0u;
+            db[q] = 34u + (r.fr[q] & 0xFFFFu);
+            const uint32_t np = ln[q] >= 16u ? (ln[q] + 15u) >> 4 : 0u;
+            pb[q + 1] = pb[q] + np;
+            if (np) {
+                any_held = any_held || held;
+                any_frame = any_frame || !held;
+            }
         }
-        uint4 v[RS_MAX_FRAG][2];
+        const uint32_t P = pb[RS_MAX_FRAG];
+        const bool mixed = any_held && any_frame;
+        const __amdgpu_buffer_rsrc_t one = any_held ? er : fr;   // every piece's source, unless mixed
+        // piece g's source and destination offsets (g < P), from the wave-uniform tables
+        auto piece = [&](uint32_t g, uint32_t &src, uint32_t &dst, bool &held) {
+            const bool g1 = g >= pb[1], g2 = g >= pb[2], g3 = g >= pb[3];
+            auto sel = [&](uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+                return g3 ? x3 : g2 ? x2 : g1 ? x1 : x0;
+            };
+            const uint32_t j = g - sel(pb[0], pb[1], pb[2], pb[3]);
+            const uint32_t pos = min(16u * j, sel(ln[0], ln[1], ln[2], ln[3]) - 16u);
+            src = sel(sb[0], sb[1], sb[2], sb[3]) + pos;
+            dst = sel(db[0], db[1], db[2], db[3]) + pos;
+            held = sel(r.where[0], r.where[1], r.where[2], r.where[3]) == RS_HELD;
+        };
+        uint4 v[2];
+        uint32_t dv[2];
         auto load_round = [&](uint32_t c0) {
 #pragma unroll
-            for (uint32_t q = 0; q < RS_MAX_FRAG; ++q) {
-                const __amdgpu_buffer_rsrc_t sr = r.where[q] == RS_HELD ? er : fr;
-#pragma unroll
-                for (uint32_t u = 0; u < 2; ++u) {
-                    const uint32_t j = 128u * c0 + 64u * u + lane;
-                    v[q][u] = load16(sr, j < np[q] ? sb[q] + min(16u * j, ln[q] - 16u) : 0x80000000u);
+            for (uint32_t u = 0; u < 2; ++u) {
+                const uint32_t g = c0 + 64u * u + lane;
+                if (c0 + 64u * u >= P) continue;                          // uniform
+                uint32_t src, dst;
+                bool held;
+                piece(g < P ? g : P - 1u, src, dst, held);
+                dv[u] = g < P ? dst : 0xFFFFFFFFu;
+                if (!mixed) {
+                    v[u] = load16(one, g < P ? src : 0x80000000u);
+                } else {   // pieces from the entry buffer and from the batch: one load each, OR'd
+                    const uint4 x = load16(er, g < P && held ? src : 0x80000000u);
+                    const uint4 y = load16(fr, g < P && !held ? src : 0x80000000u);
+                    v[u] = make_uint4(x.x | y.x, x.y | y.y, x.z | y.z, x.w | y.w);
                 }
             }
         };
         auto store_round = [&](uint32_t c0) {
 #pragma unroll
-            for (uint32_t q = 0; q < RS_MAX_FRAG; ++q)
-#pragma unroll
-                for (uint32_t u = 0; u < 2; ++u) {
-                    const uint32_t j = 128u * c0 + 64u * u + lane;
-                    if (j < np[q]) store16(orr, 34u + (r.fr[q] & 0xFFFFu) + min(16u * j, ln[q] - 16u), v[q][u]);
-                }
+            for (uint32_t u = 0; u < 2; ++u) {
+                if (c0 + 64u * u >= P) continue;                          // uniform
+                if (dv[u] != 0xFFFFFFFFu) store16(orr, dv[u], v[u]);
+            }
         };
+        const uint32_t rounds = (P + 127u) >> 7;
         // header: the first fragment's 34 bytes (ipv4_frag_reassemble keeps the first mbuf's)
         const bool hh = r.where[0] == RS_HELD;
         const __amdgpu_buffer_rsrc_t hr = hh ? er : fr;
@@ -939,9 +971,9 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
         if (lane < 8) reinterpret_cast<uint32_t *>(o)[lane] = hw;      // o is 16-byte aligned
         if (lane == 8) { o[32] = (uint8_t)hw; o[33] = (uint8_t)(hw >> 8); }
         if (rounds) store_round(0);
-        for (uint32_t c0 = 1; c0 < rounds; ++c0) {   // fragments over 2 KiB
-            load_round(c0);
-            store_round(c0);
+        for (uint32_t c0 = 1; c0 < rounds; ++c0) {   // datagrams of over 128 pieces
+            load_round(128u * c0);
+            store_round(128u * c0);
         }
         // fragments shorter than 16 bytes, byte by byte
 #pragma unroll
