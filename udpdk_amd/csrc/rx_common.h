@@ -18,6 +18,9 @@ constexpr uint32_t RX_TILE_MAX = 8192;   // classify LDS: <= 143 KiB at 16384 la
 #define UDPDK_RX_HIST_CAP (1u << 21)
 #endif
 constexpr uint32_t RX_HIST_CAP = UDPDK_RX_HIST_CAP;  // target bound on lanes x tiles
+#ifndef UDPDK_SCAN_MIN_WG
+#define UDPDK_SCAN_MIN_WG 64u                 // rx_scan_cols: fewest workgroups before narrowing columns
+#endif
 #ifndef UDPDK_CLS_BLOCK
 #define UDPDK_CLS_BLOCK 256
 #endif

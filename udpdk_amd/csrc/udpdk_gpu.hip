@@ -625,11 +625,13 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     const bool lane_once = cols && S >= LANE_ONCE_MIN;
     if (cols) {
         // lanes per workgroup: as many as the chunking allows (<= 64, 256 B rows), then fewer
-        // until the grid has >= 128 workgroups, never under 8 lanes (32 B row segments)
+        // until the grid has >= UDPDK_SCAN_MIN_WG workgroups, never under 8 lanes (32 B row
+        // segments). Wider rows beat more workgroups: at 1024 lanes x 1024 tiles, 16-lane
+        // columns (64 workgroups) take 8.0 us, 8-lane (128) 11.9 us, 4-lane (256) 13.0 us.
         const uint32_t cmin = ceil_div(tiles, SCAN_COLS_TPT);
         uint32_t lb = 0;
         while ((2u << lb) <= std::min<uint32_t>(64u, SCAN_COLS_BLOCK / cmin)) ++lb;
-        while (lb > 3 && ceil_div(S, 1u << lb) < 128u) --lb;
+        while (lb > 3 && ceil_div(S, 1u << lb) < UDPDK_SCAN_MIN_WG) --lb;
         HIPC(c, launch(st, ts, 1, true, !lane_once, rx_scan_cols, dim3(ceil_div(S, 1u << lb)),
                        dim3(SCAN_COLS_BLOCK), 0u, sa, lb));
         if (lane_once)
