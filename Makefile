@@ -63,6 +63,25 @@ $(PROF_LIB): $(HIP_OBJ) $(PROF_OBJ)
 	@mkdir -p tools/diag/pollprof
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -Wl,--no-undefined -Wl,-soname,libudpdk_amd.so
 
+# A/B variant of the library (tools/ab.py): `make variant VAR=name VFLAGS="-DX=1"` builds
+# tools/var/name.so from the same sources with extra compile flags; never used by tests/bench
+VAR       ?= new
+VFLAGS    ?=
+VAR_OBJ   := $(patsubst udpdk_amd/csrc/%.hip,build/var/$(VAR)/%.o,$(HIP_SRC)) \
+             $(patsubst udpdk_amd/csrc/host/%.c,build/var/$(VAR)/host/%.o,$(C_SRC))
+variant: tools/var/$(VAR).so
+build/var/$(VAR)/%.o: udpdk_amd/csrc/%.hip $(HDRS) FORCE
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) $(INC) -c $< -o $@
+build/var/$(VAR)/host/%.o: udpdk_amd/csrc/host/%.c $(HDRS) FORCE
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS_H) $(VFLAGS) $(INC) -c $< -o $@
+tools/var/$(VAR).so: $(VAR_OBJ)
+	@mkdir -p tools/var
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -Wl,--no-undefined \
+	    -Wl,-soname,libudpdk_amd.so -Wl,--version-script=udpdk_amd/csrc/libudpdk_amd.map
+FORCE:
+
 asm: udpdk_amd/csrc/rx_kernels.hip $(HDRS)
 	@mkdir -p build/asm
 	$(HIPCC) $(HIPFLAGS) -Wno-unused-command-line-argument $(INC) -S --cuda-device-only -o build/asm/rx_kernels.s $<
@@ -72,4 +91,4 @@ clean:
 	rm -rf build $(LIB) $(TOOLS)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean asm stamps pollprof
+.PHONY: all oracle clean asm stamps pollprof variant FORCE

@@ -38,8 +38,8 @@ extern "C" {
 /* ---- reference surface (udpdk_api.h:19-41) ------------------------------------------------ */
 
 /* Parse "-c <file.ini>" (keys [port0] mac_addr / ip_addr, [port0_dst] mac_addr as in
- * udpdk_args.c:21-49; optional [gpu] device / max_frames / max_lanes) and create the GPU
- * context. Returns 0, or -1 with errno. */
+ * udpdk_args.c:21-49; optional [gpu] device / devices / max_frames / max_lanes / port ...,
+ * INTEGRATION.md) and create the GPU context(s). Returns 0, or -1 with errno. */
 int udpdk_init(int argc, char *argv[]);
 
 /* Make blocking calls (udpdk_recvfrom) return -1/EINTR (udpdk_init.c:374-378). */
@@ -87,6 +87,11 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
                   const uint16_t *length, const uint32_t *ptype, uint32_t n,
                   udpdk_rx_stats_t *stats);
 
+/* Deliveries udpdk_poll_rx dropped because the pinned payload slabs ([gpu] slab_bytes_max /
+ * slab_count_max, default 4 GiB / 1024 slabs) were all held by datagrams not yet received: the
+ * reference's mbuf pool exhausted. */
+uint64_t udpdk_rx_nobufs(void);
+
 /* TX exit point (the poller's TX half, udpdk_poller.c:453-514): take queued datagrams in the
  * poller's order (sockets in index order, each drained while the burst holds fewer than
  * BURST_SIZE frames), build their frames on the GPU (header build, rte_ipv4_cksum, payload copy,
@@ -99,6 +104,10 @@ int udpdk_tx_drain(uint8_t *out, uint64_t out_cap, uint32_t *out_off, uint16_t *
 
 /* Datagrams waiting in the TX rings. */
 uint64_t udpdk_tx_pending(void);
+
+/* Datagrams udpdk_tx_drain dropped because they needed more frames or bytes than a drain with
+ * the caller's limits can ever carry (they would otherwise block their socket's ring). */
+uint64_t udpdk_tx_dropped(void);
 
 /* ---- the poller thread ----------------------------------------------------------------------
  * The reference forks a poller process that busy-polls NIC port 0 (udpdk_init.c:293-368,
@@ -130,6 +139,14 @@ int udpdk_btable_snapshot(udpdk_bind_snapshot_t *snap, int compat);
 
 /* The GPU context created by udpdk_init (NULL before). */
 udpdk_gpu_ctx *udpdk_gpu_context(void);
+
+/* The devices polls run on: with "[gpu] devices = 0-7" (two or more entries) udpdk_init creates
+ * one RX shard context per entry and udpdk_poll_rx splits every batch into that many contiguous
+ * shards, each classified, demultiplexed and gathered on its own device by its own pool thread;
+ * the shards' lanes are concatenated in shard order before ring admission, so the rings are those
+ * of a single-context poll. Fragments go through the main context's reassembly table. Writes up
+ * to max device ids and returns how many there are (1 without "devices", 0 before udpdk_init). */
+int udpdk_shard_devices(int *devices, int max);
 
 /* TX header configuration (what udpdk_init reads from the .ini). Raw network-order IPv4. */
 int udpdk_config_set(const uint8_t src_mac[6], const uint8_t dst_mac[6], uint32_t src_ip_raw);

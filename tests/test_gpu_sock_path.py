@@ -26,14 +26,17 @@ SRC_MAC, DST_MAC, SRC_IP = "68:05:ca:95:f8:ec", "68:05:ca:95:fa:64", "172.31.100
 
 @pytest.fixture()
 def api(tmp_path, host_api, request):
-    """udpdk_init over a test ini; indirect parametrization sets [gpu] poll_threads."""
-    threads = getattr(request, "param", None)
+    """udpdk_init over a test ini; indirect parametrization sets [gpu] poll_threads (an int) or
+    adds [gpu] lines (a str)."""
+    param = getattr(request, "param", None)
+    threads = param if isinstance(param, int) else None
+    extra = param if isinstance(param, str) else ""
     ini = tmp_path / "udpdk.ini"
     ini.write_text(f"[port0]\nmac_addr = {SRC_MAC}\nip_addr = {SRC_IP}\n"
                    f"[port0_dst]\nmac_addr = {DST_MAC}\n"
                    "[gpu]\ndevice = 0\nmax_frames = 65536\nmax_lanes = 64\n"
                    "frag_buckets = 64\nfrag_bucket_entries = 16\nfrag_max_dgram = 16384\n"
-                   + (f"poll_threads = {threads}\n" if threads else ""))
+                   + (f"poll_threads = {threads}\n" if threads else "") + extra)
     L = abi.lib()
     argv = (C.c_char_p * 4)(b"prog", b"-c", str(ini).encode(), None)
     assert L.udpdk_init(3, argv) == 0
@@ -287,3 +290,79 @@ def test_two_threads_poller_and_app_over_loopback(api):
     finally:
         watchdog.cancel()
         assert L.udpdk_port_detach() == 0
+
+
+def test_autobind_sendto_while_poller_runs(api):
+    """A sendto that auto-binds its socket (or a close + socket + bind) while the poller thread
+    drains TX: every frame carries the source port the socket had when its datagram was queued,
+    never the slot row of the previous owner or of the unbound socket (udpdk_tx_drain takes the
+    TX lock before it releases the table lock that covers its slot-table refresh)."""
+    L = abi.lib()
+    ops = abi.PortOps()
+    assert L.udpdk_port_loopback(C.byref(ops)) == 0
+    ops.batch_frames = 256
+    rcv, hold = api.socket(), api.socket()
+    assert api.bind(rcv, "0.0.0.0", 10001) == 0
+    assert api.bind(hold, "0.0.0.0", 0) == 0         # raw port 0 taken: auto-bind gets raw 1 (256)
+    assert L.udpdk_port_attach(C.byref(ops)) == 0
+    watchdog = threading.Timer(60.0, L.udpdk_interrupt, [0])
+    watchdog.start()
+    try:
+        for k in range(400):
+            s = api.socket()
+            want = 256
+            if k % 2:
+                want = 12000 + k
+                assert api.bind(s, "0.0.0.0", want) == 0
+            pl = bytes([k & 0xFF, k >> 8]) * 4
+            assert api.sendto(s, pl, SRC_IP, 10001) == 8
+            n, data, addr = api.recvfrom(rcv, 64)
+            assert (n, data, addr) == (8, pl, (SRC_IP, want)), k
+            assert api.close(s) == 0
+    finally:
+        watchdog.cancel()
+        assert L.udpdk_port_detach() == 0
+
+
+@pytest.mark.parametrize("api", ["slab_bytes_max = 606208\nslab_count_max = 2\n"], indirect=True)
+def test_slab_budget_drops_polls_like_an_exhausted_pool(api):
+    """Payload slabs are pinned host memory held until every datagram in them is received: with
+    the budget at two slabs, a third poll while both are held is dropped whole (rx_nobufs, as
+    rte_eth_rx_burst returns nothing from an exhausted mempool); once one slab's datagrams are
+    read it is reused. Slab footprint here: 4096 slots x 64 B + 10 B per slot = 303,104 B."""
+    socks = [api.socket() for _ in range(4)]
+    for k, s in enumerate(socks):
+        assert api.bind(s, "0.0.0.0", 10001 + k) == 0
+    batches = [_rx_batch([10001 + k] * 1000, seed=40 + k) for k in range(4)]
+    _poll(batches[0])
+    _poll(batches[1])
+    assert api.rx_nobufs() == 0
+    _poll(batches[2])                                   # both slabs held: dropped
+    assert api.rx_nobufs() == 1000
+    for i in range(1000):
+        n, data, _ = api.recvfrom(socks[0], 2048)
+        o, ln = int(batches[0].offset[i]), int(batches[0].length[i])
+        assert data == bytes(batches[0].frames[o + 42:o + ln])
+    _poll(batches[3])                                   # slab 0 is free again
+    assert api.rx_nobufs() == 1000
+    for k in (1, 3):
+        for i in range(1000):
+            n, data, _ = api.recvfrom(socks[k], 2048)
+            o, ln = int(batches[k].offset[i]), int(batches[k].length[i])
+            assert data == bytes(batches[k].frames[o + 42:o + ln])
+    abi.lib().udpdk_interrupt(0)
+    assert api.recvfrom(socks[2], 64)[0] == -1          # the dropped poll left nothing queued
+
+
+def test_tx_datagram_larger_than_any_drain_is_dropped(api):
+    """A queued datagram that needs more frames than the drain's limit (8000 B = 6 fragments at
+    MTU 1500, max_frames 4) can never be carried: it is dropped and counted instead of blocking
+    its socket's ring forever; the datagrams behind it still go out."""
+    s = api.socket()
+    assert api.bind(s, "0.0.0.0", 10000) == 0
+    assert api.sendto(s, _payload(8000, 1), "172.31.100.1", 10001) == 8000
+    small = _payload(100, 2)
+    assert api.sendto(s, small, "172.31.100.1", 10001) == 100
+    frames = api.tx_drain(max_frames=4, cap=1 << 16)
+    assert api.tx_dropped() == 1 and api.tx_pending() == 0
+    assert len(frames) == 1 and frames[0][42:] == small

@@ -156,3 +156,30 @@ def test_init_requires_config():
     L = abi.lib()
     argv = (C.c_char_p * 2)(b"prog", None)
     assert L.udpdk_init(1, argv) == -1
+
+
+def test_close_unblocks_a_blocked_recvfrom(host_api):
+    """A recvfrom blocked on an empty ring in another thread (the reference busy-waits,
+    udpdk_syscall.c:424-426) returns -1/EBADF when the socket is closed under it, instead of
+    reading ring entries close has freed; the slot is reusable afterwards."""
+    import threading
+    s = host_api.socket()
+    assert host_api.bind(s, "0.0.0.0", 10001) == 0
+    out = {}
+
+    def reader():
+        n, _, _ = host_api.recvfrom(s, 64)
+        out["rc"], out["errno"] = n, host_api.errno()    # errno is per thread
+    for _ in range(20):
+        t = threading.Thread(target=reader)
+        t.start()
+        t.join(0.02)
+        assert t.is_alive()                              # blocked: nothing was queued
+        assert host_api.close(s) == 0
+        t.join(10)
+        assert not t.is_alive() and out == {"rc": -1, "errno": errno.EBADF}
+        assert host_api.socket() == s and host_api.bind(s, "0.0.0.0", 10001) == 0
+        out.clear()
+    # a recvfrom on a closed socket fails at once
+    assert host_api.close(s) == 0
+    assert host_api.recvfrom(s, 64)[0] == -1 and host_api.errno() == errno.EBADF

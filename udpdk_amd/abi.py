@@ -194,10 +194,13 @@ _PROTOS = {
     "udpdk_tx_drain": (C.c_int, [_P, C.c_uint64, _P, _P, C.c_uint32, C.POINTER(C.c_uint32)]),
     "udpdk_btable_snapshot": (C.c_int, [C.POINTER(BindSnapshot), C.c_int]),
     "udpdk_gpu_context": (_P, []),
+    "udpdk_shard_devices": (C.c_int, [_P, C.c_int]),
     "udpdk_config_set": (C.c_int, [_P, _P, C.c_uint32]),
     "udpdk_config_get": (C.c_int, [_P, _P, C.POINTER(C.c_uint32)]),
     "udpdk_config_mtu": (C.c_int, [C.c_uint32]),
     "udpdk_tx_pending": (C.c_uint64, []),
+    "udpdk_tx_dropped": (C.c_uint64, []),
+    "udpdk_rx_nobufs": (C.c_uint64, []),
     "udpdk_port_attach": (C.c_int, [C.POINTER(PortOps)]),
     "udpdk_port_detach": (C.c_int, []),
     "udpdk_port_loopback": (C.c_int, [C.POINTER(PortOps)]),
@@ -659,6 +662,12 @@ class HostApi:
 
     def tx_pending(self) -> int:
         return int(self.L.udpdk_tx_pending())
+
+    def tx_dropped(self) -> int:
+        return int(self.L.udpdk_tx_dropped())
+
+    def rx_nobufs(self) -> int:
+        return int(self.L.udpdk_rx_nobufs())
 
     def slots(self, n: int = 8):
         t = (Slot * n)()

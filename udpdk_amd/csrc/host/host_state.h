@@ -56,6 +56,11 @@ struct h_ring {                  /* SP/SC ring of EXCH_RING_SIZE entries (udpdk_
      * per run of a slab's entries instead of one per recvfrom) */
     struct h_arena *rel_arena;
     uint32_t rel_n;
+    /* close vs a recvfrom blocked on another thread: recvfrom raises busy for its whole call and
+     * leaves with EBADF once closing is set; close sets closing and waits for busy to drop before
+     * it clears the ring (both seq_cst, so one of the two sees the other) */
+    atomic_int busy;
+    atomic_int closing;
 };
 
 struct h_txd {                   /* one sendto waiting for the poller's TX half                  */
@@ -81,6 +86,34 @@ struct h_slot {                  /* exch_slot_info (udpdk_types.h:40-47) + bind 
     uint8_t  reuse_addr, reuse_port;
     struct h_ring rx;
     struct h_txq  tx;
+};
+
+/* Device buffers of one context's payload gather (the gather list + the kernel's outputs). */
+struct h_gbuf {
+    void     *acc, *pay, *len, *sip, *spt;
+    uint64_t  acc_cap, pay_cap, len_cap, sip_cap, spt_cap;
+};
+
+#define H_MAX_DEVS 16            /* [gpu] devices: RX shard contexts */
+
+/* One RX shard of a multi-device poll ([gpu] devices = 0-7): a contiguous range of the poll's
+ * frames processed by its own GPU context (one pool thread drives each). */
+struct h_shard {
+    udpdk_gpu_ctx *g;
+    int       device;
+    uint32_t  i0, n;             /* frames [i0, i0 + n) of the poll                             */
+    uint64_t  lo, bytes;         /* the frame bytes they span (lo 16-byte aligned)              */
+    uint32_t *off;  uint64_t off_cap;                 /* offsets rebased to lo                  */
+    uint32_t *meta, *loff, *lpkt;
+    uint64_t  meta_cap, loff_cap, lpkt_cap;
+    udpdk_rx_stats_t st;
+    int       err;               /* errno of a failed step, 0 = fine                             */
+    /* payload gather of the accepted entries that are this shard's frames */
+    uint32_t  nacc;
+    uint64_t  acc_bytes;
+    uint32_t *acc, *acco;  uint64_t acc_cap, acco_cap;  /* local frame index, packed slot offset */
+    struct h_gbuf gb;
+    struct h_arena *arena;
 };
 
 struct h_state {
@@ -119,15 +152,34 @@ struct h_state {
     uint32_t *acc_do, *acc_fo;                   /* their packed slot offsets (+ the total)    */
     uint32_t *acc_sock;                          /* per accepted entry: socket | from-frag<<31 */
     uint64_t  acc_d_cap, acc_f_cap, acc_do_cap, acc_fo_cap, acc_sock_cap;
-    void     *dv_acc, *dv_pay, *dv_len, *dv_sip, *dv_spt;   /* device: gather list + outputs */
-    uint64_t  dv_acc_cap, dv_pay_cap, dv_len_cap, dv_sip_cap, dv_spt_cap;
+    struct h_gbuf gb;                            /* device: gather list + outputs (context 0)  */
+    /* multi-device RX ([gpu] devices): n_shards > 1 splits every poll into contiguous shards over
+     * the shard contexts; the context above (g_udpdk.gpu) keeps TX and the reassembly table */
+    uint32_t  n_shards;
+    int       shard_dev[H_MAX_DEVS];
+    struct h_shard shard[H_MAX_DEVS];
+    uint8_t  *acc_dk;                            /* per accepted direct entry: its shard        */
+    uint32_t *acc_di;                            /* ... and its index in that shard's slab      */
+    uint64_t  acc_dk_cap, acc_di_cap;
+    uint8_t  *fb_frames;                         /* FRAG frames of a sharded poll, host copy    */
+    uint32_t *fb_off, *fb_idx, *fb_meta, *fb_loff, *fb_lpkt, *fb_pt;
+    uint16_t *fb_len;
+    uint64_t  fb_frames_cap, fb_off_cap, fb_idx_cap, fb_meta_cap, fb_loff_cap, fb_lpkt_cap, fb_pt_cap,
+              fb_len_cap;
     void     *dv_meta2, *dv_loff2, *dv_lpkt2;              /* device: RX of reassembled batch */
     uint64_t  dv_meta2_cap, dv_loff2_cap, dv_lpkt2_cap;
     struct h_arena *arena_free;
+    /* pinned slab budget (the mbuf pool's fixed size, udpdk_init.c:78-79): bytes and slabs held
+     * by live + free slabs, capped by [gpu] slab_bytes_max / slab_count_max; a poll whose payloads
+     * find no slab within the budget drops its bursts (rx_nobufs), as rte_eth_rx_burst does when
+     * the mempool is exhausted */
+    uint64_t  arena_bytes, arena_bytes_max, rx_nobufs;
+    uint32_t  arena_count, arena_count_max, arena_free_n;
     /* TX: per-socket rings of struct h_txd + the payload store they point into */
     uint8_t  *txp;
     uint64_t  txp_bytes, txp_cap;
     uint64_t  tx_queued;                         /* datagrams in all TX rings                   */
+    uint64_t  tx_dropped;                        /* too large for the drain's limits (tx_drain)  */
     /* TX work buffers (tx_drain), grow-only: host pinned staging + device */
     void     *tx_h, *tx_d, *tx_fr_d;
     uint64_t  tx_h_cap, tx_d_cap, tx_fr_d_cap;
@@ -168,8 +220,10 @@ void h_pool_stop(void);
 /* rx_poll.c */
 int  h_snapshot_refresh(void);            /* under g_udpdk.lock */
 void h_rx_buffers_free(void);
+void h_shards_destroy(void);
 void udpdk_poll_profile_dump(void);   /* -DUDPDK_POLL_PROFILE builds: phase times to stderr */
 int  h_grow_dev(void **p, uint64_t *cap, uint64_t need);
+int  h_grow_dev_on(udpdk_gpu_ctx *g, void **p, uint64_t *cap, uint64_t need);
 int  h_grow_host(void **p, uint64_t *cap, uint64_t need);
 
 /* tx_drain.c */

@@ -19,6 +19,23 @@
 
 #include "host_state.h"
 
+/* The [gpu] tunables' defaults: set at load and again by every udpdk_init that creates the
+ * context, so one session's .ini never leaks into the next. */
+static void h_config_defaults(void)
+{
+    g_udpdk.gpu_device = 0;
+    g_udpdk.n_shards = 0;
+    g_udpdk.poll_threads = 0;
+    g_udpdk.gpu_max_frames = 1u << 20;
+    g_udpdk.gpu_max_lanes = UDPDK_MAX_SOCKETS;
+    g_udpdk.frag_buckets = 0x1000;     /* NUM_FLOWS_DEF, udpdk_constants.h:32 */
+    g_udpdk.frag_entries = 16;         /* IP_FRAG_TBL_BUCKET_ENTRIES */
+    g_udpdk.frag_max_dgram = 65515;
+    g_udpdk.frag_ttl_ms = 1000;        /* MAX_FLOW_TTL = MS_PER_S */
+    g_udpdk.arena_bytes_max = 4ull << 30;
+    g_udpdk.arena_count_max = 1024;
+}
+
 __attribute__((constructor)) static void h_lib_load(void)
 {
     pthread_mutex_init(&g_udpdk.lock, NULL);
@@ -28,17 +45,15 @@ __attribute__((constructor)) static void h_lib_load(void)
     h_btable_reset();
     h_sockets_reset();
     g_udpdk.snap_version = UINT64_MAX;
-    g_udpdk.gpu_max_frames = 1u << 20;
-    g_udpdk.gpu_max_lanes = UDPDK_MAX_SOCKETS;
-    g_udpdk.frag_buckets = 0x1000;     /* NUM_FLOWS_DEF, udpdk_constants.h:32 */
-    g_udpdk.frag_entries = 16;         /* IP_FRAG_TBL_BUCKET_ENTRIES */
-    g_udpdk.frag_max_dgram = 65515;
-    g_udpdk.frag_ttl_ms = 1000;        /* MAX_FLOW_TTL = MS_PER_S */
+    h_config_defaults();
 }
+
+static void h_lo_reset(void);
 
 void udpdk_host_reset(void)
 {
     udpdk_port_detach();
+    h_lo_reset();
     pthread_mutex_lock(&g_udpdk.lock);
     pthread_mutex_lock(&g_udpdk.tx_lock);
     h_btable_reset();
@@ -67,6 +82,38 @@ static char *h_trim(char *s)
     char *e = s + strlen(s);
     while (e > s && isspace((unsigned char)e[-1])) *--e = 0;
     return s;
+}
+
+/* "[gpu] devices = 0-3,5,5": the RX shard contexts, one per entry, in shard order (a device
+ * may repeat: several contexts on one GPU). The first entry is also the main context's device. */
+static int h_parse_devices(const char *v)
+{
+    uint32_t n = 0;
+    const char *p = v;
+    while (*p) {
+        char *e;
+        const long a = strtol(p, &e, 10);
+        if (e == p || a < 0) return -1;
+        long b = a;
+        p = e;
+        if (*p == '-') {
+            b = strtol(p + 1, &e, 10);
+            if (e == p + 1 || b < a) return -1;
+            p = e;
+        }
+        for (long d = a; d <= b; d++) {
+            if (n == H_MAX_DEVS) return -1;
+            g_udpdk.shard_dev[n++] = (int)d;
+        }
+        while (*p == ' ' || *p == '\t') p++;
+        if (*p == ',') p++;
+        else if (*p) return -1;
+        while (*p == ' ' || *p == '\t') p++;
+    }
+    if (!n) return -1;
+    g_udpdk.n_shards = n;
+    g_udpdk.gpu_device = g_udpdk.shard_dev[0];
+    return 0;
 }
 
 /* Minimal INI reader for the keys the reference understands plus a [gpu] section. */
@@ -100,6 +147,8 @@ static int h_load_ini(const char *path)
             if (udpdk_config_mtu((uint32_t)strtoul(v, NULL, 0))) { rc = -1; break; }
         } else if (!strcmp(section, "gpu") && !strcmp(k, "device")) {
             g_udpdk.gpu_device = atoi(v);
+        } else if (!strcmp(section, "gpu") && !strcmp(k, "devices")) {
+            if (h_parse_devices(v)) { rc = -1; break; }
         } else if (!strcmp(section, "gpu") && !strcmp(k, "max_frames")) {
             g_udpdk.gpu_max_frames = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "max_lanes")) {
@@ -112,6 +161,10 @@ static int h_load_ini(const char *path)
             g_udpdk.frag_entries = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "frag_max_dgram")) {
             g_udpdk.frag_max_dgram = (uint32_t)strtoul(v, NULL, 0);
+        } else if (!strcmp(section, "gpu") && !strcmp(k, "slab_bytes_max")) {
+            g_udpdk.arena_bytes_max = strtoull(v, NULL, 0);
+        } else if (!strcmp(section, "gpu") && !strcmp(k, "slab_count_max")) {
+            g_udpdk.arena_count_max = (uint32_t)strtoul(v, NULL, 0);
         }
         /* [dpdk] lcores / n_mem_channels configure EAL, which does not exist here */
     }
@@ -128,13 +181,40 @@ int udpdk_init(int argc, char *argv[])
         else if (!strncmp(argv[i], "-c", 2) && argv[i][2]) cfg = argv[i] + 2;
     }
     if (!cfg) { errno = EINVAL; return -1; }       /* config file is mandatory (args.c:150-155) */
+    if (!g_udpdk.gpu) h_config_defaults();
     if (h_load_ini(cfg)) { errno = EINVAL; return -1; }
     if (g_udpdk.gpu) return 0;
-    const int rc = udpdk_gpu_ctx_create(g_udpdk.gpu_device, g_udpdk.gpu_max_frames,
-                                        g_udpdk.gpu_max_lanes, &g_udpdk.gpu);
+    int rc = udpdk_gpu_ctx_create(g_udpdk.gpu_device, g_udpdk.gpu_max_frames,
+                                  g_udpdk.gpu_max_lanes, &g_udpdk.gpu);
     if (rc) { errno = rc == -ENODEV ? ENODEV : -rc; g_udpdk.gpu = NULL; return -1; }
+    /* [gpu] devices with two or more entries: one RX shard context per entry (SURVEY.md §7 step
+     * 8); a poll splits its batch into that many contiguous shards */
+    if (g_udpdk.n_shards > 1) {
+        for (uint32_t k = 0; k < g_udpdk.n_shards && !rc; k++) {
+            g_udpdk.shard[k].device = g_udpdk.shard_dev[k];
+            rc = udpdk_gpu_ctx_create(g_udpdk.shard_dev[k], g_udpdk.gpu_max_frames, g_udpdk.gpu_max_lanes,
+                                      &g_udpdk.shard[k].g);
+        }
+        if (rc) {
+            h_shards_destroy();
+            udpdk_gpu_ctx_destroy(g_udpdk.gpu);
+            g_udpdk.gpu = NULL;
+            errno = rc == -ENODEV ? ENODEV : -rc;
+            return -1;
+        }
+    } else {
+        g_udpdk.n_shards = 0;
+    }
     g_udpdk.snap_version = UINT64_MAX;
     return 0;
+}
+
+int udpdk_shard_devices(int *devices, int max)
+{
+    const int n = g_udpdk.n_shards > 1 ? (int)g_udpdk.n_shards : (g_udpdk.gpu ? 1 : 0);
+    for (int k = 0; devices && k < n && k < max; k++)
+        devices[k] = g_udpdk.n_shards > 1 ? g_udpdk.shard[k].device : g_udpdk.gpu_device;
+    return n;
 }
 
 void udpdk_interrupt(int signum)
@@ -146,6 +226,7 @@ void udpdk_interrupt(int signum)
 void udpdk_cleanup(void)
 {
     udpdk_port_detach();
+    h_lo_reset();
     udpdk_poll_profile_dump();
     h_pool_stop();
     for (int s = 0; s < UDPDK_MAX_SOCKETS; s++)
@@ -155,6 +236,7 @@ void udpdk_cleanup(void)
     h_tx_buffers_free();
     h_arenas_free_all();
     g_udpdk.frag_ready = 0;
+    h_shards_destroy();
     udpdk_gpu_ctx_destroy(g_udpdk.gpu);
     g_udpdk.gpu = NULL;
     g_udpdk.snap_version = UINT64_MAX;
@@ -273,6 +355,15 @@ static struct {
     uint64_t n, ncap, nhead;
 } h_lo = {PTHREAD_MUTEX_INITIALIZER, NULL, 0, 0, 0, NULL, 0, 0, 0};
 
+/* Empty the FIFO: frames of an earlier session never reach a later one's RX. */
+static void h_lo_reset(void)
+{
+    pthread_mutex_lock(&h_lo.mu);
+    h_lo.bytes = h_lo.head = 0;
+    h_lo.n = h_lo.nhead = 0;
+    pthread_mutex_unlock(&h_lo.mu);
+}
+
 static void h_lo_tx(void *user, const uint8_t *frames, const uint32_t *off, const uint16_t *len, uint32_t n)
 {
     (void)user;
@@ -335,6 +426,7 @@ int udpdk_port_loopback(udpdk_port_ops_t *ops)
 {
     if (!ops) { errno = EINVAL; return -1; }
     memset(ops, 0, sizeof(*ops));
+    h_lo_reset();
     ops->rx_burst = h_lo_rx;
     ops->tx_burst = h_lo_tx;
     return 0;

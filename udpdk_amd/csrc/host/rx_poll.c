@@ -13,6 +13,15 @@
  *   5. the ring entries are published; recvfrom copies from the slab and releases it.
  * The bind snapshot is uploaded only when the bind table's version has moved since the last
  * upload (no per-call walk of the 65,536 ports).
+ *
+ * Multi-device ([gpu] devices = 0-7): step 1 runs per contiguous
+ * shard of the batch on its own context (one pool thread per shard: H2D, kernels, D2H on that
+ * device), and the shards' per-socket lanes are concatenated in shard order, which is global
+ * arrival order because each shard is contiguous and its lanes are stable. The FRAG frames of
+ * all shards go, in arrival order, through the one reassembly table of the main context (a flow's
+ * fragments may straddle shards). Step 4 gathers each shard's admitted payloads on its own device
+ * into a slab of its own. Admission (3) and publication (5) are the single-device code on the
+ * merged lanes, so the rings equal a single-context poll's.
  */
 #include <errno.h>
 #include <stdlib.h>
@@ -49,17 +58,27 @@ __attribute__((visibility("hidden"))) void udpdk_poll_profile_dump(void)
 void udpdk_poll_profile_dump(void) {}
 #endif
 
-int h_grow_dev(void **p, uint64_t *cap, uint64_t need)
+int h_grow_dev_on(udpdk_gpu_ctx *g, void **p, uint64_t *cap, uint64_t need)
 {
     if (*p && *cap >= need) return 0;
-    if (*p) udpdk_gpu_free(g_udpdk.gpu, *p);
+    if (*p) udpdk_gpu_free(g, *p);
     *p = NULL;
     *cap = 0;
     uint64_t nc = need < 4096 ? 4096 : need + need / 4;
-    const int rc = udpdk_gpu_alloc(g_udpdk.gpu, nc, p);
+    const int rc = udpdk_gpu_alloc(g, nc, p);
     if (rc) { errno = -rc; return -1; }
     *cap = nc;
     return 0;
+}
+
+int h_grow_dev(void **p, uint64_t *cap, uint64_t need) { return h_grow_dev_on(g_udpdk.gpu, p, cap, need); }
+
+static void h_gbuf_free(udpdk_gpu_ctx *g, struct h_gbuf *b)
+{
+    void *d[] = {b->acc, b->pay, b->len, b->sip, b->spt};
+    for (unsigned k = 0; k < 5; k++)
+        if (d[k] && g) udpdk_gpu_free(g, d[k]);
+    memset(b, 0, sizeof(*b));
 }
 
 int h_grow_host(void **p, uint64_t *cap, uint64_t need)
@@ -78,26 +97,45 @@ void h_rx_buffers_free(void)
     void **host[] = {(void **)&g_udpdk.rx_meta, (void **)&g_udpdk.rx_loff, (void **)&g_udpdk.rx_lpkt,
                      (void **)&g_udpdk.fr_loff, (void **)&g_udpdk.fr_lpkt, (void **)&g_udpdk.fr_org,
                      (void **)&g_udpdk.fr_len, (void **)&g_udpdk.acc_d, (void **)&g_udpdk.acc_f,
-                     (void **)&g_udpdk.acc_do, (void **)&g_udpdk.acc_fo, (void **)&g_udpdk.acc_sock};
+                     (void **)&g_udpdk.acc_do, (void **)&g_udpdk.acc_fo, (void **)&g_udpdk.acc_sock,
+                     (void **)&g_udpdk.acc_dk, (void **)&g_udpdk.acc_di, (void **)&g_udpdk.fb_frames,
+                     (void **)&g_udpdk.fb_off, (void **)&g_udpdk.fb_idx, (void **)&g_udpdk.fb_meta,
+                     (void **)&g_udpdk.fb_loff, (void **)&g_udpdk.fb_lpkt, (void **)&g_udpdk.fb_pt,
+                     (void **)&g_udpdk.fb_len};
     uint64_t *hcap[] = {&g_udpdk.rx_meta_cap, &g_udpdk.rx_loff_cap, &g_udpdk.rx_lpkt_cap,
                         &g_udpdk.fr_loff_cap, &g_udpdk.fr_lpkt_cap, &g_udpdk.fr_org_cap,
                         &g_udpdk.fr_len_cap, &g_udpdk.acc_d_cap, &g_udpdk.acc_f_cap,
-                        &g_udpdk.acc_do_cap, &g_udpdk.acc_fo_cap, &g_udpdk.acc_sock_cap};
+                        &g_udpdk.acc_do_cap, &g_udpdk.acc_fo_cap, &g_udpdk.acc_sock_cap,
+                        &g_udpdk.acc_dk_cap, &g_udpdk.acc_di_cap, &g_udpdk.fb_frames_cap,
+                        &g_udpdk.fb_off_cap, &g_udpdk.fb_idx_cap, &g_udpdk.fb_meta_cap,
+                        &g_udpdk.fb_loff_cap, &g_udpdk.fb_lpkt_cap, &g_udpdk.fb_pt_cap,
+                        &g_udpdk.fb_len_cap};
     for (unsigned k = 0; k < sizeof(host) / sizeof(host[0]); k++) {
         free(*host[k]);
         *host[k] = NULL;
         *hcap[k] = 0;
     }
-    void **dev[] = {&g_udpdk.dv_acc, &g_udpdk.dv_pay, &g_udpdk.dv_len, &g_udpdk.dv_sip,
-                    &g_udpdk.dv_spt, &g_udpdk.dv_meta2, &g_udpdk.dv_loff2, &g_udpdk.dv_lpkt2};
-    uint64_t *dcap[] = {&g_udpdk.dv_acc_cap, &g_udpdk.dv_pay_cap, &g_udpdk.dv_len_cap,
-                        &g_udpdk.dv_sip_cap, &g_udpdk.dv_spt_cap, &g_udpdk.dv_meta2_cap,
-                        &g_udpdk.dv_loff2_cap, &g_udpdk.dv_lpkt2_cap};
+    void **dev[] = {&g_udpdk.dv_meta2, &g_udpdk.dv_loff2, &g_udpdk.dv_lpkt2};
+    uint64_t *dcap[] = {&g_udpdk.dv_meta2_cap, &g_udpdk.dv_loff2_cap, &g_udpdk.dv_lpkt2_cap};
     for (unsigned k = 0; k < sizeof(dev) / sizeof(dev[0]); k++) {
         if (*dev[k] && g_udpdk.gpu) udpdk_gpu_free(g_udpdk.gpu, *dev[k]);
         *dev[k] = NULL;
         *dcap[k] = 0;
     }
+    h_gbuf_free(g_udpdk.gpu, &g_udpdk.gb);
+}
+
+/* The shard contexts and their buffers (udpdk_cleanup). */
+void h_shards_destroy(void)
+{
+    for (uint32_t k = 0; k < H_MAX_DEVS; k++) {
+        struct h_shard *S = &g_udpdk.shard[k];
+        h_gbuf_free(S->g, &S->gb);
+        free(S->off); free(S->meta); free(S->loff); free(S->lpkt); free(S->acc); free(S->acco);
+        if (S->g) udpdk_gpu_ctx_destroy(S->g);
+        memset(S, 0, sizeof(*S));
+    }
+    g_udpdk.n_shards = 0;
 }
 
 /* Upload the bind snapshot when the table changed since the last upload; keep its lane count
@@ -107,7 +145,9 @@ int h_snapshot_refresh(void)
     if (g_udpdk.snap_version == g_udpdk.version) return 0;
     udpdk_bind_snapshot_t snap;
     if (udpdk_btable_snapshot(&snap, 0)) return -1;
-    const int rc = udpdk_gpu_bind_snapshot_upload(g_udpdk.gpu, &snap);
+    int rc = udpdk_gpu_bind_snapshot_upload(g_udpdk.gpu, &snap);
+    for (uint32_t k = 0; !rc && g_udpdk.n_shards > 1 && k < g_udpdk.n_shards; k++)
+        rc = udpdk_gpu_bind_snapshot_upload(g_udpdk.shard[k].g, &snap);
     if (rc) { errno = -rc; return -1; }
     uint32_t maxfan = 1;
     for (uint32_t p = 0; p < 65536; p++)
@@ -177,33 +217,32 @@ static int h_frag_pass(const udpdk_rx_batch_t *staged, const uint32_t *meta_dev,
  * slab of packed slots (entry k at offs[k], offs[count] bytes in all, each slot its frame's
  * payload room rounded up to 16): one gather launch, one D2H of each output, and only the
  * bytes that exist cross PCIe (a slot per longest datagram moved 4.6x the IMIX payload). */
-static int h_gather(const udpdk_rx_batch_t *b, const uint32_t *acc, const uint32_t *offs, uint32_t count,
-                    struct h_arena **out)
+static int h_gather(udpdk_gpu_ctx *g, struct h_gbuf *gb, const udpdk_rx_batch_t *b, const uint32_t *acc,
+                    const uint32_t *offs, uint32_t count, struct h_arena **out)
 {
     *out = NULL;
     if (!count) return 0;
-    udpdk_gpu_ctx *g = g_udpdk.gpu;
     const uint64_t bytes = offs[count] ? offs[count] : 16u;
     struct h_arena *a = h_arena_get(count, bytes);
-    if (!a) { errno = ENOMEM; return -1; }
+    if (!a) return -1;                             /* ENOBUFS (budget) or ENOMEM */
     int rc;
-    if (h_grow_dev(&g_udpdk.dv_acc, &g_udpdk.dv_acc_cap, 8ull * count + 4) ||
-        h_grow_dev(&g_udpdk.dv_pay, &g_udpdk.dv_pay_cap, bytes) ||
-        h_grow_dev(&g_udpdk.dv_len, &g_udpdk.dv_len_cap, 4ull * count) ||
-        h_grow_dev(&g_udpdk.dv_sip, &g_udpdk.dv_sip_cap, 4ull * count) ||
-        h_grow_dev(&g_udpdk.dv_spt, &g_udpdk.dv_spt_cap, 2ull * count)) {
+    if (h_grow_dev_on(g, &gb->acc, &gb->acc_cap, 8ull * count + 4) ||
+        h_grow_dev_on(g, &gb->pay, &gb->pay_cap, bytes) ||
+        h_grow_dev_on(g, &gb->len, &gb->len_cap, 4ull * count) ||
+        h_grow_dev_on(g, &gb->sip, &gb->sip_cap, 4ull * count) ||
+        h_grow_dev_on(g, &gb->spt, &gb->spt_cap, 2ull * count)) {
         h_arena_put(a);
         return -1;
     }
-    udpdk_rx_gather_t go = {g_udpdk.dv_pay, 16u, g_udpdk.dv_len, g_udpdk.dv_sip, g_udpdk.dv_spt};
-    uint32_t *dacc = g_udpdk.dv_acc, *doff = dacc + count;
+    udpdk_rx_gather_t go = {gb->pay, 16u, gb->len, gb->sip, gb->spt};
+    uint32_t *dacc = gb->acc, *doff = dacc + count;
     if ((rc = udpdk_gpu_h2d(g, dacc, acc, 4ull * count)) ||
         (rc = udpdk_gpu_h2d(g, doff, offs, 4ull * count + 4)) ||
         (rc = udpdk_gpu_rx_gather_packed(g, b, dacc, 0, count, doff, &go)) ||
-        (rc = udpdk_gpu_d2h(g, a->payload, g_udpdk.dv_pay, bytes)) ||
-        (rc = udpdk_gpu_d2h(g, a->len, g_udpdk.dv_len, 4ull * count)) ||
-        (rc = udpdk_gpu_d2h(g, a->src_ip, g_udpdk.dv_sip, 4ull * count)) ||
-        (rc = udpdk_gpu_d2h(g, a->src_port, g_udpdk.dv_spt, 2ull * count))) {
+        (rc = udpdk_gpu_d2h(g, a->payload, gb->pay, bytes)) ||
+        (rc = udpdk_gpu_d2h(g, a->len, gb->len, 4ull * count)) ||
+        (rc = udpdk_gpu_d2h(g, a->src_ip, gb->sip, 4ull * count)) ||
+        (rc = udpdk_gpu_d2h(g, a->src_port, gb->spt, 2ull * count))) {
         h_arena_put(a);
         errno = -rc;
         return -1;
@@ -325,6 +364,7 @@ static void h_adm_job(void *ctx, uint32_t part, uint32_t parts)
 struct h_pub {
     const struct h_adm *A;
     struct h_arena *ad, *af;
+    int sharded;                 /* direct entries in per-shard slabs (acc_dk / acc_di) */
 };
 
 static void h_pub_job(void *ctx, uint32_t part, uint32_t parts)
@@ -349,12 +389,13 @@ static void h_pub_job(void *ctx, uint32_t part, uint32_t parts)
                     d->src_port = af->src_port[kf];
                     kf++;
                 } else {
-                    struct h_arena *ad = P->ad;
+                    struct h_arena *ad = P->sharded ? g_udpdk.shard[g_udpdk.acc_dk[kd]].arena : P->ad;
+                    const uint32_t j = P->sharded ? g_udpdk.acc_di[kd] : kd;
                     d->arena = ad;
                     d->data = ad->payload + g_udpdk.acc_do[kd];
-                    d->len = ad->len[kd];
-                    d->src_ip = ad->src_ip[kd];
-                    d->src_port = ad->src_port[kd];
+                    d->len = ad->len[j];
+                    d->src_ip = ad->src_ip[j];
+                    d->src_port = ad->src_port[j];
                     kd++;
                 }
                 k++;
@@ -364,6 +405,236 @@ static void h_pub_job(void *ctx, uint32_t part, uint32_t parts)
             }
         }
     }
+}
+
+/* ---- multi-device shards ------------------------------------------------------------------ */
+struct h_sjob {
+    const uint8_t *frames;
+    uint64_t frames_bytes;
+    const uint32_t *offset;
+    const uint16_t *length;
+    const uint32_t *ptype;
+    uint32_t maxfan;
+};
+
+/* Shard k's RX on its own context: descriptors rebased to the 16-byte-aligned start of the frame
+ * bytes the shard spans (a descriptor outside the caller's frames keeps pointing outside the
+ * shard's, so it stays BAD_DESC), then udpdk_gpu_rx_host (H2D, kernels, D2H of its lanes). */
+static void h_shard_rx(const struct h_sjob *J, struct h_shard *S)
+{
+    S->err = 0;
+    memset(&S->st, 0, sizeof(S->st));
+    const uint32_t lanes = g_udpdk.snap_lanes;
+    if (h_grow_host((void **)&S->loff, &S->loff_cap, 4ull * (lanes + 1))) { S->err = errno; return; }
+    if (!S->n) {
+        memset(S->loff, 0, 4ull * (lanes + 1));
+        return;
+    }
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint32_t i = 0; i < S->n; i++) {
+        const uint64_t o = J->offset[S->i0 + i], e = o + J->length[S->i0 + i];
+        if (J->length[S->i0 + i] <= J->frames_bytes && o <= J->frames_bytes - J->length[S->i0 + i]) {
+            if (o < lo) lo = o;
+            if (e > hi) hi = e;
+        }
+    }
+    if (lo == UINT64_MAX) lo = hi = 0;
+    lo &= ~(uint64_t)15u;
+    S->lo = lo;
+    S->bytes = hi - lo;
+    const uint64_t cap = (uint64_t)S->n * J->maxfan;
+    if (h_grow_host((void **)&S->off, &S->off_cap, 4ull * S->n) ||
+        h_grow_host((void **)&S->meta, &S->meta_cap, 4ull * S->n + 4) ||
+        h_grow_host((void **)&S->lpkt, &S->lpkt_cap, 4ull * cap + 4)) { S->err = errno; return; }
+    for (uint32_t i = 0; i < S->n; i++) {
+        const uint64_t o = J->offset[S->i0 + i];
+        const uint32_t l = J->length[S->i0 + i];
+        const int ok = l <= J->frames_bytes && o <= J->frames_bytes - l;
+        S->off[i] = ok ? (uint32_t)(o - lo) : 0xFFFFFFFFu;    /* out of the shard: BAD_DESC */
+    }
+    const int rc = udpdk_gpu_rx_host(S->g, J->frames + lo, S->bytes, S->off, J->length + S->i0,
+                                     J->ptype ? J->ptype + S->i0 : NULL, S->n, S->meta, S->loff, S->lpkt,
+                                     cap > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)cap, &S->st);
+    if (rc) S->err = -rc;
+}
+
+static void h_shard_rx_job(void *ctx, uint32_t part, uint32_t parts)
+{
+    for (uint32_t k = part; k < g_udpdk.n_shards; k += parts) h_shard_rx(ctx, &g_udpdk.shard[k]);
+}
+
+/* the shards' lanes concatenated per socket in shard order, sockets split over the pool */
+struct h_merge {
+    uint32_t lanes;
+    uint32_t *loff, *lpkt;
+    uint32_t sb[H_MAX_WORKERS + 3];
+};
+
+static void h_merge_job(void *ctx, uint32_t part, uint32_t parts)
+{
+    const struct h_merge *M = ctx;
+    (void)parts;
+    for (uint32_t l = M->sb[part]; l < M->sb[part + 1]; l++) {
+        uint32_t w = M->loff[l];
+        for (uint32_t k = 0; k < g_udpdk.n_shards; k++) {
+            const struct h_shard *S = &g_udpdk.shard[k];
+            if (!S->n) continue;
+            const uint32_t a = S->loff[l], b = S->loff[l + 1], base = S->i0;
+            for (uint32_t e = a; e < b; e++) M->lpkt[w++] = S->lpkt[e] + base;
+        }
+    }
+}
+
+/* Step 1 over the shards: per-shard RX in parallel, then stats summed, lanes merged, verdict
+ * words concatenated (the FRAG frames are found in them). */
+static int h_shards_rx(const struct h_sjob *J, uint32_t n, uint32_t lanes, uint32_t *meta, uint32_t *loff,
+                       uint32_t *lpkt, udpdk_rx_stats_t *st)
+{
+    const uint32_t N = g_udpdk.n_shards;
+    for (uint32_t k = 0; k < N; k++) {
+        struct h_shard *S = &g_udpdk.shard[k];
+        S->i0 = (uint32_t)((uint64_t)n * k / N);
+        S->n = (uint32_t)((uint64_t)n * (k + 1) / N) - S->i0;
+    }
+    h_pool_run(h_shard_rx_job, (void *)J);
+    memset(st, 0, sizeof(*st));
+    for (uint32_t k = 0; k < N; k++) {
+        const struct h_shard *S = &g_udpdk.shard[k];
+        if (S->err) { errno = S->err; return -1; }
+        for (int c = 0; c < UDPDK_N_COUNTERS; c++) st->counters[c] += S->st.counters[c];
+        st->deliveries += S->st.deliveries;
+        st->overflow |= S->st.overflow;
+        if (S->n) memcpy(meta + S->i0, S->meta, 4ull * S->n);
+    }
+    for (uint32_t l = 0; l <= lanes; l++) {
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < N; k++)
+            if (g_udpdk.shard[k].n) v += g_udpdk.shard[k].loff[l];
+        loff[l] = v;
+    }
+    struct h_merge M = {lanes, loff, lpkt, {0}};
+    const uint32_t parts = h_pool_parts(), D = loff[lanes];
+    uint32_t l = 0;
+    for (uint32_t p = 1; p < parts; p++) {
+        const uint64_t want = (uint64_t)D * p / parts;
+        while (l < lanes && loff[l] < want) l++;
+        M.sb[p] = l;
+    }
+    M.sb[0] = 0;
+    M.sb[parts] = lanes;
+    h_pool_run(h_merge_job, &M);
+    return 0;
+}
+
+/* The FRAG frames of a sharded poll, in arrival order, copied into one host batch that the main
+ * context classifies (staging it on its device for the reassembly pass). fb_idx[j] = the poll
+ * index of sub-batch frame j. */
+static int h_frag_subbatch(const struct h_sjob *J, const uint32_t *meta, uint32_t n, uint32_t nfrag,
+                           uint32_t maxfan, udpdk_rx_batch_t *staged, const uint32_t **meta_dev)
+{
+    uint64_t bytes = 0;
+    for (uint32_t i = 0; i < n; i++)
+        if (UDPDK_META_VERDICT(meta[i]) == UDPDK_V_FRAG) bytes += J->length[i];
+    const uint32_t lanes = g_udpdk.snap_lanes;
+    if (h_grow_host((void **)&g_udpdk.fb_frames, &g_udpdk.fb_frames_cap, bytes + 64) ||
+        h_grow_host((void **)&g_udpdk.fb_off, &g_udpdk.fb_off_cap, 4ull * nfrag) ||
+        h_grow_host((void **)&g_udpdk.fb_len, &g_udpdk.fb_len_cap, 2ull * nfrag) ||
+        h_grow_host((void **)&g_udpdk.fb_idx, &g_udpdk.fb_idx_cap, 4ull * nfrag) ||
+        h_grow_host((void **)&g_udpdk.fb_pt, &g_udpdk.fb_pt_cap, 4ull * nfrag) ||
+        h_grow_host((void **)&g_udpdk.fb_meta, &g_udpdk.fb_meta_cap, 4ull * nfrag) ||
+        h_grow_host((void **)&g_udpdk.fb_loff, &g_udpdk.fb_loff_cap, 4ull * (lanes + 1)) ||
+        h_grow_host((void **)&g_udpdk.fb_lpkt, &g_udpdk.fb_lpkt_cap, 4ull * nfrag * maxfan + 4))
+        return -1;
+    uint32_t j = 0;
+    uint64_t pos = 0;
+    for (uint32_t i = 0; i < n && j < nfrag; i++) {
+        if (UDPDK_META_VERDICT(meta[i]) != UDPDK_V_FRAG) continue;
+        memcpy(g_udpdk.fb_frames + pos, J->frames + J->offset[i], J->length[i]);
+        g_udpdk.fb_off[j] = (uint32_t)pos;
+        g_udpdk.fb_len[j] = J->length[i];
+        g_udpdk.fb_pt[j] = J->ptype ? J->ptype[i] : 0u;
+        g_udpdk.fb_idx[j++] = i;
+        pos += J->length[i];
+    }
+    memset(g_udpdk.fb_frames + pos, 0, 16);
+    udpdk_rx_stats_t st;
+    int rc = udpdk_gpu_rx_host(g_udpdk.gpu, g_udpdk.fb_frames, pos, g_udpdk.fb_off, g_udpdk.fb_len,
+                               J->ptype ? g_udpdk.fb_pt : NULL, j, g_udpdk.fb_meta, g_udpdk.fb_loff,
+                               g_udpdk.fb_lpkt, j * maxfan, &st);
+    if (rc && rc != -ENOSPC) { errno = -rc; return -1; }
+    if ((rc = udpdk_gpu_rx_host_batch(g_udpdk.gpu, staged, meta_dev))) { errno = -rc; return -1; }
+    return 0;
+}
+
+static void h_shard_gather_job(void *ctx, uint32_t part, uint32_t parts)
+{
+    (void)ctx;
+    for (uint32_t k = part; k < g_udpdk.n_shards; k += parts) {
+        struct h_shard *S = &g_udpdk.shard[k];
+        S->err = 0;
+        S->arena = NULL;
+        if (!S->nacc) continue;
+        udpdk_rx_batch_t b;
+        int rc = udpdk_gpu_rx_host_batch(S->g, &b, NULL);
+        if (rc) { S->err = -rc; continue; }
+        if (h_gather(S->g, &S->gb, &b, S->acc, S->acco, S->nacc, &S->arena)) { S->err = errno; continue; }
+        if ((rc = udpdk_gpu_sync(S->g))) S->err = -rc;
+    }
+}
+
+/* Step 4 over the shards: each accepted direct entry goes to its frame's shard (acc_dk), at the
+ * next index of that shard's slab (acc_di) and slot offset (acc_do, rewritten per shard); each
+ * shard gathers its entries on its own device into a slab of its own. */
+static int h_shards_gather(uint32_t nad)
+{
+    const uint32_t N = g_udpdk.n_shards;
+    if (h_grow_host((void **)&g_udpdk.acc_dk, &g_udpdk.acc_dk_cap, (uint64_t)nad + 1) ||
+        h_grow_host((void **)&g_udpdk.acc_di, &g_udpdk.acc_di_cap, 4ull * nad + 4))
+        return -1;
+    for (uint32_t k = 0; k < N; k++) {
+        struct h_shard *S = &g_udpdk.shard[k];
+        S->nacc = 0;
+        S->acc_bytes = 0;
+        const uint64_t d = S->n ? (uint64_t)S->loff[g_udpdk.snap_lanes] : 0u;
+        if (h_grow_host((void **)&S->acc, &S->acc_cap, 4ull * d + 4) ||
+            h_grow_host((void **)&S->acco, &S->acco_cap, 4ull * d + 8))
+            return -1;
+    }
+    const uint32_t *slot = g_udpdk.acc_do;           /* packed slot offsets: sizes by difference */
+    for (uint32_t kd = 0; kd < nad; kd++) {
+        const uint32_t fi = g_udpdk.acc_d[kd];
+        uint32_t k = N - 1;
+        while (k && g_udpdk.shard[k].i0 > fi) k--;
+        struct h_shard *S = &g_udpdk.shard[k];
+        const uint32_t r = S->nacc++;
+        const uint32_t sz = slot[kd + 1] - slot[kd];
+        g_udpdk.acc_dk[kd] = (uint8_t)k;
+        g_udpdk.acc_di[kd] = r;
+        S->acc[r] = fi - S->i0;
+        S->acco[r] = (uint32_t)S->acc_bytes;
+        S->acc_bytes += sz;
+    }
+    for (uint32_t k = 0; k < N; k++) {
+        struct h_shard *S = &g_udpdk.shard[k];
+        if (S->acc_bytes > 0xFFFFFFF0ull) { errno = ENOBUFS; return -1; }
+        S->acco[S->nacc] = (uint32_t)S->acc_bytes;
+    }
+    /* the slot offsets now index the shards' slabs */
+    for (uint32_t kd = 0; kd < nad; kd++)
+        g_udpdk.acc_do[kd] = g_udpdk.shard[g_udpdk.acc_dk[kd]].acco[g_udpdk.acc_di[kd]];
+    h_pool_run(h_shard_gather_job, NULL);
+    int err = 0;
+    for (uint32_t k = 0; k < N; k++)
+        if (g_udpdk.shard[k].err && !err) err = g_udpdk.shard[k].err;
+    if (err) {
+        for (uint32_t k = 0; k < N; k++) {
+            if (g_udpdk.shard[k].arena) h_arena_put(g_udpdk.shard[k].arena);
+            g_udpdk.shard[k].arena = NULL;
+        }
+        errno = err;
+        return -1;
+    }
+    return 0;
 }
 
 int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *offset,
@@ -388,15 +659,32 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
         goto out;
     uint32_t *meta = g_udpdk.rx_meta, *loff = g_udpdk.rx_loff, *lpkt = g_udpdk.rx_lpkt;
     udpdk_rx_stats_t st;
-    if ((rc = udpdk_gpu_rx_host(g, frames, frames_bytes, offset, length, ptype, n, meta, loff, lpkt,
-                                cap, &st))) { errno = -rc; goto out; }
-    PROF_T(p2);
+    const int sharded = g_udpdk.n_shards > 1;
+    const struct h_sjob J = {frames, frames_bytes, offset, length, ptype, maxfan};
     udpdk_rx_batch_t staged;
     const uint32_t *meta_dev = NULL;
-    if ((rc = udpdk_gpu_rx_host_batch(g, &staged, &meta_dev))) { errno = -rc; goto out; }
+    if (sharded) {
+        if (h_shards_rx(&J, n, lanes, meta, loff, lpkt, &st)) goto out;
+    } else {
+        if ((rc = udpdk_gpu_rx_host(g, frames, frames_bytes, offset, length, ptype, n, meta, loff, lpkt,
+                                    cap, &st))) { errno = -rc; goto out; }
+        if ((rc = udpdk_gpu_rx_host_batch(g, &staged, &meta_dev))) { errno = -rc; goto out; }
+    }
+    PROF_T(p2);
     udpdk_rx_batch_t rb;
     uint32_t nd = 0;
-    if (h_frag_pass(&staged, meta_dev, st.counters[UDPDK_V_FRAG], lanes, maxfan, &rb, &nd)) goto out;
+    const uint32_t nfrag = (uint32_t)st.counters[UDPDK_V_FRAG];
+    if (sharded && nfrag) {
+        /* every shard's FRAG frames, in arrival order, through the main context's table */
+        udpdk_rx_batch_t fsub;
+        const uint32_t *fmeta = NULL;
+        if (h_frag_subbatch(&J, meta, n, nfrag, maxfan, &fsub, &fmeta) ||
+            h_frag_pass(&fsub, fmeta, nfrag, lanes, maxfan, &rb, &nd))
+            goto out;
+        for (uint32_t d = 0; d < nd; d++) g_udpdk.fr_org[d] = g_udpdk.fb_idx[g_udpdk.fr_org[d]];
+    } else if (!sharded) {
+        if (h_frag_pass(&staged, meta_dev, nfrag, lanes, maxfan, &rb, &nd)) goto out;
+    }
     PROF_T(p3);
     const uint32_t *floff = nd ? g_udpdk.fr_loff : NULL, *flpkt = g_udpdk.fr_lpkt, *forg = g_udpdk.fr_org;
 
@@ -431,19 +719,31 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
     PROF_T(p4);
     g_udpdk.acc_do[nad] = (uint32_t)offd;
     g_udpdk.acc_fo[naf] = (uint32_t)offf;
-    if (h_gather(&staged, g_udpdk.acc_d, g_udpdk.acc_do, nad, &ad)) goto out;
-    if (naf && h_gather(&rb, g_udpdk.acc_f, g_udpdk.acc_fo, naf, &af)) goto out;
+    if ((sharded ? h_shards_gather(nad) : h_gather(g, &g_udpdk.gb, &staged, g_udpdk.acc_d, g_udpdk.acc_do,
+                                                    nad, &ad)) ||
+        (naf && h_gather(g, &g_udpdk.gb, &rb, g_udpdk.acc_f, g_udpdk.acc_fo, naf, &af))) {
+        if (errno != ENOBUFS) goto out;
+        /* slab budget exhausted by datagrams still queued: this poll's bursts are dropped */
+        __atomic_fetch_add(&g_udpdk.rx_nobufs, (uint64_t)nad + naf, __ATOMIC_RELAXED);
+        if (stats_out) *stats_out = st;
+        ret = 0;
+        goto out;
+    }
     PROF_T(p5);
     if ((rc = udpdk_gpu_sync(g))) { errno = -rc; goto out; }
     PROF_T(p6);
     if (ad) atomic_store_explicit(&ad->refs, nad, memory_order_relaxed);
     if (af) atomic_store_explicit(&af->refs, naf, memory_order_relaxed);
+    for (uint32_t k = 0; sharded && k < g_udpdk.n_shards; k++)
+        if (g_udpdk.shard[k].arena)
+            atomic_store_explicit(&g_udpdk.shard[k].arena->refs, g_udpdk.shard[k].nacc, memory_order_relaxed);
     /* publish: each socket's entries go to its ring in bulk enqueues, sockets over the pool */
     {
-        struct h_pub P = {&A, ad, af};
+        struct h_pub P = {&A, ad, af, sharded};
         h_pool_run(h_pub_job, &P);
     }
     ad = af = NULL;
+    for (uint32_t k = 0; sharded && k < g_udpdk.n_shards; k++) g_udpdk.shard[k].arena = NULL;
     if (stats_out) *stats_out = st;
     ret = 0;
 #ifdef UDPDK_POLL_PROFILE
@@ -461,6 +761,10 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
 out:
     if (ad) h_arena_put(ad);
     if (af) h_arena_put(af);
+    for (uint32_t k = 0; k < g_udpdk.n_shards; k++) {
+        if (g_udpdk.shard[k].arena) h_arena_put(g_udpdk.shard[k].arena);
+        g_udpdk.shard[k].arena = NULL;
+    }
     pthread_mutex_unlock(&g_udpdk.lock);
     return ret;
 }

@@ -66,19 +66,25 @@ int h_ring_push_bulk(struct h_ring *r, const struct h_dgram *d, uint32_t n)
 }
 
 /* ---- payload slabs ------------------------------------------------------------------------ */
+#define H_ARENA_FREE_KEEP 8      /* free slabs kept for reuse; the rest go back to the runtime */
+
+/* frees a slab's memory; the budget accounting is the caller's */
 static void h_arena_destroy(struct h_arena *a)
 {
     if (!a) return;
     void *p[] = {a->payload, a->len, a->src_ip, a->src_port};
     for (unsigned k = 0; k < 4; k++)
-        if (p[k]) {
-            if (g_udpdk.gpu) udpdk_gpu_host_free(g_udpdk.gpu, p[k]);
-        }
+        if (p[k] && g_udpdk.gpu) udpdk_gpu_host_free(g_udpdk.gpu, p[k]);
     free(a);
 }
 
+static uint64_t h_arena_footprint(uint64_t cb, uint32_t cn) { return cb + 10ull * cn; }
+
 /* A slab for n datagrams in `need` bytes of packed slots: the first free one that is large
- * enough, else a new one (pinned, so the gather's D2H is a straight DMA). */
+ * enough, else a new one (pinned, so the gather's D2H is a straight DMA) if the slab budget
+ * allows it after the free slabs that do not fit have been released. NULL + ENOBUFS when the
+ * budget is exhausted by slabs that queued datagrams still hold (the reference's mbuf pool
+ * exhausted: the burst is not received). */
 struct h_arena *h_arena_get(uint32_t n, uint64_t need)
 {
     pthread_mutex_lock(&g_udpdk.arena_lock);
@@ -87,19 +93,48 @@ struct h_arena *h_arena_get(uint32_t n, uint64_t need)
         if ((*pp)->cap_bytes >= need && (*pp)->cap_n >= n) {
             a = *pp;
             *pp = a->next;
+            g_udpdk.arena_free_n--;
             break;
         }
+    const uint32_t cn = n < 4096 ? 4096 : n;
+    const uint64_t cb = need < ((uint64_t)cn * 64) ? (uint64_t)cn * 64 : need;
+    if (!a) {
+        const uint64_t fp = h_arena_footprint(cb, cn);
+        /* release free slabs (none fits) until the new one fits the budget */
+        while ((g_udpdk.arena_bytes + fp > g_udpdk.arena_bytes_max ||
+                g_udpdk.arena_count + 1 > g_udpdk.arena_count_max) && g_udpdk.arena_free) {
+            struct h_arena *f = g_udpdk.arena_free;
+            g_udpdk.arena_free = f->next;
+            g_udpdk.arena_free_n--;
+            g_udpdk.arena_bytes -= h_arena_footprint(f->cap_bytes, f->cap_n);
+            g_udpdk.arena_count--;
+            h_arena_destroy(f);
+        }
+        if (g_udpdk.arena_bytes + fp > g_udpdk.arena_bytes_max ||
+            g_udpdk.arena_count + 1 > g_udpdk.arena_count_max) {
+            pthread_mutex_unlock(&g_udpdk.arena_lock);
+            errno = ENOBUFS;
+            return NULL;
+        }
+        g_udpdk.arena_bytes += fp;         /* reserved before the allocation */
+        g_udpdk.arena_count++;
+    }
     pthread_mutex_unlock(&g_udpdk.arena_lock);
     if (!a) {
         a = calloc(1, sizeof(*a));
-        if (!a) return NULL;
-        const uint32_t cn = n < 4096 ? 4096 : n;
-        const uint64_t cb = need < ((uint64_t)cn * 64) ? (uint64_t)cn * 64 : need;
-        if (udpdk_gpu_host_alloc(g_udpdk.gpu, cb, (void **)&a->payload) ||
-            udpdk_gpu_host_alloc(g_udpdk.gpu, 4ull * cn, (void **)&a->len) ||
-            udpdk_gpu_host_alloc(g_udpdk.gpu, 4ull * cn, (void **)&a->src_ip) ||
-            udpdk_gpu_host_alloc(g_udpdk.gpu, 2ull * cn, (void **)&a->src_port)) {
+        if (a && (udpdk_gpu_host_alloc(g_udpdk.gpu, cb, (void **)&a->payload) ||
+                  udpdk_gpu_host_alloc(g_udpdk.gpu, 4ull * cn, (void **)&a->len) ||
+                  udpdk_gpu_host_alloc(g_udpdk.gpu, 4ull * cn, (void **)&a->src_ip) ||
+                  udpdk_gpu_host_alloc(g_udpdk.gpu, 2ull * cn, (void **)&a->src_port))) {
             h_arena_destroy(a);
+            a = NULL;
+        }
+        if (!a) {
+            pthread_mutex_lock(&g_udpdk.arena_lock);
+            g_udpdk.arena_bytes -= h_arena_footprint(cb, cn);
+            g_udpdk.arena_count--;
+            pthread_mutex_unlock(&g_udpdk.arena_lock);
+            errno = ENOMEM;
             return NULL;
         }
         a->cap_bytes = cb;
@@ -110,12 +145,27 @@ struct h_arena *h_arena_get(uint32_t n, uint64_t need)
     return a;
 }
 
+/* Back to the pool; beyond H_ARENA_FREE_KEEP free slabs the largest goes back to the runtime,
+ * so one burst of huge polls does not keep its slabs pinned forever. */
 void h_arena_put(struct h_arena *a)
 {
     pthread_mutex_lock(&g_udpdk.arena_lock);
     a->next = g_udpdk.arena_free;
     g_udpdk.arena_free = a;
+    g_udpdk.arena_free_n++;
+    struct h_arena *victim = NULL;
+    if (g_udpdk.arena_free_n > H_ARENA_FREE_KEEP) {
+        struct h_arena **vp = &g_udpdk.arena_free;
+        for (struct h_arena **pp = &g_udpdk.arena_free; *pp; pp = &(*pp)->next)
+            if ((*pp)->cap_bytes > (*vp)->cap_bytes) vp = pp;
+        victim = *vp;
+        *vp = victim->next;
+        g_udpdk.arena_free_n--;
+        g_udpdk.arena_bytes -= h_arena_footprint(victim->cap_bytes, victim->cap_n);
+        g_udpdk.arena_count--;
+    }
     pthread_mutex_unlock(&g_udpdk.arena_lock);
+    h_arena_destroy(victim);
 }
 
 /* Drop refs references (recvfrom of one datagram, or a ring cleared by close); the last one
@@ -131,13 +181,18 @@ void h_arenas_free_all(void)
     pthread_mutex_lock(&g_udpdk.arena_lock);
     struct h_arena *a = g_udpdk.arena_free;
     g_udpdk.arena_free = NULL;
-    pthread_mutex_unlock(&g_udpdk.arena_lock);
+    g_udpdk.arena_free_n = 0;
     while (a) {
         struct h_arena *n = a->next;
+        g_udpdk.arena_bytes -= h_arena_footprint(a->cap_bytes, a->cap_n);
+        g_udpdk.arena_count--;
         h_arena_destroy(a);
         a = n;
     }
+    pthread_mutex_unlock(&g_udpdk.arena_lock);
 }
+
+uint64_t udpdk_rx_nobufs(void) { return __atomic_load_n(&g_udpdk.rx_nobufs, __ATOMIC_RELAXED); }
 
 /* ---- TX rings ----------------------------------------------------------------------------- */
 void h_tx_reset(void)
@@ -152,6 +207,7 @@ void h_tx_reset(void)
     g_udpdk.txp = NULL;
     g_udpdk.txp_bytes = g_udpdk.txp_cap = 0;
     g_udpdk.tx_queued = 0;
+    g_udpdk.tx_dropped = 0;
     pthread_mutex_unlock(&g_udpdk.tx_lock);
 }
 
@@ -159,6 +215,14 @@ uint64_t udpdk_tx_pending(void)
 {
     pthread_mutex_lock(&g_udpdk.tx_lock);
     const uint64_t q = g_udpdk.tx_queued;
+    pthread_mutex_unlock(&g_udpdk.tx_lock);
+    return q;
+}
+
+uint64_t udpdk_tx_dropped(void)
+{
+    pthread_mutex_lock(&g_udpdk.tx_lock);
+    const uint64_t q = g_udpdk.tx_dropped;
     pthread_mutex_unlock(&g_udpdk.tx_lock);
     return q;
 }
@@ -176,6 +240,7 @@ void h_sockets_reset(void)
     g_udpdk.txp = NULL;
     g_udpdk.txp_bytes = g_udpdk.txp_cap = 0;
     g_udpdk.tx_queued = 0;
+    g_udpdk.tx_dropped = 0;
     g_udpdk.version++;
 }
 
@@ -271,6 +336,10 @@ int udpdk_close(int s)
         return -1;
     }
     struct h_slot *sl = &g_udpdk.slots[s];
+    /* a recvfrom blocked on this socket in another thread leaves with EBADF before the ring's
+     * entries and storage go (it would otherwise read freed entries) */
+    atomic_store(&sl->rx.closing, 1);
+    while (atomic_load(&sl->rx.busy)) sched_yield();
     if (sl->bound) h_btable_del(s, sl->udp_port);
     h_ring_clear(&sl->rx);
     pthread_mutex_lock(&g_udpdk.tx_lock);
@@ -286,6 +355,7 @@ int udpdk_close(int s)
     sl->so_options = 0;
     g_udpdk.n_active--;
     g_udpdk.version++;
+    atomic_store(&sl->rx.closing, 0);          /* later calls see used == 0 */
     pthread_mutex_unlock(&g_udpdk.lock);
     return 0;
 }
@@ -359,11 +429,19 @@ ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
     if (flags != 0) { errno = EINVAL; return -1; }
     if (buf == NULL && addrlen != NULL) { errno = EINVAL; return -1; }
     struct h_ring *r = &g_udpdk.slots[s].rx;
+    atomic_store(&r->busy, 1);                 /* seq_cst: see udpdk_close */
+    if (atomic_load(&r->closing) || !g_udpdk.slots[s].used) {
+        atomic_store_explicit(&r->busy, 0, memory_order_release);
+        errno = EBADF;
+        return -1;
+    }
     const uint32_t h = atomic_load_explicit(&r->head, memory_order_relaxed);
     /* busy wait like udpdk_syscall.c:424-426; datagrams arrive from the poller (udpdk_poll_rx) */
     while (atomic_load_explicit(&r->tail, memory_order_acquire) == h) {
-        if (atomic_load_explicit(&g_udpdk.interrupted, memory_order_relaxed)) {
-            errno = EINTR;
+        const int intr = atomic_load_explicit(&g_udpdk.interrupted, memory_order_relaxed);
+        if (intr || atomic_load_explicit(&r->closing, memory_order_relaxed)) {
+            atomic_store_explicit(&r->busy, 0, memory_order_release);
+            errno = intr ? EINTR : EBADF;
             return -1;
         }
         sched_yield();
@@ -398,6 +476,7 @@ ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
         r->rel_arena = NULL;
         r->rel_n = 0;
     }
+    atomic_store_explicit(&r->busy, 0, memory_order_release);
     return (ssize_t)n;
 }
 

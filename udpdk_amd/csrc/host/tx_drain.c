@@ -50,12 +50,19 @@ int udpdk_tx_drain(uint8_t *out, uint64_t out_cap, uint32_t *out_off, uint16_t *
     if (!g_udpdk.gpu) { errno = ENODEV; return -1; }
     udpdk_gpu_ctx *g = g_udpdk.gpu;
     const uint32_t mtu = g_udpdk.mtu;
-    /* the slot table the TX kernel reads (source port and address per socket) */
+    /* the slot table the TX kernel reads (source port and address per socket). tx_lock is taken
+     * before the table lock is dropped (the order udpdk_close uses): a sendto that auto-binds, or
+     * a close + socket + bind, either lands before the refresh (and is in the uploaded table) or
+     * queues its datagram only after this drain has released tx_lock, so no datagram selected
+     * below is built from a slot row older than its socket's binding. */
     pthread_mutex_lock(&g_udpdk.lock);
     const int src = h_snapshot_refresh();
-    pthread_mutex_unlock(&g_udpdk.lock);
-    if (src) return -1;
+    if (src) {
+        pthread_mutex_unlock(&g_udpdk.lock);
+        return -1;
+    }
     pthread_mutex_lock(&g_udpdk.tx_lock);
+    pthread_mutex_unlock(&g_udpdk.lock);
     int ret = -1, rc;
     /* 1. selection in the poller's order */
     uint32_t nsel = 0, nframes = 0, burst = 0;
@@ -72,7 +79,19 @@ int udpdk_tx_drain(uint8_t *out, uint64_t out_cap, uint32_t *out_off, uint16_t *
                 const struct h_txd *t = &q->e[(q->head + taken[s]) % UDPDK_RX_RING_SIZE];
                 uint32_t nf = 1;
                 const uint64_t span = udpdk_gpu_tx_span(t->len, mtu, &nf);
-                if (nframes + nf > max || bytes + span > out_cap) { full = 1; break; }
+                if (nframes + nf > max || bytes + span > out_cap) {
+                    if (nframes == 0 && taken[s] == 0 && (nf > max || span > out_cap)) {
+                        /* larger than any drain with these limits can carry: it would block
+                         * the ring's head forever. Dropped and counted (udpdk_tx_dropped), as
+                         * the reference's poller drops a burst it cannot send. */
+                        q->head++;
+                        g_udpdk.tx_queued--;
+                        g_udpdk.tx_dropped++;
+                        continue;
+                    }
+                    full = 1;
+                    break;
+                }
                 if (nsel + 1 > g_udpdk.tx_sel_cap) {
                     const uint64_t nc = g_udpdk.tx_sel_cap ? 2 * g_udpdk.tx_sel_cap : 4096;
                     void *ns = realloc(g_udpdk.tx_sel, nc * sizeof(*g_udpdk.tx_sel));
@@ -95,7 +114,11 @@ int udpdk_tx_drain(uint8_t *out, uint64_t out_cap, uint32_t *out_off, uint16_t *
         }
         burst = 0;                                           /* end of the loop's TX half */
     }
-    if (!nsel) { ret = 0; goto out; }
+    if (!nsel) {
+        if (!g_udpdk.tx_queued) g_udpdk.txp_bytes = 0;   /* only dropped ones were left */
+        ret = 0;
+        goto out;
+    }
     /* 2. host staging (pinned): payloads packed, then the per-datagram arrays */
     const uint64_t o_pay = 0, o_poff = a16(pay), o_len = o_poff + a16(4ull * nsel),
                    o_sock = o_len + a16(2ull * nsel), o_ip = o_sock + a16(4ull * nsel),

@@ -624,7 +624,11 @@ rx_classify(RxArgs a)
                 // aggregated with a wave multi-split first (all 64 lanes may share one lane)
                 // (one lane: the tile's count is its delivery counter, written at the tile end)
                 const uint32_t key = first & a.lane_mask;
+#ifdef UDPDK_DIAG_NO_HIST
+                if (true) {                           // timing only: histogram skipped
+#else
                 if (a.n_lanes == 1u) {
+#endif
                 } else if (a.key_bits <= 4u) {
                     unsigned long long peers = __ballot(delivered);
                     for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
