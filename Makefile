@@ -33,7 +33,7 @@ $(LIB): $(HIP_OBJ) $(C_OBJ) udpdk_amd/csrc/libudpdk_amd.map
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(HIP_OBJ) $(C_OBJ) -Wl,--no-undefined \
 	    -Wl,-soname,libudpdk_amd.so -Wl,--version-script=udpdk_amd/csrc/libudpdk_amd.map
 
-oracle:
+oracle: $(LIB)
 	$(MAKE) -C oracle
 
 # the reference-API path end to end, written against udpdk_api.h like a reference app (bench.py)

@@ -190,6 +190,8 @@ struct h_state {
     atomic_int poller_run;
     int       poller_started;
     udpdk_port_ops_t port;
+    /* [gpu] port / port_peer: the port udpdk_init attaches the poller thread to (port_udp.c) */
+    char      port_spec[128], port_peer[128];
 };
 
 extern struct h_state g_udpdk;
@@ -225,6 +227,10 @@ void udpdk_poll_profile_dump(void);   /* -DUDPDK_POLL_PROFILE builds: phase time
 int  h_grow_dev(void **p, uint64_t *cap, uint64_t need);
 int  h_grow_dev_on(udpdk_gpu_ctx *g, void **p, uint64_t *cap, uint64_t need);
 int  h_grow_host(void **p, uint64_t *cap, uint64_t need);
+
+/* port_udp.c: the UDP test wire */
+int  h_wire_open(const char *local, const char *peer, udpdk_port_ops_t *ops);
+void h_wire_close(void);
 
 /* tx_drain.c */
 void h_tx_buffers_free(void);

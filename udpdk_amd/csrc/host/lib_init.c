@@ -34,6 +34,7 @@ static void h_config_defaults(void)
     g_udpdk.frag_ttl_ms = 1000;        /* MAX_FLOW_TTL = MS_PER_S */
     g_udpdk.arena_bytes_max = 4ull << 30;
     g_udpdk.arena_count_max = 1024;
+    g_udpdk.port_spec[0] = g_udpdk.port_peer[0] = 0;
 }
 
 __attribute__((constructor)) static void h_lib_load(void)
@@ -161,6 +162,10 @@ static int h_load_ini(const char *path)
             g_udpdk.frag_entries = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "frag_max_dgram")) {
             g_udpdk.frag_max_dgram = (uint32_t)strtoul(v, NULL, 0);
+        } else if (!strcmp(section, "gpu") && !strcmp(k, "port")) {
+            snprintf(g_udpdk.port_spec, sizeof(g_udpdk.port_spec), "%s", v);
+        } else if (!strcmp(section, "gpu") && !strcmp(k, "port_peer")) {
+            snprintf(g_udpdk.port_peer, sizeof(g_udpdk.port_peer), "%s", v);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "slab_bytes_max")) {
             g_udpdk.arena_bytes_max = strtoull(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "slab_count_max")) {
@@ -206,6 +211,26 @@ int udpdk_init(int argc, char *argv[])
         g_udpdk.n_shards = 0;
     }
     g_udpdk.snap_version = UINT64_MAX;
+    /* [gpu] port: start the poller thread on it now, as the reference forks its poller here
+     * (udpdk_init.c:293, :362-368), so an unmodified application's sendto / recvfrom move
+     * packets without further calls */
+    if (g_udpdk.port_spec[0]) {
+        udpdk_port_ops_t ops;
+        int prc;
+        if (!strncmp(g_udpdk.port_spec, "udp:", 4))
+            prc = h_wire_open(g_udpdk.port_spec + 4, g_udpdk.port_peer, &ops);
+        else if (!strcmp(g_udpdk.port_spec, "loopback"))
+            prc = udpdk_port_loopback(&ops);
+        else
+            prc = (errno = EINVAL, -1);
+        if (prc || udpdk_port_attach(&ops)) {
+            const int e = errno;
+            h_wire_close();
+            udpdk_cleanup();
+            errno = e;
+            return -1;
+        }
+    }
     return 0;
 }
 
@@ -226,6 +251,7 @@ void udpdk_interrupt(int signum)
 void udpdk_cleanup(void)
 {
     udpdk_port_detach();
+    h_wire_close();
     h_lo_reset();
     udpdk_poll_profile_dump();
     h_pool_stop();
