@@ -5,10 +5,15 @@ batches: rx_classify + rx_compact1; otherwise rx_classify + rx_scan + rx_scatter
 region is exactly K steps between a barrier + hipDeviceSynchronize on each side (host wall
 clock: `value`); an untimed pass of K steps before it gives the GPU time (two events on the
 library stream) and the per-kernel durations (events carried by the kernel dispatches
-themselves, hipExtLaunchKernelGGL, so they agree with rocprofv3's kernel trace). Default workload at N = 1: BASELINE.json configs[1], 1 M synthetic 64 B Eth/IPv4/UDP frames, 1 bound
-port. At N > 1 the default is the scaling workload BASELINE.json configs[4] (config 5): every rank
-processes its own independent 4 M x 64 B shard over 4096 ports, Zipf-0.99 (ports seeded 1000 +
-rank, frames 0x5EED ^ rank) with no data-path collective: weak scaling.
+themselves, hipExtLaunchKernelGGL, so they agree with rocprofv3's kernel trace).
+
+Workload: BASELINE.json configs[1] at every N (1 M synthetic 64 B Eth/IPv4/UDP frames, 1 bound
+port, per GPU: weak scaling, no data-path collective), so the driver's per-N values compare one
+workload. Beside it, at every N, the `scale` object measures the scaling workload BASELINE.json
+configs[4] (config 5) the same way: every rank processes its own independent 4 M x 64 B shard
+over 4096 ports, Zipf-0.99 (ports seeded 1000 + rank, frames 0x5EED ^ rank), barrier + max over
+ranks, aggregate over all GPUs. Each rank reports its GPU's PCI bus id; with N > 1 they must be
+distinct (UDPDK_BENCH_SHARED_DEVICE=1 allows a rehearsal with every rank on one GPU).
 
 `--gpus N` is honoured two ways: under torchrun (WORLD_SIZE set) it must equal WORLD_SIZE; run
 directly with N > 1, bench.py spawns N worker processes itself (one per GPU, gloo rendezvous on
@@ -47,7 +52,8 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--config", type=int, default=None,
-                   help="BASELINE.json config number (1..5); default 2 at N = 1, 5 at N > 1")
+                   help="BASELINE.json config number (1..5) of the headline line; default 2")
+    p.add_argument("--no-scale", action="store_true", help="skip the config-5 `scale` object")
     p.add_argument("--frames", type=int, default=None, help="override frames per GPU")
     p.add_argument("--strong-total", type=int, default=None,
                    help="strong scaling: this many frames in total, split into contiguous equal "
@@ -55,7 +61,7 @@ def parse():
     p.add_argument("--rotate-mib", type=int, default=640, help="device bytes cycled by the loop")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1500 B / IMIX side lines")
-    p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU time per baseline leg")
+    p.add_argument("--cpu-seconds", type=float, default=4.0, help="target CPU time per baseline leg")
     p.add_argument("--pipeline", type=int, default=None, choices=(1, 2, 3, 4),
                    help="udpdk_gpu_pipeline_depth: d > 1 overlaps consecutive batches on d streams "
                         "(default: 3 for one socket, 4 when the batch takes the multi-lane path)")
@@ -112,6 +118,9 @@ class Rx:
             self.args.append((C.byref(bt), C.byref(ot), bt, ot, db, out))
         self.f = abi.lib().udpdk_gpu_rx
         self.h = ctx.handle
+        # the single-lane path (one bound socket, no fan-out) compacts with rx_compact1 where
+        # the multi-lane path scans and scatters: the third timed kernel id is named by what ran
+        self.third = "rx_compact1" if w.n_sockets <= 1 else "rx_scatter"
 
     def step(self, i: int):
         a = self.args[i % self.copies]
@@ -207,7 +216,7 @@ def time_loop(rx: Rx, steps: int, warmup: int, barrier, timing_every: int):
     ms, n = ctx.timing_read() if timing_every else ([0.0] * abi.N_KERNEL_IDS, [0] * abi.N_KERNEL_IDS)
     ctx.timing(0)
     kt = {name: 1e3 * ms[k] / n[k] for k, name in
-          enumerate(("rx_classify", "rx_scan", "rx_scatter")) if n[k]}
+          enumerate(("rx_classify", "rx_scan", rx.third)) if n[k]}
     # the timed region
     barrier()
     device_sync()
@@ -238,6 +247,34 @@ def host_cores() -> int:
         return os.cpu_count() or 1
 
 
+def pci_bus_id(device: int) -> str:
+    """hipDeviceGetPCIBusId of a device (the process already uses it): names the physical GPU a
+    rank ran on, whatever device numbering its environment gives it."""
+    global _HIP
+    if _HIP is None:
+        _HIP = C.CDLL("libamdhip64.so")
+    buf = C.create_string_buffer(64)
+    rc = _HIP.hipDeviceGetPCIBusId(buf, 64, device)
+    return buf.value.decode() if rc == 0 else f"unknown(rc={rc})"
+
+
+def cpu_quota() -> str:
+    """The cgroup CPU limit of this process (v2 cpu.max, else v1 cfs quota/period): the share of
+    the host cores the affinity mask may not show."""
+    for f in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(f).read().split()[:2]
+            return "unlimited" if q == "max" else f"{int(q) / int(per):.2f} cpus ({f})"
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return "unlimited" if q < 0 else f"{q / per:.2f} cpus (cgroup v1)"
+    except (OSError, ValueError):
+        return "unknown"
+
+
 def oracle_digest(w: F.Workload):
     """64-bit digest of the oracle's verdict words and lanes for workload w (parity mode,
     SURVEY.md §8(d)); compared with the digest of the GPU outputs of the same batch."""
@@ -256,13 +293,14 @@ def gpu_digest(ctx, out, n: int, n_lanes: int):
     return _digest(meta, loff, pkt)
 
 
-def cpu_baseline(w: F.Workload, target_s: float, gpu_dig: str | None = None):
-    """Oracle (the C restatement, kind "port") on the host cores, one independent shard per
-    pinned thread, with the RX checksum verification: 1 thread, 16 threads (the per-GPU CPU
-    share of the box) and every core the process may run on (`host_cores()`, nproc unless the
-    host partitions it). With gpu_dig (digest of the GPU outputs of the measured batch) the leg
-    also runs the restatement once on that batch and compares digests (SURVEY.md §8(d) "parity
-    mode")."""
+def cpu_baseline(w: F.Workload, target_s: float, gpu_dig: str | None = None, sweep=True):
+    """Oracle (the C restatement, kind "port") on the host cores: every pinned thread runs the
+    poller over its own full, NUMA-local copy of the batch with preallocated poller state (one
+    independent shard per thread), with the RX checksum verification; a sweep over thread counts
+    (1, 16, 32, 64, 128, 256 and every core the process may run on), the best reported as the
+    baseline with its thread count. With gpu_dig (digest of the GPU outputs of the measured
+    batch) the leg also runs the restatement once on that batch and compares digests (SURVEY.md
+    §8(d) "parity mode")."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     b = w.batch
@@ -271,21 +309,23 @@ def cpu_baseline(w: F.Workload, target_s: float, gpu_dig: str | None = None):
     if gpu_dig is not None:
         parity = {"oracle": oracle_digest(w), "gpu": gpu_dig}
         parity["match"] = parity["oracle"] == parity["gpu"]
-    res = {"parity": parity}
+    res = {"parity": parity, "sweep": {}}
     cores = host_cores()
-    legs = [(1, True), (1, False), (min(16, cores), True), (cores, True), (cores, False)]
-    for th, csum in dict.fromkeys(legs):
-        # calibrate reps so the timed leg takes ~target_s: grow the pass count until a run
-        # lasts >= 0.2 s (a single pass of many threads is dominated by starting them)
-        reps, secs = 1, 0.0
-        while True:
-            secs = O.rx_parallel(bt, b.frames, b.frames_bytes, b.offset, b.length, w.n_sockets, csum, th, reps)
-            if secs >= 0.2 or reps >= 1 << 20:
-                break
-            reps *= 4
-        reps = max(1, int(reps * target_s / max(secs, 1e-6)))
+    counts = sorted({t for t in (1, 16, 32, 64, 128, 256) if t <= cores} | {cores}) if sweep else [1, cores]
+
+    def leg(th, csum):
+        # calibrate reps so the timed leg takes ~target_s (every rep: th x n frames)
+        reps, secs = 1, O.rx_parallel(bt, b.frames, b.frames_bytes, b.offset, b.length, w.n_sockets, csum, th, 1)
+        if secs < 0:
+            raise RuntimeError(f"oracle_rx_parallel failed at {th} threads")
+        reps = max(1, int(target_s / max(secs, 1e-6)))
         secs = O.rx_parallel(bt, b.frames, b.frames_bytes, b.offset, b.length, w.n_sockets, csum, th, reps)
-        res[(th, csum)] = (b.n * reps / secs / 1e6, reps, secs)
+        return (th * b.n * reps / secs / 1e6, reps, secs)
+    for th in counts:
+        res["sweep"][th] = leg(th, True)
+    res[(1, False)] = leg(1, False)
+    res[(cores, False)] = leg(cores, False)
+    res["best"] = max(res["sweep"], key=lambda t: res["sweep"][t][0])
     return res, cores
 
 
@@ -295,12 +335,12 @@ def config1_line(target_s: float):
     path, here the C restatement of reassemble() + flush_rx_queue (the reference needs DPDK,
     absent), on 1 thread and on every host core."""
     w = F.config_batch(1)
-    res, cores = cpu_baseline(w, target_s)
+    res, cores = cpu_baseline(w, target_s, sweep=False)
     return {"workload": w.name, "kind": "port",
-            "one_thread_mpkt_s": round(res[(1, True)][0], 2),
+            "one_thread_mpkt_s": round(res["sweep"][1][0], 2),
             "one_thread_no_csum_mpkt_s": round(res[(1, False)][0], 2),
-            "all_cores_mpkt_s": round(res[(cores, True)][0], 2), "cores": cores,
-            "gbps_all_cores": round(res[(cores, True)][0] * 106 / 1e3, 2)}
+            "all_cores_mpkt_s": round(res["sweep"][cores][0], 2), "cores": cores,
+            "gbps_all_cores": round(res["sweep"][cores][0] * 106 / 1e3, 2)}
 
 
 def auto_depth(w) -> int:
@@ -624,6 +664,36 @@ def socket_path_lines(specs=((1 << 20, 64, 1024, 5), (1 << 20, 0, 1024, 3), (1 <
     return out
 
 
+def scale_line(ctx, world: int, rank: int, barrier, dist, steps: int, warmup: int, rotate: int):
+    """The scaling workload (BASELINE.json configs[4], config 5) at this N: each rank its own
+    independent 4 M x 64 B shard over 4096 ports, Zipf-0.99 (seed 1000 + rank), pipelined, the K
+    steps bracketed by a barrier + device sync on each side, the MAX wall over ranks; value = all
+    ranks' frames / that time. The same object at N = 1, 2, 4, 8 gives config 5's curve."""
+    w5 = F.config_batch(5, shard=rank)
+    rx5 = Rx(ctx, w5, rotate)
+    depth = auto_depth(w5)
+    ctx.pipeline(depth)
+    wall, gpu_step, _, _ = time_loop(rx5, steps, warmup, barrier, 0)
+    ctx.pipeline(1)
+    mine = rx5.n * steps / wall / 1e6
+    if dist is not None:
+        import torch
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    total = rx5.n * steps * world
+    gbps = rx5.pipeline_bytes() * steps * world / wall / 1e9
+    out = {"workload": w5.name, "baseline_config": 5, "n_gpus": world, "frames_per_gpu": rx5.n,
+           "value": round(total / wall / 1e6, 2), "unit": "Mpkt/s", "steps": steps,
+           "ms_per_step": round(1e3 * wall / steps, 5), "scaling": "weak", "pipeline_depth": depth,
+           "gbps_pipeline": round(gbps, 1), "frac_hbm_pipeline_per_gpu": round(gbps / world / HBM_PEAK_GBS, 4),
+           "rank0_mpkt_s": round(mine, 2), "rank0_gpu_us_per_step": round(1e3 * gpu_step, 3)}
+    for a in rx5.args:
+        a[4].frames.free(); a[4].offset.free(); a[4].length.free()
+        a[5].meta.free(); a[5].lane_off.free(); a[5].lane_pkt.free()
+    return out
+
+
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -635,7 +705,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.config is None:
-        args.config = 2 if world == 1 else 5
+        args.config = 2
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -688,7 +758,7 @@ def main():
     single_us = 1e3 * ev1.elapsed_ms()
     ev1.close()
     cls_bytes = rx.classify_bytes()
-    mine = {"rank": rank, "device": device, "frames": rx.n,
+    mine = {"rank": rank, "device": device, "pci_bus_id": pci_bus_id(device), "frames": rx.n,
             "mpkt_s": round(rx.n * args.steps / wall / 1e6, 2),
             "gbps": round(rx.pipeline_bytes() * args.steps / wall / 1e9, 1),
             "classify_us": round(kt.get("rx_classify", 0.0), 3),
@@ -701,6 +771,15 @@ def main():
         wall = float(t.item())
         per_rank = [None] * world
         dist.all_gather_object(per_rank, mine)
+    distinct = len({p["pci_bus_id"] for p in per_rank}) == world
+    if world > 1 and not distinct and os.environ.get("UDPDK_BENCH_SHARED_DEVICE") != "1":
+        raise SystemExit(f"ranks share a GPU: {[p['pci_bus_id'] for p in per_rank]} "
+                         "(set UDPDK_BENCH_SHARED_DEVICE=1 for a one-GPU rehearsal)")
+    scale = None
+    if not args.no_scale and not args.strong_total:
+        scale = scale_line(ctx, world, rank, barrier, dist, max(10, args.steps // 4), 5,
+                           args.rotate_mib << 20)
+        scale["distinct_gpus"] = distinct
     total_pkts = rx.n * args.steps * world
     mpkt_s = total_pkts / wall / 1e6
     ms_step = 1e3 * wall / args.steps
@@ -747,20 +826,25 @@ def main():
                      "algorithmic_bytes_per_launch": cls_bytes},
         "cpu_baseline": None,
     }
-    if world > 1:
-        line["per_rank"] = per_rank
+    line["per_rank"] = per_rank
+    line["distinct_gpus"] = distinct
+    if scale is not None:
+        line["scale"] = scale
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         gdig = gpu_digest(ctx, rx.args[0][5], rx.n, w.n_sockets) if rx.n <= (1 << 22) else None
         res, cores = cpu_baseline(w, args.cpu_seconds, gdig)
-        v, reps, secs = res[(cores, True)]
+        best = res["best"]
+        v, reps, secs = res["sweep"][best]
         line["cpu_baseline"] = {
-            "value": round(v, 2), "unit": "Mpkt/s", "cores": cores, "kind": "port",
-            "sample": f"{rx.n} frames of {w.name} x {reps} passes ({secs:.1f} s), {cores} pinned "
-                      f"threads = every host core this process may use (one shard each), RX "
-                      f"checksum verification on",
-            "one_thread": round(res[(1, True)][0], 2),
+            "value": round(v, 2), "unit": "Mpkt/s", "cores": best, "kind": "port",
+            "sample": f"{best} pinned threads (the best of the sweep), each running the poller "
+                      f"restatement over its own NUMA-local copy of the {rx.n}-frame {w.name} batch "
+                      f"x {reps} passes ({secs:.1f} s), RX checksum verification on",
+            "threads_sweep_mpkt_s": {str(t): round(x[0], 2) for t, x in res["sweep"].items()},
+            "all_cores": {"threads": cores, "mpkt_s": round(res["sweep"][cores][0], 2)},
+            "affinity_cores": cores, "cgroup_cpu_quota": cpu_quota(),
+            "one_thread": round(res["sweep"][1][0], 2),
             "one_thread_no_csum": round(res[(1, False)][0], 2),
-            f"{min(16, cores)}_threads": round(res[(min(16, cores), True)][0], 2),
             f"{cores}_threads_no_csum": round(res[(cores, False)][0], 2),
             "parity": res["parity"],
         }
@@ -842,6 +926,11 @@ def dry_run(args, world, rank, dist):
     w = F.config_batch(args.config, n=frames, shard=rank)
     mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "workload": w.name,
             "frames": w.batch.n, "digest": _digest(w.batch.frames[:w.batch.frames_bytes], w.batch.length)}
+    if not args.no_scale and not args.strong_total:
+        w5 = F.config_batch(5, n=frames, shard=rank)
+        mine["scale_workload"] = w5.name
+        mine["scale_frames"] = w5.batch.n
+        mine["scale_digest"] = _digest(w5.batch.frames[:w5.batch.frames_bytes], w5.batch.length)
     per_rank = [mine]
     wall = 1.0 + rank
     if dist is not None:

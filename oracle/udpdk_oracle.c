@@ -331,61 +331,99 @@ static uint32_t o_reassemble(const oracle_btable *bt, const uint8_t *frames,
     return w | V_DELIVERED | ((fan > 127 ? 127u : fan) << 9) | ((first & 0xFFFFu) << 16);
 }
 
-int64_t oracle_rx(const oracle_btable *bt, const uint8_t *frames, uint64_t frames_bytes,
-                  const uint32_t *offset, const uint16_t *length, const uint32_t *ptype,
-                  uint32_t n, uint32_t lane_mask, uint32_t n_lanes, int do_csum,
-                  uint32_t *meta, uint32_t *lane_off, uint32_t *lane_pkt, uint32_t lane_cap,
-                  uint64_t counters[16])
+/* The per-socket state the poller keeps between bursts (exch_slots + rings): allocated once and
+ * reused across calls, so a timed loop of oracle_rx_ws calls measures the poller's work, not the
+ * allocator (the reference's rings and slot buffers are preallocated too, udpdk_init.c:252-279). */
+struct o_rx_ws {
+    struct o_lane     *lanes;
+    struct o_rx_state  st;
+    uint32_t           n_lanes;
+};
+
+static void o_ws_free(struct o_rx_ws *w)
 {
-    struct o_rx_state st = {0};
-    struct o_lane *lanes = calloc(n_lanes ? n_lanes : 1, sizeof(*lanes));
-    st.slots = calloc(n_lanes ? n_lanes : 1, sizeof(*st.slots));
-    st.touched = calloc(n_lanes ? n_lanes : 1, sizeof(uint32_t));
+    if (w->lanes) for (uint32_t k = 0; k < w->n_lanes; k++) free(w->lanes[k].v);
+    if (w->st.slots) for (uint32_t k = 0; k < w->n_lanes; k++) free(w->st.slots[k].pkt);
+    free(w->lanes);
+    free(w->st.slots);
+    free(w->st.touched);
+    memset(w, 0, sizeof(*w));
+}
+
+static int o_ws_init(struct o_rx_ws *w, uint32_t n_lanes)
+{
+    memset(w, 0, sizeof(*w));
+    w->n_lanes = n_lanes ? n_lanes : 1;
+    w->lanes = calloc(w->n_lanes, sizeof(*w->lanes));
+    w->st.slots = calloc(w->n_lanes, sizeof(*w->st.slots));
+    w->st.touched = calloc(w->n_lanes, sizeof(uint32_t));
+    if (!w->lanes || !w->st.slots || !w->st.touched) { o_ws_free(w); return -1; }
+    return 0;
+}
+
+static int64_t o_rx_run(struct o_rx_ws *w, const oracle_btable *bt, const uint8_t *frames,
+                        uint64_t frames_bytes, const uint32_t *offset, const uint16_t *length,
+                        const uint32_t *ptype, uint32_t n, uint32_t lane_mask, uint32_t n_lanes,
+                        int do_csum, uint32_t *meta, uint32_t *lane_off, uint32_t *lane_pkt,
+                        uint32_t lane_cap, uint64_t counters[16])
+{
+    struct o_rx_state *st = &w->st;
+    struct o_lane *lanes = w->lanes;
     uint64_t cnt[16] = {0};
-    int64_t ret = 0;
-    if (!lanes || !st.slots || !st.touched) { ret = -1; goto out; }
+    st->err = 0;
+    st->n_touched = 0;
+    for (uint32_t k = 0; k < n_lanes; k++) lanes[k].n = 0;
 
     /* poller_body RX half, poller.c:516-545: bursts of BURST_SIZE frames */
     for (uint32_t b0 = 0; b0 < n; b0 += O_BURST) {
         uint32_t b1 = b0 + O_BURST < n ? b0 + O_BURST : n;
         for (uint32_t i = b0; i < b1; i++)                                  /* :526-534 */
             meta[i] = o_reassemble(bt, frames, frames_bytes, offset[i], length[i], ptype, i,
-                                   lane_mask, n_lanes, do_csum, &st, cnt);
-        if (st.err) { ret = -1; goto out; }
+                                   lane_mask, n_lanes, do_csum, st, cnt);
+        if (st->err) return -1;
         /* flush every slot holding frames (:537-541 scans all slots in index order; the order
          * across slots cannot change any lane's contents) via flush_rx_queue (:274-292).
          * A full ring would drop the whole batch (:287-290); lanes here are unbounded. */
-        for (uint32_t t = 0; t < st.n_touched; t++) {
-            struct o_slot_buf *sb = &st.slots[st.touched[t]];
+        for (uint32_t t = 0; t < st->n_touched; t++) {
+            struct o_slot_buf *sb = &st->slots[st->touched[t]];
             for (uint32_t j = 0; j < sb->count; j++)
-                if (o_lane_push(&lanes[st.touched[t]], sb->pkt[j])) { ret = -1; goto out; }
+                if (o_lane_push(&lanes[st->touched[t]], sb->pkt[j])) return -1;
             sb->count = 0;                                                  /* :291 */
         }
-        st.n_touched = 0;
+        st->n_touched = 0;
     }
 
     uint64_t d = 0;
     for (uint32_t k = 0; k < n_lanes; k++) {
         lane_off[k] = (uint32_t)d;
-        for (uint32_t j = 0; j < lanes[k].n; j++, d++) {
-            if (d >= lane_cap) { ret = -1; goto out; }
-            lane_pkt[d] = lanes[k].v[j];
-        }
+        if (d + lanes[k].n > lane_cap) return -1;
+        memcpy(lane_pkt + d, lanes[k].v, (size_t)lanes[k].n * sizeof(uint32_t));
+        d += lanes[k].n;
     }
     lane_off[n_lanes] = (uint32_t)d;
-    ret = (int64_t)d;
     if (counters) memcpy(counters, cnt, sizeof(cnt));
-out:
-    if (lanes) for (uint32_t k = 0; k < n_lanes; k++) free(lanes[k].v);
-    if (st.slots) for (uint32_t k = 0; k < n_lanes; k++) free(st.slots[k].pkt);
-    free(lanes);
-    free(st.slots);
-    free(st.touched);
-    return ret;
+    return (int64_t)d;
+}
+
+int64_t oracle_rx(const oracle_btable *bt, const uint8_t *frames, uint64_t frames_bytes,
+                  const uint32_t *offset, const uint16_t *length, const uint32_t *ptype,
+                  uint32_t n, uint32_t lane_mask, uint32_t n_lanes, int do_csum,
+                  uint32_t *meta, uint32_t *lane_off, uint32_t *lane_pkt, uint32_t lane_cap,
+                  uint64_t counters[16])
+{
+    struct o_rx_ws w;
+    if (o_ws_init(&w, n_lanes)) return -1;
+    const int64_t r = o_rx_run(&w, bt, frames, frames_bytes, offset, length, ptype, n, lane_mask,
+                               n_lanes, do_csum, meta, lane_off, lane_pkt, lane_cap, counters);
+    o_ws_free(&w);
+    return r;
 }
 
 /* ---------------------------------------------------------------------------------------------
- * CPU baseline harness: one shard per pinned thread.
+ * CPU baseline harness: every pinned thread runs the poller over its own full copy of the batch
+ * (one independent shard per thread). The copy, the poller state and the
+ * outputs are allocated and first touched by the thread itself after pinning (NUMA-local), and
+ * one untimed pass grows the per-socket vectors to size before the timed passes.
  * ------------------------------------------------------------------------------------------- */
 struct o_job {
     const oracle_btable *bt;
@@ -394,8 +432,7 @@ struct o_job {
     const uint32_t *offset;
     const uint16_t *length;
     uint32_t n, lane_mask, n_lanes;
-    int do_csum, reps, cpu;
-    uint32_t *meta, *lane_off, *lane_pkt;
+    int do_csum, reps, cpu, err;
     pthread_barrier_t *bar;
 };
 
@@ -406,12 +443,33 @@ static void *o_job_run(void *arg)
     CPU_ZERO(&set);
     CPU_SET(j->cpu, &set);
     pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+    const uint32_t cap = j->n * 2u + 64u;     /* fan-out <= 2 in the bench workloads */
+    uint8_t *fr = malloc(j->frames_bytes + 64);
+    uint32_t *off = malloc((size_t)j->n * 4 + 4), *meta = malloc((size_t)j->n * 4 + 4);
+    uint16_t *len = malloc((size_t)j->n * 2 + 2);
+    uint32_t *loff = malloc(((size_t)j->n_lanes + 1) * 4), *pkt = malloc((size_t)cap * 4);
+    struct o_rx_ws w;
+    const int ok = fr && off && meta && len && loff && pkt && o_ws_init(&w, j->n_lanes) == 0;
+    if (ok) {
+        memcpy(fr, j->frames, j->frames_bytes);
+        memset(fr + j->frames_bytes, 0, 64);
+        memcpy(off, j->offset, (size_t)j->n * 4);
+        memcpy(len, j->length, (size_t)j->n * 2);
+        memset(meta, 0, (size_t)j->n * 4);
+        memset(pkt, 0, (size_t)cap * 4);
+        if (o_rx_run(&w, j->bt, fr, j->frames_bytes, off, len, NULL, j->n, j->lane_mask, j->n_lanes,
+                     j->do_csum, meta, loff, pkt, cap, NULL) < 0)
+            j->err = 1;
+    } else {
+        j->err = 1;
+    }
     pthread_barrier_wait(j->bar);
-    for (int r = 0; r < j->reps; r++)
-        oracle_rx(j->bt, j->frames, j->frames_bytes, j->offset, j->length, NULL, j->n,
-                  j->lane_mask, j->n_lanes, j->do_csum, j->meta, j->lane_off, j->lane_pkt,
-                  j->n * 8u + 64u, NULL);
+    for (int r = 0; ok && r < j->reps; r++)
+        o_rx_run(&w, j->bt, fr, j->frames_bytes, off, len, NULL, j->n, j->lane_mask, j->n_lanes,
+                 j->do_csum, meta, loff, pkt, cap, NULL);
     pthread_barrier_wait(j->bar);
+    if (ok) o_ws_free(&w);
+    free(fr); free(off); free(meta); free(len); free(loff); free(pkt);
     return NULL;
 }
 
@@ -432,19 +490,12 @@ double oracle_rx_parallel(const oracle_btable *bt, const uint8_t *frames, uint64
     if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0)
         for (int c = 0; c < CPU_SETSIZE; c++)
             if (CPU_ISSET(c, &allowed)) cpus[ncpu++] = c;
-    double secs = -1.0;
-    uint32_t per = (n + (uint32_t)nthreads - 1) / (uint32_t)nthreads;
     for (int t = 0; t < nthreads; t++) {
-        uint32_t a = (uint32_t)t * per, b = a + per < n ? a + per : n;
-        if (a > b) a = b;
         struct o_job *j = &jobs[t];
         j->bt = bt; j->frames = frames; j->frames_bytes = frames_bytes;
-        j->offset = offset + a; j->length = length + a; j->n = b - a;
+        j->offset = offset; j->length = length; j->n = n;
         j->lane_mask = lane_mask; j->n_lanes = n_lanes; j->do_csum = do_csum; j->reps = reps;
         j->cpu = ncpu > 0 ? cpus[t % ncpu] : 0;
-        j->meta = malloc(((size_t)j->n + 1) * 4);
-        j->lane_off = malloc(((size_t)n_lanes + 1) * 4);
-        j->lane_pkt = malloc(((size_t)j->n * 8u + 64u) * 4);
         j->bar = &bar;
     }
     for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, o_job_run, &jobs[t]);
@@ -453,15 +504,16 @@ double oracle_rx_parallel(const oracle_btable *bt, const uint8_t *frames, uint64
     clock_gettime(CLOCK_MONOTONIC, &t0);
     pthread_barrier_wait(&bar);
     clock_gettime(CLOCK_MONOTONIC, &t1);
-    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
-    secs = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    int err = 0;
     for (int t = 0; t < nthreads; t++) {
-        free(jobs[t].meta); free(jobs[t].lane_off); free(jobs[t].lane_pkt);
+        pthread_join(th[t], NULL);
+        err |= jobs[t].err;
     }
+    const double secs = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
     pthread_barrier_destroy(&bar);
     free(jobs);
     free(th);
-    return secs;
+    return err ? -1.0 : secs;
 }
 
 /* ---------------------------------------------------------------------------------------------

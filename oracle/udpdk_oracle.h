@@ -50,8 +50,9 @@ int64_t oracle_rx(const oracle_btable *bt, const uint8_t *frames, uint64_t frame
                   uint32_t *meta, uint32_t *lane_off, uint32_t *lane_pkt, uint32_t lane_cap,
                   uint64_t counters[16]);
 
-/* CPU baseline: nthreads pinned threads, thread t runs oracle_rx over its contiguous slice of
- * the batch (one independent shard per thread) `reps` times. Returns wall seconds. */
+/* CPU baseline: nthreads pinned threads, each runs the poller `reps` times over its own full,
+ * NUMA-local copy of the batch with preallocated poller state (one independent shard per thread:
+ * nthreads x n frames per rep in all). Returns the wall seconds of the timed passes, or -1. */
 double  oracle_rx_parallel(const oracle_btable *bt, const uint8_t *frames, uint64_t frames_bytes,
                            const uint32_t *offset, const uint16_t *length, uint32_t n,
                            uint32_t lane_mask, uint32_t n_lanes, int do_csum, int nthreads,
