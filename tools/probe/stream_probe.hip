@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(256) k_flat(const uint4 *fr, uint32_t *out, ui
 
 int main()
 {
-    const size_t N = 1u << 20, COPIES = 10;
+    const size_t N = getenv("PROBE_N") ? (size_t)atol(getenv("PROBE_N")) : (1u << 20), COPIES = 10;
     uint4 *fr; uint32_t *out;
     (void)hipMalloc(&fr, N * 64 * COPIES);
     (void)hipMalloc(&out, N * 4);
@@ -356,6 +356,10 @@ int main()
     time("laneA4", [&](const uint4 *f) { hipLaunchKernelGGL(k_laneA<4>, dim3(N / 1024), dim3(256), 0, 0, f, out); });
     time("coal1", [&](const uint4 *f) { hipLaunchKernelGGL(k_coal<1>, dim3(N / 256), dim3(256), 0, 0, f, out); });
     time("coal4", [&](const uint4 *f) { hipLaunchKernelGGL(k_coal<4>, dim3(N / 1024), dim3(256), 0, 0, f, out); });
+    time("laneS16", [&](const uint4 *f) { hipLaunchKernelGGL(k_laneS<16>, dim3(N / 4096), dim3(256), 0, 0, f, out); });
+    time("laneS32", [&](const uint4 *f) { hipLaunchKernelGGL(k_laneS<32>, dim3(N / 8192), dim3(256), 0, 0, f, out); });
+    time("coal16", [&](const uint4 *f) { hipLaunchKernelGGL(k_coal<16>, dim3(N / 4096), dim3(256), 0, 0, f, out); });
+    time("coal32", [&](const uint4 *f) { hipLaunchKernelGGL(k_coal<32>, dim3(N / 8192), dim3(256), 0, 0, f, out); });
     for (int g : {1024, 2048, 4096, 8192, 16384})
         time(g == 1024 ? "flat1024" : g == 2048 ? "flat2048" : g == 4096 ? "flat4096" : g == 8192 ? "flat8192" : "flat16384",
              [&](const uint4 *f) { hipLaunchKernelGGL(k_flat, dim3(g), dim3(256), 0, 0, f, out, (uint32_t)(N * 4)); });

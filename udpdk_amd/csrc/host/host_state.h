@@ -142,6 +142,9 @@ struct h_state {
     uint32_t frag_buckets, frag_entries, frag_max_dgram;
     uint64_t frag_ttl_ms;
     uint32_t poll_threads;       /* [gpu] poll_threads: threads of udpdk_poll_rx's socket loops  */
+    uint32_t host_copy_min;      /* [gpu] host_copy_min: mean payload bytes from which a poll copies
+                                  * its payloads on the host instead of gathering them on the GPU
+                                  * (0: always the GPU gather)                                     */
     /* RX work buffers (poller thread only), grow-only */
     uint32_t *rx_meta, *rx_loff, *rx_lpkt;
     uint64_t  rx_meta_cap, rx_loff_cap, rx_lpkt_cap;

@@ -26,6 +26,7 @@ static void h_config_defaults(void)
     g_udpdk.gpu_device = 0;
     g_udpdk.n_shards = 0;
     g_udpdk.poll_threads = 0;
+    g_udpdk.host_copy_min = 512;
     g_udpdk.gpu_max_frames = 1u << 20;
     g_udpdk.gpu_max_lanes = UDPDK_MAX_SOCKETS;
     g_udpdk.frag_buckets = 0x1000;     /* NUM_FLOWS_DEF, udpdk_constants.h:32 */
@@ -156,6 +157,8 @@ static int h_load_ini(const char *path)
             g_udpdk.gpu_max_lanes = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "poll_threads")) {
             g_udpdk.poll_threads = (uint32_t)strtoul(v, NULL, 0);
+        } else if (!strcmp(section, "gpu") && !strcmp(k, "host_copy_min")) {
+            g_udpdk.host_copy_min = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "frag_buckets")) {
             g_udpdk.frag_buckets = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "frag_bucket_entries")) {

@@ -407,6 +407,56 @@ static void h_pub_job(void *ctx, uint32_t part, uint32_t parts)
     }
 }
 
+/* ---- payload copy on the host ---------------------------------------------------------------
+ * The poll's frames are in host memory already (the caller's batch, a NIC's DMA target), so for
+ * long datagrams the payloads are copied from there into the slab on the pool's threads instead of
+ * being gathered on the GPU and copied back across PCIe (the 1500 B poll paid the link twice for
+ * its payloads). Same result as rx_gather (rx_gather.hip): n = min(data_len - 42, dgram_len - 8
+ * as uint16_t, slot room), source address and port as raw wire words (udpdk_syscall.c:436-466). */
+struct h_hcopy {
+    const uint8_t *frames;
+    const uint32_t *offset;
+    const uint16_t *length;
+    const uint32_t *acc, *offs;
+    uint32_t count;
+    struct h_arena *a;
+};
+
+static void h_hcopy_job(void *ctx, uint32_t part, uint32_t parts)
+{
+    const struct h_hcopy *H = ctx;
+    const uint32_t k0 = (uint32_t)((uint64_t)H->count * part / parts);
+    const uint32_t k1 = (uint32_t)((uint64_t)H->count * (part + 1) / parts);
+    for (uint32_t k = k0; k < k1; k++) {
+        const uint32_t fi = H->acc[k];
+        const uint8_t *f = H->frames + H->offset[fi];
+        const uint32_t len = H->length[fi];
+        const uint32_t seg = len >= 42u ? len - 42u : 0u;
+        const uint32_t dl = ((uint32_t)f[38] << 8) | f[39];
+        const uint32_t pl = (dl - 8u) & 0xFFFFu;
+        const uint32_t cap = H->offs[k + 1] - H->offs[k];
+        uint32_t n = seg < pl ? seg : pl;
+        if (n > cap) n = cap;
+        memcpy(H->a->payload + H->offs[k], f + 42, n);
+        H->a->len[k] = n;
+        memcpy(&H->a->src_ip[k], f + 26, 4);
+        memcpy(&H->a->src_port[k], f + 34, 2);
+    }
+}
+
+static int h_host_gather(const uint8_t *frames, const uint32_t *offset, const uint16_t *length,
+                         const uint32_t *acc, const uint32_t *offs, uint32_t count, struct h_arena **out)
+{
+    *out = NULL;
+    if (!count) return 0;
+    struct h_arena *a = h_arena_get(count, offs[count] ? offs[count] : 16u);
+    if (!a) return -1;
+    struct h_hcopy H = {frames, offset, length, acc, offs, count, a};
+    h_pool_run(h_hcopy_job, &H);
+    *out = a;
+    return 0;
+}
+
 /* ---- multi-device shards ------------------------------------------------------------------ */
 struct h_sjob {
     const uint8_t *frames;
@@ -719,8 +769,12 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
     PROF_T(p4);
     g_udpdk.acc_do[nad] = (uint32_t)offd;
     g_udpdk.acc_fo[naf] = (uint32_t)offf;
-    if ((sharded ? h_shards_gather(nad) : h_gather(g, &g_udpdk.gb, &staged, g_udpdk.acc_d, g_udpdk.acc_do,
-                                                    nad, &ad)) ||
+    /* direct payloads: host copy when the poll's datagrams are long on average ([gpu]
+     * host_copy_min payload bytes, measured in bench.py's socket_path), else the GPU gather */
+    const int hcopy = nad && g_udpdk.host_copy_min && offd >= (uint64_t)nad * g_udpdk.host_copy_min;
+    if ((hcopy ? h_host_gather(frames, offset, length, g_udpdk.acc_d, g_udpdk.acc_do, nad, &ad)
+               : sharded ? h_shards_gather(nad)
+                         : h_gather(g, &g_udpdk.gb, &staged, g_udpdk.acc_d, g_udpdk.acc_do, nad, &ad)) ||
         (naf && h_gather(g, &g_udpdk.gb, &rb, g_udpdk.acc_f, g_udpdk.acc_fo, naf, &af))) {
         if (errno != ENOBUFS) goto out;
         /* slab budget exhausted by datagrams still queued: this poll's bursts are dropped */
@@ -734,12 +788,12 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
     PROF_T(p6);
     if (ad) atomic_store_explicit(&ad->refs, nad, memory_order_relaxed);
     if (af) atomic_store_explicit(&af->refs, naf, memory_order_relaxed);
-    for (uint32_t k = 0; sharded && k < g_udpdk.n_shards; k++)
+    for (uint32_t k = 0; sharded && !hcopy && k < g_udpdk.n_shards; k++)
         if (g_udpdk.shard[k].arena)
             atomic_store_explicit(&g_udpdk.shard[k].arena->refs, g_udpdk.shard[k].nacc, memory_order_relaxed);
     /* publish: each socket's entries go to its ring in bulk enqueues, sockets over the pool */
     {
-        struct h_pub P = {&A, ad, af, sharded};
+        struct h_pub P = {&A, ad, af, sharded && !hcopy};
         h_pool_run(h_pub_job, &P);
     }
     ad = af = NULL;

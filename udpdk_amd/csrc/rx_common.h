@@ -92,6 +92,7 @@ struct RxArgs {
     uint32_t n_tiles;
     uint32_t lane_mask;
     uint32_t n_lanes;
+    uint32_t hist16;      // hist rows are u16[(n_lanes + 1) & ~1] (multi-lane, no fan-out)
 };
 
 struct ScanArgs {
@@ -103,25 +104,24 @@ struct ScanArgs {
     uint32_t n_elems;
     uint32_t n_tiles;
     uint32_t n_lanes;
+    // rx_scan_cols only: absolute positions out (base[tile][lane] = lane_off + column prefix), the
+    // lane-block look-back words (epoch << 32 | flag << 30 | value) and the block ticket
+    uint32_t *base;
+    unsigned long long *agg;
+    uint32_t *ticket;
+    uint32_t epoch;
+    uint32_t hist16;
 };
 
 // rx_scan_cols: one launch, workgroup = a block of 2^lb lanes x every tile; each thread keeps up
 // to SCAN_COLS_TPT tiles of one lane in registers, so tiles <= SCAN_COLS_TPT * (256 >> lb).
 constexpr int SCAN_COLS_BLOCK = 256;
-// lanes from which rx_lane_off scans lane_off once instead of every scatter workgroup
-#ifndef UDPDK_LANE_ONCE_MIN
-#define UDPDK_LANE_ONCE_MIN 2048
-#endif
-constexpr uint32_t LANE_ONCE_MIN = UDPDK_LANE_ONCE_MIN;
 constexpr uint32_t SCAN_COLS_TPT = 64;
 constexpr uint32_t SCAN_COLS_MAX_TILES = SCAN_COLS_TPT * SCAN_COLS_BLOCK;
 
 struct ScatterArgs {
     const uint32_t *meta;
-    const uint32_t *base;  // scanned hist: per-lane exclusive prefix over the earlier tiles
-    const uint32_t *tot;   // lane totals (rx_scan_cols); null: base already includes lane_off
-    uint32_t *lane_off;    // written by the workgroup of tile 0 when tot is given
-    const uint32_t *lane_base;  // lane_off computed by rx_lane_off: cursor = lane_base + base
+    const uint32_t *base;  // [tiles][lanes] absolute start of each tile's deliveries per lane
     uint32_t *total;
     const uint8_t  *frames;
     const uint32_t *offset;
@@ -202,20 +202,18 @@ __global__ void rx_scan_top(ScanArgs a, uint32_t n_part);
 __global__ void rx_scan_down(ScanArgs a);
 __global__ void rx_scatter(ScatterArgs a);
 __global__ void rx_scatterw(ScatterArgs a);
-__global__ void rx_lane_off(const uint32_t *tot, uint32_t n_lanes, uint32_t *lane_off, uint32_t *total);
 constexpr uint32_t SCATTER_WAVES = 8;           // rx_scatterw workgroup: 8 waves per tile
 constexpr uint32_t SCATTERW_MAX_LANES = 4096;   // rx_scatterw LDS: (4 + 2 x 8) x lanes bytes
 __host__ __device__ constexpr uint32_t scatterw_lds_bytes(uint32_t n_lanes)
 {
-    // cursors + per-wave slice offsets (u16), which double as the prologue's S + 16 words of
-    // scratch: 80 KiB at 4096 lanes, so two workgroups share a CU's 160 KiB
-    return 4u * n_lanes + (2u * SCATTER_WAVES * n_lanes > 4u * n_lanes + 64u
-                           ? 2u * SCATTER_WAVES * n_lanes : 4u * n_lanes + 64u);
+    // cursors + per-wave slice offsets (u16): 80 KiB at 4096 lanes, so two workgroups share a
+    // CU's 160 KiB
+    return 4u * n_lanes + 2u * SCATTER_WAVES * n_lanes;
 }
 constexpr int SCATTER1_BLOCK = 256;             // rx_scatter: prologue by 4 waves, walk by wave 0
 __host__ __device__ constexpr uint32_t scatter1_lds_bytes(uint32_t n_lanes)
 {
-    return 8u * n_lanes + 64u;                  // cursors + the base row staged for the prologue
+    return 4u * n_lanes + 64u;                  // cursors
 }
 __global__ void rx_compact1(Compact1Args a);
 __global__ void rx_tile_base(const uint32_t *cnt, uint32_t *base, uint32_t n);

@@ -255,8 +255,12 @@ rx_classify(RxArgs a)
     uint2 *dstash = reinterpret_cast<uint2 *>(dgl + RX_ROUND);       // [RX_ROUND]
 
     // (hist is only used with several lanes; its zeroing is ordered by the staging barrier)
+    // hist16: two lanes per LDS word (lane k in the half k & 1), counts < 2^16 (a tile's
+    // deliveries per lane, <= 8192 without fan-out), stored as a u16 row
+    const uint32_t hsh = a.hist16 ? 1u : 0u;
+    auto hist_add = [&](uint32_t k, uint32_t v) { atomicAdd(&hist[k >> hsh], v << ((k & hsh) << 4)); };
     if (a.n_lanes > 1u)
-        for (uint32_t s = tid; s < a.n_lanes; s += CLS_BLOCK) hist[s] = 0;
+        for (uint32_t s = tid; s < ((a.n_lanes + hsh) >> hsh); s += CLS_BLOCK) hist[s] = 0;
     // Tiles in dispatch order (consecutive tiles on different XCDs). An XCD-contiguous remap
     // (each XCD's L2 streaming one contiguous eighth of the batch) measured 1.7 us slower per
     // 1 M x 64 B launch (tools/probe/stream_probe.hip, feat4).
@@ -562,6 +566,7 @@ rx_classify(RxArgs a)
             if ((st / CLS_WAVES) % SPR == SPR - 2u && st / RSTEPS + 1u < steps / RSTEPS) {
                 stage(st / RSTEPS + 1u);
                 __syncthreads();
+                STAMP(5);
             }
             W = NW;
             c_off = n_off;
@@ -597,7 +602,7 @@ rx_classify(RxArgs a)
                             if (dip == bd.x || bd.x == 0u) {
                                 const uint32_t sock = bd.y & 0x7FFFFFFFu;
                                 if (fan > 0 && a.n_lanes > 1u)
-                                    atomicAdd(&hist[sock & a.lane_mask], 1u);   // clones (rare)
+                                    hist_add(sock & a.lane_mask, 1u);           // clones (rare)
                                 if (fan == 0) first = sock;
                                 ++fan;
                                 if (!(bd.y >> 31)) break;
@@ -637,12 +642,13 @@ rx_classify(RxArgs a)
                         peers &= kb ? bal : ~bal;
                     }
                     if (delivered && lane == (uint32_t)__ffsll((long long)peers) - 1u)
-                        atomicAdd(&hist[key], (uint32_t)__popcll(peers));
+                        hist_add(key, (uint32_t)__popcll(peers));
                 } else if (delivered) {
-                    atomicAdd(&hist[key], 1u);
+                    hist_add(key, 1u);
                 }
             }
         }
+        STAMP(3);
     }
 
     // ---- tile counters: one row per wave (lanes 0-15), summed by the readers ----
@@ -697,8 +703,13 @@ rx_classify(RxArgs a)
     if (a.n_lanes == 1u) {
         if (tid == 0) a.hist[tile] = tile_counter(UDPDK_C_DELIVERIES);
     } else {
-        for (uint32_t s = tid; s < a.n_lanes; s += CLS_BLOCK)
-            a.hist[(size_t)tile * a.n_lanes + s] = hist[s];
+        if (a.hist16) {           // u16 row of n_lanes (rounded up to even) counts
+            const uint32_t hw = (a.n_lanes + 1u) >> 1;
+            for (uint32_t s = tid; s < hw; s += CLS_BLOCK) a.hist[(size_t)tile * hw + s] = hist[s];
+        } else {
+            for (uint32_t s = tid; s < a.n_lanes; s += CLS_BLOCK)
+                a.hist[(size_t)tile * a.n_lanes + s] = hist[s];
+        }
     }
     if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = tile_counter(tid);
 }
@@ -878,29 +889,57 @@ __device__ __forceinline__ void scan_lane_totals(const uint32_t *tot, uint32_t n
     if (tid == 0) { lane_off[n_lanes] = total; *total_out = total; }
 }
 
-// rx_scan_cols: the whole column scan in one launch. Workgroup = a block of LB = 2^lb lanes
-// and every tile; thread (c, l) holds lane l's counts of the c-th of 256 / LB contiguous tile
-// chunks (<= SCAN_COLS_TPT tiles) in registers, all loaded at once (LB lanes x 4 B contiguous per
-// tile row). The chunk sums meet in LDS; each thread then writes its chunk's running prefix back
-// in place: hist[t][l] = sum over t' < t of hist[t'][l] (lane_off NOT included), and the lane
-// total goes to tot[l]. lane_off = exclusive scan of tot is folded into the scatter's prologue
-// (lane_cursors), so no launch waits for a scan over lanes. One read and one write of the
-// histogram, in place of the reduce / top / down chain's three launches.
+// rx_scan_cols: the whole scan in one launch. Workgroup = a block of LB = 2^lb lanes x every
+// tile; thread (c, l) holds lane l's counts of the c-th of 256 / LB contiguous tile chunks
+// (<= SCAN_COLS_TPT tiles) in registers, all loaded at once (LB lanes x 2 or 4 B contiguous per
+// tile row). The chunk sums meet in LDS and give the lane totals; the lane offsets (the exclusive
+// scan of the totals over ALL lanes, which other workgroups hold) come from a decoupled look-back
+// over the lane blocks: blocks take tickets in dispatch order, publish their total (A) at once
+// and their inclusive prefix (P) once they know it, and a block sums its predecessors' words back
+// to the nearest P, one 64-word window per wave load. Each thread then writes its tiles' absolute
+// positions base[t][l] = lane_off[l] + sum over t' < t of hist[t'][l], so the scatter reads one
+// row per tile and no launch runs between this one and it (the former rx_lane_off).
+// Look-back words: epoch << 32 | flag << 30 | value, flag 1 = A, 2 = P; a word from an earlier
+// call (older epoch) is not ready. Value < 2^30: deliveries <= max_frames x fan-out.
+__device__ __forceinline__ unsigned long long lb_poll(unsigned long long *p, uint32_t epoch)
+{
+    unsigned long long v;
+    for (;;) {
+        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(v >> 32) == epoch && ((v >> 30) & 3u)) return v;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 __global__ void __launch_bounds__(SCAN_COLS_BLOCK)
 rx_scan_cols(ScanArgs a, uint32_t lb)
 {
     __shared__ uint32_t part[SCAN_COLS_BLOCK];
+    __shared__ uint32_t loff_sh[64];
+    __shared__ uint32_t jb;
     const uint32_t LB = 1u << lb, C = (uint32_t)SCAN_COLS_BLOCK >> lb;
     const uint32_t l = threadIdx.x & (LB - 1u), c = threadIdx.x >> lb;
-    const uint32_t S = a.n_lanes, lanei = blockIdx.x * LB + l;
+    if (threadIdx.x == 0) {
+        const uint32_t j = atomicAdd(a.ticket, 1u);
+        if (j == gridDim.x - 1u) atomicExch(a.ticket, 0u); // every ticket taken: reset for the next call
+        jb = j;
+    }
+    __syncthreads();
+    const uint32_t j = jb;
+    const uint32_t S = a.n_lanes, lanei = j * LB + l;
     const uint32_t tpc = (a.n_tiles + C - 1u) / C;
     const uint32_t t0 = min(a.n_tiles, c * tpc), t1 = min(a.n_tiles, t0 + tpc);
     const bool ok = lanei < S;
-    uint32_t *col = a.hist + lanei;
+    const uint32_t hs = a.hist16 ? ((S + 1u) & ~1u) : S;   // row stride in counts
+    const uint16_t *col16 = reinterpret_cast<const uint16_t *>(a.hist) + lanei;
+    const uint32_t *col32 = a.hist + lanei;
     uint32_t v[SCAN_COLS_TPT];
 #pragma unroll
-    for (uint32_t k = 0; k < SCAN_COLS_TPT; ++k)
-        v[k] = (ok && t0 + k < t1) ? col[(size_t)(t0 + k) * S] : 0u;
+    for (uint32_t k = 0; k < SCAN_COLS_TPT; ++k) {
+        const bool in = ok && t0 + k < t1;
+        const size_t o = (size_t)(in ? t0 + k : 0u) * hs;
+        v[k] = !in ? 0u : a.hist16 ? (uint32_t)col16[o] : col32[o];
+    }
     uint32_t sum = 0;
 #pragma unroll
     for (uint32_t k = 0; k < SCAN_COLS_TPT; ++k) sum += v[k];
@@ -912,10 +951,47 @@ rx_scan_cols(ScanArgs a, uint32_t lb)
         run += i < c ? x : 0u;
         tot += x;
     }
-    if (ok && c == 0) a.tot[lanei] = tot;
+    if (threadIdx.x < 64) {                                  // wave 0: threads (0, l), l < LB <= 64
+        const uint32_t lane = lane_id();
+        const uint32_t mine = lane < LB && ok ? tot : 0u;
+        const uint32_t incl = wave_incl_scan(mine);
+        const uint32_t btot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const unsigned long long tag = (unsigned long long)a.epoch << 32;
+        if (lane == 0)
+            __hip_atomic_store(&a.agg[j], tag | (1ull << 30) | btot,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // look-back: the predecessors' words, 64 at a time, down to the nearest inclusive one
+        uint32_t pre = 0;
+        for (uint32_t k = j; k > 0;) {
+            const uint32_t idx = k - 1u - lane;                 // lane 0 = nearest predecessor
+            const bool in = lane < k;
+            const unsigned long long wv = in ? lb_poll(&a.agg[idx], a.epoch) : (tag | (2ull << 30));
+            const unsigned long long pm = __ballot(((wv >> 30) & 3u) == 2u);
+            const uint32_t stop = pm ? (uint32_t)__ffsll((long long)pm) - 1u : 64u;
+            const uint32_t val = in && lane <= stop ? (uint32_t)(wv & 0x3FFFFFFFu) : 0u;
+            pre += wave_sum(val);
+            if (pm) break;
+            k = k > 64u ? k - 64u : 0u;
+        }
+        if (lane == 0)
+            __hip_atomic_store(&a.agg[j], tag | (2ull << 30) | (pre + btot),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane < LB) {
+            const uint32_t lo = pre + incl - mine;
+            loff_sh[lane] = lo;
+            if (ok) a.lane_off[lanei] = lo;
+        }
+        if (lane == 0 && (j + 1u) * LB >= S) {             // the last block: the grand total
+            a.lane_off[S] = pre + btot;
+            *a.total = pre + btot;
+        }
+    }
+    __syncthreads();
+    run += loff_sh[l];
+    uint32_t *out = a.base + lanei;
 #pragma unroll
     for (uint32_t k = 0; k < SCAN_COLS_TPT; ++k) {
-        if (ok && t0 + k < t1) col[(size_t)(t0 + k) * S] = run;
+        if (ok && t0 + k < t1) out[(size_t)(t0 + k) * S] = run;
         run += v[k];
     }
 }
@@ -983,15 +1059,6 @@ rx_scan_down(ScanArgs a)
     }
 }
 
-// lane_off = exclusive scan of the lane totals rx_scan_cols left, once per batch (one
-// workgroup), instead of in every scatter workgroup's prologue.
-__global__ void __launch_bounds__(1024)
-rx_lane_off(const uint32_t *tot, uint32_t n_lanes, uint32_t *lane_off, uint32_t *total)
-{
-    __shared__ uint32_t lds16[16];
-    scan_lane_totals(tot, n_lanes, lane_off, total, lds16);
-}
-
 // Tile of workgroup b out of n so that each XCD walks a contiguous run of tiles (blocks are dealt
 // round-robin over the 8 XCDs, MI355X_MICROARCH.md §Workgroup dispatch; b % 8 labels the blocks
 // sharing one). Bijective for any n. A lane's entries from consecutive tiles are adjacent in
@@ -1004,83 +1071,22 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n)
     return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + (b >> 3);
 }
 
-// Scatter prologue: cur[k] = lane_off[k] + base[tile][k] for the S lanes, where lane_off is the
-// exclusive scan of the lane totals (every workgroup scans them itself, S <= 16384 words from L2;
-// the workgroup of tile 0 also stores lane_off[0..S] and the total). tmp: >= S + 16 words of LDS
-// scratch (no static LDS here: rx_scatterw's dynamic carve is sized so two workgroups share a
-// CU, and one more word would halve that). With a.tot == null (the 3-launch scan) base is
-// already absolute.
-__device__ __forceinline__ void lane_cursors(const ScatterArgs &a, uint32_t tile, uint32_t *cur, uint32_t *tmp)
+// Scatter prologue: cur[k] = base[tile][k], the absolute start of the tile's deliveries in lane k
+// (rx_scan_cols / rx_scan_down fold lane_off in), for the S lanes, CU loads per thread in flight at
+// once (clamped indices, stores guarded): a plain strided loop waited for each iteration's loads,
+// one L2 / HBM round trip per NT lanes (8 at 4096 lanes and 512 threads).
+__device__ __forceinline__ void lane_cursors(const ScatterArgs &a, uint32_t tile, uint32_t *cur)
 {
     const uint32_t tid = threadIdx.x, NT = blockDim.x, S = a.n_lanes;
     const uint32_t *base = a.base + (size_t)tile * S;
-    // x[k] -> d0[k], y[k] -> d1[k] for k < S, CU loads per thread in flight at once (clamped
-    // indices, stores guarded): a plain strided loop waited for each iteration's loads, one L2 /
-    // HBM round trip per NT lanes (8 at 4096 lanes and 512 threads)
-    auto stage2 = [&](const uint32_t *x, const uint32_t *y, uint32_t *d0, uint32_t *d1, bool sum) {
-        constexpr uint32_t CU = 8;
-        for (uint32_t k0 = tid; k0 < S; k0 += NT * CU) {
-            uint32_t vx[CU], vy[CU];
+    constexpr uint32_t CU = 8;
+    for (uint32_t k0 = tid; k0 < S; k0 += NT * CU) {
+        uint32_t vy[CU];
 #pragma unroll
-            for (uint32_t u = 0; u < CU; ++u) {
-                const uint32_t k = min(k0 + u * NT, S - 1u);
-                vx[u] = x ? x[k] : 0u;
-                vy[u] = y[k];
-            }
+        for (uint32_t u = 0; u < CU; ++u) vy[u] = base[min(k0 + u * NT, S - 1u)];
 #pragma unroll
-            for (uint32_t u = 0; u < CU; ++u) {
-                const uint32_t k = k0 + u * NT;
-                if (k < S) {
-                    if (sum) {
-                        d0[k] = vx[u] + vy[u];
-                    } else {
-                        d0[k] = vx[u];
-                        d1[k] = vy[u];
-                    }
-                }
-            }
-        }
-    };
-    if (a.lane_base) {                                  // lane_off scanned once (rx_lane_off)
-        stage2(a.lane_base, base, cur, nullptr, true);
-        __syncthreads();
-        return;
-    }
-    if (!a.tot) {
-        stage2(nullptr, base, cur, nullptr, true);
-        __syncthreads();
-        return;
-    }
-    stage2(a.tot, base, cur, tmp, false);
-    __syncthreads();
-    const uint32_t L = (S + NT - 1u) / NT, l0 = min(S, tid * L), l1 = min(S, l0 + L);
-    uint32_t s = 0;
-    for (uint32_t k = l0; k < l1; ++k) s += cur[k];
-    uint32_t *wsum = tmp + S;
-    const uint32_t inc = scan_dpp(s), w = tid >> 6;
-    if (lane_id() == 63) wsum[w] = inc;
-    __syncthreads();
-    uint32_t pre = inc - s, total = 0;
-    for (uint32_t i = 0; i < NT / 64u; ++i) {
-        const uint32_t x = wsum[i];
-        pre += i < w ? x : 0u;
-        total += x;
-    }
-    for (uint32_t k = l0; k < l1; ++k) {
-        const uint32_t v = cur[k];
-        cur[k] = pre;
-        pre += v;
-    }
-    __syncthreads();
-    const bool first = tile == 0;
-    for (uint32_t k = tid; k < S; k += NT) {
-        const uint32_t o = cur[k];
-        if (first) a.lane_off[k] = o;
-        cur[k] = o + tmp[k];
-    }
-    if (first && tid == 0) {
-        a.lane_off[S] = total;
-        *a.total = total;
+        for (uint32_t u = 0; u < CU; ++u)
+            if (k0 + u * NT < S) cur[k0 + u * NT] = vy[u];
     }
     __syncthreads();
 }
@@ -1141,7 +1147,7 @@ rx_scatterw(ScatterArgs a)
 #else
 #define SSTAMP(k) do {} while (0)
 #endif
-    lane_cursors(a, tile, cur, cnt);                                   // cnt doubles as scratch
+    lane_cursors(a, tile, cur);
     SSTAMP(0);
     for (uint32_t k = tid; k < (W / 2) * S; k += 64 * W) cnt[k] = 0;
     __syncthreads();
@@ -1203,7 +1209,7 @@ rx_scatter(ScatterArgs a)
     const uint32_t lane = lane_id();
     const uint32_t tile = xcd_tile(blockIdx.x, a.n_tiles);
     // cursor of every lane for this tile: the whole workgroup runs the prologue, wave 0 the walk
-    lane_cursors(a, tile, cur, cur + a.n_lanes);
+    lane_cursors(a, tile, cur);
     if (threadIdx.x >= 64) return;
     const uint32_t t0 = tile * a.tile_frames;
     const uint32_t t1 = min(a.n, t0 + a.tile_frames);

@@ -48,7 +48,10 @@ struct Pipe {
     hipStream_t stream = nullptr;
     uint32_t *hist = nullptr;
     uint32_t *partial = nullptr;
-    uint32_t *tot = nullptr;                  // [max_lanes] lane totals (rx_scan_cols)
+    uint32_t *base = nullptr;                 // [tiles][lanes] absolute positions (rx_scan_cols)
+    unsigned long long *agg = nullptr;        // rx_scan_cols look-back words, one per lane block
+    uint32_t *ticket = nullptr;               // rx_scan_cols lane-block tickets
+    uint32_t epoch = 0;                       // rx_scan_cols calls on this pipe (look-back tag)
     uint32_t *tile_cnt = nullptr;
     DevResult *res = nullptr;                 // counters, total (device)
     DevResult *h_res = nullptr;               // pinned mirror, filled by udpdk_gpu_rx_stats
@@ -283,7 +286,11 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
         for (Pipe &P : c->pipes) {
             ok = ok && hipMalloc((void **)&P.hist, e_cap * 4) == hipSuccess;
             ok = ok && hipMalloc((void **)&P.partial, c->partial_cap * 4) == hipSuccess;
-            ok = ok && hipMalloc((void **)&P.tot, ((size_t)max_lanes + 1) * 4) == hipSuccess;
+            ok = ok && hipMalloc((void **)&P.base, e_cap * 4) == hipSuccess;
+            ok = ok && hipMalloc((void **)&P.agg, ((size_t)max_lanes / 8 + 1) * 8) == hipSuccess;
+            ok = ok && hipMemset(P.agg, 0, ((size_t)max_lanes / 8 + 1) * 8) == hipSuccess;
+            ok = ok && hipMalloc((void **)&P.ticket, 64) == hipSuccess;
+            ok = ok && hipMemset(P.ticket, 0, 64) == hipSuccess;
             ok = ok && hipMalloc((void **)&P.tile_cnt, c->tiles_cap * UDPDK_N_COUNTERS * 4) == hipSuccess;
             ok = ok && hipMalloc((void **)&P.res, sizeof(DevResult)) == hipSuccess;
             ok = ok && hipMemset(P.res, 0, sizeof(DevResult)) == hipSuccess;
@@ -297,7 +304,7 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
                                 (int)scatter1_lds_bytes(UDPDK_GPU_MAX_LANES)) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatterw, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 scatterw_lds_bytes(SCATTERW_MAX_LANES)) != hipSuccess) break;
-        // lane totals: 4 B per lane, up to UDPDK_GPU_MAX_LANES (64 KiB) beside a few static words
+        // rx_scan_top's lane totals: 4 B per lane, up to UDPDK_GPU_MAX_LANES (64 KiB)
         if (hipFuncSetAttribute((const void *)rx_scan_top, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 4 * UDPDK_GPU_MAX_LANES) != hipSuccess) break;
         rc = 0;
@@ -327,7 +334,8 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
     for (Pipe &P : c->pipes) {
         void *ph[] = {P.st_frames_h, P.st_desc_h};
         for (void *p : ph) if (p) (void)hipHostFree(p);
-        void *pd[] = {P.hist, P.partial, P.tot, P.tile_cnt, P.res, P.st_frames_d, P.st_desc_d, P.st_out_d};
+        void *pd[] = {P.hist, P.partial, P.base, P.agg, P.ticket, P.tile_cnt, P.res, P.st_frames_d,
+                      P.st_desc_d, P.st_out_d};
         for (void *p : pd) if (p) (void)hipFree(p);
         if (P.h_res) (void)hipHostFree(P.h_res);
         if (P.tail) (void)hipEventDestroy(P.tail);
@@ -560,8 +568,15 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     const bool one_lane = S == 1 && c->max_fanout <= 1;
     P.last_tiles = tiles;
 
+    // the one-launch column scan while each thread's tile chunk fits its registers; beyond (very
+    // large batches over few lanes) the reduce / top / down chain over u32 counts
+    const bool cols = !one_lane && tiles <= SCAN_COLS_MAX_TILES;
+    // u16 tile histograms where a lane's count per tile cannot pass 2^16 (no fan-out): half the
+    // bytes classify stores at its tile ends and the scan reads
+    const bool hist16 = cols && c->max_fanout <= 1;
     RxArgs ra;
     memset(&ra, 0, sizeof(ra));
+    ra.hist16 = hist16 ? 1u : 0u;
     ra.frames = bt->frames_dev;
     ra.offset = bt->offset_dev;
     ra.length = bt->length_dev;
@@ -609,20 +624,19 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     }
 
     ScanArgs sa;
+    memset(&sa, 0, sizeof(sa));
     sa.hist = P.hist;
     sa.partial = P.partial;
     sa.lane_off = o->lane_off_dev;
     sa.total = &P.res->total;
-    sa.tot = P.tot;
     sa.n_elems = (uint32_t)E;
     sa.n_tiles = tiles;
     sa.n_lanes = S;
-    // one-launch column scan while each thread's tile chunk fits its registers; beyond (very
-    // large batches over few lanes) the reduce / top / down chain, which also writes lane_off
-    const bool cols = tiles <= SCAN_COLS_MAX_TILES;
-    // with many lanes, lane_off is scanned once by rx_lane_off rather than by every scatter
-    // workgroup
-    const bool lane_once = cols && S >= LANE_ONCE_MIN;
+    sa.base = P.base;
+    sa.agg = P.agg;
+    sa.ticket = P.ticket;
+    sa.epoch = ++P.epoch ? P.epoch : ++P.epoch;        // 0 marks a never-written look-back word
+    sa.hist16 = ra.hist16;
     if (cols) {
         // lanes per workgroup: as many as the chunking allows (<= 64, 256 B rows), then fewer
         // until the grid has >= UDPDK_SCAN_MIN_WG workgroups, never under 8 lanes (32 B row
@@ -632,11 +646,8 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
         uint32_t lb = 0;
         while ((2u << lb) <= std::min<uint32_t>(64u, SCAN_COLS_BLOCK / cmin)) ++lb;
         while (lb > 3 && ceil_div(S, 1u << lb) < UDPDK_SCAN_MIN_WG) --lb;
-        HIPC(c, launch(st, ts, 1, true, !lane_once, rx_scan_cols, dim3(ceil_div(S, 1u << lb)),
+        HIPC(c, launch(st, ts, 1, true, true, rx_scan_cols, dim3(ceil_div(S, 1u << lb)),
                        dim3(SCAN_COLS_BLOCK), 0u, sa, lb));
-        if (lane_once)
-            HIPC(c, launch(st, ts, 1, false, true, rx_lane_off, dim3(1), dim3(1024), 0u,
-                           (const uint32_t *)P.tot, S, o->lane_off_dev, &P.res->total));
     } else {
         const uint32_t nc = ceil_div(tiles, SCAN_COL_CHUNK);
         if ((uint64_t)nc * S > c->partial_cap) return -EINVAL;
@@ -648,10 +659,7 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
 
     ScatterArgs xa;
     xa.meta = o->meta_dev;
-    xa.base = P.hist;
-    xa.tot = cols && !lane_once ? P.tot : nullptr;
-    xa.lane_base = lane_once ? o->lane_off_dev : nullptr;
-    xa.lane_off = o->lane_off_dev;
+    xa.base = cols ? P.base : P.hist;
     xa.total = &P.res->total;
     xa.frames = bt->frames_dev;
     xa.offset = bt->offset_dev;
