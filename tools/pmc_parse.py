@@ -39,6 +39,12 @@ for cfg in (1, 2, 3, 4, 5):
     out[name] = {"kernels": kern,
                  "rx_classify_hbm_bytes_per_launch": kern.get("rx_classify", {}).get("hbm_bytes_per_launch")}
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
-    json.dump({"method": __doc__.strip().split("\n\n")[1].replace("\n", " "), "workloads": out}, f, indent=1)
+path = os.path.join(ROOT, "profiles", "traffic.json")
+# workloads not measured in this pass keep their earlier entries
+prev = json.load(open(path))["workloads"] if os.path.exists(path) else {}
+for k, v in out.items():
+    v["measured_with"] = os.environ.get("PMC_TAG", "")
+prev.update(out)
+with open(path, "w") as f:
+    json.dump({"method": __doc__.strip().split("\n\n")[1].replace("\n", " "), "workloads": prev}, f, indent=1)
 print(json.dumps(out, indent=1))
