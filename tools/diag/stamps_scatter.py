@@ -4,13 +4,13 @@ import ctypes as C
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["UDPDK_LIB_OVERRIDE"] = os.path.join(ROOT, "tools", "diag", "libudpdk_amd.so")
 sys.path.insert(0, ROOT)
 import numpy as np
 from udpdk_amd import abi, frames as F
 
-PH = ["lane_cursors", "woff zero", "pass0 count", "slice offsets", "pass1 place"]
+PH = ["lane_cursors", "woff zero", "pass0 count", "slice offsets", "pass1 place (ranks)", "staged key-order write-out"]
 L = abi.lib()
 L.udpdk_gpu_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 ctx = abi.GpuContext(0, max_frames=1 << 22, max_lanes=4096)
