@@ -90,6 +90,19 @@ def test_compat_uint8_lanes(gpu_ctx):
     assert int(np.sum(abi.meta_sockfd(got[0]) >= 256)) > 0
 
 
+@pytest.mark.parametrize("n_lanes", [2, 3, 7, 8, 9, 16, 33, 100])
+def test_lane_counts_no_fanout(gpu_ctx, n_lanes):
+    """Small and odd lane counts on the general path without fan-out (rx_scatterw: wave-total
+    scratch, 16-byte LDS zeroing only at lanes % 4 == 0, staging only at tiles <= 2 x lanes), one
+    binding per port, frames to bound and unbound ports, several tiles."""
+    lists = {abi.raw_port(20000 + i): [(0, i, 0)] for i in range(n_lanes)}
+    rng = np.random.default_rng(n_lanes)
+    ports = 20000 + rng.integers(0, n_lanes + 2, 9000)        # 2 unbound ports among them
+    b = F.build_frames(np.full(len(ports), 64, np.uint32), ports, 9)
+    want, got = _rx_both(gpu_ctx, b, lists, n_lanes)
+    _assert_same(want, got, f"lanes={n_lanes}")
+
+
 @pytest.mark.parametrize("cfg,n", [(2, 70001), (3, 20000), (4, 50000), (5, 100000), (1, 4096)])
 def test_configs_reduced(gpu_ctx, cfg, n):
     w = F.config_batch(cfg, n=n)

@@ -266,6 +266,8 @@ struct h_adm {
     uint32_t lanes;
     int fill;
     uint32_t sb[H_MAX_WORKERS + 3];   /* part p takes sockets [sb[p], sb[p + 1]) */
+    uint32_t n;                       /* frames in the batch: every lane entry is below it */
+    atomic_int bad;                   /* a lane entry was not (the device returned garbage) */
 };
 
 /* socket ranges of about equal delivery counts */
@@ -300,6 +302,14 @@ static void h_adm_socket(const struct h_adm *A, uint32_t s)
     uint32_t kd = s_kd[s], kf = s_kf[s], ka = s_kd[s] + s_kf[s];
     uint64_t od = s_od[s], of = s_of[s];
     uint32_t e = a0, q = b0;
+    if (!A->fill) {
+        for (uint32_t x = a0; x < a1; x++) {
+            if (lpkt[x] >= A->n) {
+                atomic_store_explicit((atomic_int *)&A->bad, 1, memory_order_relaxed);
+                return;
+            }
+        }
+    }
     while (e < a1 || q < b1) {
         /* the burst of the next delivery in arrival order, and its deliveries */
         const uint32_t ie = e < a1 ? lpkt[e] : UINT32_MAX, iq = q < b1 ? forg[flpkt[q]] : UINT32_MAX;
@@ -747,9 +757,15 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
         h_grow_host((void **)&g_udpdk.acc_fo, &g_udpdk.acc_fo_cap, 4ull * DF + 8) ||
         h_grow_host((void **)&g_udpdk.acc_sock, &g_udpdk.acc_sock_cap, 4ull * (D + DF) + 4))
         goto out;
-    struct h_adm A = {loff, lpkt, floff, flpkt, forg, length, lanes < UDPDK_MAX_SOCKETS ? lanes : UDPDK_MAX_SOCKETS, 0, {0}};
+    struct h_adm A = {loff, lpkt, floff, flpkt, forg, length, lanes < UDPDK_MAX_SOCKETS ? lanes : UDPDK_MAX_SOCKETS, 0, {0}, n, 0};
+    /* the lanes as the device returned them: offsets from 0, non-decreasing, within the entry
+     * buffer, entries below n (pass 1) — never trusted blindly as host indices */
+    int lanes_ok = loff[0] == 0u && D <= cap;
+    for (uint32_t s = 0; lanes_ok && s < lanes; s++) lanes_ok = loff[s] <= loff[s + 1];
+    if (!lanes_ok) { errno = EIO; goto out; }
     h_adm_split(&A, h_pool_parts());
     h_pool_run(h_adm_job, &A);                       /* pass 1: what each socket admits */
+    if (atomic_load(&A.bad)) { errno = EIO; goto out; }
     uint32_t nad = 0, naf = 0;
     uint64_t offd = 0, offf = 0;                    /* packed slot offsets (payload room / 16) */
     for (uint32_t s = 0; s < A.lanes; s++) {
