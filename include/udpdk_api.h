@@ -148,6 +148,14 @@ udpdk_gpu_ctx *udpdk_gpu_context(void);
  * to max device ids and returns how many there are (1 without "devices", 0 before udpdk_init). */
 int udpdk_shard_devices(int *devices, int max);
 
+/* With "[gpu] dispatch = rss" (and two or more devices) a poll sends each frame to the shard of
+ * its RSS queue instead: one RX queue per device, queue = reta[Toeplitz hash] with
+ * udpdk_gpu_rss's hash definition, default key and redirection table (the NIC's ETH_MQ_RX_RSS
+ * that udpdk_init.c:112-137 asks for and leaves as a TODO); the shards' lanes are merged back in
+ * arrival order, so the rings are still a single-context poll's. Writes the number of frames
+ * each shard took in the last poll (up to max) and returns the shard count (0 without shards). */
+int udpdk_shard_frames(uint32_t *frames, int max);
+
 /* TX header configuration (what udpdk_init reads from the .ini). Raw network-order IPv4. */
 int udpdk_config_set(const uint8_t src_mac[6], const uint8_t dst_mac[6], uint32_t src_ip_raw);
 int udpdk_config_get(uint8_t src_mac[6], uint8_t dst_mac[6], uint32_t *src_ip_raw);

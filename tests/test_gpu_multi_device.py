@@ -1,7 +1,8 @@
 """Multi-device RX in the library (f4's "RX queues to GPUs"): with
 "[gpu] devices = ..." udpdk_init creates one RX shard context per entry, and udpdk_poll_rx splits
-each batch into contiguous shards, classifies / demultiplexes / gathers each on its own context
-from its own pool thread, and concatenates the shards' lanes in shard order before ring admission.
+each batch into contiguous shards (or, with "dispatch = rss", by each frame's RSS queue, one queue
+per device), classifies / demultiplexes / gathers each on its own context from its own pool
+thread, and merges the shards' lanes in arrival order before ring admission.
 The rings must then equal a single-context session's on the same traffic, fragments included
 (their flows straddle shard boundaries and go through the main context's reassembly table).
 The box has one GPU, so the shard contexts all sit on device 0; the code path is the same as on
@@ -80,6 +81,10 @@ def _session(tmp_path, host_api, gpu_lines, polls):
             assert L.udpdk_poll_rx(buf.ctypes.data, len(buf) - 64, off.ctypes.data, ln.ctypes.data,
                                    None, len(off), C.byref(st)) == 0
             stats.append((list(st.counters), st.deliveries))
+        fr = (C.c_uint32 * 16)()
+        L.udpdk_shard_frames.argtypes = [C.c_void_p, C.c_int]
+        ns = L.udpdk_shard_frames(fr, 16)
+        shard_frames = [fr[i] for i in range(ns)]
         L.udpdk_interrupt(0)
         rings = []
         for s in socks:
@@ -90,7 +95,7 @@ def _session(tmp_path, host_api, gpu_lines, polls):
                     break
                 got.append((data, addr))
             rings.append(got)
-        return nd, [devs[i] for i in range(nd)], stats, rings
+        return nd, [devs[i] for i in range(nd)], stats, rings, shard_frames
     finally:
         L.udpdk_cleanup()
 
@@ -99,9 +104,9 @@ def _session(tmp_path, host_api, gpu_lines, polls):
 def test_shard_contexts_give_the_single_context_rings(tmp_path, host_api, devices, n_shards, threads):
     polls = _traffic(7)
     extra = f"poll_threads = {threads}\n" if threads else ""
-    n1, d1, st1, r1 = _session(tmp_path, host_api, "device = 0\n" + extra, polls)
+    n1, d1, st1, r1, _ = _session(tmp_path, host_api, "device = 0\n" + extra, polls)
     host_api.reset()
-    nk, dk, stk, rk = _session(tmp_path, host_api, f"devices = {devices}\n" + extra, polls)
+    nk, dk, stk, rk, _ = _session(tmp_path, host_api, f"devices = {devices}\n" + extra, polls)
     assert n1 == 1 and d1 == [0]
     assert nk == n_shards and dk == [0] * n_shards
     assert stk == st1                                  # counters and deliveries, summed over shards
@@ -112,6 +117,32 @@ def test_shard_contexts_give_the_single_context_rings(tmp_path, host_api, device
     # reassembled datagrams delivered (payloads > 1480 B)
     assert len(r1[0]) < sum(1 for p in polls for f in p if len(f) >= 38 and f[36:38] == _port(10001).to_bytes(2, "little"))
     assert any(len(d) > 1480 for r in r1 for d, _ in r)
+
+
+@pytest.mark.parametrize("devices,n_shards", [("0,0", 2), ("0,0,0,0", 4)])
+def test_rss_dispatch_gives_the_single_context_rings(tmp_path, host_api, gpu_ctx, devices, n_shards):
+    """[gpu] dispatch = rss (f4: one RX queue per device, the frame's queue from its Toeplitz
+    hash): the rings still equal a single-context session's (lanes merged back in arrival order),
+    and each shard took exactly the frames udpdk_gpu_rss puts in its queue (the same hash, key and
+    redirection table on the GPU, n_queues = the shard count)."""
+    polls = _traffic(11)
+    n1, _, st1, r1, _ = _session(tmp_path, host_api, "device = 0\n", polls)
+    host_api.reset()
+    nk, _, stk, rk, sfr = _session(tmp_path, host_api, f"devices = {devices}\ndispatch = rss\n", polls)
+    assert nk == n_shards
+    assert stk == st1
+    assert [len(r) for r in rk] == [len(r) for r in r1]
+    for a, b in zip(rk, r1):
+        assert a == b
+    # the last poll's split against the GPU RSS kernel's queues for the same frames
+    buf, off, ln = batch(polls[-1])
+    db = abi.rx_upload(gpu_ctx, buf, off, ln)
+    db.frames_bytes = len(buf) - 64
+    qoff = abi.rss_run(gpu_ctx, db, abi.rss_conf(n_shards))[1]
+    for x in (db.frames, db.offset, db.length):
+        x.free()
+    want = [int(qoff[q + 1] - qoff[q]) for q in range(n_shards)]
+    assert sfr == want and min(want) > 0
 
 
 def test_devices_key_errors(tmp_path):

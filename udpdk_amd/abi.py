@@ -195,6 +195,7 @@ _PROTOS = {
     "udpdk_btable_snapshot": (C.c_int, [C.POINTER(BindSnapshot), C.c_int]),
     "udpdk_gpu_context": (_P, []),
     "udpdk_shard_devices": (C.c_int, [_P, C.c_int]),
+    "udpdk_shard_frames": (C.c_int, [_P, C.c_int]),
     "udpdk_config_set": (C.c_int, [_P, _P, C.c_uint32]),
     "udpdk_config_get": (C.c_int, [_P, _P, C.POINTER(C.c_uint32)]),
     "udpdk_config_mtu": (C.c_int, [C.c_uint32]),

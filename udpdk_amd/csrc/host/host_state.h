@@ -101,7 +101,13 @@ struct h_gbuf {
 struct h_shard {
     udpdk_gpu_ctx *g;
     int       device;
-    uint32_t  i0, n;             /* frames [i0, i0 + n) of the poll                             */
+    uint32_t  i0, n;             /* frames [i0, i0 + n) of the poll (contiguous dispatch)        */
+    /* RSS dispatch ([gpu] dispatch = rss): the poll indices of the shard's frames (arrival
+     * order) and their bytes packed back to back, with their lengths and ptypes */
+    uint32_t *idx;  uint64_t idx_cap;
+    uint8_t  *pack; uint64_t pack_cap;
+    uint16_t *plen; uint64_t plen_cap;
+    uint32_t *ppt;  uint64_t ppt_cap;
     uint64_t  lo, bytes;         /* the frame bytes they span (lo 16-byte aligned)              */
     uint32_t *off;  uint64_t off_cap;                 /* offsets rebased to lo                  */
     uint32_t *meta, *loff, *lpkt;
@@ -160,6 +166,15 @@ struct h_state {
      * the shard contexts; the context above (g_udpdk.gpu) keeps TX and the reassembly table */
     uint32_t  n_shards;
     int       shard_dev[H_MAX_DEVS];
+    /* [gpu] dispatch = rss: frames go to shard reta[Toeplitz hash] (the NIC's RSS queue, one
+     * queue per device, udpdk_gpu_rss's hash and default key/RETA) instead of contiguous ranges;
+     * lanes are merged back in arrival order */
+    int       dispatch_rss;
+    uint32_t  rss_tab[12][256];
+    uint16_t  rss_reta[UDPDK_RSS_RETA_MAX];
+    uint32_t  rss_reta_size, rss_types, rss_ready;
+    uint8_t  *rss_sh;  uint64_t rss_sh_cap;      /* per poll frame: its shard                   */
+    uint32_t *rss_loc; uint64_t rss_loc_cap;     /* ... and its index in that shard             */
     struct h_shard shard[H_MAX_DEVS];
     uint8_t  *acc_dk;                            /* per accepted direct entry: its shard        */
     uint32_t *acc_di;                            /* ... and its index in that shard's slab      */
@@ -229,6 +244,7 @@ void h_shards_destroy(void);
 void udpdk_poll_profile_dump(void);   /* -DUDPDK_POLL_PROFILE builds: phase times to stderr */
 int  h_grow_dev(void **p, uint64_t *cap, uint64_t need);
 int  h_grow_dev_on(udpdk_gpu_ctx *g, void **p, uint64_t *cap, uint64_t need);
+int  h_rss_setup(void);
 int  h_grow_host(void **p, uint64_t *cap, uint64_t need);
 
 /* port_udp.c: the UDP test wire */

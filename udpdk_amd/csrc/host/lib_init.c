@@ -25,6 +25,8 @@ static void h_config_defaults(void)
 {
     g_udpdk.gpu_device = 0;
     g_udpdk.n_shards = 0;
+    g_udpdk.dispatch_rss = 0;
+    g_udpdk.rss_ready = 0;
     g_udpdk.poll_threads = 0;
     g_udpdk.host_copy_min = 512;
     g_udpdk.gpu_max_frames = 1u << 20;
@@ -151,6 +153,10 @@ static int h_load_ini(const char *path)
             g_udpdk.gpu_device = atoi(v);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "devices")) {
             if (h_parse_devices(v)) { rc = -1; break; }
+        } else if (!strcmp(section, "gpu") && !strcmp(k, "dispatch")) {
+            if (!strcmp(v, "rss")) g_udpdk.dispatch_rss = 1;
+            else if (!strcmp(v, "contiguous")) g_udpdk.dispatch_rss = 0;
+            else { rc = -1; break; }
         } else if (!strcmp(section, "gpu") && !strcmp(k, "max_frames")) {
             g_udpdk.gpu_max_frames = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "max_lanes")) {
@@ -210,6 +216,13 @@ int udpdk_init(int argc, char *argv[])
             errno = rc == -ENODEV ? ENODEV : -rc;
             return -1;
         }
+        if (g_udpdk.dispatch_rss && h_rss_setup()) {
+            h_shards_destroy();
+            udpdk_gpu_ctx_destroy(g_udpdk.gpu);
+            g_udpdk.gpu = NULL;
+            errno = EINVAL;
+            return -1;
+        }
     } else {
         g_udpdk.n_shards = 0;
     }
@@ -235,6 +248,13 @@ int udpdk_init(int argc, char *argv[])
         }
     }
     return 0;
+}
+
+int udpdk_shard_frames(uint32_t *frames, int max)
+{
+    const int n = g_udpdk.n_shards > 1 ? (int)g_udpdk.n_shards : 0;
+    for (int k = 0; k < n && k < max; k++) frames[k] = g_udpdk.shard[k].n;
+    return n;
 }
 
 int udpdk_shard_devices(int *devices, int max)

@@ -132,10 +132,15 @@ void h_shards_destroy(void)
         struct h_shard *S = &g_udpdk.shard[k];
         h_gbuf_free(S->g, &S->gb);
         free(S->off); free(S->meta); free(S->loff); free(S->lpkt); free(S->acc); free(S->acco);
+        free(S->idx); free(S->pack); free(S->plen); free(S->ppt);
         if (S->g) udpdk_gpu_ctx_destroy(S->g);
         memset(S, 0, sizeof(*S));
     }
     g_udpdk.n_shards = 0;
+    free(g_udpdk.rss_sh); free(g_udpdk.rss_loc);
+    g_udpdk.rss_sh = NULL; g_udpdk.rss_loc = NULL;
+    g_udpdk.rss_sh_cap = g_udpdk.rss_loc_cap = 0;
+    g_udpdk.rss_ready = 0;
 }
 
 /* Upload the bind snapshot when the table changed since the last upload; keep its lane count
@@ -477,6 +482,124 @@ struct h_sjob {
     uint32_t maxfan;
 };
 
+/* ---- RSS dispatch ([gpu] dispatch = rss) ---------------------------------------------------
+ * The NIC's receive-side scaling in software (the reference asks for
+ * ETH_MQ_RX_RSS with one ring and a "TODO add RSS support", udpdk_init.c:112-137): one RX queue
+ * per device, a frame's queue = reta[Toeplitz hash], with udpdk_gpu_rss's hash definition
+ * (rx_rss.hip: IPv4 gate as rx_classify, source + destination address, + ports for unfragmented
+ * UDP) and its default key and redirection table, by the same 12 x 256 key-window table. Each
+ * device then classifies its queue's frames; lanes are merged back in arrival order, so the rings
+ * are the single-queue poller's. */
+static uint32_t h_key_window(const uint8_t *key, uint32_t b)   /* key bits [b, b + 32), MSB first */
+{
+    uint64_t w = 0;
+    for (uint32_t i = 0; i < 5; i++) w = (w << 8) | key[(b >> 3) + i];
+    return (uint32_t)(w >> (8u - (b & 7u)));
+}
+
+int h_rss_setup(void)
+{
+    udpdk_rss_conf_t conf;
+    if (udpdk_gpu_rss_default_conf(&conf, g_udpdk.n_shards)) return -1;
+    for (uint32_t p = 0; p < 12; p++)
+        for (uint32_t v = 0; v < 256; v++) {
+            uint32_t t = 0;
+            for (uint32_t j = 0; j < 8; j++)
+                if (v & (0x80u >> j)) t ^= h_key_window(conf.key, 8u * p + j);
+            g_udpdk.rss_tab[p][v] = t;
+        }
+    memcpy(g_udpdk.rss_reta, conf.reta, sizeof(uint16_t) * conf.reta_size);
+    g_udpdk.rss_reta_size = conf.reta_size;
+    g_udpdk.rss_types = conf.hash_types;
+    g_udpdk.rss_ready = 1;
+    return 0;
+}
+
+/* frame i's RX queue (= shard) */
+static uint32_t h_rss_queue(const struct h_sjob *J, uint32_t i)
+{
+    const uint64_t o = J->offset[i];
+    const uint32_t len = J->length[i];
+    uint32_t hash = 0;
+    if (len >= 34u && o + len <= J->frames_bytes) {
+        const uint8_t *f = J->frames + o;
+        const uint32_t pt = J->ptype ? J->ptype[i] : (f[12] == 0x08 && f[13] == 0x00 ? 0x211u : 0x1u);
+        if (pt & 0x10u) {
+            const uint32_t ff = ((uint32_t)f[20] << 8) | f[21];
+            const int udp4 = !(ff & 0x3FFFu) && f[23] == 17 && len >= 38u && (g_udpdk.rss_types & 2u);
+            if (udp4 || (g_udpdk.rss_types & 1u)) {
+                const uint32_t (*T)[256] = g_udpdk.rss_tab;
+                for (uint32_t b = 0; b < (udp4 ? 12u : 8u); b++) hash ^= T[b][f[26 + b]];
+            }
+        }
+    }
+    return g_udpdk.rss_reta[hash & (g_udpdk.rss_reta_size - 1u)];
+}
+
+/* Two passes over contiguous parts of the poll: queue of every frame and per-part counts per
+ * shard, then (at per-part, per-shard bases) every shard's frames in arrival order. */
+struct h_rss {
+    const struct h_sjob *J;
+    uint32_t n, N;
+    int fill;
+    uint32_t cnt[H_MAX_WORKERS + 2][H_MAX_DEVS];
+};
+
+static void h_rss_job(void *ctx, uint32_t part, uint32_t parts)
+{
+    struct h_rss *R = ctx;
+    const uint32_t i0 = (uint32_t)((uint64_t)R->n * part / parts), i1 = (uint32_t)((uint64_t)R->n * (part + 1) / parts);
+    uint8_t *sh = g_udpdk.rss_sh;
+    if (!R->fill) {
+        uint32_t c[H_MAX_DEVS] = {0};
+        for (uint32_t i = i0; i < i1; i++) {
+            const uint32_t k = h_rss_queue(R->J, i) % R->N;
+            sh[i] = (uint8_t)k;
+            c[k]++;
+        }
+        memcpy(R->cnt[part], c, sizeof(c));
+    } else {
+        uint32_t w[H_MAX_DEVS];
+        memcpy(w, R->cnt[part], sizeof(w));
+        for (uint32_t i = i0; i < i1; i++) {
+            const uint32_t k = sh[i], r = w[k]++;
+            g_udpdk.shard[k].idx[r] = i;
+            g_udpdk.rss_loc[i] = r;
+        }
+    }
+}
+
+static int h_rss_assign(const struct h_sjob *J, uint32_t n)
+{
+    const uint32_t N = g_udpdk.n_shards;
+    if (h_grow_host((void **)&g_udpdk.rss_sh, &g_udpdk.rss_sh_cap, (uint64_t)n + 1) ||
+        h_grow_host((void **)&g_udpdk.rss_loc, &g_udpdk.rss_loc_cap, 4ull * n + 4))
+        return -1;
+    struct h_rss R;
+    memset(&R, 0, sizeof(R));
+    R.J = J;
+    R.n = n;
+    R.N = N;
+    const uint32_t parts = h_pool_parts();
+    h_pool_run(h_rss_job, &R);
+    uint32_t tot[H_MAX_DEVS] = {0};
+    for (uint32_t p = 0; p < parts; p++)          /* per-part counts -> per-part bases */
+        for (uint32_t k = 0; k < N; k++) {
+            const uint32_t c = R.cnt[p][k];
+            R.cnt[p][k] = tot[k];
+            tot[k] += c;
+        }
+    for (uint32_t k = 0; k < N; k++) {
+        struct h_shard *S = &g_udpdk.shard[k];
+        S->n = tot[k];
+        S->i0 = 0;
+        if (h_grow_host((void **)&S->idx, &S->idx_cap, 4ull * tot[k] + 4)) return -1;
+    }
+    R.fill = 1;
+    h_pool_run(h_rss_job, &R);
+    return 0;
+}
+
 /* Shard k's RX on its own context: descriptors rebased to the 16-byte-aligned start of the frame
  * bytes the shard spans (a descriptor outside the caller's frames keeps pointing outside the
  * shard's, so it stays BAD_DESC), then udpdk_gpu_rx_host (H2D, kernels, D2H of its lanes). */
@@ -488,6 +611,42 @@ static void h_shard_rx(const struct h_sjob *J, struct h_shard *S)
     if (h_grow_host((void **)&S->loff, &S->loff_cap, 4ull * (lanes + 1))) { S->err = errno; return; }
     if (!S->n) {
         memset(S->loff, 0, 4ull * (lanes + 1));
+        return;
+    }
+    if (g_udpdk.dispatch_rss) {
+        /* the queue's frames packed back to back (+ 16 readable bytes), descriptors and ptypes
+         * in queue order; a descriptor outside the caller's frames stays out of range */
+        uint64_t bytes = 0;
+        for (uint32_t i = 0; i < S->n; i++) bytes += J->length[S->idx[i]];
+        const uint64_t cap = (uint64_t)S->n * J->maxfan;
+        if (h_grow_host((void **)&S->pack, &S->pack_cap, bytes + 64) ||
+            h_grow_host((void **)&S->off, &S->off_cap, 4ull * S->n) ||
+            h_grow_host((void **)&S->plen, &S->plen_cap, 2ull * S->n) ||
+            h_grow_host((void **)&S->ppt, &S->ppt_cap, 4ull * S->n) ||
+            h_grow_host((void **)&S->meta, &S->meta_cap, 4ull * S->n + 4) ||
+            h_grow_host((void **)&S->lpkt, &S->lpkt_cap, 4ull * cap + 4)) { S->err = errno; return; }
+        uint64_t pos = 0;
+        for (uint32_t i = 0; i < S->n; i++) {
+            const uint32_t gi = S->idx[i];
+            const uint64_t o = J->offset[gi];
+            const uint32_t l = J->length[gi];
+            S->plen[i] = (uint16_t)l;
+            S->ppt[i] = J->ptype ? J->ptype[gi] : 0u;
+            if (l <= J->frames_bytes && o <= J->frames_bytes - l) {
+                memcpy(S->pack + pos, J->frames + o, l);
+                S->off[i] = (uint32_t)pos;
+                pos += l;
+            } else {
+                S->off[i] = 0xFFFFFFFFu;
+            }
+        }
+        memset(S->pack + pos, 0, 16);
+        S->lo = 0;
+        S->bytes = pos;
+        const int rc = udpdk_gpu_rx_host(S->g, S->pack, pos, S->off, S->plen, J->ptype ? S->ppt : NULL, S->n,
+                                         S->meta, S->loff, S->lpkt, cap > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)cap,
+                                         &S->st);
+        if (rc) S->err = -rc;
         return;
     }
     uint64_t lo = UINT64_MAX, hi = 0;
@@ -534,6 +693,31 @@ static void h_merge_job(void *ctx, uint32_t part, uint32_t parts)
 {
     const struct h_merge *M = ctx;
     (void)parts;
+    if (g_udpdk.dispatch_rss) {
+        /* every shard's list for the socket holds its frames in arrival order: merge them by
+         * poll index (the single-queue arrival order) */
+        const uint32_t N = g_udpdk.n_shards;
+        for (uint32_t l = M->sb[part]; l < M->sb[part + 1]; l++) {
+            uint32_t w = M->loff[l], e[H_MAX_DEVS], b[H_MAX_DEVS];
+            for (uint32_t k = 0; k < N; k++) {
+                const struct h_shard *S = &g_udpdk.shard[k];
+                e[k] = S->n ? S->loff[l] : 0u;
+                b[k] = S->n ? S->loff[l + 1] : 0u;
+            }
+            for (;;) {
+                uint32_t best = UINT32_MAX, bk = 0;
+                for (uint32_t k = 0; k < N; k++) {
+                    if (e[k] >= b[k]) continue;
+                    const uint32_t gi = g_udpdk.shard[k].idx[g_udpdk.shard[k].lpkt[e[k]]];
+                    if (gi < best) { best = gi; bk = k; }
+                }
+                if (best == UINT32_MAX) break;
+                M->lpkt[w++] = best;
+                e[bk]++;
+            }
+        }
+        return;
+    }
     for (uint32_t l = M->sb[part]; l < M->sb[part + 1]; l++) {
         uint32_t w = M->loff[l];
         for (uint32_t k = 0; k < g_udpdk.n_shards; k++) {
@@ -551,10 +735,14 @@ static int h_shards_rx(const struct h_sjob *J, uint32_t n, uint32_t lanes, uint3
                        uint32_t *lpkt, udpdk_rx_stats_t *st)
 {
     const uint32_t N = g_udpdk.n_shards;
-    for (uint32_t k = 0; k < N; k++) {
-        struct h_shard *S = &g_udpdk.shard[k];
-        S->i0 = (uint32_t)((uint64_t)n * k / N);
-        S->n = (uint32_t)((uint64_t)n * (k + 1) / N) - S->i0;
+    if (g_udpdk.dispatch_rss) {
+        if (h_rss_assign(J, n)) return -1;
+    } else {
+        for (uint32_t k = 0; k < N; k++) {
+            struct h_shard *S = &g_udpdk.shard[k];
+            S->i0 = (uint32_t)((uint64_t)n * k / N);
+            S->n = (uint32_t)((uint64_t)n * (k + 1) / N) - S->i0;
+        }
     }
     h_pool_run(h_shard_rx_job, (void *)J);
     memset(st, 0, sizeof(*st));
@@ -564,7 +752,11 @@ static int h_shards_rx(const struct h_sjob *J, uint32_t n, uint32_t lanes, uint3
         for (int c = 0; c < UDPDK_N_COUNTERS; c++) st->counters[c] += S->st.counters[c];
         st->deliveries += S->st.deliveries;
         st->overflow |= S->st.overflow;
-        if (S->n) memcpy(meta + S->i0, S->meta, 4ull * S->n);
+        if (!S->n) continue;
+        if (g_udpdk.dispatch_rss)
+            for (uint32_t i = 0; i < S->n; i++) meta[S->idx[i]] = S->meta[i];
+        else
+            memcpy(meta + S->i0, S->meta, 4ull * S->n);
     }
     for (uint32_t l = 0; l <= lanes; l++) {
         uint32_t v = 0;
@@ -663,14 +855,20 @@ static int h_shards_gather(uint32_t nad)
     const uint32_t *slot = g_udpdk.acc_do;           /* packed slot offsets: sizes by difference */
     for (uint32_t kd = 0; kd < nad; kd++) {
         const uint32_t fi = g_udpdk.acc_d[kd];
-        uint32_t k = N - 1;
-        while (k && g_udpdk.shard[k].i0 > fi) k--;
+        uint32_t k = N - 1, local;
+        if (g_udpdk.dispatch_rss) {
+            k = g_udpdk.rss_sh[fi];
+            local = g_udpdk.rss_loc[fi];
+        } else {
+            while (k && g_udpdk.shard[k].i0 > fi) k--;
+            local = fi - g_udpdk.shard[k].i0;
+        }
         struct h_shard *S = &g_udpdk.shard[k];
         const uint32_t r = S->nacc++;
         const uint32_t sz = slot[kd + 1] - slot[kd];
         g_udpdk.acc_dk[kd] = (uint8_t)k;
         g_udpdk.acc_di[kd] = r;
-        S->acc[r] = fi - S->i0;
+        S->acc[r] = local;
         S->acco[r] = (uint32_t)S->acc_bytes;
         S->acc_bytes += sz;
     }
