@@ -825,6 +825,91 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_sizes(const ReasmDone *done, c
         sizes[k] = (34u + done[perm[k]].total + 15u) & ~15u;
 }
 
+// Grouped path: the completions in position (= arrival) order and their output offsets in two
+// launches (per 2048-position block: count and bytes; then each block's base from its
+// predecessors' totals and a block scan), instead of a rocPRIM select, a size pass and a rocPRIM
+// scan (three passes, six launches with the scans' state initialisation).
+constexpr uint32_t RS_CL = 2048;                 // positions per block, 8 per thread
+
+__device__ __forceinline__ uint32_t done_bytes(const ReasmDone *done, uint32_t q)
+{
+    return (34u + done[q].total + 15u) & ~15u;    // as reasm_sizes
+}
+
+__global__ void __launch_bounds__(RS_BLOCK) reasm_clist_count(const uint32_t *dk, const ReasmDone *done,
+                                                             uint32_t F, uint32_t *blk)
+{
+    __shared__ uint32_t red[2 * RS_WAVES];
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+    const uint32_t p0 = blockIdx.x * RS_CL + tid * (RS_CL / RS_BLOCK);
+    uint32_t c = 0, by = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < RS_CL / RS_BLOCK; ++j) {
+        const uint32_t q = p0 + j;
+        if (q < F && dk[q] != RS_NONE) {
+            ++c;
+            by += done_bytes(done, q);
+        }
+    }
+    uint32_t tc, tb;
+    (void)wave_excl_scan(c, &tc);
+    (void)wave_excl_scan(by, &tb);
+    if (lane == 0) { red[w] = tc; red[RS_WAVES + w] = tb; }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t sc = 0, sb = 0;
+        for (uint32_t i = 0; i < RS_WAVES; ++i) { sc += red[i]; sb += red[RS_WAVES + i]; }
+        blk[2 * blockIdx.x] = sc;
+        blk[2 * blockIdx.x + 1] = sb;
+    }
+}
+
+__global__ void __launch_bounds__(RS_BLOCK) reasm_clist_write(const uint32_t *dk, const ReasmDone *done,
+                                                             uint32_t F, const uint32_t *blk,
+                                                             uint32_t *perm, uint32_t *offs)
+{
+    __shared__ uint32_t red[4 * RS_WAVES];
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6, b = blockIdx.x;
+    // this block's base: the earlier blocks' totals
+    uint32_t pc = 0, pb = 0;
+    for (uint32_t i = tid; i < b; i += RS_BLOCK) { pc += blk[2 * i]; pb += blk[2 * i + 1]; }
+    uint32_t t0, t1;
+    (void)wave_excl_scan(pc, &t0);
+    (void)wave_excl_scan(pb, &t1);
+    // the thread's positions, then a block scan of their counts and bytes
+    constexpr uint32_t PT = RS_CL / RS_BLOCK;
+    const uint32_t p0 = b * RS_CL + tid * PT;
+    uint32_t c = 0, by = 0, sz[PT];
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+        const uint32_t q = p0 + j;
+        sz[j] = q < F && dk[q] != RS_NONE ? done_bytes(done, q) : 0u;
+        c += sz[j] ? 1u : 0u;
+        by += sz[j];
+    }
+    uint32_t wc, wb;
+    uint32_t ec = wave_excl_scan(c, &wc), eb = wave_excl_scan(by, &wb);
+    if (lane == 0) { red[w] = wc; red[RS_WAVES + w] = wb; red[2 * RS_WAVES + w] = t0; red[3 * RS_WAVES + w] = t1; }
+    __syncthreads();
+    uint32_t bc = 0, bb = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < RS_WAVES; ++i) {
+        bc += red[2 * RS_WAVES + i] + (i < w ? red[i] : 0u);
+        bb += red[3 * RS_WAVES + i] + (i < w ? red[RS_WAVES + i] : 0u);
+    }
+    ec += bc;
+    eb += bb;
+#pragma unroll
+    for (uint32_t j = 0; j < PT; ++j) {
+        if (sz[j]) {
+            perm[ec] = p0 + j;
+            offs[ec] = eb;
+            ++ec;
+            eb += sz[j];
+        }
+    }
+}
+
 struct EmitArgs {
     const uint8_t *frames;
     const uint32_t *offset;
@@ -1356,18 +1441,22 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         const uint32_t gC = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_BLOCK - 1) / RS_BLOCK, 4096));
         tb = r->tmp_bytes;
         if (grouped) {
-            RS_HIP(rocprim::select(r->tmp, tb, rocprim::counting_iterator<uint32_t>(0u), r->perm, r->counts + 5,
-                                   (size_t)F, HasDone{r->dk}, st));
+            const uint32_t nb = (F + RS_CL - 1) / RS_CL;
+            hipLaunchKernelGGL(reasm_clist_count, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
+                               (const ReasmDone *)r->done, F, r->sizes);
+            hipLaunchKernelGGL(reasm_clist_write, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
+                               (const ReasmDone *)r->done, F, (const uint32_t *)r->sizes, r->perm, r->offs);
+            RS_HIP(hipGetLastError());
         } else {
             RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->dk, r->dks, r->dv, r->perm, (size_t)F, 0,
                                              bits_for(n), st));
+            hipLaunchKernelGGL(reasm_sizes, dim3(gC), dim3(RS_BLOCK), 0, st, (const ReasmDone *)r->done,
+                               (const uint32_t *)r->perm, r->sizes, Cn);
+            RS_HIP(hipGetLastError());
+            tb = r->tmp_bytes;
+            RS_HIP(rocprim::exclusive_scan(r->tmp, tb, r->sizes, r->offs, 0u, (size_t)Cn,
+                                           rocprim::plus<uint32_t>(), st));
         }
-        hipLaunchKernelGGL(reasm_sizes, dim3(gC), dim3(RS_BLOCK), 0, st, (const ReasmDone *)r->done,
-                           (const uint32_t *)r->perm, r->sizes, Cn);
-        RS_HIP(hipGetLastError());
-        tb = r->tmp_bytes;
-        RS_HIP(rocprim::exclusive_scan(r->tmp, tb, r->sizes, r->offs, 0u, (size_t)Cn,
-                                       rocprim::plus<uint32_t>(), st));
         EmitArgs ea;
         ea.frames = bt->frames_dev;
         ea.offset = bt->offset_dev;
