@@ -255,8 +255,57 @@ struct HasDone {
     __device__ bool operator()(uint32_t q) const { return dk[q] != RS_NONE; }
 };
 
-// Over the fragment list (arrival order; F = counts[0], from the select): the (id << ib | index)
-// sort keys, and whether every flow key forms a single run. A run's first fragment inserts a
+// src | dst << 32 of the fragments in (id, index) order (the second, stable, sort key).
+__global__ void __launch_bounds__(RS_BLOCK) reasm_keys(ReasmArgs a, uint32_t F)
+{
+    const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
+    for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
+        const uint32_t o = a.offset[a.v1s[p]];
+        a.k2[p] = (unsigned long long)ld32(fr, o + 26) | ((unsigned long long)ld32(fr, o + 30) << 32);
+    }
+}
+
+// Per sorted position: the fragment's frame, key, signature and length class (all lanes in
+// parallel, so the flow walk below reads one coalesced record per fragment).
+__device__ __forceinline__ void prep_record(const ReasmArgs &a, uint32_t p, uint32_t i, const FragHdr &h)
+{
+        const int32_t ip_len = (int32_t)h.tl - 20;                    // l3_len = 20
+        const uint32_t ofs = (h.ff & 0x1FFFu) * 8u;
+        uint32_t cls = 0, len = 0;
+        if (ip_len <= 0) {
+            cls = 1;
+        } else {
+            len = (uint32_t)ip_len;
+            if (34u + len > h.flen || ofs + len > a.max_dgram) cls = 2;
+        }
+        uint32_t v = crc32c_u32(0xeaad8405u, h.src);
+        v = crc32c_u32(v, h.dst);
+        v = crc32c_u32(v, h.id);
+        a.s_i[p] = i;
+        a.s_src[p] = h.src;
+        a.s_dst[p] = h.dst;
+        a.s_id[p] = h.id;
+        a.s_sig[p] = v;
+        a.s_meta[p] = (cls ? 0u : len) | ((h.ff & 0x1FFFu) << 16) | ((h.ff & 0x2000u) << 16) | (cls << 30);
+        a.dv[p] = p;
+        a.dk[p] = RS_NONE;                                           // no completion / store job yet
+        a.jobs[p] = ReasmJob{RS_NONE, RS_NONE, RS_NONE, RS_NONE};
+}
+
+__global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
+{
+    const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
+    for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
+        const uint32_t i = a.order[p];
+        prep_record(a, p, i, frag_hdr(a, fr, i));
+    }
+}
+
+// Over the fragment list (arrival order; F = counts[0], from the select): whether every flow key
+// forms a single run, and each position's record as reasm_prep writes it for that case (sorted
+// position = arrival position), so a grouped batch needs no reasm_prep pass over the frame
+// headers; a batch that is not grouped gets its sort keys from reasm_keys1 and its records
+// rewritten by reasm_prep after the sorts. A run's first fragment inserts a
 // 64-bit fingerprint of its key into an open-addressing set; meeting it again (the key has
 // another run, or two keys share a fingerprint) sets counts[4] and the batch takes the sorts.
 __global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned long long *hset, uint32_t hmask)
@@ -269,9 +318,10 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned lon
     for (uint32_t pb = blockIdx.x * RS_BLOCK + (threadIdx.x & ~63u); pb < F; pb += gridDim.x * RS_BLOCK) {
         const uint32_t p = pb + lane;
         const bool valid = p < F;
-        const uint32_t i = valid ? a.frag_list[p] : 0u, o = valid ? a.offset[i] : 0u;
-        const uint32_t id = ld32(fr, o + 16) >> 16, src = ld32(fr, o + 26), dst = ld32(fr, o + 30);
-        if (valid) a.k1[p] = ((unsigned long long)id << a.ib) | i;
+        const uint32_t i = valid ? a.frag_list[p] : 0u;
+        const FragHdr h = frag_hdr(a, fr, i);
+        const uint32_t id = h.id, src = h.src, dst = h.dst;
+        if (valid) prep_record(a, p, i, h);
         uint32_t pid = __shfl_up(id, 1, 64), psrc = __shfl_up(src, 1, 64), pdst = __shfl_up(dst, 1, 64);
         if (lane == 0u && valid && p > 0u) {
             const uint32_t op = a.offset[a.frag_list[p - 1]];
@@ -296,45 +346,14 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned lon
     }
 }
 
-// src | dst << 32 of the fragments in (id, index) order (the second, stable, sort key).
-__global__ void __launch_bounds__(RS_BLOCK) reasm_keys(ReasmArgs a, uint32_t F)
+// The first sort's keys (id << ib | index) over the fragment list, for a batch that is not
+// grouped.
+__global__ void __launch_bounds__(RS_BLOCK) reasm_keys1(ReasmArgs a, uint32_t F)
 {
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
     for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
-        const uint32_t o = a.offset[a.v1s[p]];
-        a.k2[p] = (unsigned long long)ld32(fr, o + 26) | ((unsigned long long)ld32(fr, o + 30) << 32);
-    }
-}
-
-// Per sorted position: the fragment's frame, key, signature and length class (all lanes in
-// parallel, so the flow walk below reads one coalesced record per fragment).
-__global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
-{
-    const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
-    for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
-        const uint32_t i = a.order[p];
-        const FragHdr h = frag_hdr(a, fr, i);
-        const int32_t ip_len = (int32_t)h.tl - 20;                    // l3_len = 20
-        const uint32_t ofs = (h.ff & 0x1FFFu) * 8u;
-        uint32_t cls = 0, len = 0;
-        if (ip_len <= 0) {
-            cls = 1;
-        } else {
-            len = (uint32_t)ip_len;
-            if (34u + len > h.flen || ofs + len > a.max_dgram) cls = 2;
-        }
-        uint32_t v = crc32c_u32(0xeaad8405u, h.src);
-        v = crc32c_u32(v, h.dst);
-        v = crc32c_u32(v, h.id);
-        a.s_i[p] = i;
-        a.s_src[p] = h.src;
-        a.s_dst[p] = h.dst;
-        a.s_id[p] = h.id;
-        a.s_sig[p] = v;
-        a.s_meta[p] = (cls ? 0u : len) | ((h.ff & 0x1FFFu) << 16) | ((h.ff & 0x2000u) << 16) | (cls << 30);
-        a.dv[p] = p;
-        a.dk[p] = RS_NONE;                                           // no completion / store job yet
-        a.jobs[p] = ReasmJob{RS_NONE, RS_NONE, RS_NONE, RS_NONE};
+        const uint32_t i = a.frag_list[p];
+        a.k1[p] = ((unsigned long long)(ld32(fr, a.offset[i] + 16) >> 16) << a.ib) | i;
     }
 }
 
@@ -1323,6 +1342,14 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     a.call = r->calls;
     a.ib = bits_for(n - 1u);
     RS_HIP(hipMemsetAsync(r->stats, 0, RS_ZERO_WORDS * sizeof(unsigned long long), st));
+    // per-position records (written by reasm_runs for a grouped batch, else by reasm_prep after
+    // the sorts, when the sort keys sharing their buffers are dead): cap-strided halves
+    a.s_i = reinterpret_cast<uint32_t *>(r->k1);
+    a.s_src = a.s_i + r->cap;
+    a.s_dst = reinterpret_cast<uint32_t *>(r->k1s);
+    a.s_id = a.s_dst + r->cap;
+    a.s_sig = reinterpret_cast<uint32_t *>(r->k2);
+    a.s_meta = a.s_sig + r->cap;
     uint32_t hsize = 1024;                   // the run-key set: >= 2 x fragments, power of 2
     while (hsize < 2u * n && hsize < r->hcap) hsize <<= 1;
     // the fragment list in arrival order (F to counts[0]), then its sort keys and the run test
@@ -1351,6 +1378,8 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
             a.order = r->frag_list;
         } else {
             // group by key keeping arrival order: stable sorts by (id, index), then src|dst
+            hipLaunchKernelGGL(reasm_keys1, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
+            RS_HIP(hipGetLastError());
             tb = r->tmp_bytes;
             RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k1, r->k1s, r->frag_list, r->v1s, (size_t)F, 0,
                                              16 + a.ib, st));
@@ -1359,15 +1388,12 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
             tb = r->tmp_bytes;
             RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k2, r->k2s, r->v1s, r->v2s, (size_t)F, 0, 64, st));
         }
-        // the sort keys are dead now: their buffers hold the per-position records
-        a.s_i = reinterpret_cast<uint32_t *>(r->k1);
-        a.s_src = a.s_i + F;
-        a.s_dst = reinterpret_cast<uint32_t *>(r->k1s);
-        a.s_id = a.s_dst + F;
-        a.s_sig = reinterpret_cast<uint32_t *>(r->k2);
-        a.s_meta = a.s_sig + F;
-        hipLaunchKernelGGL(reasm_prep, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
-        RS_HIP(hipGetLastError());
+        // (grouped: reasm_runs wrote the records; else the sort keys are dead now and their
+        // buffers take the records in sorted order)
+        if (!grouped) {
+            hipLaunchKernelGGL(reasm_prep, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
+            RS_HIP(hipGetLastError());
+        }
         // flow analysis: which flows can run without the table (see the top of this file)
         const uint32_t gb = std::max<uint32_t>(1, std::min<uint32_t>((r->entries + RS_BLOCK - 1) / RS_BLOCK, 4096));
         hipLaunchKernelGGL(reasm_bsum, dim3(gb), dim3(RS_BLOCK), 0, st, a);
