@@ -521,8 +521,21 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_bsum(ReasmArgs a)
 // pending after its last one. PF_COMPLEX when it is pending, its key is in the table, or one of
 // its buckets holds an expired entry; complex flows are counted per bucket. Each flow adds one
 // (bucket << ib | tf) record per distinct bucket of its pair for the overlap test.
+// F = RS_F_DEV: a speculative launch of the grouped path, made before the host knows F or
+// whether the batch is grouped: F comes from counts[0], and the kernel does nothing when
+// reasm_runs found a key in two runs (counts[4]).
+constexpr uint32_t RS_F_DEV = 0xFFFFFFFFu;
+__device__ __forceinline__ bool spec_f(const ReasmArgs &a, uint32_t &F)
+{
+    if (F != RS_F_DEV) return true;
+    if (a.counts[4]) return false;
+    F = a.counts[0];
+    return true;
+}
+
 __global__ void __launch_bounds__(RS_BLOCK) reasm_flows(ReasmArgs a, uint32_t F)
 {
+    if (!spec_f(a, F)) return;
     constexpr uint32_t PER = RS_FLOW_CHUNK / RS_BLOCK;
     __shared__ uint32_t s_st[RS_BLOCK][E_WORDS];
     __shared__ unsigned long long s_rk[2 * RS_FLOW_CHUNK];   // the chunk's records, reserved at once
@@ -641,6 +654,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_overlap(ReasmArgs a, const uns
 // that could hold one of them. Otherwise every flow of the batch takes the serial path.
 __global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
 {
+    if (!spec_f(a, F)) return;
     for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
         const uint32_t f = a.pflag[p];
         if (!(f & PF_TOUCH) || (f & (PF_COMPLEX | PF_SHARED))) continue;
@@ -659,6 +673,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
 // sorted position). Length-class drops are counted for every flow.
 __global__ void __launch_bounds__(RS_BLOCK) reasm_process(ReasmArgs a, uint32_t F)
 {
+    if (!spec_f(a, F)) return;
     __shared__ uint32_t s_st[RS_BLOCK][E_WORDS];
     __shared__ unsigned long long s_cnt[UDPDK_RS_N + 1];    // block totals: stats, out bytes
     uint32_t *st = s_st[threadIdx.x];
@@ -1362,22 +1377,69 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         hipLaunchKernelGGL(reasm_runs, dim3(g1), dim3(RS_BLOCK), 0, st, a, r->hset, hsize - 1u);
         RS_HIP(hipGetLastError());
     }
-    RS_HIP(hipMemcpyAsync(r->host, r->counts, 32, hipMemcpyDeviceToHost, st));
-    RS_HIP(hipStreamSynchronize(st));
-    const uint32_t F = n ? r->host[0] : 0u;
-    // every key one run in arrival order: the list is already grouped, and no flow's span can
-    // overlap another's (each span holds only its own fragments)
-    const bool grouped = r->host[4] == 0u;
-    a.grouped = grouped ? 1u : 0u;
+    // Flow analysis and the parallel flows (see the top of this file). Fk = RS_F_DEV: the
+    // grouped path launched speculatively (grids sized for n, F read on the device, every kernel
+    // returning at once if the batch is not grouped), so a grouped batch makes no host round trip
+    // between the run test and the stats read-back.
+    auto analysis = [&](uint32_t Fk, uint32_t Fgrid, bool grp) -> int {
+        const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((Fgrid + RS_BLOCK - 1) / RS_BLOCK, 4096));
+        const uint32_t gb = std::max<uint32_t>(1, std::min<uint32_t>((r->entries + RS_BLOCK - 1) / RS_BLOCK, 4096));
+        hipLaunchKernelGGL(reasm_bsum, dim3(gb), dim3(RS_BLOCK), 0, st, a);
+        RS_HIP(hipGetLastError());
+        const uint32_t gfl = std::max<uint32_t>(1, std::min<uint32_t>((Fgrid + RS_FLOW_CHUNK - 1) / RS_FLOW_CHUNK, 2048));
+        hipLaunchKernelGGL(reasm_flows, dim3(gfl), dim3(RS_BLOCK), 0, st, a, Fk);
+        RS_HIP(hipGetLastError());
+        uint32_t R = 0;                      // overlap records (none when grouped)
+        if (!grp) {
+            RS_HIP(hipMemcpyAsync(r->host, r->counts, 8, hipMemcpyDeviceToHost, st));
+            RS_HIP(hipStreamSynchronize(st));
+            R = r->host[1];
+        }
+        if (R) {
+            size_t tbr = r->tmp_bytes;
+            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tbr, r->rk, r->rks, r->rv, r->rvs, (size_t)R, 0,
+                                             a.ib + bits_for(r->nbuckets - 1u), st));
+            const uint32_t gR = std::max<uint32_t>(1, std::min<uint32_t>((R + RS_BLOCK - 1) / RS_BLOCK, 4096));
+            hipLaunchKernelGGL(reasm_rec, dim3(gR), dim3(RS_BLOCK), 0, st, a,
+                               (const unsigned long long *)r->rks, (const uint32_t *)r->rvs, r->rk, R);
+            RS_HIP(hipGetLastError());
+            tbr = r->tmp_bytes;
+            RS_HIP(rocprim::inclusive_scan(r->tmp, tbr, r->rk, r->rx, (size_t)R,
+                                           rocprim::maximum<unsigned long long>(), st));
+            hipLaunchKernelGGL(reasm_overlap, dim3(gR), dim3(RS_BLOCK), 0, st, a,
+                               (const unsigned long long *)r->rks, (const uint32_t *)r->rvs,
+                               (const unsigned long long *)r->rx, R);
+            RS_HIP(hipGetLastError());
+        }
+        hipLaunchKernelGGL(reasm_ec, dim3(gF), dim3(RS_BLOCK), 0, st, a, Fk);
+        RS_HIP(hipGetLastError());
+        hipLaunchKernelGGL(reasm_process, dim3(gF), dim3(RS_BLOCK), 0, st, a, Fk);
+        RS_HIP(hipGetLastError());
+        // the serial list's size comes back with the stats and counts
+        RS_HIP(hipMemcpyAsync(r->host, r->stats, RS_ZERO_WORDS * 8, hipMemcpyDeviceToHost, st));
+        RS_HIP(hipStreamSynchronize(st));
+        return 0;
+    };
+    const uint32_t *hc = reinterpret_cast<const uint32_t *>(r->host + 2 * (UDPDK_RS_N + 1));   // counts
+    uint32_t F = 0;
+    bool grouped = true;
     uint32_t K = 0;                          // fragments on the serial path
     bool read_back = true;                   // the stats block still to be read back
     memset(o, 0, sizeof(*o));
-    if (F) {
-        const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((F + RS_BLOCK - 1) / RS_BLOCK, 4096));
-        if (grouped) {
-            a.order = r->frag_list;
-        } else {
-            // group by key keeping arrival order: stable sorts by (id, index), then src|dst
+    if (n) {
+        // every key one run in arrival order: the list is already grouped, and no flow's span can
+        // overlap another's (each span holds only its own fragments)
+        a.grouped = 1u;
+        a.order = r->frag_list;
+        if (int e = analysis(RS_F_DEV, n, true)) return e;
+        F = hc[0];
+        grouped = hc[4] == 0u;
+        if (F && !grouped) {
+            // group by key keeping arrival order: stable sorts by (id, index), then src|dst; the
+            // sort keys are then dead and their buffers take the records in sorted order
+            a.grouped = 0u;
+            a.order = r->v2s;
+            const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((F + RS_BLOCK - 1) / RS_BLOCK, 4096));
             hipLaunchKernelGGL(reasm_keys1, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
             RS_HIP(hipGetLastError());
             tb = r->tmp_bytes;
@@ -1387,51 +1449,13 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
             RS_HIP(hipGetLastError());
             tb = r->tmp_bytes;
             RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k2, r->k2s, r->v1s, r->v2s, (size_t)F, 0, 64, st));
-        }
-        // (grouped: reasm_runs wrote the records; else the sort keys are dead now and their
-        // buffers take the records in sorted order)
-        if (!grouped) {
             hipLaunchKernelGGL(reasm_prep, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
             RS_HIP(hipGetLastError());
+            if (int e = analysis(F, F, false)) return e;
         }
-        // flow analysis: which flows can run without the table (see the top of this file)
-        const uint32_t gb = std::max<uint32_t>(1, std::min<uint32_t>((r->entries + RS_BLOCK - 1) / RS_BLOCK, 4096));
-        hipLaunchKernelGGL(reasm_bsum, dim3(gb), dim3(RS_BLOCK), 0, st, a);
-        RS_HIP(hipGetLastError());
-        const uint32_t gfl = std::max<uint32_t>(1, std::min<uint32_t>((F + RS_FLOW_CHUNK - 1) / RS_FLOW_CHUNK, 2048));
-        hipLaunchKernelGGL(reasm_flows, dim3(gfl), dim3(RS_BLOCK), 0, st, a, F);
-        RS_HIP(hipGetLastError());
-        uint32_t R = 0;                      // overlap records (none when grouped)
-        if (!grouped) {
-            RS_HIP(hipMemcpyAsync(r->host, r->counts, 8, hipMemcpyDeviceToHost, st));
-            RS_HIP(hipStreamSynchronize(st));
-            R = r->host[1];
-        }
-        if (R) {
-            tb = r->tmp_bytes;
-            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->rk, r->rks, r->rv, r->rvs, (size_t)R, 0,
-                                             a.ib + bits_for(r->nbuckets - 1u), st));
-            const uint32_t gR = std::max<uint32_t>(1, std::min<uint32_t>((R + RS_BLOCK - 1) / RS_BLOCK, 4096));
-            hipLaunchKernelGGL(reasm_rec, dim3(gR), dim3(RS_BLOCK), 0, st, a,
-                               (const unsigned long long *)r->rks, (const uint32_t *)r->rvs, r->rk, R);
-            RS_HIP(hipGetLastError());
-            tb = r->tmp_bytes;
-            RS_HIP(rocprim::inclusive_scan(r->tmp, tb, r->rk, r->rx, (size_t)R,
-                                           rocprim::maximum<unsigned long long>(), st));
-            hipLaunchKernelGGL(reasm_overlap, dim3(gR), dim3(RS_BLOCK), 0, st, a,
-                               (const unsigned long long *)r->rks, (const uint32_t *)r->rvs,
-                               (const unsigned long long *)r->rx, R);
-            RS_HIP(hipGetLastError());
-        }
-        hipLaunchKernelGGL(reasm_ec, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
-        RS_HIP(hipGetLastError());
-        hipLaunchKernelGGL(reasm_process, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
-        RS_HIP(hipGetLastError());
-        // the serial list's size comes back with the stats (one round trip; a second one only
-        // when the serial path runs and adds to them)
-        RS_HIP(hipMemcpyAsync(r->host, r->stats, RS_ZERO_WORDS * 8, hipMemcpyDeviceToHost, st));
-        RS_HIP(hipStreamSynchronize(st));
-        K = reinterpret_cast<const uint32_t *>(r->host + 2 * (UDPDK_RS_N + 1))[2];
+    }
+    if (F) {
+        K = hc[2];
         read_back = K != 0;
         if (K) {
             tb = r->tmp_bytes;
