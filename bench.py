@@ -634,7 +634,8 @@ def end_to_end(ctx, cfg: int, reps: int):
             "path": "pinned host frames -> H2D -> rx pipeline -> D2H meta+lanes, synchronous"}
 
 
-def socket_path_lines(specs=((1 << 20, 64, 1024, 5), (1 << 20, 0, 1024, 3), (1 << 20, 1500, 1024, 3))):
+def socket_path_lines(specs=((1 << 20, 64, 1024, 5), (1 << 20, 0, 1024, 3), (1 << 20, 1500, 1024, 3)),
+                      gpu_extra: str = ""):
     """The reference-API path end to end: tools/bin/bench_sock, a C program
     written against include/udpdk_api.h like the reference's apps, times udpdk_poll_rx (frames in
     pinned host memory -> H2D -> GPU classify/demux -> GPU payload gather -> D2H -> ring
@@ -649,7 +650,7 @@ def socket_path_lines(specs=((1 << 20, 64, 1024, 5), (1 << 20, 0, 1024, 3), (1 <
     with tempfile.NamedTemporaryFile("w", suffix=".ini", delete=False) as f:
         f.write("[port0]\nmac_addr = 68:05:ca:95:f8:ec\nip_addr = 172.31.100.1\n"
                 "[port0_dst]\nmac_addr = 68:05:ca:95:fa:64\n"
-                "[gpu]\ndevice = 0\nmax_frames = 1048576\nmax_lanes = 1024\n")
+                "[gpu]\ndevice = 0\nmax_frames = 1048576\nmax_lanes = 1024\n" + gpu_extra)
         ini = f.name
     try:
         for n, fb, socks, reps in specs:

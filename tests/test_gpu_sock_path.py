@@ -208,11 +208,12 @@ def test_rx_many_sockets_over_poll_threads(api):
     assert all(api.recvfrom(s, 64)[0] == -1 for s in socks)
 
 
-@pytest.mark.parametrize("api", [None, 3], indirect=True)
+@pytest.mark.parametrize("api", [None, 3, "poll_threads = 3\nhost_copy_min = 1\n"], indirect=True)
 def test_rx_burst_admission_and_payloads(api):
     """A socket gets more deliveries in one poll than its ring holds, with the ring partly full:
     each burst of 128 frames is admitted whole or dropped whole (poller.c:287-290); payloads and
-    source addresses come from the GPU gather."""
+    source addresses come from the GPU gather, or (host_copy_min = 1) from the host copy out of
+    the caller's frames."""
     s0, s1 = api.socket(), api.socket()
     assert api.bind(s0, "0.0.0.0", 10001) == 0 and api.bind(s1, "0.0.0.0", 10002) == 0
     pre = _rx_batch([10001] * 700, seed=1)

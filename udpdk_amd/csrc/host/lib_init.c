@@ -28,7 +28,7 @@ static void h_config_defaults(void)
     g_udpdk.dispatch_rss = 0;
     g_udpdk.rss_ready = 0;
     g_udpdk.poll_threads = 0;
-    g_udpdk.host_copy_min = 512;
+    g_udpdk.host_copy_min = 0;         /* off: the GPU gather (tools/sock_tune.py) */
     g_udpdk.gpu_max_frames = 1u << 20;
     g_udpdk.gpu_max_lanes = UDPDK_MAX_SOCKETS;
     g_udpdk.frag_buckets = 0x1000;     /* NUM_FLOWS_DEF, udpdk_constants.h:32 */

@@ -983,8 +983,10 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
     PROF_T(p4);
     g_udpdk.acc_do[nad] = (uint32_t)offd;
     g_udpdk.acc_fo[naf] = (uint32_t)offf;
-    /* direct payloads: host copy when the poll's datagrams are long on average ([gpu]
-     * host_copy_min payload bytes, measured in bench.py's socket_path), else the GPU gather */
+    /* direct payloads: the GPU gather, or, with [gpu] host_copy_min set, a host copy from the
+     * caller's frames when the poll's datagrams carry at least that many payload bytes on average
+     * (off by default: on three boxes the GPU gather + slab D2H took 58-62 ms per 1 M x 1500 B
+     * poll against 54-85 ms for the host copy, which depends on the host's memory bandwidth) */
     const int hcopy = nad && g_udpdk.host_copy_min && offd >= (uint64_t)nad * g_udpdk.host_copy_min;
     if ((hcopy ? h_host_gather(frames, offset, length, g_udpdk.acc_d, g_udpdk.acc_do, nad, &ad)
                : sharded ? h_shards_gather(nad)
