@@ -121,3 +121,32 @@ def test_rss_repeats_of_different_sizes(gpu_ctx):
         (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, b, abi.rss_conf(nq))
         assert np.array_equal(wh, gh) and np.array_equal(wo, go) and np.array_equal(wp, gp)
         assert go[-1] == b.n
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_rss_fuzzed_headers_and_descriptors(gpu_ctx, seed):
+    """Header bits flipped in 30 % of the frames (ether_type, flags, protocol, addresses, ports),
+    5 % of the offsets moved to any byte (past the batch included), 5 % of the lengths set to edge
+    values around the 34- and 38-byte hash inputs: hashes and queue lists equal the oracle's."""
+    rng = np.random.default_rng(seed)
+    base = F.mixed_batch(seed, 4000, [10001, 10002], [9, 20000], ["172.31.100.1", "172.31.100.9"],
+                         with_ptype=seed % 2 == 0)
+    fr = base.frames.copy()
+    for i in rng.choice(base.n, base.n * 3 // 10, replace=False):
+        o = int(base.offset[i])
+        for _ in range(int(rng.integers(1, 4))):
+            pos = o + 12 + int(rng.integers(0, 28))
+            if pos < base.frames_bytes:
+                fr[pos] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    off = base.offset.astype(np.uint64).copy()
+    ln = base.length.astype(np.uint32).copy()
+    k = rng.choice(base.n, base.n // 20, replace=False)
+    off[k] = rng.integers(0, base.frames_bytes + 5000, len(k))
+    k = rng.choice(base.n, base.n // 20, replace=False)
+    ln[k] = rng.choice([0, 13, 14, 33, 34, 35, 37, 38, 39, 65535], len(k))
+    b = F.Batch(fr, off.astype(np.uint32), ln.astype(np.uint16), base.frames_bytes, base.ptype)
+    cf = abi.rss_conf(8, reta=rng.integers(0, 8, 128), hash_types=3)
+    (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, b, cf, b.ptype)
+    assert np.array_equal(wh, gh)
+    assert np.array_equal(wo, go)
+    assert np.array_equal(wp, gp)

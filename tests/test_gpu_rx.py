@@ -78,6 +78,35 @@ def test_fixture_batch(gpu_ctx):
     assert np.array_equal(got[2], z["lane_pkt"])
 
 
+@pytest.mark.parametrize("seed", [31, 32, 33, 34])
+def test_fuzzed_headers_and_descriptors(gpu_ctx, seed):
+    """The mixed batch with random header bits flipped in 30 % of the frames (ether_type, IHL,
+    flags, protocol, lengths, checksums, ports), 5 % of the offsets moved to any byte (frames
+    overlapping, starting mid-frame, at odd offsets or past the batch) and 5 % of the lengths
+    replaced by edge values (0, 1, 13, 14, 33, 41-43, 63-65, 2047, 65535): the verdict words,
+    lanes and counters equal the oracle's on whatever the bytes say."""
+    rng = np.random.default_rng(seed)
+    base = F.mixed_batch(seed, 4000, [10001, 10002, 10003, 10004, 10005], [9, 20000, 65535],
+                         [IP1, IP9], with_ptype=seed % 2 == 0)
+    fr = base.frames.copy()
+    for i in rng.choice(base.n, base.n * 3 // 10, replace=False):
+        o = int(base.offset[i])
+        for _ in range(int(rng.integers(1, 4))):
+            pos = o + 12 + int(rng.integers(0, 40))
+            if pos < base.frames_bytes:
+                fr[pos] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    off = base.offset.astype(np.uint64).copy()
+    ln = base.length.astype(np.uint32).copy()
+    k = rng.choice(base.n, base.n // 20, replace=False)
+    off[k] = rng.integers(0, base.frames_bytes + 5000, len(k))
+    k = rng.choice(base.n, base.n // 20, replace=False)
+    ln[k] = rng.choice([0, 1, 13, 14, 33, 41, 42, 43, 63, 64, 65, 2047, 65535], len(k))
+    b = F.Batch(fr, off.astype(np.uint32), ln.astype(np.uint16), base.frames_bytes, base.ptype)
+    want, got = _rx_both(gpu_ctx, b, MIXED_LISTS, 8)
+    _assert_same(want, got, f"fuzz seed={seed}")
+    assert len(set(abi.meta_verdict(want[0]).tolist())) >= 6
+
+
 def test_compat_uint8_lanes(gpu_ctx):
     """Compat mode: lanes keyed by (uint8_t)sockfd exactly like exch_slots[(uint8_t)fd]."""
     n = 600
