@@ -170,12 +170,26 @@ __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, uint32_t off, 
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
-__device__ __forceinline__ uint32_t crc32c_u32(uint32_t crc, uint32_t v)
+// crc32c (reflected, poly 0x82F63B78) of one dword, a byte at a time from a 256-entry table of
+// the byte steps in LDS (crc_table_init): 4 lookups instead of 32 dependent bit steps (the
+// bit-serial form was ~450 VALU instructions per fragment, a sixth of reasm_runs).
+__device__ __forceinline__ uint32_t crc32c_u32(const uint32_t *tab, uint32_t crc, uint32_t v)
 {
     crc ^= v;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1u)));
+    for (int i = 0; i < 4; ++i) crc = (crc >> 8) ^ tab[crc & 0xFFu];
     return crc;
+}
+
+// The block's crc32c byte table (RS_BLOCK >= 256 threads, one entry each); the caller syncs.
+__device__ __forceinline__ void crc_table_init(uint32_t *tab)
+{
+    if (threadIdx.x < 256u) {
+        uint32_t c = threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+        tab[threadIdx.x] = c;
+    }
 }
 
 // Fragment header fields of frame i.
@@ -267,7 +281,8 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_keys(ReasmArgs a, uint32_t F)
 
 // Per sorted position: the fragment's frame, key, signature and length class (all lanes in
 // parallel, so the flow walk below reads one coalesced record per fragment).
-__device__ __forceinline__ void prep_record(const ReasmArgs &a, uint32_t p, uint32_t i, const FragHdr &h)
+__device__ __forceinline__ void prep_record(const ReasmArgs &a, const uint32_t *crc_tab, uint32_t p, uint32_t i,
+                                            const FragHdr &h)
 {
         const int32_t ip_len = (int32_t)h.tl - 20;                    // l3_len = 20
         const uint32_t ofs = (h.ff & 0x1FFFu) * 8u;
@@ -278,9 +293,9 @@ __device__ __forceinline__ void prep_record(const ReasmArgs &a, uint32_t p, uint
             len = (uint32_t)ip_len;
             if (34u + len > h.flen || ofs + len > a.max_dgram) cls = 2;
         }
-        uint32_t v = crc32c_u32(0xeaad8405u, h.src);
-        v = crc32c_u32(v, h.dst);
-        v = crc32c_u32(v, h.id);
+        uint32_t v = crc32c_u32(crc_tab, 0xeaad8405u, h.src);
+        v = crc32c_u32(crc_tab, v, h.dst);
+        v = crc32c_u32(crc_tab, v, h.id);
         a.s_i[p] = i;
         a.s_src[p] = h.src;
         a.s_dst[p] = h.dst;
@@ -294,10 +309,13 @@ __device__ __forceinline__ void prep_record(const ReasmArgs &a, uint32_t p, uint
 
 __global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
 {
+    __shared__ uint32_t crc_tab[256];
+    crc_table_init(crc_tab);
+    __syncthreads();
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
     for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
         const uint32_t i = a.order[p];
-        prep_record(a, p, i, frag_hdr(a, fr, i));
+        prep_record(a, crc_tab, p, i, frag_hdr(a, fr, i));
     }
 }
 
@@ -310,6 +328,9 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
 // another run, or two keys share a fingerprint) sets counts[4] and the batch takes the sorts.
 __global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned long long *hset, uint32_t hmask)
 {
+    __shared__ uint32_t crc_tab[256];
+    crc_table_init(crc_tab);
+    __syncthreads();
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
     const uint32_t F = a.counts[0];
     const uint32_t lane = __lane_id();
@@ -321,7 +342,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned lon
         const uint32_t i = valid ? a.frag_list[p] : 0u;
         const FragHdr h = frag_hdr(a, fr, i);
         const uint32_t id = h.id, src = h.src, dst = h.dst;
-        if (valid) prep_record(a, p, i, h);
+        if (valid) prep_record(a, crc_tab, p, i, h);
         uint32_t pid = __shfl_up(id, 1, 64), psrc = __shfl_up(src, 1, 64), pdst = __shfl_up(dst, 1, 64);
         if (lane == 0u && valid && p > 0u) {
             const uint32_t op = a.offset[a.frag_list[p - 1]];
@@ -865,15 +886,40 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_sizes(const ReasmDone *done, c
 // scan (three passes, six launches with the scans' state initialisation).
 constexpr uint32_t RS_CL = 2048;                 // positions per block, 8 per thread
 
+// The grouped path's tail (completion list, offsets, emit) launched right behind reasm_process,
+// before the host has read the call's counts back (counts == nullptr: an ordinary launch). It runs
+// only when the batch was grouped, no fragment went to the serial list (so no fragment is held
+// or stored, and every datagram's bytes are in the batch) and the output fits the buffer; F and
+// the completion count then come from the device. The host re-derives the same decision from the
+// read-back and runs the tail itself otherwise, so a grouped batch makes one host round trip.
+struct SpecTail {
+    const uint32_t *counts;                      // [0] F, [2] serial list, [4] not grouped
+    const unsigned long long *stats;             // [UDPDK_RS_DONE] completions, [UDPDK_RS_N] bytes
+    unsigned long long out_cap;
+};
+
+__device__ __forceinline__ bool spec_tail_go(const SpecTail &g, uint32_t &F, uint32_t &C)
+{
+    if (!g.counts) return true;
+    if (g.counts[4] || g.counts[2]) return false;
+    const unsigned long long c = g.stats[UDPDK_RS_DONE], ob = g.stats[UDPDK_RS_N];
+    if (!c || ob + UDPDK_GPU_FRAMES_TAILROOM > g.out_cap) return false;
+    F = g.counts[0];
+    C = (uint32_t)c;
+    return true;
+}
+
 __device__ __forceinline__ uint32_t done_bytes(const ReasmDone *done, uint32_t q)
 {
     return (34u + done[q].total + 15u) & ~15u;    // as reasm_sizes
 }
 
 __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_count(const uint32_t *dk, const ReasmDone *done,
-                                                             uint32_t F, uint32_t *blk)
+                                                             uint32_t F, uint32_t *blk, SpecTail g)
 {
     __shared__ uint32_t red[2 * RS_WAVES];
+    uint32_t C_unused;
+    if (!spec_tail_go(g, F, C_unused) || blockIdx.x * RS_CL >= F) return;
     const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
     const uint32_t p0 = blockIdx.x * RS_CL + tid * (RS_CL / RS_BLOCK);
     uint32_t c = 0, by = 0;
@@ -900,9 +946,11 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_count(const uint32_t *dk
 
 __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_write(const uint32_t *dk, const ReasmDone *done,
                                                              uint32_t F, const uint32_t *blk,
-                                                             uint32_t *perm, uint32_t *offs)
+                                                             uint32_t *perm, uint32_t *offs, SpecTail g)
 {
     __shared__ uint32_t red[4 * RS_WAVES];
+    uint32_t C_unused;
+    if (!spec_tail_go(g, F, C_unused) || blockIdx.x * RS_CL >= F) return;
     const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6, b = blockIdx.x;
     // this block's base: the earlier blocks' totals
     uint32_t pc = 0, pb = 0;
@@ -959,6 +1007,7 @@ struct EmitArgs {
     uint32_t *out_ptype;
     uint32_t *out_origin;
     uint32_t C;
+    SpecTail g;                   // speculative launch: C from the device, or nothing to do
 };
 
 // One wave per datagram. The output datagram is written as aligned 16-byte chunks (lane =
@@ -997,20 +1046,22 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
     // wave-uniform scalar loads and SGPRs, not per-lane copies
     const uint32_t lane = __lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
+    uint32_t F_unused, C = a.C;
+    if (!spec_tail_go(a.g, F_unused, C)) return;
     // The next datagram's record and output offset are loaded while this one is copied.
     const uint32_t stride = gridDim.x * RS_WAVES;
     uint32_t k = blockIdx.x * RS_WAVES + w;
     ReasmDone rn{};
     uint32_t oon = 0;
-    if (k < a.C) {
+    if (k < C) {
         rn = a.done[a.perm[k]];
         oon = a.out_off_in[k];
     }
     constexpr uint32_t OOR = 0x80000000u;         // out of any buffer's range: no access, zeros
-    for (; k < a.C; k += stride) {
+    for (; k < C; k += stride) {
         const ReasmDone r = rn;
         const uint32_t oo = oon;
-        if (k + stride < a.C) {
+        if (k + stride < C) {
             rn = a.done[a.perm[k + stride]];
             oon = a.out_off_in[k + stride];
         }
@@ -1381,6 +1432,52 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     // grouped path launched speculatively (grids sized for n, F read on the device, every kernel
     // returning at once if the batch is not grouped), so a grouped batch makes no host round trip
     // between the run test and the stats read-back.
+    // Completion list + output offsets + emit (the grouped path's list by clist_count/write, else a
+    // sort by origin + sizes + scan). spec: launched before the read-back (grids from the batch
+    // size, counts from the device, see SpecTail).
+    auto tail = [&](bool grp, uint32_t Fn, uint32_t Cn, bool spec) -> int {
+        SpecTail g{nullptr, nullptr, 0};
+        if (spec) g = SpecTail{r->counts, r->stats, (unsigned long long)r->out_cap};
+        size_t tbt = r->tmp_bytes;
+        if (grp) {
+            const uint32_t nb = (Fn + RS_CL - 1) / RS_CL;
+            hipLaunchKernelGGL(reasm_clist_count, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
+                               (const ReasmDone *)r->done, Fn, r->sizes, g);
+            hipLaunchKernelGGL(reasm_clist_write, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
+                               (const ReasmDone *)r->done, Fn, (const uint32_t *)r->sizes, r->perm, r->offs, g);
+            RS_HIP(hipGetLastError());
+        } else {
+            const uint32_t gC = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_BLOCK - 1) / RS_BLOCK, 4096));
+            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tbt, r->dk, r->dks, r->dv, r->perm, (size_t)Fn, 0,
+                                             bits_for(n), st));
+            hipLaunchKernelGGL(reasm_sizes, dim3(gC), dim3(RS_BLOCK), 0, st, (const ReasmDone *)r->done,
+                               (const uint32_t *)r->perm, r->sizes, Cn);
+            RS_HIP(hipGetLastError());
+            tbt = r->tmp_bytes;
+            RS_HIP(rocprim::exclusive_scan(r->tmp, tbt, r->sizes, r->offs, 0u, (size_t)Cn,
+                                           rocprim::plus<uint32_t>(), st));
+        }
+        EmitArgs ea;
+        ea.frames = bt->frames_dev;
+        ea.offset = bt->offset_dev;
+        ea.rsrc_bytes = a.rsrc_bytes;
+        ea.ebuf = r->ebuf;
+        ea.stride = r->stride;
+        ea.done = r->done;
+        ea.perm = r->perm;
+        ea.out_off_in = r->offs;
+        ea.out = r->out;
+        ea.out_off = r->out_off;
+        ea.out_len = r->out_len;
+        ea.out_ptype = r->out_ptype;
+        ea.out_origin = r->out_origin;
+        ea.C = Cn;
+        ea.g = g;
+        const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_WAVES - 1) / RS_WAVES, 8192));
+        hipLaunchKernelGGL(reasm_emit, dim3(ge), dim3(RS_BLOCK), 0, st, ea);
+        RS_HIP(hipGetLastError());
+        return 0;
+    };
     auto analysis = [&](uint32_t Fk, uint32_t Fgrid, bool grp) -> int {
         const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((Fgrid + RS_BLOCK - 1) / RS_BLOCK, 4096));
         const uint32_t gb = std::max<uint32_t>(1, std::min<uint32_t>((r->entries + RS_BLOCK - 1) / RS_BLOCK, 4096));
@@ -1415,6 +1512,8 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         RS_HIP(hipGetLastError());
         hipLaunchKernelGGL(reasm_process, dim3(gF), dim3(RS_BLOCK), 0, st, a, Fk);
         RS_HIP(hipGetLastError());
+        if (grp && r->out)
+            if (int e = tail(true, Fgrid, Fgrid, true)) return e;
         // the serial list's size comes back with the stats and counts
         RS_HIP(hipMemcpyAsync(r->host, r->stats, RS_ZERO_WORDS * 8, hipMemcpyDeviceToHost, st));
         RS_HIP(hipStreamSynchronize(st));
@@ -1425,6 +1524,9 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     bool grouped = true;
     uint32_t K = 0;                          // fragments on the serial path
     bool read_back = true;                   // the stats block still to be read back
+    bool spec_done = false;                  // the speculative tail ran (see SpecTail)
+    const uint8_t *spec_out = r->out;        // the buffer it wrote to
+    const uint64_t spec_cap = r->out_cap;
     memset(o, 0, sizeof(*o));
     if (n) {
         // every key one run in arrival order: the list is already grouped, and no flow's span can
@@ -1434,6 +1536,12 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         if (int e = analysis(RS_F_DEV, n, true)) return e;
         F = hc[0];
         grouped = hc[4] == 0u;
+        {
+            uint64_t ob0;
+            memcpy(&ob0, r->host + 2 * UDPDK_RS_N, 8);
+            const uint64_t c0 = reinterpret_cast<const uint64_t *>(r->host)[UDPDK_RS_DONE];
+            spec_done = spec_out && grouped && hc[2] == 0u && c0 && ob0 + UDPDK_GPU_FRAMES_TAILROOM <= spec_cap;
+        }
         if (F && !grouped) {
             // group by key keeping arrival order: stable sorts by (id, index), then src|dst; the
             // sort keys are then dead and their buffers take the records in sorted order
@@ -1476,7 +1584,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     o->stats[UDPDK_RS_SERIAL] = K;
     o->stats[UDPDK_RS_SORTED] = F && !grouped ? 1u : 0u;
     const uint32_t Cn = (uint32_t)o->stats[UDPDK_RS_DONE], J = (uint32_t)o->stats[UDPDK_RS_STORED];
-    if (Cn) {
+    if (Cn && !spec_done) {
         if (ob + UDPDK_GPU_FRAMES_TAILROOM > r->out_cap) {
             if (r->out) RS_HIP(hipFree(r->out));
             r->out = nullptr;
@@ -1488,43 +1596,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         // completions in origin (arrival) order, then their frame offsets. Grouped: positions are
         // in arrival order, so the positions holding one, in order; else a sort by origin
         // (positions without one have all-ones keys and sort last)
-        const uint32_t gC = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_BLOCK - 1) / RS_BLOCK, 4096));
-        tb = r->tmp_bytes;
-        if (grouped) {
-            const uint32_t nb = (F + RS_CL - 1) / RS_CL;
-            hipLaunchKernelGGL(reasm_clist_count, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
-                               (const ReasmDone *)r->done, F, r->sizes);
-            hipLaunchKernelGGL(reasm_clist_write, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
-                               (const ReasmDone *)r->done, F, (const uint32_t *)r->sizes, r->perm, r->offs);
-            RS_HIP(hipGetLastError());
-        } else {
-            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->dk, r->dks, r->dv, r->perm, (size_t)F, 0,
-                                             bits_for(n), st));
-            hipLaunchKernelGGL(reasm_sizes, dim3(gC), dim3(RS_BLOCK), 0, st, (const ReasmDone *)r->done,
-                               (const uint32_t *)r->perm, r->sizes, Cn);
-            RS_HIP(hipGetLastError());
-            tb = r->tmp_bytes;
-            RS_HIP(rocprim::exclusive_scan(r->tmp, tb, r->sizes, r->offs, 0u, (size_t)Cn,
-                                           rocprim::plus<uint32_t>(), st));
-        }
-        EmitArgs ea;
-        ea.frames = bt->frames_dev;
-        ea.offset = bt->offset_dev;
-        ea.rsrc_bytes = a.rsrc_bytes;
-        ea.ebuf = r->ebuf;
-        ea.stride = r->stride;
-        ea.done = r->done;
-        ea.perm = r->perm;
-        ea.out_off_in = r->offs;
-        ea.out = r->out;
-        ea.out_off = r->out_off;
-        ea.out_len = r->out_len;
-        ea.out_ptype = r->out_ptype;
-        ea.out_origin = r->out_origin;
-        ea.C = Cn;
-        const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_WAVES - 1) / RS_WAVES, 8192));
-        hipLaunchKernelGGL(reasm_emit, dim3(ge), dim3(RS_BLOCK), 0, st, ea);
-        RS_HIP(hipGetLastError());
+        if (int e = tail(grouped, F, Cn, false)) return e;
     }
     if (J) {   // after every read of the entry buffers (reasm_emit)
         StoreArgs sa;
