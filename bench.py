@@ -137,9 +137,12 @@ class Rx:
 
     def classify_bytes(self) -> int:
         # rx_classify algorithmic bytes per launch: every frame byte + u32 offset + u16 length
-        # read, u32 verdict written, plus the tile histogram column (lanes x tiles x 4 B)
+        # read, u32 verdict written, plus the tile histogram column (lanes x tiles x 4 B); on
+        # the single-lane path classify also writes the lane entries (speculative compaction,
+        # DESIGN.md §3; every frame of configs 1-3 is delivered)
         t, k = abi.geometry(self.n, self.w.n_sockets)
-        return self.sum_len + 6 * self.n + 4 * self.n + 4 * self.w.n_sockets * k
+        spec = 4 * self.n if self.w.n_sockets == 1 else 0
+        return self.sum_len + 6 * self.n + 4 * self.n + 4 * self.w.n_sockets * k + spec
 
     def pipeline_bytes(self) -> int:
         # sum(frame_len) + 8 N (descriptor) + 4 N (verdict) + 4 D (lane entry)

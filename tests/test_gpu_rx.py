@@ -209,6 +209,28 @@ def test_edge_sizes(gpu_ctx):
         _assert_same(want, got, f"n={n}")
 
 
+@pytest.mark.parametrize("drops", [(), (0,), (5,), (9,), (3, 7), ("all", 3)])
+def test_single_lane_speculation(gpu_ctx, drops):
+    """Single lane, 1024-frame tiles: rx_classify writes each tile's entries where they belong if
+    every earlier tile delivered all its frames, and rx_compact1 keeps them up to the first tile
+    that did not (flagged per call) and rewrites the rest. Ten tiles plus a partial one; frames
+    dropped (unbound port) in the listed tiles, or a whole tile; each case runs after a call with
+    every frame delivered, so a stale flag from an earlier call would show."""
+    lists = {abi.raw_port(10001): [(0, 0, 0)]}
+    n = 10 * 1024 + 300
+    for k in range(2):
+        b = F.build_frames(np.full(n, 64, np.uint32), np.full(n, 10001, np.uint32), 40 + k)
+        if k == 1:
+            v = b.frames[:n * 64].reshape(n, 64)
+            whole = drops[:1] == ("all",)
+            for t in (drops[1:] if whole else drops):
+                rows = np.arange(t * 1024, min(n, t * 1024 + 1024)) if whole else np.arange(t * 1024 + 17, min(n, t * 1024 + 1024), 101)
+                v[rows, 36] = 0x4E                              # dst port 20000: not bound
+                v[rows, 37] = 0x20
+        want, got = _rx_both(gpu_ctx, b, lists, 1)
+        _assert_same(want, got, f"drops={drops} call={k}")
+
+
 def test_empty_batch(gpu_ctx):
     lists = {abi.raw_port(10001): [(0, 0, 0)]}
     hs = abi.snapshot_from_lists(lists, 3)

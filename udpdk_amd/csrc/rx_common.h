@@ -93,7 +93,17 @@ struct RxArgs {
     uint32_t lane_mask;
     uint32_t n_lanes;
     uint32_t hist16;      // hist rows are u16[(n_lanes + 1) & ~1] (multi-lane, no fan-out)
+    // single lane, no fan-out, one-round 1024-frame tiles: each tile also writes its deliveries
+    // at tile x tile_frames + rank, their place if every earlier tile delivered all its frames
+    // (rx_compact1 then only checks that); null otherwise
+    uint32_t *spec_pkt;
+    uint32_t spec_cap;
+    uint32_t spec_epoch;
+    unsigned long long *spec_nonfull;   // atomicMax of epoch << 32 | ~tile for tiles not full
 };
+#ifndef UDPDK_SPEC_COMPACT
+#define UDPDK_SPEC_COMPACT 1
+#endif
 
 struct ScanArgs {
     uint32_t *hist;
@@ -151,6 +161,9 @@ struct Compact1Args {
     uint32_t n_tiles;
     uint32_t lane_cap;
     const uint32_t *base;         // [n_tiles] exclusive prefix of tile_count (rx_tile_base), or null
+    uint32_t spec;                // rx_classify wrote speculative entries (RxArgs::spec_pkt)
+    uint32_t spec_epoch;
+    const unsigned long long *spec_nonfull;
 };
 
 struct TxArgs {

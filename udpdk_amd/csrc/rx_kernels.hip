@@ -685,6 +685,50 @@ rx_classify(RxArgs a)
         for (int i = 0; i < CLS_WAVES; ++i) v += cntw[i * 16 + c];
         return v;
     };
+    if (a.spec_pkt) {
+        // Speculative lane entries (single lane, 1024-frame one-round tile, 4 frames per
+        // thread): the tile's delivered frames in order at t0 + rank, which is where they belong
+        // when every earlier tile delivered all its frames. rx_compact1 keeps them then (its
+        // check: the predecessors' counts sum to t0) and rewrites the tile otherwise, so the
+        // dependent compaction pass reads no verdict word and writes no entry in that case.
+        __shared__ uint32_t spec_ws[CLS_WAVES];
+        const uint32_t nv = t1 - t0, j0 = 4u * tid;
+        uint32_t d = 0;
+        if (j0 < nv) {
+            const uint4 v = reinterpret_cast<const uint4 *>(mstage)[tid];
+            d = ((v.x & 0xFu) == UDPDK_V_DELIVERED ? 1u : 0u) |
+                ((v.y & 0xFu) == UDPDK_V_DELIVERED && j0 + 1u < nv ? 2u : 0u) |
+                ((v.z & 0xFu) == UDPDK_V_DELIVERED && j0 + 2u < nv ? 4u : 0u) |
+                ((v.w & 0xFu) == UDPDK_V_DELIVERED && j0 + 3u < nv ? 8u : 0u);
+        }
+        const uint32_t cnt = (uint32_t)__builtin_popcount(d);
+        const uint32_t incl = scan_dpp(cnt);
+        if (lane == 63) spec_ws[w] = incl;
+        __syncthreads();
+        uint32_t pos = t0 + incl - cnt;
+#pragma unroll
+        for (uint32_t i = 0; i < CLS_WAVES; ++i) pos += i < w ? spec_ws[i] : 0u;
+        // a tile short of a full tile's deliveries (the last tile never counts: nothing follows
+        // it) marks its successors' entries wrong; every other word of the flag stays untouched
+        if (tid == 0 && tile + 1u < a.n_tiles) {
+            uint32_t tc = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < CLS_WAVES; ++i) tc += spec_ws[i];
+            if (tc != a.tile_frames)
+                atomicMax(a.spec_nonfull, ((unsigned long long)a.spec_epoch << 32) | (0xFFFFFFFFu - tile));
+        }
+        const uint32_t f = t0 + j0;
+        if (d == 0xFu && (pos & 3u) == 0u && pos + 4u <= a.spec_cap) {
+            *reinterpret_cast<uint4 *>(a.spec_pkt + pos) = make_uint4(f, f + 1u, f + 2u, f + 3u);
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                if ((d >> j) & 1u) {
+                    if (pos < a.spec_cap) a.spec_pkt[pos] = f + j;
+                    ++pos;
+                }
+        }
+    }
     if (nbuf == 1u) {
         const uint32_t nv = t1 - t0;
         uint32_t *dst = a.meta + t0;
@@ -739,6 +783,21 @@ rx_compact1(Compact1Args a)
     // are in flight together with the verdict words: one memory round trip for both
     const uint32_t tl = a.n_tiles - 1u;
     const uint32_t c0 = a.tile_count[min(tid, tl)], c1 = a.tile_count[min(tid + RX_BLOCK, tl)];
+    if (a.spec) {
+        // rx_classify placed this tile's entries at tile x tile_frames + rank: right when every
+        // earlier tile delivered all its frames, i.e. no tile before this one is in the flag
+        const unsigned long long nf = __hip_atomic_load(a.spec_nonfull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t first = (uint32_t)(nf >> 32) == a.spec_epoch ? 0xFFFFFFFFu - (uint32_t)nf : 0xFFFFFFFFu;
+        if (tile <= first) {
+            if (tile == tl && tid == 0) {
+                const uint32_t total = tile * a.tile_frames + a.tile_count[tile];
+                a.lane_off[0] = 0u;
+                a.lane_off[1] = total;
+                *a.total = total;
+            }
+            return;
+        }
+    }
     uint32_t wcount = 0;
     for (uint32_t s0 = 0; s0 < steps; s0 += 4) {
         uint32_t mv[4];

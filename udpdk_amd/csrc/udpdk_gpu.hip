@@ -28,6 +28,9 @@ struct DevResult {
     unsigned long long counters[UDPDK_N_COUNTERS];
     uint32_t total;
     uint32_t pad;
+    // speculative single-lane compaction: max of (call epoch << 32 | ~tile) over the tiles that
+    // did not deliver all their frames (rx_classify), i.e. the call's first such tile
+    unsigned long long nonfull;
 };
 
 // Per-call kernel timing: start/stop events carried by the kernel dispatches themselves
@@ -52,6 +55,7 @@ struct Pipe {
     unsigned long long *agg = nullptr;        // rx_scan_cols look-back words, one per lane block
     uint32_t *ticket = nullptr;               // rx_scan_cols lane-block tickets
     uint32_t epoch = 0;                       // rx_scan_cols calls on this pipe (look-back tag)
+    uint32_t spec_epoch = 0;                  // speculative compaction calls (DevResult::nonfull tag)
     uint32_t *tile_cnt = nullptr;
     DevResult *res = nullptr;                 // counters, total (device)
     DevResult *h_res = nullptr;               // pinned mirror, filled by udpdk_gpu_rx_stats
@@ -595,6 +599,13 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     ra.n_tiles = tiles;
     ra.lane_mask = c->lane_mask;
     ra.n_lanes = S;
+    // speculative single-lane entries from classify (see RxArgs::spec_pkt)
+    const bool spec = UDPDK_SPEC_COMPACT && one_lane && T == (uint32_t)RX_ROUND && CLS_BLOCK * 4 == RX_ROUND;
+    ra.spec_pkt = spec ? o->lane_pkt_dev : nullptr;
+    ra.spec_cap = spec ? o->lane_cap : 0u;
+    if (spec && ++P.spec_epoch == 0) P.spec_epoch = 1;       // 0: the zeroed word's tag
+    ra.spec_nonfull = spec ? &P.res->nonfull : nullptr;
+    ra.spec_epoch = P.spec_epoch;
 
     if (ts) for (int k = 0; k < TIMED_KERNELS; ++k) ts->used[k] = false;
     HIPC(c, launch(st, ts, 0, true, true, rx_classify, dim3(tiles), dim3(CLS_BLOCK),
@@ -611,6 +622,9 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
         ca.n_tiles = tiles;
         ca.lane_cap = o->lane_cap;
         ca.base = nullptr;
+        ca.spec = spec ? 1u : 0u;
+        ca.spec_nonfull = &P.res->nonfull;
+        ca.spec_epoch = P.spec_epoch;
         if (tiles > COMPACT1_DIRECT_TILES && tiles <= c->partial_cap) {
             // past a few thousand tiles each workgroup's sum over its predecessors costs more
             // than one extra launch scanning the counts once
