@@ -89,6 +89,12 @@ constexpr uint32_t PF_TOUCH = 1;      // has a fragment that reaches ip_frag_fin
 constexpr uint32_t PF_COMPLEX = 2;    // pending after its last fragment, key in the table, or an
                                       // expired entry in one of its buckets
 constexpr uint32_t PF_SHARED = 4;     // its span overlaps another flow's on a shared bucket
+constexpr uint32_t PF_START = 8;      // the first sorted position of a flow segment
+// A flow's outcome as reasm_flows found it walking the flow on its own (reasm_process uses it
+// for a flow that runs without the table): 6-bit counts of length-class drops, completions,
+// holes and errors, OC_OVF when a count or the completed bytes did not fit (the flow is then
+// walked again by reasm_process).
+constexpr uint32_t OC_OVF = 1u << 30;
 
 struct ReasmDone {            // one reassembled datagram
     uint32_t origin, total, n, entry;
@@ -126,12 +132,14 @@ struct ReasmArgs {
     // flow analysis (per first sorted position of a flow) and the serial path
     uint32_t assoc_log2, nbuckets;
     uint32_t *pflag, *sb1, *sb2, *tf, *tl;   // [F] flags, bucket pair, span
+    uint32_t *oc, *ob;                 // [F] per flow start: outcome counts, completed bytes
     unsigned long long *rk;            // [2F] overlap records: bucket << ib | tf
     uint32_t *rv;                      // [2F] their flow's first position
     uint32_t *bsum, *cplx;             // [buckets] valid | stale << 31; complex flows
     uint32_t *sl_k, *sl_v;             // [F] serial list: arrival index, sorted position
     uint32_t *tpos;                    // [entries][4] sorted position of a slot's fragment (this call)
     uint32_t call;                     // this call's number (E_CALL), from 1
+    uint32_t hset_tag;                 // reasm_runs' run-key set tag, 1..65535
     uint32_t grouped;                  // every key one run in arrival order: no span overlaps
 };
 
@@ -281,8 +289,11 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_keys(ReasmArgs a, uint32_t F)
 
 // Per sorted position: the fragment's frame, key, signature and length class (all lanes in
 // parallel, so the flow walk below reads one coalesced record per fragment).
+// dv (the identity permutation the origin sort of an ungrouped batch starts from) is written by
+// reasm_prep only; the store jobs are reset by the host right before reasm_serial, the only
+// kernel that sets them (a grouped batch with no serial fragment never reads either).
 __device__ __forceinline__ void prep_record(const ReasmArgs &a, const uint32_t *crc_tab, uint32_t p, uint32_t i,
-                                            const FragHdr &h)
+                                            const FragHdr &h, bool with_dv)
 {
         const int32_t ip_len = (int32_t)h.tl - 20;                    // l3_len = 20
         const uint32_t ofs = (h.ff & 0x1FFFu) * 8u;
@@ -302,9 +313,8 @@ __device__ __forceinline__ void prep_record(const ReasmArgs &a, const uint32_t *
         a.s_id[p] = h.id;
         a.s_sig[p] = v;
         a.s_meta[p] = (cls ? 0u : len) | ((h.ff & 0x1FFFu) << 16) | ((h.ff & 0x2000u) << 16) | (cls << 30);
-        a.dv[p] = p;
-        a.dk[p] = RS_NONE;                                           // no completion / store job yet
-        a.jobs[p] = ReasmJob{RS_NONE, RS_NONE, RS_NONE, RS_NONE};
+        if (with_dv) a.dv[p] = p;
+        a.dk[p] = RS_NONE;                                           // no completion yet
 }
 
 __global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
@@ -315,7 +325,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
     for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
         const uint32_t i = a.order[p];
-        prep_record(a, crc_tab, p, i, frag_hdr(a, fr, i));
+        prep_record(a, crc_tab, p, i, frag_hdr(a, fr, i), true);
     }
 }
 
@@ -342,7 +352,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned lon
         const uint32_t i = valid ? a.frag_list[p] : 0u;
         const FragHdr h = frag_hdr(a, fr, i);
         const uint32_t id = h.id, src = h.src, dst = h.dst;
-        if (valid) prep_record(a, crc_tab, p, i, h);
+        if (valid) prep_record(a, crc_tab, p, i, h, false);
         uint32_t pid = __shfl_up(id, 1, 64), psrc = __shfl_up(src, 1, 64), pdst = __shfl_up(dst, 1, 64);
         if (lane == 0u && valid && p > 0u) {
             const uint32_t op = a.offset[a.frag_list[p - 1]];
@@ -355,14 +365,27 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned lon
         unsigned long long fp = ((unsigned long long)dst << 32 | src) * 0x9E3779B97F4A7C15ull;
         fp ^= (unsigned long long)(id + 1u) * 0xC2B2AE3D27D4EB4Full;
         fp ^= fp >> 29;
-        fp |= 1ull;                                     // 0 marks a free slot
-        for (uint32_t slot = (uint32_t)fp & hmask, k = 0; k <= hmask; ++k, slot = (slot + 1u) & hmask) {
-            const unsigned long long old = atomicCAS(&hset[slot], 0ull, fp);
-            if (old == 0ull) break;
-            if (old == fp) {
+        // slot word: the call's 16-bit tag above a 48-bit fingerprint; a word with another tag is
+        // free (left by an earlier call), so the set needs no clearing between calls (the host
+        // clears it once every 65535 calls, when the tags come round)
+        const unsigned long long tag = (unsigned long long)a.hset_tag << 48;
+        const unsigned long long val = tag | (fp >> 16);
+        uint32_t slot = (uint32_t)fp & hmask, k = 0;
+        unsigned long long cur = ld_a(&hset[slot]);
+        while (k <= hmask) {
+            if ((cur >> 48) != a.hset_tag) {
+                const unsigned long long old = atomicCAS(&hset[slot], cur, val);
+                if (old == cur) break;                  // claimed
+                cur = old;                              // another run won the slot: look at it
+                continue;
+            }
+            if (cur == val) {                           // the key (or its fingerprint) again
                 a.counts[4] = 1u;
                 break;
             }
+            ++k;
+            slot = (slot + 1u) & hmask;
+            cur = ld_a(&hset[slot]);
         }
     }
 }
@@ -572,18 +595,41 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_flows(ReasmArgs a, uint32_t F)
             if (p < F && seg_start(a, p)) {
                 uint32_t tlast = 0;
                 bool live = false;
+                // the walk reasm_process makes for a flow without the table: its completions
+                // are written now (and taken back below if the flow turns out complex) and its
+                // outcome counted, so reasm_process only adds them up for such a flow
+                uint32_t c_len = 0, c_short = 0, c_done = 0, c_holes = 0, c_err = 0;
+                unsigned long long c_bytes = 0;
                 for (uint32_t q = p; q < F && (q == p || same_key(a, p, q)); ++q) {
-                    const uint32_t m = a.s_meta[q];
-                    if (m >> 30) continue;
+                    const uint32_t m = a.s_meta[q], cls = m >> 30;
+                    if (cls) {
+                        if (cls == 1) ++c_len;
+                        else ++c_short;
+                        continue;
+                    }
                     const uint32_t i = a.s_i[q];
                     if (tfirst == RS_NONE) tfirst = i;
                     tlast = i;
                     if (!live) state_reset(st, 0, 0, 0, 0, 0);
                     uint32_t idx;
-                    live = frag_apply(st, m & 0xFFFFu, ((m >> 16) & 0x1FFFu) * 8u, (m >> 29) & 1u, i, &idx) == FA_KEEP;
+                    const uint32_t r = frag_apply(st, m & 0xFFFFu, ((m >> 16) & 0x1FFFu) * 8u, (m >> 29) & 1u, i, &idx);
+                    live = r == FA_KEEP;
+                    if (r == FA_DONE) {
+                        write_done(a, st, q, i, RS_NONE);
+                        ++c_done;
+                        c_bytes += (34u + st[E_TOTAL] + 15u) & ~15u;
+                    } else if (r == FA_HOLE) {
+                        ++c_holes;
+                    } else if (r != FA_KEEP) {
+                        ++c_err;
+                    }
                 }
+                const bool ovf = (c_len | c_short | c_done | c_holes | c_err) > 62u || c_bytes >= (1ull << 31);
+                a.oc[p] = c_len | c_short << 6 | c_done << 12 | c_holes << 18 | c_err << 24 | (ovf ? OC_OVF : 0u);
+                a.ob[p] = (uint32_t)c_bytes;
+                flag = PF_START;
                 if (tfirst != RS_NONE) {
-                    flag = PF_TOUCH | (live ? PF_COMPLEX : 0u);
+                    flag |= PF_TOUCH | (live ? PF_COMPLEX : 0u);
                     const uint32_t sig = a.s_sig[p];
                     bk1 = bucket_of(a, sig);
                     bk2 = bucket2_of(a, sig);
@@ -608,6 +654,9 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_flows(ReasmArgs a, uint32_t F)
                     if (flag & PF_COMPLEX) {
                         atomicAdd(&a.cplx[bk1], 1u);
                         if (bk2 != bk1) atomicAdd(&a.cplx[bk2], 1u);
+                        // a complex flow goes through the table: no completion of its own
+                        if (c_done)
+                            for (uint32_t q = p; q < F && (q == p || same_key(a, p, q)); ++q) a.dk[q] = RS_NONE;
                     }
                 }
             }
@@ -707,9 +756,18 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_process(ReasmArgs a, uint32_t 
         const uint32_t p = p0 + __lane_id();
         uint32_t nser = 0;
         bool serial = false;
-        if (p < F && seg_start(a, p)) {
-            const uint32_t f = a.pflag[p];
-            serial = (f & PF_TOUCH) && (fallback || (f & (PF_COMPLEX | PF_SHARED)));
+        const uint32_t f = p < F ? a.pflag[p] : 0u;
+        const uint32_t oc = (f & PF_START) ? a.oc[p] : 0u;
+        serial = (f & PF_TOUCH) && (fallback || (f & (PF_COMPLEX | PF_SHARED)));
+        if ((f & PF_START) && !serial && !(oc & OC_OVF)) {
+            // reasm_flows walked this flow on its own and wrote its completions: add up
+            c_len += oc & 63u;
+            c_short += (oc >> 6) & 63u;
+            c_done += (oc >> 12) & 63u;
+            c_holes += (oc >> 18) & 63u;
+            c_err += (oc >> 24) & 63u;
+            c_bytes += a.ob[p];
+        } else if (f & PF_START) {
             bool live = false;
             for (uint32_t q = p; q < F && (q == p || same_key(a, p, q)); ++q) {
                 const uint32_t m = a.s_meta[q], cls = m >> 30;
@@ -718,7 +776,11 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_process(ReasmArgs a, uint32_t 
                     else ++c_short;
                     continue;
                 }
-                if (serial) { ++nser; continue; }
+                if (serial) {
+                    ++nser;
+                    a.dk[q] = RS_NONE;                 // reasm_flows' completion, if any, is void
+                    continue;
+                }
                 const uint32_t i = a.s_i[q];
                 if (!live) state_reset(st, 0, 0, 0, 0, 0);
                 uint32_t idx;
@@ -1227,6 +1289,7 @@ struct Reasm {
     uint32_t *dk = nullptr, *dks = nullptr;
     uint32_t *dv = nullptr, *perm = nullptr, *sizes = nullptr, *offs = nullptr;
     uint32_t *pflag = nullptr, *sb1 = nullptr, *sb2 = nullptr, *tf = nullptr, *tl = nullptr;
+    uint32_t *oc = nullptr, *ob = nullptr;
     unsigned long long *rk = nullptr, *rks = nullptr, *rx = nullptr;
     uint32_t *rv = nullptr, *rvs = nullptr, *bsum = nullptr, *cplx = nullptr, *tpos = nullptr;
     uint32_t *sl_k = nullptr, *sl_ks = nullptr, *sl_v = nullptr, *sl_vs = nullptr;
@@ -1262,7 +1325,7 @@ void reasm_destroy(Reasm *r)
     void *dev[] = {r->tab, r->ebuf, r->frag_list, r->v1, r->v1s, r->v2s, r->k1, r->k1s, r->k2,
                    r->k2s, r->stats, r->done, r->jobs, r->dk, r->dks,
                    r->dv, r->perm, r->sizes, r->offs, r->tmp, r->out, r->out_off, r->out_ptype,
-                   r->out_origin, r->out_len, r->pflag, r->sb1, r->sb2, r->tf, r->tl, r->rk, r->rks,
+                   r->out_origin, r->out_len, r->pflag, r->sb1, r->sb2, r->tf, r->tl, r->oc, r->ob, r->rk, r->rks,
                    r->rx, r->rv, r->rvs, r->bsum, r->cplx, r->tpos, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs, r->hset};
     for (void *p : dev)
         if (p) (void)hipFree(p);
@@ -1309,6 +1372,7 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
         (e = dalloc(&r->out_off, C)) != hipSuccess || (e = dalloc(&r->out_len, C)) != hipSuccess ||
         (e = dalloc(&r->out_ptype, C)) != hipSuccess || (e = dalloc(&r->out_origin, C)) != hipSuccess ||
         (e = dalloc(&r->pflag, C)) != hipSuccess || (e = dalloc(&r->sb1, C)) != hipSuccess ||
+        (e = dalloc(&r->oc, C)) != hipSuccess || (e = dalloc(&r->ob, C)) != hipSuccess ||
         (e = dalloc(&r->sb2, C)) != hipSuccess || (e = dalloc(&r->tf, C)) != hipSuccess ||
         (e = dalloc(&r->tl, C)) != hipSuccess || (e = dalloc(&r->rk, C2)) != hipSuccess ||
         (e = dalloc(&r->rks, C2)) != hipSuccess || (e = dalloc(&r->rx, C2)) != hipSuccess ||
@@ -1393,6 +1457,8 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     a.assoc_log2 = r->assoc_log2;
     a.nbuckets = r->nbuckets;
     a.pflag = r->pflag;
+    a.oc = r->oc;
+    a.ob = r->ob;
     a.sb1 = r->sb1;
     a.sb2 = r->sb2;
     a.tf = r->tf;
@@ -1423,7 +1489,9 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     if (n) {
         RS_HIP(rocprim::select(r->tmp, tb, rocprim::counting_iterator<uint32_t>(0u), r->frag_list, r->counts,
                                (size_t)n, IsFrag{meta_dev}, st));
-        RS_HIP(hipMemsetAsync(r->hset, 0, (size_t)hsize * sizeof(unsigned long long), st));
+        a.hset_tag = (a.call - 1u) % 65535u + 1u;
+        if (a.hset_tag == 1u)                 // the tags come round: no word may carry one
+            RS_HIP(hipMemsetAsync(r->hset, 0, (size_t)r->hcap * sizeof(unsigned long long), st));
         const uint32_t g1 = std::max<uint32_t>(1, std::min<uint32_t>((n + RS_BLOCK - 1) / RS_BLOCK, 4096));
         hipLaunchKernelGGL(reasm_runs, dim3(g1), dim3(RS_BLOCK), 0, st, a, r->hset, hsize - 1u);
         RS_HIP(hipGetLastError());
@@ -1510,7 +1578,9 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         }
         hipLaunchKernelGGL(reasm_ec, dim3(gF), dim3(RS_BLOCK), 0, st, a, Fk);
         RS_HIP(hipGetLastError());
-        hipLaunchKernelGGL(reasm_process, dim3(gF), dim3(RS_BLOCK), 0, st, a, Fk);
+        // at most 256 workgroups: each adds its six block totals to the call's stats words with
+        // agent-scope atomics on the same six addresses, which serialise (2048 workgroups: 27 us)
+        hipLaunchKernelGGL(reasm_process, dim3(std::min<uint32_t>(gF, 256)), dim3(RS_BLOCK), 0, st, a, Fk);
         RS_HIP(hipGetLastError());
         if (grp && r->out)
             if (int e = tail(true, Fgrid, Fgrid, true)) return e;
@@ -1566,6 +1636,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         K = hc[2];
         read_back = K != 0;
         if (K) {
+            RS_HIP(hipMemsetAsync(r->jobs, 0xFF, (size_t)F * sizeof(ReasmJob), st));   // no store job
             tb = r->tmp_bytes;
             RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs, (size_t)K, 0,
                                              bits_for(n - 1u), st));
