@@ -99,11 +99,12 @@ struct RxArgs {
     uint32_t *spec_pkt;
     uint32_t spec_cap;
     uint32_t spec_epoch;
-    unsigned long long *spec_nonfull;   // atomicMax of epoch << 32 | ~tile for tiles not full
+    unsigned long long *spec_nonfull;   // [UDPDK_SPEC_WORDS] atomicMax of epoch << 32 | ~tile, tiles not full
 };
 #ifndef UDPDK_SPEC_COMPACT
 #define UDPDK_SPEC_COMPACT 1
 #endif
+#define UDPDK_SPEC_WORDS 64u                 // flag words of the speculative compaction
 
 struct ScanArgs {
     uint32_t *hist;

@@ -715,7 +715,8 @@ rx_classify(RxArgs a)
 #pragma unroll
             for (uint32_t i = 0; i < CLS_WAVES; ++i) tc += spec_ws[i];
             if (tc != a.tile_frames)
-                atomicMax(a.spec_nonfull, ((unsigned long long)a.spec_epoch << 32) | (0xFFFFFFFFu - tile));
+                atomicMax(&a.spec_nonfull[tile % UDPDK_SPEC_WORDS],
+                          ((unsigned long long)a.spec_epoch << 32) | (0xFFFFFFFFu - tile));
         }
         const uint32_t f = t0 + j0;
         if (d == 0xFu && (pos & 3u) == 0u && pos + 4u <= a.spec_cap) {
@@ -786,8 +787,12 @@ rx_compact1(Compact1Args a)
     if (a.spec) {
         // rx_classify placed this tile's entries at tile x tile_frames + rank: right when every
         // earlier tile delivered all its frames, i.e. no tile before this one is in the flag
-        const unsigned long long nf = __hip_atomic_load(a.spec_nonfull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t first = (uint32_t)(nf >> 32) == a.spec_epoch ? 0xFFFFFFFFu - (uint32_t)nf : 0xFFFFFFFFu;
+        // every wave reads the 64 words (one load per lane) and takes the smallest flagged tile
+        const unsigned long long nf = __hip_atomic_load(&a.spec_nonfull[lane % UDPDK_SPEC_WORDS], __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t first = (uint32_t)(nf >> 32) == a.spec_epoch ? 0xFFFFFFFFu - (uint32_t)nf : 0xFFFFFFFFu;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) first = min(first, (uint32_t)__shfl_xor((int)first, d, 64));
         if (tile <= first) {
             if (tile == tl && tid == 0) {
                 const uint32_t total = tile * a.tile_frames + a.tile_count[tile];

@@ -28,9 +28,11 @@ struct DevResult {
     unsigned long long counters[UDPDK_N_COUNTERS];
     uint32_t total;
     uint32_t pad;
-    // speculative single-lane compaction: max of (call epoch << 32 | ~tile) over the tiles that
-    // did not deliver all their frames (rx_classify), i.e. the call's first such tile
-    unsigned long long nonfull;
+    // speculative single-lane compaction: word k = max of (call epoch << 32 | ~tile) over the
+    // tiles t = k mod 64 that did not deliver all their frames (rx_classify); the smallest tile
+    // over the 64 words is the call's first such tile (64 words: a batch with many short tiles
+    // does not serialise on one address)
+    unsigned long long nonfull[UDPDK_SPEC_WORDS];
 };
 
 // Per-call kernel timing: start/stop events carried by the kernel dispatches themselves
@@ -604,7 +606,7 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     ra.spec_pkt = spec ? o->lane_pkt_dev : nullptr;
     ra.spec_cap = spec ? o->lane_cap : 0u;
     if (spec && ++P.spec_epoch == 0) P.spec_epoch = 1;       // 0: the zeroed word's tag
-    ra.spec_nonfull = spec ? &P.res->nonfull : nullptr;
+    ra.spec_nonfull = spec ? P.res->nonfull : nullptr;
     ra.spec_epoch = P.spec_epoch;
 
     if (ts) for (int k = 0; k < TIMED_KERNELS; ++k) ts->used[k] = false;
@@ -623,7 +625,7 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
         ca.lane_cap = o->lane_cap;
         ca.base = nullptr;
         ca.spec = spec ? 1u : 0u;
-        ca.spec_nonfull = &P.res->nonfull;
+        ca.spec_nonfull = P.res->nonfull;
         ca.spec_epoch = P.spec_epoch;
         if (tiles > COMPACT1_DIRECT_TILES && tiles <= c->partial_cap) {
             // past a few thousand tiles each workgroup's sum over its predecessors costs more
