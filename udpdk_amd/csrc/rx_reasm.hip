@@ -277,6 +277,82 @@ struct HasDone {
     __device__ bool operator()(uint32_t q) const { return dk[q] != RS_NONE; }
 };
 
+// The FRAG-verdict frames in arrival order (the fragment list, F to counts[0]) in two launches:
+// per block of RS_FS frames its FRAG count, then each block's base from its predecessors'
+// counts and a block scan. Workgroup 0 of the first also zeroes the call's stats block, so a
+// call starts with two launches where it made four (a memset and rocPRIM's select: its state
+// initialisation and two passes).
+constexpr uint32_t RS_FS = 2048;                 // frames per block, 8 per thread
+
+__device__ __forceinline__ uint32_t frag_bits8(const uint32_t *meta, uint32_t i0, uint32_t n)
+{
+    uint32_t m = 0;
+    if (i0 + 8u <= n && ((uintptr_t)meta & 15u) == 0) {
+        const uint4 a = *reinterpret_cast<const uint4 *>(meta + i0);
+        const uint4 b = *reinterpret_cast<const uint4 *>(meta + i0 + 4u);
+        const uint32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) m |= (v[j] & 0xFu) == UDPDK_V_FRAG ? 1u << j : 0u;
+    } else {
+        for (uint32_t j = 0; j < 8 && i0 + j < n; ++j) m |= (meta[i0 + j] & 0xFu) == UDPDK_V_FRAG ? 1u << j : 0u;
+    }
+    return m;
+}
+
+__global__ void __launch_bounds__(RS_BLOCK) reasm_fsel_count(const uint32_t *meta, uint32_t n, uint32_t *blk,
+                                                            unsigned long long *stats_block)
+{
+    __shared__ uint32_t red[RS_WAVES];
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+    if (blockIdx.x == 0 && tid < RS_ZERO_WORDS) stats_block[tid] = 0ull;
+    uint32_t c = (uint32_t)__builtin_popcount(frag_bits8(meta, blockIdx.x * RS_FS + 8u * tid, n));
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+    if (lane == 0) red[w] = c;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < RS_WAVES; ++i) t += red[i];
+        blk[blockIdx.x] = t;
+    }
+}
+
+__global__ void __launch_bounds__(RS_BLOCK) reasm_fsel_write(const uint32_t *meta, uint32_t n, const uint32_t *blk,
+                                                            uint32_t *frag_list, uint32_t *counts)
+{
+    __shared__ uint32_t red[2 * RS_WAVES];
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6, b = blockIdx.x;
+    uint32_t pre = 0;
+    for (uint32_t i = tid; i < b; i += RS_BLOCK) pre += blk[i];
+    const uint32_t i0 = b * RS_FS + 8u * tid;
+    const uint32_t m = frag_bits8(meta, i0, n);
+    const uint32_t c = (uint32_t)__builtin_popcount(m);
+    uint32_t inc = c;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += u;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d, 64);
+    if (lane == 63) red[w] = inc;
+    if (lane == 0) red[RS_WAVES + w] = pre;
+    __syncthreads();
+    uint32_t pos = inc - c, base = 0, tot = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < RS_WAVES; ++i) {
+        pos += i < w ? red[i] : 0u;
+        base += red[RS_WAVES + i];
+        tot += red[i];
+    }
+    pos += base;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j)
+        if ((m >> j) & 1u) frag_list[pos++] = i0 + j;
+    if (b == gridDim.x - 1u && tid == 0) counts[0] = base + tot;     // F
+}
+
 // src | dst << 32 of the fragments in (id, index) order (the second, stable, sort key).
 __global__ void __launch_bounds__(RS_BLOCK) reasm_keys(ReasmArgs a, uint32_t F)
 {
@@ -1473,7 +1549,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     if (++r->calls == 0) r->calls = 1;          // 0 marks entries never touched
     a.call = r->calls;
     a.ib = bits_for(n - 1u);
-    RS_HIP(hipMemsetAsync(r->stats, 0, RS_ZERO_WORDS * sizeof(unsigned long long), st));
+    if (!n) RS_HIP(hipMemsetAsync(r->stats, 0, RS_ZERO_WORDS * sizeof(unsigned long long), st));
     // per-position records (written by reasm_runs for a grouped batch, else by reasm_prep after
     // the sorts, when the sort keys sharing their buffers are dead): cap-strided halves
     a.s_i = reinterpret_cast<uint32_t *>(r->k1);
@@ -1487,8 +1563,12 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     // the fragment list in arrival order (F to counts[0]), then its sort keys and the run test
     size_t tb = r->tmp_bytes;
     if (n) {
-        RS_HIP(rocprim::select(r->tmp, tb, rocprim::counting_iterator<uint32_t>(0u), r->frag_list, r->counts,
-                               (size_t)n, IsFrag{meta_dev}, st));
+        const uint32_t nfs = (n + RS_FS - 1) / RS_FS;   // blocks of the fragment select (their
+        hipLaunchKernelGGL(reasm_fsel_count, dim3(nfs), dim3(RS_BLOCK), 0, st, meta_dev, n, r->sizes,
+                           r->stats);            // counts sit in sizes, dead until the completion list)
+        hipLaunchKernelGGL(reasm_fsel_write, dim3(nfs), dim3(RS_BLOCK), 0, st, meta_dev, n,
+                           (const uint32_t *)r->sizes, r->frag_list, r->counts);
+        RS_HIP(hipGetLastError());
         a.hset_tag = (a.call - 1u) % 65535u + 1u;
         if (a.hset_tag == 1u)                 // the tags come round: no word may carry one
             RS_HIP(hipMemsetAsync(r->hset, 0, (size_t)r->hcap * sizeof(unsigned long long), st));
