@@ -17,7 +17,7 @@
 //  * every other flow's fragments go through the table in arrival order on one wave
 //    (reasm_serial), which is then exactly the reference's sequence of ip_frag_find calls.
 // Launch sequence (udpdk_gpu_rx_reassemble, synchronous):
-//   select          FRAG verdicts -> fragment list in arrival order
+//   reasm_fsel_*    FRAG verdicts -> fragment list in arrival order (+ the stats block zeroed)
 //   reasm_runs      (id << ib | index) sort keys; does every flow key form one run? (grouped)
 //   [not grouped]   radix sort 1 by (id, index); reasm_keys: src|dst keys in that order; radix
 //                   sort 2 (stable). Grouped batches skip both: the list is already grouped
@@ -266,8 +266,8 @@ __device__ void wave_copy16(uint8_t *dst, __amdgpu_buffer_rsrc_t r, uint32_t src
 
 } // namespace
 
-// rocPRIM select predicates: FRAG verdicts (the fragment list in arrival order) and positions
-// holding a completion (the completions in arrival order on the grouped path).
+// rocPRIM select predicates, used for sizing its temporary storage only (the fragment list and
+// the grouped completion list are built by reasm_fsel_* and reasm_clist_*).
 struct IsFrag {
     const uint32_t *meta;
     __device__ bool operator()(uint32_t i) const { return (meta[i] & 0xFu) == UDPDK_V_FRAG; }
