@@ -464,6 +464,49 @@ def reasm_line(ctx, n_dgrams: int, payload_len: int, reps: int):
             "timing": "host wall clock per synchronous call"}
 
 
+def reasm_inplace_line(ctx, n_dgrams: int, payload_len: int, reps: int):
+    """udpdk_gpu_rx_reassemble_inplace (f2, zero-copy as DPDK chains the fragment mbufs) over the
+    same batch as reasm_line: every datagram's fragments are back to back and in order, so the
+    first fragment's frame is extended over the second's (its data moves 34 bytes back, the
+    header is patched). The call consumes the batch, so each timed call gets the batch restored
+    first (outside the timed region); host wall clock per call. Bytes: the later fragments' data
+    read + written, the fragment headers read (the flow analysis), the first header patched."""
+    b = F.frag_batch(n_dgrams, payload_len)
+    ctx.upload_snapshot(abi.snapshot_from_lists({abi.raw_port(F.PORT_RECV): [(0, 0, 0)]}, 1))
+    abi.frag_table_create(ctx, 0x1000, 16, 1 << 40, 65515)
+    db = abi.rx_upload(ctx, b.frames, b.offset, b.length)
+    db.frames_bytes = b.frames_bytes
+    out = abi.rx_alloc_out(ctx, b.n, 1, b.n)
+    abi.rx_run(ctx, db, out)
+
+    def restore():
+        abi._check(abi.lib().udpdk_gpu_h2d(ctx.handle, C.c_void_p(db.frames.ptr), C.c_void_p(b.frames.ctypes.data),
+                                           b.frames_bytes), "h2d")
+        ctx.sync()
+    ts = []
+    for r in range(reps + 1):
+        restore()
+        t0 = time.perf_counter()
+        rb, _, st = abi.rx_reassemble(ctx, db, out.meta, r, inplace=True)
+        ts.append(time.perf_counter() - t0)
+        assert st["done"] == n_dgrams and rb.frames.ptr == db.frames.ptr, st
+    us = 1e6 * sum(ts[1:]) / reps
+    out2 = abi.rx_alloc_out(ctx, n_dgrams, 1, n_dgrams)
+    m2 = abi.rx_run(ctx, rb, out2)[0]
+    ok = bool(np.all(abi.meta_verdict(m2) == 0) and np.all(abi.meta_udp(m2) == 1))
+    for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt, out2.meta,
+              out2.lane_off, out2.lane_pkt):
+        x.free()
+    nf = b.n // n_dgrams
+    moved = n_dgrams * (2 * (payload_len + 8 - 1480) + 64 * nf + 20)
+    return {"workload": f"in-place reassembly {n_dgrams} x {payload_len} B datagrams ({nf} fragments each, "
+                        f"MTU 1500), one batch", "mdgram_s": round(n_dgrams / us, 2),
+            "us_per_call": round(us, 1), "bytes_moved_per_call": moved,
+            "gbps_moved": round(moved / us / 1e3, 1), "frac_hbm_moved": round(moved / us / 1e3 / HBM_PEAK_GBS, 4),
+            "all_delivered_udp_ok": ok,
+            "timing": "host wall clock per synchronous call, the batch restored before each"}
+
+
 def rss_line(ctx, cfg: int, n_queues: int, steps: int):
     """udpdk_gpu_rss (f4) over one batch of config `cfg`: Toeplitz hash, redirection table and
     per-queue lists, GPU time from events around `steps` back-to-back calls. Algorithmic bytes
@@ -894,6 +937,10 @@ def main():
         line["tx"] = tx
         try:
             line["reassembly"] = [reasm_line(ctx, 1 << 18, 2952, 10)]
+            try:
+                line["reassembly"].append(reasm_inplace_line(ctx, 1 << 18, 2952, 10))
+            except Exception as e:
+                line["reassembly"].append({"in_place": True, "error": repr(e)})
         except Exception as e:
             line["reassembly"] = [{"error": repr(e)}]
         rs = []

@@ -341,6 +341,16 @@ int udpdk_gpu_frag_table_create(udpdk_gpu_ctx *ctx, const udpdk_frag_table_cfg_t
  * that cannot meet another flow in the table run in parallel, the rest in arrival order. */
 int udpdk_gpu_rx_reassemble(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch,
                             const uint32_t *meta_dev, uint64_t tms, udpdk_reasm_out_t *out);
+/* As udpdk_gpu_rx_reassemble, consuming the FRAG frames' bytes the way DPDK chains the fragment
+ * mbufs instead of copying them: when every datagram the call completes has its fragments back
+ * to back in batch->frames_dev, in data order, each exactly 34 header bytes + its data (a
+ * fragmenting sender's frames received in order), the first fragment's frame is extended over its
+ * followers (each later fragment's data moves back over the headers before it, the header is
+ * patched) and out->batch.frames_dev is batch->frames_dev, with the datagrams at their first
+ * fragment's offset. Otherwise the call copies, exactly as udpdk_gpu_rx_reassemble. The frame
+ * buffer must be writable and its frames must not overlap; other frames are not touched. */
+int udpdk_gpu_rx_reassemble_inplace(udpdk_gpu_ctx *ctx, udpdk_rx_batch_t *batch,
+                                    const uint32_t *meta_dev, uint64_t tms, udpdk_reasm_out_t *out);
 
 /* ---------------------------------------------------------------------------------------------
  * Receive-side scaling: the reference configures ETH_MQ_RX_RSS with a single

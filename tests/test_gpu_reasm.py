@@ -26,7 +26,7 @@ def _frames(ctx, rb):
     return buf, off, ln
 
 
-def _check_scenario(gpu_ctx, frames_tms, geometry):
+def _check_scenario(gpu_ctx, frames_tms, geometry, inplace=False):
     """Run a multi-batch scenario through the GPU and the oracle: every datagram, origin, length
     and outcome count exact (including "expired" and "stored", which depend on which flow gets
     which table entry when); then the demux of the reassembled datagrams. Returns the totals."""
@@ -44,8 +44,9 @@ def _check_scenario(gpu_ctx, frames_tms, geometry):
         gm, gl, gp, gc, rc = abi.rx_run(gpu_ctx, db, out)
         wm, wl, wp, wc = O.rx(bt, buf, len(buf) - 64, off, ln, None, 4)
         assert rc == 0 and np.array_equal(gm, wm)
-        rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, out.meta, tms)
+        rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, out.meta, tms, inplace=inplace)
         wout, woo, wol, wog, wst = t.reassemble(buf, off, ln, wm, tms)
+        tot["in_place"] = tot.get("in_place", 0) + int(rb.n > 0 and rb.frames.ptr == db.frames.ptr)
         serial = gst.pop("serial")
         tot["sorted"] = tot.get("sorted", 0) + gst.pop("sorted")
         assert gst == wst, f"batch {b}: stats {gst} vs {wst}"
@@ -96,6 +97,51 @@ def test_reassembly_grouped_batches_exact(gpu_ctx, seed, buckets, entries):
     for k in ("done", "stored", "expired"):
         assert tot[k] > 0, (k, tot)
     assert tot["sorted"] == 0, tot                        # every batch took the grouped path
+
+
+@pytest.mark.parametrize("seed,buckets,entries,grouped", [(21, 256, 16, True), (24, 256, 16, True), (22, 4, 4, True),
+                                                         (11, 4, 4, False)])
+def test_reassembly_inplace_scenarios_exact(gpu_ctx, seed, buckets, entries, grouped):
+    """udpdk_gpu_rx_reassemble_inplace over the multi-batch scenarios: a batch whose completions
+    all have their fragments back to back and in order is reassembled in place, any other falls
+    back to the copy; either way every datagram, origin and count equals the oracle's."""
+    tot = _check_scenario(gpu_ctx, scenario(seed, n_batches=5, flows_per_batch=90, dt=12, grouped=grouped),
+                          dict(bucket_num=buckets, bucket_entries=entries, max_cycles=20), inplace=True)
+    assert tot["done"] > 0, tot
+
+
+@pytest.mark.parametrize("payload", [2952, 2951, 4001, 5900])
+def test_reassembly_inplace_in_order(gpu_ctx, payload):
+    """Fragments of each datagram back to back and in order (frames.frag_batch, the bench's
+    workload: 2, 3 and 4 fragments, odd frame sizes so later datagrams start at odd offsets): the
+    call reassembles every datagram in place (the output batch is the input buffer) and the
+    datagrams, origins, counts and their demux equal the oracle's."""
+    from udpdk_amd import frames as FR
+    b = FR.frag_batch(3000, payload)
+    geometry = dict(bucket_num=0x1000, bucket_entries=16, max_cycles=1 << 40)
+    abi.frag_table_create(gpu_ctx, geometry["bucket_num"], geometry["bucket_entries"], geometry["max_cycles"], 65515)
+    t = O.FragTable(**geometry)
+    gpu_ctx.upload_snapshot(abi.snapshot_from_lists({abi.raw_port(FR.PORT_RECV): [(0, 0, 0)]}, 4))
+    db = abi.rx_upload(gpu_ctx, b.frames, b.offset, b.length)
+    db.frames_bytes = b.frames_bytes
+    out = abi.rx_alloc_out(gpu_ctx, b.n, 4, 4 * b.n)
+    gm = abi.rx_run(gpu_ctx, db, out)[0]
+    rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, out.meta, 0, inplace=True)
+    wout, woo, wol, wog, wst = t.reassemble(b.frames, b.offset, b.length, gm, 0)
+    gst.pop("serial"), gst.pop("sorted")
+    assert gst == wst and gst["done"] == 3000, (gst, wst)
+    assert rb.frames.ptr == db.frames.ptr                 # reassembled in place
+    gbuf, goff, gln = _frames(gpu_ctx, rb)
+    gorg = abi.download_ptr(gpu_ctx, origin.ptr, np.uint32, rb.n)
+    assert np.array_equal(gorg, wog) and np.array_equal(gln, wol)
+    for k in range(rb.n):
+        assert gbuf[goff[k]:goff[k] + gln[k]].tobytes() == wout[woo[k]:woo[k] + wol[k]].tobytes(), k
+    out2 = abi.rx_alloc_out(gpu_ctx, rb.n, 4, 4 * rb.n)
+    g2 = abi.rx_run(gpu_ctx, rb, out2)
+    assert g2[4] == 0 and np.all(abi.meta_verdict(g2[0]) == 0) and np.all(abi.meta_udp(g2[0]) == abi.UDP_OK)
+    for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt, out2.meta,
+              out2.lane_off, out2.lane_pkt):
+        x.free()
 
 
 @pytest.mark.parametrize("seed,buckets,entries", [(11, 4, 4), (12, 8, 2), (13, 16, 4), (14, 1, 8)])

@@ -27,6 +27,7 @@ LINES = {
     "txfrag": "out(bench.tx_line(ctx, 2952, 1 << 18, 50, mtu=1500))",
     "rss": "for cfg in (2, 5): out(bench.rss_line(ctx, cfg, 8, 50))",
     "reasm": "out(bench.reasm_line(ctx, 1 << 18, 2952, 10))",
+    "reasmip": "out(bench.reasm_inplace_line(ctx, 1 << 18, 2952, 10))",
     "gather": "for cfg in (2, 3): out(bench.gather_line(ctx, cfg, 50))\n"
               "out(bench.gather_line(ctx, 2, 50, slot=0))",
     "cfg": "import os\nfor c in os.environ.get('CFGS', '4 5').split(): out(bench.side_config(ctx, int(c), 50, 640 << 20))",

@@ -167,6 +167,7 @@ _PROTOS = {
                                              C.POINTER(RxGather)]),
     "udpdk_gpu_frag_table_create": (C.c_int, [_P, C.POINTER(FragTableCfg)]),
     "udpdk_gpu_rx_reassemble": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint64, C.POINTER(ReasmOut)]),
+    "udpdk_gpu_rx_reassemble_inplace": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint64, C.POINTER(ReasmOut)]),
     "udpdk_gpu_rss_default_conf": (C.c_int, [C.POINTER(RssConf), C.c_uint32]),
     "udpdk_gpu_rss_config": (C.c_int, [_P, C.POINTER(RssConf)]),
     "udpdk_gpu_rss": (C.c_int, [_P, C.POINTER(RxBatch), C.POINTER(RssOut)]),
@@ -516,14 +517,15 @@ def frag_table_create(ctx: GpuContext, bucket_num: int = 0x1000, bucket_entries:
     _check(lib().udpdk_gpu_frag_table_create(ctx.handle, C.byref(cfg)), "udpdk_gpu_frag_table_create")
 
 
-def rx_reassemble(ctx: GpuContext, b: RxDeviceBatch, meta: DeviceBuffer, tms: int):
+def rx_reassemble(ctx: GpuContext, b: RxDeviceBatch, meta: DeviceBuffer, tms: int, inplace: bool = False):
     """Reassembly step for a batch whose verdicts are in meta. Returns (RxDeviceBatch of the
-    reassembled frames (context-owned), origin DevRef, stats dict)."""
+    reassembled frames (context-owned, or b's own frame buffer when inplace reassembled every
+    datagram in place), origin DevRef, stats dict)."""
     bt = RxBatch(b.frames.ptr, b.frames_bytes, b.offset.ptr, b.length.ptr,
                  b.ptype.ptr if b.ptype is not None else None, b.n)
     o = ReasmOut()
-    _check(lib().udpdk_gpu_rx_reassemble(ctx.handle, C.byref(bt), C.c_void_p(meta.ptr), tms,
-                                         C.byref(o)), "udpdk_gpu_rx_reassemble")
+    fn = "udpdk_gpu_rx_reassemble_inplace" if inplace else "udpdk_gpu_rx_reassemble"
+    _check(getattr(lib(), fn)(ctx.handle, C.byref(bt), C.c_void_p(meta.ptr), tms, C.byref(o)), fn)
     ob = o.batch
     rb = RxDeviceBatch(DevRef(ob.frames_dev or 0), int(ob.frames_bytes), DevRef(ob.offset_dev or 0),
                        DevRef(ob.length_dev or 0), DevRef(ob.ptype_dev or 0), int(ob.n))

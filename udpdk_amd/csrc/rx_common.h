@@ -270,7 +270,7 @@ int  reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag
                   int *hip_err);
 void reasm_destroy(Reasm *r);
 int  reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32_t *meta_dev,
-               uint64_t tms, udpdk_reasm_out_t *o, int *hip_err);
+                uint64_t tms, udpdk_reasm_out_t *o, int *hip_err, bool inplace);
 
 __global__ void tx_build(TxArgs a);
 

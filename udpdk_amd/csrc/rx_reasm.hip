@@ -1034,17 +1034,88 @@ struct SpecTail {
     const uint32_t *counts;                      // [0] F, [2] serial list, [4] not grouped
     const unsigned long long *stats;             // [UDPDK_RS_DONE] completions, [UDPDK_RS_N] bytes
     unsigned long long out_cap;
+    // in place (udpdk_gpu_rx_reassemble_inplace): reasm_clist_count checks every completion's
+    // fragments (back to back in the frame buffer, in data order, no padding) and raises refuse
+    // (counts[5]) for one that is not; reasm_emit_inplace then runs only if none did, and
+    // reasm_emit only if one did
+    uint32_t inplace;
+    uint32_t *refuse;
+    const uint32_t *offset;                      // the batch's descriptors
+    const uint16_t *length;
 };
+
+// x[i] for a runtime i without indexing a register array (which would go to scratch)
+__device__ __forceinline__ uint32_t pick4(const uint32_t (&x)[RS_MAX_FRAG], uint32_t i)
+{
+    return i == 0u ? x[0] : i == 1u ? x[1] : i == 2u ? x[2] : x[3];
+}
+
+// The fragments of completion r in data order (slot 0 holds offset 0; the others sorted by
+// offset): their number; sl[] the slots. Wave-uniform (r is).
+__device__ __forceinline__ uint32_t data_order(const ReasmDone &r, uint32_t (&sl)[RS_MAX_FRAG])
+{
+    // rank of every used slot among the used ones by data offset (slot 0 holds offset 0), then
+    // sl[rank] = slot: compare-and-count with static indices only (no private-memory arrays)
+    uint32_t m = 0;
+    bool use[RS_MAX_FRAG];
+#pragma unroll
+    for (uint32_t q = 0; q < RS_MAX_FRAG; ++q) {
+        use[q] = q < r.n && r.fr[q] != 0u;
+        m += use[q] ? 1u : 0u;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < RS_MAX_FRAG; ++i) sl[i] = 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < RS_MAX_FRAG; ++q) {
+        uint32_t rank = 0;
+#pragma unroll
+        for (uint32_t p = 0; p < RS_MAX_FRAG; ++p)
+            rank += use[p] && p != q &&
+                    ((r.fr[p] & 0xFFFFu) < (r.fr[q] & 0xFFFFu) || ((r.fr[p] & 0xFFFFu) == (r.fr[q] & 0xFFFFu) && p < q)) ? 1u : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < RS_MAX_FRAG; ++i)
+            if (use[q] && rank == i) sl[i] = q;
+    }
+    return m;
+}
+
+// Can completion r be reassembled in place? Its fragments are frames of this batch (never held:
+// the in-place tail runs only when no fragment went to the table), back to back from the first
+// in data order, each exactly 34 header bytes + its data.
+__device__ __forceinline__ bool inplace_ok(const SpecTail &g, const ReasmDone &r)
+{
+    uint32_t sl[RS_MAX_FRAG];
+    const uint32_t m = data_order(r, sl);
+    if (m < 2u || (pick4(r.fr, sl[0]) & 0xFFFFu) != 0u) return false;
+    uint32_t end = 0;
+    bool ok = true;
+#pragma unroll
+    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
+        if (k >= m) break;
+        const uint32_t q = sl[k], w = pick4(r.where, q);
+        if (w == RS_HELD) return false;
+        const uint32_t o = g.offset[w], ln = g.length[w];
+        ok = ok && ln == 34u + (pick4(r.fr, q) >> 16) && (k == 0u || o == end);
+        end = o + ln;
+    }
+    return ok;
+}
 
 __device__ __forceinline__ bool spec_tail_go(const SpecTail &g, uint32_t &F, uint32_t &C)
 {
     if (!g.counts) return true;
     if (g.counts[4] || g.counts[2]) return false;
-    const unsigned long long c = g.stats[UDPDK_RS_DONE], ob = g.stats[UDPDK_RS_N];
-    if (!c || ob + UDPDK_GPU_FRAMES_TAILROOM > g.out_cap) return false;
+    const unsigned long long c = g.stats[UDPDK_RS_DONE];
+    if (!c) return false;
     F = g.counts[0];
     C = (uint32_t)c;
     return true;
+}
+
+// the copying emit of a speculative tail: the output must fit the buffer it was launched with
+__device__ __forceinline__ bool spec_copy_fits(const SpecTail &g)
+{
+    return !g.counts || g.stats[UDPDK_RS_N] + UDPDK_GPU_FRAMES_TAILROOM <= g.out_cap;
 }
 
 __device__ __forceinline__ uint32_t done_bytes(const ReasmDone *done, uint32_t q)
@@ -1061,14 +1132,17 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_count(const uint32_t *dk
     const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
     const uint32_t p0 = blockIdx.x * RS_CL + tid * (RS_CL / RS_BLOCK);
     uint32_t c = 0, by = 0;
+    bool refuse = false;
 #pragma unroll
     for (uint32_t j = 0; j < RS_CL / RS_BLOCK; ++j) {
         const uint32_t q = p0 + j;
         if (q < F && dk[q] != RS_NONE) {
             ++c;
             by += done_bytes(done, q);
+            if (g.inplace && !refuse) refuse = !inplace_ok(g, done[q]);
         }
     }
+    if (__ballot(refuse) && lane == 0) atomicOr(g.refuse, 1u);    // rare: one atomic per wave
     uint32_t tc, tb;
     (void)wave_excl_scan(c, &tc);
     (void)wave_excl_scan(by, &tb);
@@ -1185,7 +1259,8 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
     const uint32_t lane = __lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
     uint32_t F_unused, C = a.C;
-    if (!spec_tail_go(a.g, F_unused, C)) return;
+    if (!spec_tail_go(a.g, F_unused, C) || !spec_copy_fits(a.g)) return;
+    if (a.g.inplace && !__hip_atomic_load(a.g.refuse, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     // The next datagram's record and output offset are loaded while this one is copied.
     const uint32_t stride = gridDim.x * RS_WAVES;
     uint32_t k = blockIdx.x * RS_WAVES + w;
@@ -1314,6 +1389,114 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
             a.out_off[k] = oo;
             a.out_len[k] = (uint16_t)L;
             a.out_ptype[k] = 0x211u;              // L2_ETHER | L3_IPV4 | L4_UDP
+            a.out_origin[k] = r.origin;
+        }
+    }
+}
+
+// In place (one wave per datagram): the first fragment's frame is extended over its followers.
+// Fragment k (data order, k >= 1) moves 34 k bytes back, over the headers before it, as aligned
+// 16-byte chunk rounds in ascending address order: a round's stores land below every byte a later
+// round (or fragment k itself) still reads, and fragment k + 1 starts only after fragment k's
+// last round (its destination covers the tail of fragment k's source). Then the header's total
+// length, fragment field (DF only) and checksum are patched. Datagrams are disjoint regions (the
+// caller's frames do not overlap), so waves never touch each other's bytes.
+__global__ void __launch_bounds__(RS_BLOCK) reasm_emit_inplace(EmitArgs a, uint8_t *frames)
+{
+    const uint32_t lane = __lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t F_unused, C = a.C;
+    if (!spec_tail_go(a.g, F_unused, C)) return;
+    if (!a.g.inplace || __hip_atomic_load(a.g.refuse, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    const __amdgpu_buffer_rsrc_t fr = rsrc(frames, a.rsrc_bytes);
+    constexpr uint32_t OOR = 0x80000000u;
+    const uint32_t stride = gridDim.x * RS_WAVES;
+    uint32_t k = blockIdx.x * RS_WAVES + w;
+    // the next datagram's record is loaded while this one moves (as in reasm_emit)
+    ReasmDone rn{};
+    if (k < C) rn = a.done[a.perm[k]];
+    for (; k < C; k += stride) {
+        const ReasmDone r = rn;
+        if (k + stride < C) rn = a.done[a.perm[k + stride]];
+        uint32_t sl[RS_MAX_FRAG];
+        const uint32_t m = data_order(r, sl);
+        uint32_t fo[RS_MAX_FRAG];
+#pragma unroll
+        for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) fo[f] = f < m ? a.offset[pick4(r.where, sl[f])] : 0u;
+        const uint32_t o0 = fo[0];
+        // header bytes 14..33: six dwords from the one at or below, lane 0 (issued with the first
+        // fragment's chunk loads; the moves never touch them)
+        const uint32_t ha = (o0 + 14u) & ~3u, hs = (o0 + 14u) & 3u;
+        uint32_t hw[6];
+#pragma unroll
+        for (uint32_t j = 0; j < 6; ++j) hw[j] = ld32(fr, lane == 0u && (j < 5u || hs) ? ha + 4u * j : OOR);
+#pragma unroll
+        for (uint32_t f = 1; f < RS_MAX_FRAG; ++f) {            // static indices: no scratch
+            if (f >= m) break;
+            const uint32_t q = sl[f];
+            const uint32_t fq = pick4(r.fr, q);
+            const uint32_t len = fq >> 16, ofs = fq & 0xFFFFu;
+            const uint32_t src = fo[f] + 34u, dst = o0 + 34u + ofs;
+            // bytes [dst, dst + len) <- [src, src + len), dst < src: destination-aligned 16-byte
+            // chunks (lane = chunk), two rounds' loads in flight before their stores (a round's
+            // stores land below every byte a later round reads); the two partial end chunks store
+            // only their own bytes
+            const uint32_t D0 = dst & ~15u, De = dst + len, shift = src - dst;
+            const uint32_t nch = (De - D0 + 15u) >> 4;
+            for (uint32_t c0 = 0; c0 < nch; c0 += 128u) {
+                uint4 v[2];
+                uint32_t Dv[2];
+                bool inv[2];
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u) {
+                    const uint32_t c = c0 + 64u * u + lane;
+                    inv[u] = c < nch;
+                    Dv[u] = D0 + 16u * c;
+                    const uint32_t S = Dv[u] + shift, sa = S & ~3u, sh = S & 3u;
+                    const uint4 x = load16(fr, inv[u] ? sa : OOR);
+                    const uint32_t hi = ld32(fr, inv[u] && sh ? sa + 16u : OOR);
+                    v[u] = funnel4(x, hi, sh);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u) {
+                    const uint32_t D = Dv[u];
+                    if (inv[u] && D >= dst && D + 16u <= De) {
+                        store16(fr, D, v[u]);
+                    } else if (inv[u]) {
+                        const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (uint32_t j = 0; j < 16; ++j)
+                            if (D + j >= dst && D + j < De)
+                                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(vv[j >> 2] >> (8u * (j & 3u))), fr,
+                                                                     (int)(D + j), 0, 0);
+                    }
+                }
+            }
+        }
+        // header: total length (16-17), fragment field DF only (20-21), checksum (24-25) over
+        // bytes 14..33
+        if (lane == 0) {
+            uint32_t h[5];
+#pragma unroll
+            for (uint32_t j = 0; j < 5; ++j) h[j] = __builtin_amdgcn_alignbyte(hw[j + 1], hw[j], hs);
+            // h[0] = bytes 14-17, h[1] = 18-21, h[2] = 22-25, h[3] = 26-29, h[4] = 30-33
+            const uint32_t tl = r.total + 20u;
+            h[0] = (h[0] & 0x0000FFFFu) | ((tl >> 8) & 0xFFu) << 16 | (tl & 0xFFu) << 24;
+            h[1] = (h[1] & 0x0000FFFFu) | (h[1] & 0x00400000u);
+            h[2] = h[2] & 0x0000FFFFu;
+            uint32_t sum = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 5; ++j) sum += (h[j] & 0xFFFFu) + (h[j] >> 16);
+            sum = (sum >> 16) + (sum & 0xFFFFu);
+            sum = (sum >> 16) + (sum & 0xFFFFu);
+            const uint32_t ck = ~sum & 0xFFFFu;
+            const uint8_t pb[6] = {(uint8_t)(h[0] >> 16), (uint8_t)(h[0] >> 24), (uint8_t)(h[1] >> 16),
+                                   (uint8_t)(h[1] >> 24), (uint8_t)ck, (uint8_t)(ck >> 8)};
+            const uint32_t po[6] = {16, 17, 20, 21, 24, 25};
+#pragma unroll
+            for (uint32_t j = 0; j < 6; ++j) __builtin_amdgcn_raw_buffer_store_b8(pb[j], fr, (int)(o0 + po[j]), 0, 0);
+            a.out_off[k] = o0;
+            a.out_len[k] = (uint16_t)(34u + r.total);
+            a.out_ptype[k] = 0x211u;
             a.out_origin[k] = r.origin;
         }
     }
@@ -1499,7 +1682,7 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
 }
 
 int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32_t *meta_dev,
-              uint64_t tms, udpdk_reasm_out_t *o, int *hip_err)
+              uint64_t tms, udpdk_reasm_out_t *o, int *hip_err, bool inplace)
 {
     if (bt->n > r->cap) return -EINVAL;
     const uint32_t n = bt->n;
@@ -1584,8 +1767,10 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     // sort by origin + sizes + scan). spec: launched before the read-back (grids from the batch
     // size, counts from the device, see SpecTail).
     auto tail = [&](bool grp, uint32_t Fn, uint32_t Cn, bool spec) -> int {
-        SpecTail g{nullptr, nullptr, 0};
-        if (spec) g = SpecTail{r->counts, r->stats, (unsigned long long)r->out_cap};
+        SpecTail g{nullptr, nullptr, 0, 0u, nullptr, nullptr, nullptr};
+        if (spec)
+            g = SpecTail{r->counts, r->stats, (unsigned long long)r->out_cap, inplace ? 1u : 0u, r->counts + 5,
+                         bt->offset_dev, bt->length_dev};
         size_t tbt = r->tmp_bytes;
         if (grp) {
             const uint32_t nb = (Fn + RS_CL - 1) / RS_CL;
@@ -1624,6 +1809,11 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_WAVES - 1) / RS_WAVES, 8192));
         hipLaunchKernelGGL(reasm_emit, dim3(ge), dim3(RS_BLOCK), 0, st, ea);
         RS_HIP(hipGetLastError());
+        if (g.inplace) {
+            hipLaunchKernelGGL(reasm_emit_inplace, dim3(ge), dim3(RS_BLOCK), 0, st, ea,
+                               const_cast<uint8_t *>(bt->frames_dev));
+            RS_HIP(hipGetLastError());
+        }
         return 0;
     };
     auto analysis = [&](uint32_t Fk, uint32_t Fgrid, bool grp) -> int {
@@ -1662,7 +1852,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         // agent-scope atomics on the same six addresses, which serialise (2048 workgroups: 27 us)
         hipLaunchKernelGGL(reasm_process, dim3(std::min<uint32_t>(gF, 256)), dim3(RS_BLOCK), 0, st, a, Fk);
         RS_HIP(hipGetLastError());
-        if (grp && r->out)
+        if (grp && (r->out || inplace))
             if (int e = tail(true, Fgrid, Fgrid, true)) return e;
         // the serial list's size comes back with the stats and counts
         RS_HIP(hipMemcpyAsync(r->host, r->stats, RS_ZERO_WORDS * 8, hipMemcpyDeviceToHost, st));
@@ -1675,6 +1865,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     uint32_t K = 0;                          // fragments on the serial path
     bool read_back = true;                   // the stats block still to be read back
     bool spec_done = false;                  // the speculative tail ran (see SpecTail)
+    bool in_place = false;                   // ... and reassembled every datagram in place
     const uint8_t *spec_out = r->out;        // the buffer it wrote to
     const uint64_t spec_cap = r->out_cap;
     memset(o, 0, sizeof(*o));
@@ -1690,7 +1881,9 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
             uint64_t ob0;
             memcpy(&ob0, r->host + 2 * UDPDK_RS_N, 8);
             const uint64_t c0 = reinterpret_cast<const uint64_t *>(r->host)[UDPDK_RS_DONE];
-            spec_done = spec_out && grouped && hc[2] == 0u && c0 && ob0 + UDPDK_GPU_FRAMES_TAILROOM <= spec_cap;
+            const bool spec_grouped = (spec_out || inplace) && grouped && hc[2] == 0u && c0;
+            in_place = inplace && spec_grouped && hc[5] == 0u;
+            spec_done = in_place || (spec_out && spec_grouped && ob0 + UDPDK_GPU_FRAMES_TAILROOM <= spec_cap);
         }
         if (F && !grouped) {
             // group by key keeping arrival order: stable sorts by (id, index), then src|dst; the
@@ -1763,8 +1956,8 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         RS_HIP(hipGetLastError());
     }
     RS_HIP(hipStreamSynchronize(st));
-    o->batch.frames_dev = r->out;
-    o->batch.frames_bytes = Cn ? ob : 0;
+    o->batch.frames_dev = in_place ? bt->frames_dev : r->out;
+    o->batch.frames_bytes = in_place ? bt->frames_bytes : Cn ? ob : 0;
     o->batch.offset_dev = r->out_off;
     o->batch.length_dev = r->out_len;
     o->batch.ptype_dev = r->out_ptype;

@@ -1117,7 +1117,19 @@ int udpdk_gpu_rx_reassemble(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const 
     if (bt->frames_bytes >= (1ull << 32) || bt->n > c->max_frames) return -EINVAL;
     HIPC(c, hipSetDevice(c->device));
     { int r = join_pipes(c); if (r) return r; }
-    return reasm_run(c->reasm, c->stream, bt, meta_dev, tms, o, &c->last_err);
+    return reasm_run(c->reasm, c->stream, bt, meta_dev, tms, o, &c->last_err, false);
+}
+
+int udpdk_gpu_rx_reassemble_inplace(udpdk_gpu_ctx *c, udpdk_rx_batch_t *bt, const uint32_t *meta_dev,
+                                    uint64_t tms, udpdk_reasm_out_t *o)
+{
+    if (!c || !bt || !o) return -EINVAL;
+    if (!c->reasm) return -EINVAL;
+    if (bt->n && (!bt->frames_dev || !bt->offset_dev || !bt->length_dev || !meta_dev)) return -EINVAL;
+    if (bt->frames_bytes >= (1ull << 32) || bt->n > c->max_frames) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    { int r = join_pipes(c); if (r) return r; }
+    return reasm_run(c->reasm, c->stream, bt, meta_dev, tms, o, &c->last_err, true);
 }
 
 uint64_t udpdk_gpu_tx_span(uint32_t len, uint32_t mtu, uint32_t *n_frames)
