@@ -1411,17 +1411,26 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit_inplace(EmitArgs a, uint8
     constexpr uint32_t OOR = 0x80000000u;
     const uint32_t stride = gridDim.x * RS_WAVES;
     uint32_t k = blockIdx.x * RS_WAVES + w;
-    // the next datagram's record is loaded while this one moves (as in reasm_emit)
-    ReasmDone rn{};
-    if (k < C) rn = a.done[a.perm[k]];
-    for (; k < C; k += stride) {
-        const ReasmDone r = rn;
-        if (k + stride < C) rn = a.done[a.perm[k + stride]];
-        uint32_t sl[RS_MAX_FRAG];
-        const uint32_t m = data_order(r, sl);
-        uint32_t fo[RS_MAX_FRAG];
+    // Software pipeline over the wave's datagrams: the next datagram's fragment offsets (which
+    // need its record) are loaded while this one moves, and the record after it is loaded then.
+    auto offsets = [&](const ReasmDone &x, uint32_t (&o)[RS_MAX_FRAG], uint32_t (&sx)[RS_MAX_FRAG]) -> uint32_t {
+        const uint32_t mx = data_order(x, sx);
 #pragma unroll
-        for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) fo[f] = f < m ? a.offset[pick4(r.where, sl[f])] : 0u;
+        for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) o[f] = f < mx ? a.offset[pick4(x.where, sx[f])] : 0u;
+        return mx;
+    };
+    ReasmDone r{}, rn{};
+    uint32_t fo[RS_MAX_FRAG] = {0, 0, 0, 0}, sl[RS_MAX_FRAG] = {0, 0, 0, 0}, m = 0;
+    if (k < C) {
+        r = a.done[a.perm[k]];
+        m = offsets(r, fo, sl);
+    }
+    if (k + stride < C) rn = a.done[a.perm[k + stride]];
+    for (; k < C; k += stride) {
+        uint32_t fon[RS_MAX_FRAG] = {0, 0, 0, 0}, sln[RS_MAX_FRAG] = {0, 0, 0, 0}, mn = 0;
+        ReasmDone rnn{};
+        if (k + stride < C) mn = offsets(rn, fon, sln);
+        if (k + 2u * stride < C) rnn = a.done[a.perm[k + 2u * stride]];
         const uint32_t o0 = fo[0];
         // header bytes 14..33: six dwords from the one at or below, lane 0 (issued with the first
         // fragment's chunk loads; the moves never touch them)
@@ -1499,6 +1508,11 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit_inplace(EmitArgs a, uint8
             a.out_ptype[k] = 0x211u;
             a.out_origin[k] = r.origin;
         }
+        r = rn;
+        rn = rnn;
+        m = mn;
+#pragma unroll
+        for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) { fo[f] = fon[f]; sl[f] = sln[f]; }
     }
 }
 
