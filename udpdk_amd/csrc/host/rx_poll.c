@@ -187,8 +187,12 @@ static int h_frag_pass(const udpdk_rx_batch_t *staged, const uint32_t *meta_dev,
         if ((rc = udpdk_gpu_frag_table_create(g, &fc))) { errno = -rc; return -1; }
         g_udpdk.frag_ready = 1;
     }
+    /* the staged frames are the library's device copy of the burst and the FRAG frames' bytes
+     * are not read again after this pass: datagrams whose fragments arrived back to back are
+     * closed up in that buffer instead of copied (udpdk_gpu_rx_reassemble_inplace) */
     udpdk_reasm_out_t ro;
-    if ((rc = udpdk_gpu_rx_reassemble(g, staged, meta_dev, h_now_ms(), &ro))) { errno = -rc; return -1; }
+    udpdk_rx_batch_t sb = *staged;
+    if ((rc = udpdk_gpu_rx_reassemble_inplace(g, &sb, meta_dev, h_now_ms(), &ro))) { errno = -rc; return -1; }
     const uint32_t C = ro.batch.n;
     if (!C) return 0;
     const uint64_t cap64 = (uint64_t)C * maxfan;
