@@ -105,6 +105,9 @@ struct RxArgs {
 #define UDPDK_SPEC_COMPACT 1
 #endif
 #define UDPDK_SPEC_WORDS 64u                 // flag words of the speculative compaction
+#ifndef UDPDK_COMPACT1_SPEC_GRID
+#define UDPDK_COMPACT1_SPEC_GRID 256u        // rx_compact1 workgroups after a speculative classify
+#endif
 
 struct ScanArgs {
     uint32_t *hist;

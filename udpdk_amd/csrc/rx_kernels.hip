@@ -762,21 +762,19 @@ rx_classify(RxArgs a)
 
 // ------------------------------------------------------------------------------------------
 // rx_compact1: the single-lane batch's lane (no fan-out: every delivery is a whole frame).
-// Workgroup = tile. Each wave ballots its quarter of the tile's verdict words (delivered =
+// Workgroup = tile (grid-stride over the tiles after the first flagged one when rx_classify
+// wrote speculative entries). Each wave ballots its quarter of the tile's verdict words (delivered =
 // verdict 0) into LDS masks, the tile's base is the sum of the predecessors' delivery counts
 // (<= n_tiles words, read straight from the classify kernel's per-tile histogram: no scan
 // kernel and no cross-workgroup waits), then every delivered frame writes its index.
 // The last tile's workgroup writes lane_off[1] = total.
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(RX_BLOCK)
-rx_compact1(Compact1Args a)
+__device__ __forceinline__ void compact1_tile(const Compact1Args &a, uint32_t tile, uint32_t steps,
+                                              uint32_t tid, uint32_t lane, uint32_t w)
 {
     constexpr uint32_t MAXS = RX_TILE_MAX / RX_BLOCK;      // steps per wave, <= 64
     __shared__ unsigned long long msk[RX_WAVES][MAXS];
     __shared__ uint32_t red[2 * RX_WAVES];
-    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    const uint32_t tile = blockIdx.x;
-    const uint32_t steps = a.tile_frames / RX_BLOCK;
     const uint32_t t1 = min(a.n, (tile + 1) * a.tile_frames);
     const uint32_t wb = tile * a.tile_frames + w * steps * 64;
     const uint32_t plast = a.n - 1u;
@@ -784,25 +782,6 @@ rx_compact1(Compact1Args a)
     // are in flight together with the verdict words: one memory round trip for both
     const uint32_t tl = a.n_tiles - 1u;
     const uint32_t c0 = a.tile_count[min(tid, tl)], c1 = a.tile_count[min(tid + RX_BLOCK, tl)];
-    if (a.spec) {
-        // rx_classify placed this tile's entries at tile x tile_frames + rank: right when every
-        // earlier tile delivered all its frames, i.e. no tile before this one is in the flag
-        // every wave reads the 64 words (one load per lane) and takes the smallest flagged tile
-        const unsigned long long nf = __hip_atomic_load(&a.spec_nonfull[lane % UDPDK_SPEC_WORDS], __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t first = (uint32_t)(nf >> 32) == a.spec_epoch ? 0xFFFFFFFFu - (uint32_t)nf : 0xFFFFFFFFu;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) first = min(first, (uint32_t)__shfl_xor((int)first, d, 64));
-        if (tile <= first) {
-            if (tile == tl && tid == 0) {
-                const uint32_t total = tile * a.tile_frames + a.tile_count[tile];
-                a.lane_off[0] = 0u;
-                a.lane_off[1] = total;
-                *a.total = total;
-            }
-            return;
-        }
-    }
     uint32_t wcount = 0;
     for (uint32_t s0 = 0; s0 < steps; s0 += 4) {
         uint32_t mv[4];
@@ -848,6 +827,41 @@ rx_compact1(Compact1Args a)
             if (pos < a.lane_cap) a.lane_pkt[pos] = wb + s * 64 + lane;
         }
         run += (uint32_t)__popcll(m);
+    }
+}
+
+__global__ void __launch_bounds__(RX_BLOCK)
+rx_compact1(Compact1Args a)
+{
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const uint32_t steps = a.tile_frames / RX_BLOCK;
+    const uint32_t tl = a.n_tiles - 1u;
+    // speculative entries: rx_classify placed every tile's entries at tile x tile_frames + rank,
+    // right when every earlier tile delivered all its frames, i.e. up to and including the call's
+    // first flagged tile. Every wave reads the 64 flag words (one load per lane) and takes the
+    // smallest flagged tile; only the tiles after it are rewritten (grid-stride: the launch is
+    // small, so the common all-full call costs one flag read and the total's store).
+    uint32_t t_first = blockIdx.x;
+    if (a.spec) {
+        const unsigned long long nf = __hip_atomic_load(&a.spec_nonfull[lane % UDPDK_SPEC_WORDS], __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t first = (uint32_t)(nf >> 32) == a.spec_epoch ? 0xFFFFFFFFu - (uint32_t)nf : 0xFFFFFFFFu;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) first = min(first, (uint32_t)__shfl_xor((int)first, d, 64));
+        if (first >= tl) {
+            if (blockIdx.x == 0 && tid == 0) {
+                const uint32_t total = tl * a.tile_frames + a.tile_count[tl];
+                a.lane_off[0] = 0u;
+                a.lane_off[1] = total;
+                *a.total = total;
+            }
+            return;
+        }
+        t_first = first + 1u + blockIdx.x;
+    }
+    for (uint32_t tile = t_first; tile < a.n_tiles; tile += gridDim.x) {
+        compact1_tile(a, tile, steps, tid, lane, w);
+        __syncthreads();                       // msk / red reused by the next tile
     }
 }
 
