@@ -59,6 +59,8 @@ int udpdk_bind(int s, const struct sockaddr *addr, socklen_t addrlen);
 ssize_t udpdk_sendto(int sockfd, const void *buf, size_t len, int flags,
                      const struct sockaddr *dest_addr, socklen_t addrlen);
 
+/* One reading thread per socket at a time: the socket's receive ring is single-consumer, like
+ * the reference's SP/SC rx_q (udpdk_init.c:270-272). */
 ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
                        struct sockaddr *src_addr, socklen_t *addrlen);
 

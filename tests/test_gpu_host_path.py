@@ -59,3 +59,51 @@ def test_poll_rx_delivers_reassembled_datagrams_in_order(tmp_path, host_api, thr
                 assert addr == ("10.9.8.7", 4000)
     finally:
         L.udpdk_cleanup()
+
+
+def test_poll_rx_inplace_reassembly_keeps_aliased_frames(tmp_path, host_api):
+    """A burst whose fragments sit back to back (in-place reassembly would close the datagram up
+    in the staged buffer) and a direct frame whose descriptor aliases the second fragment's data:
+    udpdk_poll_rx only reassembles in place when the burst's frames are disjoint, so the aliased
+    frame's payload is delivered as it was received, next to the reassembled datagram.
+    A disjoint burst of the same fragments takes the in-place pass and delivers the same."""
+    ini = tmp_path / "udpdk.ini"
+    ini.write_text("[port0]\nmac_addr = 68:05:ca:95:f8:ec\nip_addr = 172.31.100.1\n"
+                   "[port0_dst]\nmac_addr = 68:05:ca:95:fa:64\n"
+                   "[gpu]\ndevice = 0\nmax_frames = 65536\nmax_lanes = 16\n"
+                   "frag_buckets = 16\nfrag_bucket_entries = 16\nfrag_max_dgram = 16384\n")
+    L = abi.lib()
+    argv = (C.c_char_p * 4)(b"prog", b"-c", str(ini).encode(), None)
+    assert L.udpdk_init(3, argv) == 0
+    try:
+        s0, s1 = host_api.socket(), host_api.socket()
+        assert host_api.bind(s0, "0.0.0.0", 10001) == 0
+        assert host_api.bind(s1, "0.0.0.0", 10002) == 0
+        src, dst = raw_ip("10.9.8.7"), raw_ip("172.31.100.1")
+
+        def plain(port, payload, pid):
+            return ip_frame(src, dst, pid, 0, udp_datagram(_port(4000), _port(port), payload), False)
+        for aliased in (True, False):
+            inner = plain(10002, bytes(range(40, 100)), 9)          # a whole frame, 102 B
+            pay = bytes([0x5A]) * 1500 + inner + bytes([0xA5]) * 1500
+            d1 = udp_datagram(_port(4000), _port(10001), pay)
+            f1 = split(src, dst, 77 + aliased, d1, [1480, 1480, len(d1) - 2960])
+            frames = [plain(10001, b"A" * 10, 1), f1[0], f1[1], f1[2]]
+            if not aliased:
+                frames.append(inner)
+            buf, off, ln = batch(frames)
+            if aliased:
+                # the inner frame inside fragment 1's data: datagram byte 8 + 1500 = 1508, i.e.
+                # 28 bytes into the fragment's data, which starts 34 bytes into its frame
+                off = np.append(off, np.uint32(off[2] + 34 + 28))
+                ln = np.append(ln, np.uint16(len(inner)))
+            st = abi.RxStats()
+            assert L.udpdk_poll_rx(buf.ctypes.data, len(buf) - 64, off.ctypes.data, ln.ctypes.data,
+                                   None, len(off), C.byref(st)) == 0
+            for s, want in ((s0, [b"A" * 10, d1[8:]]), (s1, [bytes(range(40, 100))])):
+                for w in want:
+                    n, data, addr = host_api.recvfrom(s, 8192)
+                    assert n == len(w) and data == w, (aliased, s, n)
+                    assert addr == ("10.9.8.7", 4000)
+    finally:
+        L.udpdk_cleanup()

@@ -56,9 +56,12 @@ struct h_ring {                  /* SP/SC ring of EXCH_RING_SIZE entries (udpdk_
      * per run of a slab's entries instead of one per recvfrom) */
     struct h_arena *rel_arena;
     uint32_t rel_n;
-    /* close vs a recvfrom blocked on another thread: recvfrom raises busy for its whole call and
-     * leaves with EBADF once closing is set; close sets closing and waits for busy to drop before
-     * it clears the ring (both seq_cst, so one of the two sees the other) */
+    /* close vs a recvfrom blocked on another thread: recvfrom counts itself in busy for its whole
+     * call and leaves with EBADF once closing is set; close sets closing and waits for busy to
+     * reach 0 before it clears the ring (both seq_cst, so one of the two sees the other). busy
+     * is a count, so close also waits for every one of several callers; the ring itself stays
+     * single-consumer like the reference's SP/SC rx_q (udpdk_init.c:270-272): one reading thread
+     * per socket at a time. */
     atomic_int busy;
     atomic_int closing;
 };

@@ -174,8 +174,25 @@ static uint64_t h_now_ms(void)
  * datagrams through the demux. Out: *rb = the reassembled batch (device, valid until the next
  * reassembly call), fr_loff[lanes + 1] / fr_lpkt[] its lanes (host), fr_org[] each datagram's
  * completing fragment index, fr_len[] its frame length. *nf = 0 when nothing completed. */
+/* Whether the batch's in-range frames are disjoint and in ascending buffer order (each frame ends
+ * at or before the next one starts): the precondition of udpdk_gpu_rx_reassemble_inplace, which
+ * moves fragment bytes inside the buffer that the direct frames are later gathered from. A caller
+ * whose descriptors alias (overlapping or repeated offsets, a frame inside another) keeps the
+ * copying reassembly. Out-of-range descriptors are BAD_DESC and never read. */
+static int h_desc_disjoint(const uint32_t *offset, const uint16_t *length, uint32_t n, uint64_t frames_bytes)
+{
+    uint64_t end = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t o = offset[i], l = length[i];
+        if (l > frames_bytes || o > frames_bytes - l) continue;
+        if (o < end) return 0;
+        end = o + l;
+    }
+    return 1;
+}
+
 static int h_frag_pass(const udpdk_rx_batch_t *staged, const uint32_t *meta_dev, uint64_t nfrag,
-                       uint32_t lanes, uint32_t maxfan, udpdk_rx_batch_t *rb, uint32_t *nd)
+                       uint32_t lanes, uint32_t maxfan, int inplace, udpdk_rx_batch_t *rb, uint32_t *nd)
 {
     *nd = 0;
     if (!nfrag) return 0;                   /* the batch's FRAG verdict count (RX counters) */
@@ -188,11 +205,15 @@ static int h_frag_pass(const udpdk_rx_batch_t *staged, const uint32_t *meta_dev,
         g_udpdk.frag_ready = 1;
     }
     /* the staged frames are the library's device copy of the burst and the FRAG frames' bytes
-     * are not read again after this pass: datagrams whose fragments arrived back to back are
-     * closed up in that buffer instead of copied (udpdk_gpu_rx_reassemble_inplace) */
+     * are not read again after this pass: when the burst's frames are disjoint (inplace),
+     * datagrams whose fragments arrived back to back are closed up in that buffer instead of
+     * copied (udpdk_gpu_rx_reassemble_inplace); otherwise a moved fragment could overwrite bytes
+     * another descriptor still delivers, and the pass copies */
     udpdk_reasm_out_t ro;
     udpdk_rx_batch_t sb = *staged;
-    if ((rc = udpdk_gpu_rx_reassemble_inplace(g, &sb, meta_dev, h_now_ms(), &ro))) { errno = -rc; return -1; }
+    rc = inplace ? udpdk_gpu_rx_reassemble_inplace(g, &sb, meta_dev, h_now_ms(), &ro)
+                 : udpdk_gpu_rx_reassemble(g, &sb, meta_dev, h_now_ms(), &ro);
+    if (rc) { errno = -rc; return -1; }
     const uint32_t C = ro.batch.n;
     if (!C) return 0;
     const uint64_t cap64 = (uint64_t)C * maxfan;
@@ -604,6 +625,21 @@ static int h_rss_assign(const struct h_sjob *J, uint32_t n)
     return 0;
 }
 
+/* The lanes a shard's device returned, checked before any of them is used as a host index (the
+ * merge indexes S->lpkt / S->idx with them and writes the poll's lane array): offsets from 0,
+ * non-decreasing, the total within the shard's entry buffer, every entry a frame of the shard. */
+static int h_shard_lanes_ok(const struct h_shard *S, uint32_t lanes, uint64_t cap)
+{
+    if (S->loff[0] != 0u) return 0;
+    for (uint32_t l = 0; l < lanes; l++)
+        if (S->loff[l] > S->loff[l + 1]) return 0;
+    const uint32_t D = S->loff[lanes];
+    if (D > cap) return 0;
+    for (uint32_t e = 0; e < D; e++)
+        if (S->lpkt[e] >= S->n) return 0;
+    return 1;
+}
+
 /* Shard k's RX on its own context: descriptors rebased to the 16-byte-aligned start of the frame
  * bytes the shard spans (a descriptor outside the caller's frames keeps pointing outside the
  * shard's, so it stays BAD_DESC), then udpdk_gpu_rx_host (H2D, kernels, D2H of its lanes). */
@@ -651,6 +687,7 @@ static void h_shard_rx(const struct h_sjob *J, struct h_shard *S)
                                          S->meta, S->loff, S->lpkt, cap > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)cap,
                                          &S->st);
         if (rc) S->err = -rc;
+        else if (!h_shard_lanes_ok(S, lanes, cap)) S->err = EIO;
         return;
     }
     uint64_t lo = UINT64_MAX, hi = 0;
@@ -679,6 +716,7 @@ static void h_shard_rx(const struct h_sjob *J, struct h_shard *S)
                                      J->ptype ? J->ptype + S->i0 : NULL, S->n, S->meta, S->loff, S->lpkt,
                                      cap > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)cap, &S->st);
     if (rc) S->err = -rc;
+    else if (!h_shard_lanes_ok(S, lanes, cap)) S->err = EIO;
 }
 
 static void h_shard_rx_job(void *ctx, uint32_t part, uint32_t parts)
@@ -940,12 +978,15 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
         /* every shard's FRAG frames, in arrival order, through the main context's table */
         udpdk_rx_batch_t fsub;
         const uint32_t *fmeta = NULL;
+        /* (the sub-batch packs the FRAG frames back to back: disjoint, and the direct frames
+         * are gathered from the shards' own staging) */
         if (h_frag_subbatch(&J, meta, n, nfrag, maxfan, &fsub, &fmeta) ||
-            h_frag_pass(&fsub, fmeta, nfrag, lanes, maxfan, &rb, &nd))
+            h_frag_pass(&fsub, fmeta, nfrag, lanes, maxfan, 1, &rb, &nd))
             goto out;
         for (uint32_t d = 0; d < nd; d++) g_udpdk.fr_org[d] = g_udpdk.fb_idx[g_udpdk.fr_org[d]];
     } else if (!sharded) {
-        if (h_frag_pass(&staged, meta_dev, nfrag, lanes, maxfan, &rb, &nd)) goto out;
+        const int inplace = nfrag && h_desc_disjoint(offset, length, n, frames_bytes);
+        if (h_frag_pass(&staged, meta_dev, nfrag, lanes, maxfan, inplace, &rb, &nd)) goto out;
     }
     PROF_T(p3);
     const uint32_t *floff = nd ? g_udpdk.fr_loff : NULL, *flpkt = g_udpdk.fr_lpkt, *forg = g_udpdk.fr_org;

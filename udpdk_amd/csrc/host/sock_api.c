@@ -429,9 +429,9 @@ ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
     if (flags != 0) { errno = EINVAL; return -1; }
     if (buf == NULL && addrlen != NULL) { errno = EINVAL; return -1; }
     struct h_ring *r = &g_udpdk.slots[s].rx;
-    atomic_store(&r->busy, 1);                 /* seq_cst: see udpdk_close */
+    atomic_fetch_add(&r->busy, 1);             /* seq_cst: see udpdk_close */
     if (atomic_load(&r->closing) || !g_udpdk.slots[s].used) {
-        atomic_store_explicit(&r->busy, 0, memory_order_release);
+        atomic_fetch_sub_explicit(&r->busy, 1, memory_order_release);
         errno = EBADF;
         return -1;
     }
@@ -440,7 +440,7 @@ ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
     while (atomic_load_explicit(&r->tail, memory_order_acquire) == h) {
         const int intr = atomic_load_explicit(&g_udpdk.interrupted, memory_order_relaxed);
         if (intr || atomic_load_explicit(&r->closing, memory_order_relaxed)) {
-            atomic_store_explicit(&r->busy, 0, memory_order_release);
+            atomic_fetch_sub_explicit(&r->busy, 1, memory_order_release);
             errno = intr ? EINTR : EBADF;
             return -1;
         }
@@ -476,7 +476,7 @@ ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
         r->rel_arena = NULL;
         r->rel_n = 0;
     }
-    atomic_store_explicit(&r->busy, 0, memory_order_release);
+    atomic_fetch_sub_explicit(&r->busy, 1, memory_order_release);
     return (ssize_t)n;
 }
 
