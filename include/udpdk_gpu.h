@@ -42,8 +42,9 @@ extern "C" {
 #endif
 
 /* 2: udpdk_reasm_out_t stats grew to UDPDK_RS_N = 11 (RS_SERIAL, RS_SORTED);
- *    udpdk_gpu_rx_gather_packed; TX payloads need UDPDK_GPU_FRAMES_TAILROOM readable bytes */
-#define UDPDK_GPU_ABI_VERSION 2
+ *    udpdk_gpu_rx_gather_packed; TX payloads need UDPDK_GPU_FRAMES_TAILROOM readable bytes
+ * 3: udpdk_frag_table_cfg_t grew max_entries (the table's LRU limit) and flags (32 bytes) */
+#define UDPDK_GPU_ABI_VERSION 3
 
 /* ---------------------------------------------------------------------------------------------
  * Per-frame verdict word (one uint32 per frame, written by udpdk_gpu_rx)
@@ -301,7 +302,19 @@ typedef struct {
                                  MAX_FLOW_TTL = 1 s of TSC cycles in the reference)              */
     uint32_t max_dgram;       /* IPv4 payload bytes one flow can hold, <= 65515; device memory is
                                  about entries x (max_dgram + 34) bytes                           */
+    uint32_t max_entries;     /* NUM_FLOWS_MAX = 65535 (udpdk_constants.h:34): ip_frag_find adds a
+                                 flow to a free entry only while fewer than max_entries are in
+                                 use; at the limit it deletes the least recently added (or reused)
+                                 entry if that one has expired, else drops the fragment (no
+                                 space). 0: the table's entry count (the limit never applies).  */
+    uint32_t flags;           /* UDPDK_FRAG_CKSUM_DPDK                                          */
+    uint32_t reserved;        /* 0                                                              */
 } udpdk_frag_table_cfg_t;
+
+/* A reassembled datagram's IPv4 header checksum is left 0, as DPDK 20.05's ipv4_frag_reassemble
+ * writes it and the reference delivers it ("TODO must fix the IP header checksum",
+ * udpdk_poller.c:355-360), instead of the RFC 1071 value. */
+#define UDPDK_FRAG_CKSUM_DPDK 1u
 
 enum udpdk_rs_stat {
     UDPDK_RS_FRAGS      = 0, /* FRAG-verdict frames of the batch                                */

@@ -44,7 +44,7 @@ def lib() -> C.CDLL:
         L.oracle_tx_fragment.restype = C.c_uint32
         L.oracle_tx_fragment.argtypes = [P, C.c_uint32, C.c_uint32, P]
         L.oracle_ftable_new.restype = P
-        L.oracle_ftable_new.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32]
+        L.oracle_ftable_new.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
         L.oracle_ftable_free.argtypes = [P]
         L.oracle_frag_hash.restype = C.c_uint32
         L.oracle_frag_hash.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
@@ -192,8 +192,10 @@ class FragTable:
     """The poller's reassembly table (udpdk_poller.c:130 rte_ip_frag_table_create) restated:
     state persists across reassemble() calls like the reference's."""
 
-    def __init__(self, bucket_num=0x1000, bucket_entries=16, max_cycles=1000, max_dgram=65515):
-        self.h = C.c_void_p(lib().oracle_ftable_new(bucket_num, bucket_entries, max_cycles, max_dgram))
+    def __init__(self, bucket_num=0x1000, bucket_entries=16, max_cycles=1000, max_dgram=65515,
+                 max_entries=0, flags=0):
+        self.h = C.c_void_p(lib().oracle_ftable_new(bucket_num, bucket_entries, max_cycles, max_dgram,
+                                                    max_entries, flags))
         if not self.h:
             raise ValueError("bad table geometry")
         self.fed = 0          # bytes fed so far: bounds what held fragments can add to an output

@@ -89,8 +89,10 @@ enum oracle_rs_stat {
     ORACLE_RS_STORED,         /* fragments of this call still held by the table at its end      */
     ORACLE_RS_N
 };
+/* max_entries: rte_ip_frag_table_create's max_entries (0: the entry count); flags bit 0: the
+ * reassembled header checksum left 0 as DPDK writes it (UDPDK_FRAG_CKSUM_DPDK). */
 oracle_ftable *oracle_ftable_new(uint32_t bucket_num, uint32_t bucket_entries, uint64_t max_cycles,
-                                 uint32_t max_dgram);
+                                 uint32_t max_dgram, uint32_t max_entries, uint32_t flags);
 void           oracle_ftable_free(oracle_ftable *t);
 uint32_t       oracle_frag_hash(uint32_t src, uint32_t dst, uint32_t id, uint32_t *sig2);
 /* FRAG-verdict frames of one batch in arrival order; reassembled frames 16-byte aligned into

@@ -19,10 +19,14 @@
  *                (entries - 1) & ~(bucket_entries - 1), entries = align32pow2(buckets * assoc)
  *   lookup     = ip_frag_lookup: scan p1[i], p2[i] for i < assoc; a key match wins, else the
  *                first empty and the first expired (start + max_cycles < tms) slot are noted
- *   find       = ip_frag_find: match + expired -> free its fragments and restart it at tms;
- *                no match -> a stale slot is freed and used, else an empty one; none -> NULL
- *                (the fragment is dropped). The max_entries/LRU test is not modelled: with the
- *                reference's NUM_FLOWS_MAX = 65535 it needs 65535 of 65536 entries busy.
+ *   find       = ip_frag_find: match + expired -> free its fragments and restart it at tms
+ *                (ip_frag_tbl_reuse: the entry moves to the LRU list's tail); no match -> a
+ *                stale slot is freed and used, else an empty one, but an empty one only while
+ *                use_entries < max_entries: at the limit the LRU list's head (the entry added or
+ *                reused longest ago) is deleted if it has expired, else the fragment is dropped
+ *                (fail_nospace); no slot -> NULL (dropped). use_entries counts valid entries
+ *                (ip_frag_tbl_add / _del, ip_frag_inuse after a flow ends). The reference's table
+ *                has 4096 x 16 = 65536 entries and max_entries = NUM_FLOWS_MAX = 65535.
  *   process    = ip_frag_process: frag_size += len; ofs 0 -> slot 0 (dup -> error); MF clear ->
  *                total_size = ofs + len, slot 1 (dup -> error); else slot last_idx++ (< 4, else
  *                error). frag_size < total_size: wait; == with slot 0 present: reassemble
@@ -31,9 +35,9 @@
  *                a reassembly.
  *   output     = the first fragment's 34 header bytes + the fragments' IPv4 payloads at their
  *                offsets; total_length = total_size + 20, fragment_offset keeps DF only
- *                (ipv4_frag_reassemble), and the header checksum -- DPDK writes 0 and sets
- *                PKT_TX_IP_CKSUM ("TODO must fix the IP header checksum", poller.c:358) -- is
- *                written as the RFC 1071 value.
+ *                (ipv4_frag_reassemble), and the header checksum: DPDK writes 0 ("TODO must fix
+ *                the IP header checksum", poller.c:358), kept with the DPDK flag; by default the
+ *                RFC 1071 value is written.
  *
  * Divergences: l3_len is 20 as the poller sets it (poller.c:346); a fragment whose
  * IPv4 total_length reaches past its frame, or whose data would end past the table's datagram
@@ -62,13 +66,15 @@ struct of_entry {
     uint32_t src, dst, id;
     int      valid;               /* key_len != 0                                              */
     uint64_t start;
+    uint64_t lru;                 /* position in the LRU list: the table's add/reuse counter   */
     uint32_t frag_size, total_size, last_idx;
     struct of_frag frags[OF_MAX_FRAG];
 };
 
 struct oracle_ftable {
     uint32_t entries, assoc, mask, max_dgram;
-    uint64_t max_cycles;
+    uint32_t max_entries, use_entries, flags;
+    uint64_t max_cycles, lru_seq;
     struct of_entry *e;
 };
 
@@ -89,11 +95,13 @@ uint32_t oracle_frag_hash(uint32_t src, uint32_t dst, uint32_t id, uint32_t *sig
 }
 
 oracle_ftable *oracle_ftable_new(uint32_t bucket_num, uint32_t bucket_entries,
-                                 uint64_t max_cycles, uint32_t max_dgram)
+                                 uint64_t max_cycles, uint32_t max_dgram, uint32_t max_entries,
+                                 uint32_t flags)
 {
     uint64_t n = (uint64_t)bucket_num * bucket_entries, p = 1;
     while (p < n) p <<= 1;
     if (!bucket_entries || (bucket_entries & (bucket_entries - 1)) || p > (1u << 24)) return NULL;
+    if (max_entries > p) return NULL;                /* rte_ip_frag_table_create: EINVAL */
     oracle_ftable *t = calloc(1, sizeof(*t));
     if (!t) return NULL;
     t->entries = (uint32_t)p;
@@ -101,6 +109,8 @@ oracle_ftable *oracle_ftable_new(uint32_t bucket_num, uint32_t bucket_entries,
     t->mask = (t->entries - 1) & ~(bucket_entries - 1);
     t->max_cycles = max_cycles;
     t->max_dgram = max_dgram;
+    t->max_entries = max_entries ? max_entries : t->entries;
+    t->flags = flags;
     t->e = calloc(t->entries, sizeof(struct of_entry));
     if (!t->e) { free(t); return NULL; }
     return t;
@@ -136,6 +146,22 @@ static int of_expired(const oracle_ftable *t, const struct of_entry *e, uint64_t
     return t->max_cycles + e->start < tms;
 }
 
+static void of_del(oracle_ftable *t, struct of_entry *e)      /* ip_frag_tbl_del / ip_frag_inuse */
+{
+    of_free_frags(e);
+    e->valid = 0;
+    t->use_entries--;
+}
+
+/* TAILQ_FIRST(&tbl->lru): the valid entry added or reused longest ago. */
+static struct of_entry *of_lru_head(oracle_ftable *t)
+{
+    struct of_entry *h = NULL;
+    for (uint32_t i = 0; i < t->entries; ++i)
+        if (t->e[i].valid && (!h || t->e[i].lru < h->lru)) h = &t->e[i];
+    return h;
+}
+
 /* ip_frag_find (ip_frag_lookup inlined). */
 static struct of_entry *of_find(oracle_ftable *t, uint32_t src, uint32_t dst, uint32_t id,
                                 uint64_t tms, uint64_t *st)
@@ -152,6 +178,7 @@ static struct of_entry *of_find(oracle_ftable *t, uint32_t src, uint32_t dst, ui
                     st[ORACLE_RS_EXPIRED]++;
                     of_free_frags(q);
                     of_reset(q, tms);
+                    q->lru = t->lru_seq++;
                 }
                 return q;
             }
@@ -162,9 +189,15 @@ static struct of_entry *of_find(oracle_ftable *t, uint32_t src, uint32_t dst, ui
     struct of_entry *use = NULL;
     if (old) {                                               /* ip_frag_tbl_del */
         st[ORACLE_RS_EXPIRED]++;
-        of_free_frags(old);
-        old->valid = 0;
+        of_del(t, old);
         use = old;
+    } else if (empty && t->use_entries >= t->max_entries) {
+        struct of_entry *lru = of_lru_head(t);
+        if (lru && of_expired(t, lru, tms)) {                /* the LRU head has expired */
+            st[ORACLE_RS_EXPIRED]++;
+            of_del(t, lru);
+            use = empty;
+        }                                                    /* else fail_nospace */
     } else {
         use = empty;
     }
@@ -172,6 +205,8 @@ static struct of_entry *of_find(oracle_ftable *t, uint32_t src, uint32_t dst, ui
     use->valid = 1;                                          /* ip_frag_tbl_add */
     use->src = src; use->dst = dst; use->id = id;
     of_reset(use, tms);
+    use->lru = t->lru_seq++;
+    t->use_entries++;
     return use;
 }
 
@@ -248,8 +283,7 @@ int64_t oracle_reassemble(oracle_ftable *t, const uint8_t *frames, uint64_t fram
         }
         if (idx >= OF_MAX_FRAG) {
             stats[ORACLE_RS_ERRORS]++;
-            of_free_frags(e);
-            e->valid = 0;
+            of_del(t, e);
             continue;
         }
         struct of_frag *s = &e->frags[idx];
@@ -271,8 +305,10 @@ int64_t oracle_reassemble(oracle_ftable *t, const uint8_t *frames, uint64_t fram
             o[16] = (uint8_t)(tl >> 8); o[17] = (uint8_t)tl;
             o[20] &= 0x40u; o[21] = 0;                       /* DF only */
             o[24] = o[25] = 0;
-            const uint16_t ck = of_ipcksum(o + 14);
-            memcpy(o + 24, &ck, 2);
+            if (!(t->flags & 1u)) {                          /* else DPDK's 0 (poller.c:358) */
+                const uint16_t ck = of_ipcksum(o + 14);
+                memcpy(o + 24, &ck, 2);
+            }
             for (uint32_t k = 0; k < e->last_idx; ++k)
                 if (e->frags[k].data) memcpy(o + 34 + e->frags[k].ofs, e->frags[k].data, e->frags[k].len);
             out_off[n_out] = (uint32_t)at;
@@ -285,8 +321,7 @@ int64_t oracle_reassemble(oracle_ftable *t, const uint8_t *frames, uint64_t fram
             const int sized = e->frag_size == e->total_size && e->frags[OF_FIRST].data;
             stats[sized ? ORACLE_RS_HOLES : ORACLE_RS_ERRORS]++;
         }
-        of_free_frags(e);
-        e->valid = 0;
+        of_del(t, e);
     }
     for (uint32_t i = 0; i < t->entries; ++i)
         if (t->e[i].valid)

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_geometry():
-    assert abi.lib().udpdk_gpu_abi_version() == 2
+    assert abi.lib().udpdk_gpu_abi_version() == 3
     # tile geometry policy: lanes x tiles bounded, tiles >= 1
     assert abi.geometry(1 << 20, 1) == (1024, 1024)
     assert abi.geometry(1 << 20, 1024) == (1024, 1024)

@@ -156,12 +156,14 @@ def test_reassembly_contention_exact(gpu_ctx, seed, buckets, entries):
         assert tot[k] > 0, (k, tot)
 
 
-def test_reassembly_in_order_is_parallel(gpu_ctx):
+@pytest.mark.parametrize("max_entries", [0, 0xFFFF])
+def test_reassembly_in_order_is_parallel(gpu_ctx, max_entries):
     """Datagrams whose fragments arrive back to back (frames.frag_batch, the bench's workload) never
-    meet another flow in the table: no fragment takes the serial path."""
+    meet another flow in the table: no fragment takes the serial path, also under the reference's
+    max_entries = NUM_FLOWS_MAX (the bound on the entries a grouped batch holds stays far below)."""
     from udpdk_amd import frames as FR
     b = FR.frag_batch(4096, 2952)
-    abi.frag_table_create(gpu_ctx, 0x1000, 16, 1 << 40, 65515)
+    abi.frag_table_create(gpu_ctx, 0x1000, 16, 1 << 40, 65515, max_entries=max_entries)
     db = abi.rx_upload(gpu_ctx, b.frames, b.offset, b.length)
     db.frames_bytes = b.frames_bytes
     out = abi.rx_alloc_out(gpu_ctx, b.n, 1, b.n)
@@ -260,6 +262,10 @@ def test_reassembly_edges(gpu_ctx):
     assert abi.lib().udpdk_gpu_frag_table_create(gpu_ctx.handle, C.byref(bad)) == -22
     bad = abi.FragTableCfg(16, 16, 100, 70000)                # max_dgram past IPv4
     assert abi.lib().udpdk_gpu_frag_table_create(gpu_ctx.handle, C.byref(bad)) == -22
+    bad = abi.FragTableCfg(16, 16, 100, 4096, 257)            # max_entries past the 256 entries
+    assert abi.lib().udpdk_gpu_frag_table_create(gpu_ctx.handle, C.byref(bad)) == -22
+    bad = abi.FragTableCfg(16, 16, 100, 4096, 0, 2)           # unknown flag
+    assert abi.lib().udpdk_gpu_frag_table_create(gpu_ctx.handle, C.byref(bad)) == -22
     abi.frag_table_create(gpu_ctx, 16, 16, 100, 4096)
     frames = [ip_frame(raw_ip("10.0.0.1"), raw_ip("172.31.100.1"), 1, 0, udp_datagram(1, 2, b"x" * 40), False)]
     buf, off, ln = batch(frames)
@@ -271,3 +277,91 @@ def test_reassembly_edges(gpu_ctx):
     db.n = 0
     rb, _, st = abi.rx_reassemble(gpu_ctx, db, meta, 0)
     assert rb.n == 0 and sum(st.values()) == 0
+
+
+@pytest.mark.parametrize("seed,buckets,entries,max_entries,grouped",
+                         [(31, 256, 16, 24, False), (32, 64, 4, 40, True), (33, 16, 4, 60, False),
+                          (35, 256, 16, 8, True), (34, 256, 16, 4095, True)])
+def test_reassembly_max_entries_exact(gpu_ctx, seed, buckets, entries, max_entries, grouped):
+    """rte_ip_frag_table_create's max_entries (NUM_FLOWS_MAX, udpdk_poller.c:130-131): at the limit
+    ip_frag_find deletes the LRU entry when it has expired and otherwise drops the fragment. Limits
+    far below the table size over multi-batch scenarios with expiry: every datagram, origin and
+    count equals the oracle's; a limit the batches cannot reach keeps the parallel path."""
+    tot = _check_scenario(gpu_ctx, scenario(seed, n_batches=6, flows_per_batch=90, dt=12, grouped=grouped),
+                          dict(bucket_num=buckets, bucket_entries=entries, max_cycles=20,
+                               max_entries=max_entries))
+    assert tot["done"] > 0, tot
+    if max_entries < 100:
+        assert tot["no_space"] > 0 and tot["expired"] > 0, tot
+    else:
+        assert tot["serial"] < tot["frags"], tot
+
+
+def test_reassembly_lru_rule_exact(gpu_ctx):
+    """The oracle's hand-derived max_entries sequence (tests/test_reasm_oracle.py) on the GPU: a
+    fourth flow finds no space while the oldest entry is alive, takes a slot once it has expired
+    (the LRU deletion, not a stale slot of its own buckets), and later flows see the count."""
+    from reasm_util import split, udp_datagram, raw_ip
+    src, dst = raw_ip("172.31.100.2"), raw_ip("172.31.100.1")
+
+    def bk(pid):
+        mask = (64 * 4 - 1) & ~3
+        s1, s2 = O.frag_hash(src, dst, pid)
+        return {(s1 & mask) // 4, (s2 & mask) // 4}
+    used = bk(21) | bk(22) | bk(23)
+    d = next(p for p in range(100, 10000) if not (bk(p) & used))
+    geo = dict(bucket_num=64, bucket_entries=4, max_cycles=10, max_dgram=256, max_entries=3)
+    abi.frag_table_create(gpu_ctx, **geo)
+    t = O.FragTable(**geo)
+    dg = udp_datagram(1, 2, b"q" * 24)
+    fa, fb, fc, fd = (split(src, dst, p, dg, [16, 16]) for p in (21, 22, 23, d))
+    steps = [([fa[0]], 0), ([fb[0], fc[0]], 5), ([fd[0]], 9), ([fd[0]], 11), ([fb[1], fa[1]], 12), ([fd[1]], 13)]
+    want_ns = [0, 0, 1, 0, 0, 0]
+    for (frames, tms), ns in zip(steps, want_ns):
+        buf, off, ln = batch(frames)
+        db = abi.rx_upload(gpu_ctx, buf, off, ln)
+        db.frames_bytes = len(buf) - 64
+        meta = O.rx(O.BindTable(), buf, len(buf) - 64, off, ln, None, 1)[0]
+        mb = gpu_ctx.upload(meta)
+        rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, mb, tms)
+        _, woo, _, _, wst = t.reassemble(buf, off, ln, meta, tms)
+        gst.pop("serial")
+        gst.pop("sorted")
+        assert gst == wst and rb.n == len(woo), (tms, gst, wst)
+        assert gst["no_space"] == ns, (tms, gst)
+        for bb in (db.frames, db.offset, db.length, mb):
+            bb.free()
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_reassembly_dpdk_checksum(gpu_ctx, inplace):
+    """UDPDK_FRAG_CKSUM_DPDK ([gpu] reasm_cksum = dpdk): the reassembled header's checksum is 0 as
+    DPDK's ipv4_frag_reassemble leaves it (udpdk_poller.c:355-360), through the copying and the
+    in-place emit; the datagrams equal the oracle's in the same mode, and their demux reports the
+    IPv4 checksum bad (verdict bit 4 clear) as the reference's bytes would give."""
+    from udpdk_amd import frames as FR
+    b = FR.frag_batch(500, 2952)
+    abi.frag_table_create(gpu_ctx, 0x1000, 16, 1 << 40, 65515, flags=abi.FRAG_CKSUM_DPDK)
+    t = O.FragTable(0x1000, 16, 1 << 40, 65515, flags=1)
+    gpu_ctx.upload_snapshot(abi.snapshot_from_lists({abi.raw_port(FR.PORT_RECV): [(0, 0, 0)]}, 4))
+    db = abi.rx_upload(gpu_ctx, b.frames, b.offset, b.length)
+    db.frames_bytes = b.frames_bytes
+    out = abi.rx_alloc_out(gpu_ctx, b.n, 4, 4 * b.n)
+    gm = abi.rx_run(gpu_ctx, db, out)[0]
+    rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, out.meta, 0, inplace=inplace)
+    wout, woo, wol, wog, wst = t.reassemble(b.frames, b.offset, b.length, gm, 0)
+    gst.pop("serial"), gst.pop("sorted")
+    assert gst == wst and gst["done"] == 500, (gst, wst)
+    assert (rb.frames.ptr == db.frames.ptr) == inplace
+    gbuf, goff, gln = _frames(gpu_ctx, rb)
+    for k in range(rb.n):
+        g = gbuf[goff[k]:goff[k] + gln[k]].tobytes()
+        assert g == wout[woo[k]:woo[k] + wol[k]].tobytes(), k
+        assert g[24:26] == b"\0\0"
+    out2 = abi.rx_alloc_out(gpu_ctx, rb.n, 4, 4 * rb.n)
+    g2 = abi.rx_run(gpu_ctx, rb, out2)
+    assert g2[4] == 0 and np.all(abi.meta_verdict(g2[0]) == 0)
+    assert not np.any(g2[0] & (1 << 4))                   # IPv4 checksum not ok
+    for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt, out2.meta,
+              out2.lane_off, out2.lane_pkt):
+        x.free()

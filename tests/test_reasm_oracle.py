@@ -157,3 +157,57 @@ def test_scenario_covers_every_outcome():
             tot[k] = tot.get(k, 0) + v
     for k in ("frags", "errors", "holes", "expired", "done", "stored"):
         assert tot[k] > 0, (k, tot)
+
+
+def _buckets(pid, bucket_num, assoc):
+    mask = (bucket_num * assoc - 1) & ~(assoc - 1)
+    s1, s2 = O.frag_hash(SRC, DST, pid)
+    return {(s1 & mask) // assoc, (s2 & mask) // assoc}
+
+
+def test_max_entries_lru_rule():
+    """ip_frag_find at use_entries == max_entries (DPDK 20.05, restated): a new flow with a free
+    slot in its buckets is added only after the LRU list's head (the entry added longest ago) is
+    deleted for having expired; otherwise the fragment is dropped (no space). Flow d is chosen
+    with buckets no other flow uses, so the stale-slot path cannot be what frees it a slot."""
+    B, A = 64, 4
+    a, b, c = 21, 22, 23
+    used = _buckets(a, B, A) | _buckets(b, B, A) | _buckets(c, B, A)
+    d = next(p for p in range(100, 10000) if not (_buckets(p, B, A) & used))
+    t = O.FragTable(bucket_num=B, bucket_entries=A, max_cycles=10, max_entries=3)
+    dg = udp_datagram(1, 2, b"q" * 24)                                 # 32 B: 2 fragments
+    fa, fb, fc, fd = (split(SRC, DST, p, dg, [16, 16]) for p in (a, b, c, d))
+    _, _, st = _run(t, [fa[0]], tms=0)
+    assert st["stored"] == 1
+    _, _, st = _run(t, [fb[0], fc[0]], tms=5)
+    assert st["stored"] == 2                                          # 3 entries in use
+    _, _, st = _run(t, [fd[0]], tms=9)                                # head a alive: no space
+    assert st["no_space"] == 1 and st["stored"] == 0
+    _, _, st = _run(t, [fd[0]], tms=11)                               # head a expired: deleted
+    assert st["expired"] == 1 and st["stored"] == 1 and st["no_space"] == 0
+    got, _, st = _run(t, [fb[1], fa[1]], tms=12)                      # b completes; a starts anew
+    assert len(got) == 1 and got[0][34:] == dg
+    assert st["done"] == 1 and st["stored"] == 1 and st["expired"] == 0
+    got, _, st = _run(t, [fd[1]], tms=13)
+    assert len(got) == 1 and st["done"] == 1
+    # without the limit (max_entries = 0: the entry count) the first fd[0] is simply stored
+    t2 = O.FragTable(bucket_num=B, bucket_entries=A, max_cycles=10)
+    _run(t2, [fa[0]], tms=0)
+    _run(t2, [fb[0], fc[0]], tms=5)
+    _, _, st = _run(t2, [fd[0]], tms=9)
+    assert st["stored"] == 1 and st["no_space"] == 0
+    with pytest.raises(ValueError):
+        O.FragTable(bucket_num=B, bucket_entries=A, max_entries=B * A + 1)
+
+
+def test_reassembled_checksum_dpdk_mode():
+    """flags = UDPDK_FRAG_CKSUM_DPDK: the header checksum is left 0 as ipv4_frag_reassemble writes
+    it (the reference's "TODO must fix the IP header checksum", udpdk_poller.c:355-360); every
+    other byte equals the default mode's output, whose checksum is the RFC 1071 value."""
+    dg = udp_datagram(1, 2, bytes(range(200)))
+    fr = split(SRC, DST, 31, dg, [104, 104])
+    g0, _, _ = _run(O.FragTable(), fr)
+    g1, _, _ = _run(O.FragTable(flags=1), fr)
+    assert len(g0) == len(g1) == 1
+    assert g1[0][24:26] == b"\0\0" and g0[0][24:26] != b"\0\0"
+    assert _same_but_cksum(g0[0], g1[0])

@@ -89,7 +89,11 @@ RS_STATS = ("frags", "drop_len", "drop_short", "no_space", "errors", "holes", "e
 
 class FragTableCfg(C.Structure):
     _fields_ = [("bucket_num", C.c_uint32), ("bucket_entries", C.c_uint32),
-                ("max_cycles", C.c_uint64), ("max_dgram", C.c_uint32)]
+                ("max_cycles", C.c_uint64), ("max_dgram", C.c_uint32), ("max_entries", C.c_uint32),
+                ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+FRAG_CKSUM_DPDK = 1       # UDPDK_FRAG_CKSUM_DPDK
 
 
 class ReasmOut(C.Structure):
@@ -512,8 +516,8 @@ class DevRef:
 
 
 def frag_table_create(ctx: GpuContext, bucket_num: int = 0x1000, bucket_entries: int = 16,
-                      max_cycles: int = 1000, max_dgram: int = 65515):
-    cfg = FragTableCfg(bucket_num, bucket_entries, max_cycles, max_dgram)
+                      max_cycles: int = 1000, max_dgram: int = 65515, max_entries: int = 0, flags: int = 0):
+    cfg = FragTableCfg(bucket_num, bucket_entries, max_cycles, max_dgram, max_entries, flags, 0)
     _check(lib().udpdk_gpu_frag_table_create(ctx.handle, C.byref(cfg)), "udpdk_gpu_frag_table_create")
 
 

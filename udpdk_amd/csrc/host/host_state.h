@@ -149,6 +149,7 @@ struct h_state {
      * FRAG frame; geometry from the [gpu] frag_* ini keys (defaults: the poller's table) */
     int      frag_ready;
     uint32_t frag_buckets, frag_entries, frag_max_dgram;
+    uint32_t frag_max_entries, frag_flags;    /* 0: NUM_FLOWS_MAX; [gpu] reasm_cksum = dpdk */
     uint64_t frag_ttl_ms;
     uint32_t poll_threads;       /* [gpu] poll_threads: threads of udpdk_poll_rx's socket loops  */
     uint32_t host_copy_min;      /* [gpu] host_copy_min: mean payload bytes from which a poll copies

@@ -35,6 +35,8 @@ static void h_config_defaults(void)
     g_udpdk.frag_entries = 16;         /* IP_FRAG_TBL_BUCKET_ENTRIES */
     g_udpdk.frag_max_dgram = 65515;
     g_udpdk.frag_ttl_ms = 1000;        /* MAX_FLOW_TTL = MS_PER_S */
+    g_udpdk.frag_max_entries = 0;      /* NUM_FLOWS_MAX (rx_poll.c: h_frag_max_entries) */
+    g_udpdk.frag_flags = 0;            /* RFC 1071 header checksum on reassembled datagrams */
     g_udpdk.arena_bytes_max = 4ull << 30;
     g_udpdk.arena_count_max = 1024;
     g_udpdk.port_spec[0] = g_udpdk.port_peer[0] = 0;
@@ -171,6 +173,14 @@ static int h_load_ini(const char *path)
             g_udpdk.frag_entries = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "frag_max_dgram")) {
             g_udpdk.frag_max_dgram = (uint32_t)strtoul(v, NULL, 0);
+        } else if (!strcmp(section, "gpu") && !strcmp(k, "frag_max_entries")) {
+            g_udpdk.frag_max_entries = (uint32_t)strtoul(v, NULL, 0);
+        } else if (!strcmp(section, "gpu") && !strcmp(k, "reasm_cksum")) {
+            /* dpdk: the reassembled header's checksum left 0 as DPDK writes it (the reference's
+             * "TODO must fix the IP header checksum", udpdk_poller.c:355-360); rfc1071 (default) */
+            if (!strcmp(v, "dpdk")) g_udpdk.frag_flags |= UDPDK_FRAG_CKSUM_DPDK;
+            else if (!strcmp(v, "rfc1071")) g_udpdk.frag_flags &= ~UDPDK_FRAG_CKSUM_DPDK;
+            else { rc = -1; break; }
         } else if (!strcmp(section, "gpu") && !strcmp(k, "port")) {
             snprintf(g_udpdk.port_spec, sizeof(g_udpdk.port_spec), "%s", v);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "port_peer")) {

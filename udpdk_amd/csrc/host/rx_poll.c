@@ -199,8 +199,15 @@ static int h_frag_pass(const udpdk_rx_batch_t *staged, const uint32_t *meta_dev,
     udpdk_gpu_ctx *g = g_udpdk.gpu;
     int rc;
     if (!g_udpdk.frag_ready) {
+        /* max_entries: [gpu] frag_max_entries, else the poller's NUM_FLOWS_MAX = UINT16_MAX
+         * (udpdk_poller.c:130-131, udpdk_constants.h:34) where the table has more entries than
+         * that (the reference's 4096 x 16 = 65536), else every entry */
+        uint64_t ent = 1;
+        while (ent < (uint64_t)g_udpdk.frag_buckets * g_udpdk.frag_entries) ent <<= 1;
+        const uint32_t mx = g_udpdk.frag_max_entries ? g_udpdk.frag_max_entries
+                          : ent > 0xFFFFu ? 0xFFFFu : 0u;
         udpdk_frag_table_cfg_t fc = {g_udpdk.frag_buckets, g_udpdk.frag_entries, g_udpdk.frag_ttl_ms,
-                                     g_udpdk.frag_max_dgram};
+                                     g_udpdk.frag_max_dgram, mx, g_udpdk.frag_flags, 0};
         if ((rc = udpdk_gpu_frag_table_create(g, &fc))) { errno = -rc; return -1; }
         g_udpdk.frag_ready = 1;
     }

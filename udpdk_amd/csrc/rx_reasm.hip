@@ -72,7 +72,8 @@ inline uint32_t bits_for(uint32_t v) { return v ? 32u - (uint32_t)__builtin_clz(
 // One table entry (struct ip_frag_pkt) as 20 u32 words, every one accessed with agent-scope
 // relaxed atomics; only reasm_serial writes them.
 enum : uint32_t {
-    E_LOCK = 0,         // unused (kept for the layout)
+    E_LRU_IDX = 0,      // position in DPDK's LRU list: (E_LRU_CALL, E_LRU_IDX) = the call and the
+                        // arrival index of the fragment that added or last reused the entry
     E_VALID = 1,        // key_len != 0
     E_SRC = 2, E_DST = 3, E_ID = 4,
     E_FSIZE = 5, E_TOTAL = 6, E_LAST = 7,
@@ -80,7 +81,7 @@ enum : uint32_t {
     E_FR = 10,          // [4] ofs | len << 16, 0 = empty slot (len > 0 when present)
     E_WHERE = 14,       // [4] frame index in the call E_CALL, or RS_HELD
     E_CALL = 18,        // the call whose fragments E_WHERE may name (older ones are held)
-    E_USED = 19,
+    E_LRU_CALL = 19,
     E_WORDS = 20
 };
 
@@ -139,6 +140,12 @@ struct ReasmArgs {
     uint32_t *sl_k, *sl_v;             // [F] serial list: arrival index, sorted position
     uint32_t *tpos;                    // [entries][4] sorted position of a slot's fragment (this call)
     uint32_t call;                     // this call's number (E_CALL), from 1
+    // rte_ip_frag_table's max_entries / use_entries: the valid entries after the last call (only
+    // reasm_serial changes the table, so it keeps the count); counts[6] = 1 when this call's
+    // serial path must apply ip_frag_find's limit (reasm_ec), counts[7] = the flows the bound
+    // counts (reasm_flows)
+    uint32_t entries, max_entries;
+    uint32_t *tab_used;
     uint32_t hset_tag;                 // reasm_runs' run-key set tag, 1..65535
     uint32_t grouped;                  // every key one run in arrival order: no span overlaps
 };
@@ -660,10 +667,11 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_flows(ReasmArgs a, uint32_t F)
     __shared__ uint32_t s_st[RS_BLOCK][E_WORDS];
     __shared__ unsigned long long s_rk[2 * RS_FLOW_CHUNK];   // the chunk's records, reserved at once
     __shared__ uint32_t s_rv[2 * RS_FLOW_CHUNK];
-    __shared__ uint32_t s_nr, s_base;
+    __shared__ uint32_t s_nr, s_base, s_nb;
     uint32_t *st = s_st[threadIdx.x];
+    const bool limit = a.max_entries < a.entries;
     for (uint32_t c0 = blockIdx.x * RS_FLOW_CHUNK; c0 < F; c0 += gridDim.x * RS_FLOW_CHUNK) {
-        if (threadIdx.x == 0) s_nr = 0;
+        if (threadIdx.x == 0) { s_nr = 0; s_nb = 0; }
         __syncthreads();
         for (uint32_t j = 0; j < PER; ++j) {
             const uint32_t p = c0 + j * RS_BLOCK + threadIdx.x;
@@ -737,6 +745,13 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_flows(ReasmArgs a, uint32_t F)
                 }
             }
             if (p < F) a.pflag[p] = flag;
+            if (limit) {
+                // the flows the max_entries bound counts (reasm_ec): grouped, the complex ones
+                // (a simple flow's span holds no other flow's fragment); else every touching one
+                const bool cnt = (flag & PF_TOUCH) && (!a.grouped || (flag & PF_COMPLEX));
+                const uint32_t nb = (uint32_t)__popcll(__ballot(cnt));
+                if (__lane_id() == 0 && nb) atomicAdd(&s_nb, nb);                  // LDS
+            }
             uint32_t total;
             const uint32_t off = wave_excl_scan(nrec, &total);
             uint32_t base = 0;
@@ -754,6 +769,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_flows(ReasmArgs a, uint32_t F)
         __syncthreads();
         const uint32_t nr = s_nr;
         if (threadIdx.x == 0) s_base = nr ? atomicAdd(&a.counts[1], nr) : 0u;
+        if (threadIdx.x == 0 && s_nb) atomicAdd(&a.counts[7], s_nb);
         __syncthreads();
         for (uint32_t k = threadIdx.x; k < nr; k += RS_BLOCK) {
             a.rk[s_base + k] = s_rk[k];
@@ -801,6 +817,19 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_overlap(ReasmArgs a, const uns
 __global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
 {
     if (!spec_f(a, F)) return;
+    // ip_frag_find's max_entries test (rte_ip_frag_table_create's max_entries, NUM_FLOWS_MAX in
+    // the reference): before any add in the call, use_entries <= the entries valid at call start
+    // + the entries this call's earlier flows still hold. Grouped, a simple flow's span holds no
+    // other flow's fragment, so that is at most the complex flows; otherwise at most the other
+    // touching flows. When the bound cannot stay below max_entries, the whole batch takes the
+    // serial path, which applies the test (and the LRU deletion) exactly.
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.max_entries < a.entries) {
+        const uint64_t c = (uint64_t)a.counts[7] + (a.grouped ? 1u : 0u);
+        if ((uint64_t)ld_a(a.tab_used) + c > a.max_entries) {
+            a.counts[3] = 1u;
+            a.counts[6] = 1u;
+        }
+    }
     for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
         const uint32_t f = a.pflag[p];
         if (!(f & PF_TOUCH) || (f & (PF_COMPLEX | PF_SHARED))) continue;
@@ -898,12 +927,52 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_process(ReasmArgs a, uint32_t 
     if (threadIdx.x == UDPDK_RS_N && s_cnt[UDPDK_RS_N]) atomicAdd(a.out_bytes, s_cnt[UDPDK_RS_N]);
 }
 
+// TAILQ_FIRST(&tbl->lru): the valid entry with the smallest (E_LRU_CALL, E_LRU_IDX), by the
+// whole wave (eight entries per lane in flight per round); RS_NONE when the table is empty.
+__device__ uint32_t lru_head(const ReasmArgs &a)
+{
+    const uint32_t lane = __lane_id();
+    unsigned long long best = ~0ull;
+    uint32_t bi = RS_NONE;
+    for (uint32_t x0 = 0; x0 < a.entries; x0 += 512u) {
+        uint32_t v[8], hi[8], lo[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+            const uint32_t x = x0 + 64u * u + lane;
+            const uint32_t *e = a.tab + (size_t)min(x, a.entries - 1u) * E_WORDS;
+            v[u] = x < a.entries ? ld_a(e + E_VALID) : 0u;
+            hi[u] = ld_a(e + E_LRU_CALL);
+            lo[u] = ld_a(e + E_LRU_IDX);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+            const unsigned long long key = ((unsigned long long)hi[u] << 32) | lo[u];
+            if (v[u] && key < best) {
+                best = key;
+                bi = x0 + 64u * u + lane;
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long ob = __shfl_xor(best, d, 64);
+        const uint32_t oi = __shfl_xor(bi, d, 64);
+        if (ob < best || (ob == best && oi < bi)) {
+            best = ob;
+            bi = oi;
+        }
+    }
+    return bi;
+}
+
 // The serial path: one wave takes the listed fragments in arrival order, exactly as the
 // reference's per-fragment rte_ipv4_frag_reassemble_packet does: ip_frag_find (the lanes load the
 // key's 2 x assoc candidate entries at once; match, else the first expired, else the first free
-// entry in ip_frag_lookup's order), ip_frag_process on the entry's words in LDS, write-back or
-// invalidation. It is the only writer of the table while it runs. A fragment that stays in a
-// pending entry gets a store job; a flow that ends later in the call cancels its jobs.
+// entry in ip_frag_lookup's order, the free one subject to the max_entries test when counts[6]
+// says the call needs it), ip_frag_process on the entry's words in LDS, write-back or
+// invalidation. It is the only writer of the table while it runs, and keeps its count of valid
+// entries (use_entries) across calls. A fragment that stays in a pending entry gets a store job;
+// a flow that ends later in the call cancels its jobs.
 __global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *list, uint32_t K)
 {
     __shared__ uint32_t st[E_WORDS];
@@ -911,6 +980,10 @@ __global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *
     unsigned long long c_ns = 0, c_err = 0, c_holes = 0, c_exp = 0, c_done = 0, c_bytes = 0;
     long long c_stored = 0;
     const uint32_t nslot = 2u * a.assoc;
+    const bool limit = a.counts[6] != 0u;
+    uint32_t use = ld_a(a.tab_used);
+    uint32_t head = RS_NONE;                 // the LRU head, while head_ok
+    bool head_ok = false;
     for (uint32_t k = 0; k < K; ++k) {
         const uint32_t q = list[k];
         const uint32_t i = a.s_i[q], m = a.s_meta[q];
@@ -918,12 +991,12 @@ __global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *
         const uint32_t p1 = sig & a.mask, p2 = ((sig << 7) + (sig >> 14)) & a.mask;
         // lanes scan p1[0], p2[0], p1[1], p2[1], ... (ip_frag_lookup's order), whole entries
         const uint32_t slot = (lane & 1u ? p2 : p1) + (lane >> 1);
-        uint32_t w[E_USED];
+        uint32_t w[E_WORDS];
         bool match = false, empty = false, stale = false;
         if (lane < nslot) {
             const uint32_t *e = a.tab + (size_t)slot * E_WORDS;
 #pragma unroll
-            for (uint32_t j = 1; j < E_USED; ++j) w[j] = ld_a(e + j);
+            for (uint32_t j = 0; j < E_WORDS; ++j) w[j] = ld_a(e + j);
             const unsigned long long start = ((unsigned long long)w[E_START + 1] << 32) | w[E_START];
             match = w[E_VALID] && w[E_SRC] == src && w[E_DST] == dst && w[E_ID] == id;
             stale = w[E_VALID] && !match && a.max_cycles + start < a.tms;
@@ -935,14 +1008,49 @@ __global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *
             ++c_ns;                                          // ip_frag_find: no space
             continue;
         }
+        if (limit && !mm && !ms && use >= a.max_entries) {
+            // a free entry, but max_entries in use: the LRU head goes if it has expired, else
+            // the fragment is dropped (ip_frag_find's fail_nospace)
+            if (!head_ok) {
+                head = lru_head(a);
+                head_ok = true;
+            }
+            bool del = false;
+            if (head != RS_NONE) {
+                const uint32_t *he = a.tab + (size_t)head * E_WORDS;
+                const unsigned long long hs = ((unsigned long long)ld_a(he + E_START + 1) << 32) | ld_a(he + E_START);
+                del = a.max_cycles + hs < a.tms;
+            }
+            if (!del) {
+                ++c_ns;
+                continue;
+            }
+            if (lane == 0) {                                 // ip_frag_tbl_del(lru)
+                ++c_exp;
+                uint32_t *he = a.tab + (size_t)head * E_WORDS;
+                // (this call's fragments of an expired entry cannot exist: a fragment that
+                // reached it this call would have restarted it; kept for the invariant)
+                if (ld_a(he + E_CALL) == a.call)
+                    for (uint32_t j = 0; j < RS_MAX_FRAG; ++j)
+                        if (ld_a(he + E_FR + j) && ld_a(he + E_WHERE + j) != RS_HELD) {
+                            a.jobs[a.tpos[(size_t)head * RS_MAX_FRAG + j]].frame = RS_NONE;
+                            --c_stored;
+                        }
+                st_a(he + E_VALID, 0u);
+            }
+            --use;
+            head_ok = false;
+            stores_done();
+            wave_sync_rs();
+        }
         const uint32_t cl = (uint32_t)__ffsll((long long)pick) - 1u;
         const uint32_t cand = __shfl(slot, cl, 64);
         if (lane == cl) {
 #pragma unroll
-            for (uint32_t j = 1; j < E_USED; ++j) st[j] = w[j];
+            for (uint32_t j = 0; j < E_WORDS; ++j) st[j] = w[j];
         }
         wave_sync_rs();
-        uint32_t inval = 0;
+        uint32_t inval = 0, moved = 0;
         if (lane == 0) {
             bool fresh = !mm;                                // ip_frag_tbl_add (after del if stale)
             if (ms && !mm) ++c_exp;
@@ -952,6 +1060,9 @@ __global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *
             }
             if (fresh) {
                 state_reset(st, src, dst, id, a.tms, a.call);
+                st[E_LRU_CALL] = a.call;                     // to the LRU list's tail
+                st[E_LRU_IDX] = i;
+                moved = 1;
             } else if (st[E_CALL] != a.call) {               // fragments of earlier calls are held
                 for (uint32_t j = 0; j < RS_MAX_FRAG; ++j) st[E_WHERE + j] = RS_HELD;
                 st[E_CALL] = a.call;
@@ -989,15 +1100,20 @@ __global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *
         }
         wave_sync_rs();
         inval = __shfl(inval, 0, 64);
+        moved = __shfl(moved, 0, 64);
+        if (!mm && !ms) ++use;                               // an empty entry taken
+        if (inval) --use;
+        if (head_ok && cand == head && (inval || moved)) head_ok = false;
         uint32_t *e = a.tab + (size_t)cand * E_WORDS;
         if (inval) {
             if (lane == 0) st_a(e + E_VALID, 0u);
-        } else if (lane >= E_VALID && lane < E_USED) {
+        } else if (lane < E_WORDS) {
             st_a(e + lane, st[lane]);
         }
         stores_done();
         wave_sync_rs();
     }
+    if (lane == 0) st_a(a.tab_used, use);
     if (lane == 0) {
         unsigned long long *s = a.stats;
         if (c_ns) atomicAdd(&s[UDPDK_RS_NO_SPACE], c_ns);
@@ -1220,6 +1336,7 @@ struct EmitArgs {
     uint32_t *out_origin;
     uint32_t C;
     SpecTail g;                   // speculative launch: C from the device, or nothing to do
+    uint32_t cksum_zero;          // UDPDK_FRAG_CKSUM_DPDK: header checksum left 0 (DPDK's)
 };
 
 // One wave per datagram. The output datagram is written as aligned 16-byte chunks (lane =
@@ -1381,7 +1498,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
                 uint32_t sum = (uint32_t)__builtin_amdgcn_readfirstlane((int)part);
                 sum = (sum >> 16) + (sum & 0xFFFFu);
                 sum = (sum >> 16) + (sum & 0xFFFFu);
-                if (lane == 1u) v.z |= ~sum & 0xFFFFu;
+                if (lane == 1u && !a.cksum_zero) v.z |= ~sum & 0xFFFFu;
             }
             if (in) store16(orr, b0, v);
         }
@@ -1497,7 +1614,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit_inplace(EmitArgs a, uint8
             for (uint32_t j = 0; j < 5; ++j) sum += (h[j] & 0xFFFFu) + (h[j] >> 16);
             sum = (sum >> 16) + (sum & 0xFFFFu);
             sum = (sum >> 16) + (sum & 0xFFFFu);
-            const uint32_t ck = ~sum & 0xFFFFu;
+            const uint32_t ck = a.cksum_zero ? 0u : ~sum & 0xFFFFu;
             const uint8_t pb[6] = {(uint8_t)(h[0] >> 16), (uint8_t)(h[0] >> 24), (uint8_t)(h[1] >> 16),
                                    (uint8_t)(h[1] >> 24), (uint8_t)ck, (uint8_t)(ck >> 8)};
             const uint32_t po[6] = {16, 17, 20, 21, 24, 25};
@@ -1548,6 +1665,8 @@ struct Reasm {
     uint32_t *tab = nullptr;                 // [entries][E_WORDS]
     uint8_t *ebuf = nullptr;
     uint32_t entries = 0, assoc = 0, mask = 0, max_dgram = 0, stride = 0, assoc_log2 = 0, nbuckets = 0;
+    uint32_t max_entries = 0, flags = 0;
+    uint32_t *tab_used = nullptr;            // device: valid entries (reasm_serial keeps it)
     uint64_t max_cycles = 0;
     uint32_t cap = 0;                        // fragments per call (= context max_frames)
     uint32_t *frag_list = nullptr, *v1 = nullptr, *v1s = nullptr, *v2s = nullptr;
@@ -1595,7 +1714,7 @@ hipError_t dalloc(T **p, size_t count)
 void reasm_destroy(Reasm *r)
 {
     if (!r) return;
-    void *dev[] = {r->tab, r->ebuf, r->frag_list, r->v1, r->v1s, r->v2s, r->k1, r->k1s, r->k2,
+    void *dev[] = {r->tab, r->tab_used, r->ebuf, r->frag_list, r->v1, r->v1s, r->v2s, r->k1, r->k1s, r->k2,
                    r->k2s, r->stats, r->done, r->jobs, r->dk, r->dks,
                    r->dv, r->perm, r->sizes, r->offs, r->tmp, r->out, r->out_off, r->out_ptype,
                    r->out_origin, r->out_len, r->pflag, r->sb1, r->sb2, r->tf, r->tl, r->oc, r->ob, r->rk, r->rks,
@@ -1611,10 +1730,12 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
 {
     const uint64_t want = (uint64_t)cfg->bucket_num * cfg->bucket_entries;
     if (!cfg->bucket_num || !cfg->bucket_entries || (cfg->bucket_entries & (cfg->bucket_entries - 1)) ||
-        cfg->bucket_entries > 32 || want > (1u << 22) || !cfg->max_dgram || cfg->max_dgram > 65515u)
+        cfg->bucket_entries > 32 || want > (1u << 22) || !cfg->max_dgram || cfg->max_dgram > 65515u ||
+        (cfg->flags & ~UDPDK_FRAG_CKSUM_DPDK) || cfg->reserved)
         return -EINVAL;
     uint64_t entries = 1;
     while (entries < want) entries <<= 1;
+    if (cfg->max_entries > entries) return -EINVAL;        // rte_ip_frag_table_create's check
     Reasm *r = new (std::nothrow) Reasm;
     if (!r) return -ENOMEM;
     r->device = device;
@@ -1625,6 +1746,8 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
     r->mask = (r->entries - 1u) & ~(r->assoc - 1u);
     r->max_cycles = cfg->max_cycles;
     r->max_dgram = cfg->max_dgram;
+    r->max_entries = cfg->max_entries ? cfg->max_entries : r->entries;
+    r->flags = cfg->flags;
     r->stride = (34u + cfg->max_dgram + 4u + 255u) & ~255u;   // + 4: dword loads of the last bytes
     r->cap = std::max<uint32_t>(max_frames, 1);
     int rc = 0;
@@ -1633,6 +1756,7 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
     const size_t C = r->cap, C2 = 2 * (size_t)r->cap;
     if ((e = dalloc(&r->tab, (size_t)r->entries * E_WORDS)) != hipSuccess ||
         (e = hipMemset(r->tab, 0, (size_t)r->entries * E_WORDS * sizeof(uint32_t))) != hipSuccess ||
+        (e = dalloc(&r->tab_used, 1)) != hipSuccess || (e = hipMemset(r->tab_used, 0, 4)) != hipSuccess ||
         (e = hipMalloc((void **)&r->ebuf, (size_t)r->entries * r->stride)) != hipSuccess ||
         (e = dalloc(&r->frag_list, C)) != hipSuccess || (e = dalloc(&r->v1s, C)) != hipSuccess ||
         (e = dalloc(&r->v2s, C)) != hipSuccess || (e = dalloc(&r->k1, C)) != hipSuccess ||
@@ -1745,6 +1869,9 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     a.tpos = r->tpos;
     if (++r->calls == 0) r->calls = 1;          // 0 marks entries never touched
     a.call = r->calls;
+    a.entries = r->entries;
+    a.max_entries = r->max_entries;
+    a.tab_used = r->tab_used;
     a.ib = bits_for(n - 1u);
     if (!n) RS_HIP(hipMemsetAsync(r->stats, 0, RS_ZERO_WORDS * sizeof(unsigned long long), st));
     // per-position records (written by reasm_runs for a grouped batch, else by reasm_prep after
@@ -1820,6 +1947,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         ea.out_origin = r->out_origin;
         ea.C = Cn;
         ea.g = g;
+        ea.cksum_zero = (r->flags & UDPDK_FRAG_CKSUM_DPDK) ? 1u : 0u;
         const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_WAVES - 1) / RS_WAVES, 8192));
         hipLaunchKernelGGL(reasm_emit, dim3(ge), dim3(RS_BLOCK), 0, st, ea);
         RS_HIP(hipGetLastError());
