@@ -100,7 +100,22 @@ struct RxArgs {
     uint32_t spec_cap;
     uint32_t spec_epoch;
     unsigned long long *spec_nonfull;   // [UDPDK_SPEC_WORDS] atomicMax of epoch << 32 | ~tile, tiles not full
+    // fused completion (spec entries, at most UDPDK_FUSE_MAX_TILES tiles): the last workgroup
+    // writes lane_off / total (rx_compact1's work); fan-in words [16 x (UDPDK_FUSE_SHARDS + 1)],
+    // zero between calls; null: rx_compact1 follows
+    unsigned long long *fuse;
+    uint32_t *lane_off;
+    uint32_t *total;
+    // host-visible kernel hints (pinned memory, may be null): hint[UDPDK_HINT_TAIL] = seq when the
+    // call ran a tail pass, hint[UDPDK_HINT_NONFULL] = seq when a tile before the last was not full
+    uint32_t *hint;
+    uint32_t seq;
 };
+#define UDPDK_FUSE_SHARDS 8u
+#define UDPDK_FUSE_MAX_TILES 65535u          // fan-in fields: 16-bit arrival and not-full counts
+#define UDPDK_HINT_TAIL 0
+#define UDPDK_HINT_NONFULL 16                // its own 64-byte line
+#define UDPDK_HINT_DONE 32                   // seq of the latest call whose first tile ran
 #ifndef UDPDK_SPEC_COMPACT
 #define UDPDK_SPEC_COMPACT 1
 #endif
@@ -168,6 +183,8 @@ struct Compact1Args {
     uint32_t spec;                // rx_classify wrote speculative entries (RxArgs::spec_pkt)
     uint32_t spec_epoch;
     const unsigned long long *spec_nonfull;
+    uint32_t *hint;               // see RxArgs::hint (compact1 reports a tile that was not full)
+    uint32_t seq;
 };
 
 struct TxArgs {
@@ -211,7 +228,7 @@ struct GatherArgs {
     const uint32_t *slot_off;   // [count + 1] packed slots (udpdk_gpu_rx_gather_packed), or null
 };
 
-__global__ void rx_classify(RxArgs a);
+template <int G> __global__ void rx_classify(RxArgs a);   // G: tail chunk groups in flight (1, 2)
 __global__ void rx_gather(GatherArgs a);
 __global__ void rx_scan_cols(ScanArgs a, uint32_t lb);
 __global__ void rx_scan_reduce(ScanArgs a);

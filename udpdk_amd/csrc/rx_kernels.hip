@@ -209,6 +209,112 @@ __device__ __forceinline__ uint32_t max_scan_dpp(uint32_t v)
     return v;
 }
 
+// ------------------------------------------------------------------------------------------
+// Fused single-lane completion (rx_classify with a.fuse): what rx_compact1 does in a second
+// launch, done by the last workgroup to finish. Each workgroup, once its written-through stores
+// are drained, adds {1 arrival, not-full flag, its deliveries} to its shard's fan-in word
+// (a.fuse[16 s], s = tile mod 8, 128 B apart: one word for 1024 arrivals serialises them,
+// tools/probe/ticket_probe.hip); the shard's last arrival adds the shard's sums to the top word
+// (a.fuse[128]) and the top's last arrival completes the call. Every word is reset by its last
+// arrival, so the pipe's next call starts from zeros. When every tile before the last delivered
+// all its frames (the common case of a port-bound stream) the speculative entries are the lane
+// already and the completion writes lane_off and the total only. Otherwise it rewrites the
+// entries after the first tile that was not full from the verdict words (sc1 loads behind an
+// agent acquire; one workgroup, 4096 frames per pass) -- slow, so the host goes back to the
+// two-launch form for its next calls (a.hint).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void classify_complete(const RxArgs &a, uint32_t tile, uint32_t tcount,
+                                                  uint32_t tid, uint32_t lane, uint32_t w)
+{
+    __shared__ uint32_t fz[4 + CLS_WAVES];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every wave: its stores written through
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t s = tile & (UDPDK_FUSE_SHARDS - 1u);
+        const uint32_t ns = (a.n_tiles - 1u - s) / UDPDK_FUSE_SHARDS + 1u;   // tiles of shard s
+        const bool nonfull = tile + 1u < a.n_tiles && tcount != a.tile_frames;
+        const unsigned long long mine = (1ull << 48) | (nonfull ? 1ull << 32 : 0ull) | tcount;
+        unsigned long long *sw = a.fuse + 16u * s;
+        const unsigned long long now =
+            __hip_atomic_fetch_add(sw, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + mine;
+        uint32_t last = 0;
+        unsigned long long fin = 0;
+        if ((uint32_t)(now >> 48) == ns) {
+            __hip_atomic_store(sw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long m2 = (1ull << 48) | (now & 0xFFFFFFFFFFFFull);
+            unsigned long long *tw = a.fuse + 16u * UDPDK_FUSE_SHARDS;
+            const unsigned long long now2 =
+                __hip_atomic_fetch_add(tw, m2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + m2;
+            if ((uint32_t)(now2 >> 48) == min(a.n_tiles, (uint32_t)UDPDK_FUSE_SHARDS)) {
+                __hip_atomic_store(tw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = 1;
+                fin = now2;
+            }
+        }
+        fz[0] = last;
+        fz[1] = (uint32_t)fin;                              // deliveries of the call
+        fz[2] = (uint32_t)(fin >> 32) & 0xFFFFu;            // tiles (not the last) not full
+    }
+    __syncthreads();
+    if (!fz[0]) return;
+    const uint32_t total = fz[1];
+    if (fz[2] != 0u) {
+        // the other workgroups' tile counts and verdict words: one acquire, then sc1 loads
+        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint32_t T = a.tile_frames;
+        const __amdgpu_buffer_rsrc_t hr = make_rsrc(a.hist, a.n_tiles * 4u);
+        uint32_t f = 0xFFFFFFFFu;
+        for (uint32_t t = tid; t + 1u < a.n_tiles; t += CLS_BLOCK)
+            if (__builtin_amdgcn_raw_buffer_load_b32(hr, (int)(4u * t), 0, 16) != T) f = min(f, t);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) f = min(f, (uint32_t)__shfl_xor((int)f, d, 64));
+        if (lane == 0) fz[4 + w] = f;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t i = 0; i < CLS_WAVES; ++i) f = min(f, fz[4 + i]);
+        // tiles up to f hold their entries already (every tile before f was full)
+        uint32_t run = f * T + __builtin_amdgcn_raw_buffer_load_b32(hr, (int)(4u * f), 0, 16);
+        const __amdgpu_buffer_rsrc_t mr = make_rsrc(a.meta, a.n * 4u);
+        for (uint32_t c0 = (f + 1u) * T; c0 < a.n; c0 += 16u * CLS_BLOCK) {
+            const uint32_t fb = c0 + 16u * tid;
+            uint32_t bits = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(mr, (int)(4u * (fb + 4u * k)), 0, 16);
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if ((v[j] & 0xFu) == UDPDK_V_DELIVERED && fb + 4u * k + j < a.n) bits |= 1u << (4u * k + j);
+            }
+            const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
+            const uint32_t incl = scan_dpp(cnt);
+            __syncthreads();                                // fz[4..] of the previous pass read
+            if (lane == 63) fz[4 + w] = incl;
+            __syncthreads();
+            uint32_t pos = run + incl - cnt, pass = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < CLS_WAVES; ++i) {
+                pos += i < w ? fz[4 + i] : 0u;
+                pass += fz[4 + i];
+            }
+            for (uint32_t j = 0; j < 16; ++j)
+                if ((bits >> j) & 1u) {
+                    if (pos < a.spec_cap) a.spec_pkt[pos] = fb + j;
+                    ++pos;
+                }
+            run += pass;
+        }
+        if (tid == 0 && a.hint)
+            __hip_atomic_store(&a.hint[UDPDK_HINT_NONFULL], a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (tid == 0) {
+        a.lane_off[0] = 0u;
+        a.lane_off[1] = total;
+        *a.total = total;
+    }
+}
+
 // Frame bytes [12, 64) of one frame: 14 dwords from the dword at or below frame byte 12 (3 x 16 B
 // + 8 B; at 64 B frame strides a dword-aligned start costs the same as an aligned one, a byte-
 // aligned one ~25 % more, tools/probe/align_probe.hip), funnelled to g[i] = frame bytes 12 + 4i ..
@@ -221,10 +327,17 @@ struct Win {
 // per workgroup puts 4 workgroups on each CU at 1 M frames. (Round 1: a 96-VGPR budget spilled
 // and ran 19 % slower at 64 B; four tail groups in flight at 148 VGPRs and 3 waves per SIMD were
 // no faster at 1500 B and slower at IMIX and 106 B. Round 2: three groups at 127 VGPRs, DESIGN.md
-// §4.)
-__global__ void __launch_bounds__(CLS_BLOCK) __attribute__((amdgpu_waves_per_eu(UDPDK_CLS_WPE, 8)))
+// §4.) Round 4: G = tail-pass chunk groups in flight per wave. G = 2 (122 VGPRs, 4 waves per
+// SIMD) for batches with long datagrams; G = 1 (92 VGPRs, 5 waves per SIMD, the LDS limit of a
+// one-round tile) lets a fifth workgroup per CU in, which is what consecutive short-frame
+// batches overlapping on several streams want (config 2, --steps 20, same-box A/B with the
+// compaction launch gone: 57.1 -> 63.0 Gpkt/s; config 1 (106 B, one tail chunk per frame) is
+// 8 % slower at G = 1, so the host picks G by whether recent calls had tail passes).
+template <int G>
+__global__ void __launch_bounds__(CLS_BLOCK) __attribute__((amdgpu_waves_per_eu(G == 1 ? 5 : UDPDK_CLS_WPE, 8)))
 rx_classify(RxArgs a)
 {
+    static_assert(G == 1 || G == 2, "one or two tail chunk groups in flight");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t steps = a.tile_frames / 64;
@@ -322,6 +435,8 @@ rx_classify(RxArgs a)
         return r;
     };
 
+    __shared__ uint32_t tail_any;           // some wave of the tile ran a tail pass (kernel hint)
+    if (tid == 0) tail_any = 0u;            // (ordered by the staging barrier)
     stage(0);
     __syncthreads();
     uint32_t st = __builtin_amdgcn_readfirstlane(w);             // wave-uniform step (SGPR)
@@ -357,6 +472,7 @@ rx_classify(RxArgs a)
     uint32_t *l_D = l_B + 64;                                               // [64]
     uint32_t *l_own = l_B + 128;            // [64] frame + 1 whose chunks start at k0 + slot, else 0
     l_own[lane] = 0;
+    bool tailed = false;                    // this wave ran a tail pass (the host's kernel hint)
     constexpr uint32_t OOR = 0xFFFFFFF0u;   // past any batch's range (< 4 GiB - 16)
     auto tail_step = [&](uint32_t s2) {
             const uint32_t i = s2 * 64 + lane;
@@ -432,7 +548,16 @@ rx_classify(RxArgs a)
             int la, lb;
             uint4 Ra[4], Rb[4];
             issue(0, qa, la, ea, Ra);
-            if (total <= 64u) {
+            tailed = true;
+            if constexpr (G == 1) {
+                // one group in flight: the next group's loads are issued after this one is summed
+                for (uint32_t k0 = 0;; k0 += 64) {
+                    consume(k0, la, ea, Ra);
+                    if (k0 + 64 >= total) break;
+                    issue(k0 + 64, qa, la, ea, Ra);
+                }
+                (void)qb; (void)lb; (void)eb; (void)Rb;
+            } else if (total <= 64u) {
                 // one group (e.g. every frame's tail one chunk): no groups issued past the end
                 consume(0, la, ea, Ra);
             } else {
@@ -676,6 +801,7 @@ rx_classify(RxArgs a)
 #pragma unroll
         for (int c = 0; c < UDPDK_N_COUNTERS; ++c) row = lane == (uint32_t)c ? sc[c] : row;
         if (lane < UDPDK_N_COUNTERS) cntw[w * 16 + lane] = row;
+        if (tailed && lane == 0) tail_any = 1u;
     }
     __syncthreads();
     STAMP(7);
@@ -685,12 +811,16 @@ rx_classify(RxArgs a)
         for (int i = 0; i < CLS_WAVES; ++i) v += cntw[i * 16 + c];
         return v;
     };
+    // Fused completion (a.fuse, single lane, one-round tiles): every store another workgroup may
+    // read in this launch is written through (sc1) and drained before the workgroup's arrival,
+    // as cdna_hip_programming.md Guideline 16 / MI355X_MICROARCH.md "Valid forms" require.
+    const bool fuse = a.fuse != nullptr;
+    uint32_t tcount = 0;                                   // the tile's deliveries (spec / fuse)
     if (a.spec_pkt) {
         // Speculative lane entries (single lane, 1024-frame one-round tile, 4 frames per
         // thread): the tile's delivered frames in order at t0 + rank, which is where they belong
-        // when every earlier tile delivered all its frames. rx_compact1 keeps them then (its
-        // check: the predecessors' counts sum to t0) and rewrites the tile otherwise, so the
-        // dependent compaction pass reads no verdict word and writes no entry in that case.
+        // when every earlier tile delivered all its frames. rx_compact1 (or the fused completion
+        // below) keeps them then and rewrites the later tiles otherwise.
         __shared__ uint32_t spec_ws[CLS_WAVES];
         const uint32_t nv = t1 - t0, j0 = 4u * tid;
         uint32_t d = 0;
@@ -707,19 +837,32 @@ rx_classify(RxArgs a)
         __syncthreads();
         uint32_t pos = t0 + incl - cnt;
 #pragma unroll
-        for (uint32_t i = 0; i < CLS_WAVES; ++i) pos += i < w ? spec_ws[i] : 0u;
+        for (uint32_t i = 0; i < CLS_WAVES; ++i) {
+            pos += i < w ? spec_ws[i] : 0u;
+            tcount += spec_ws[i];
+        }
         // a tile short of a full tile's deliveries (the last tile never counts: nothing follows
         // it) marks its successors' entries wrong; every other word of the flag stays untouched
-        if (tid == 0 && tile + 1u < a.n_tiles) {
-            uint32_t tc = 0;
-#pragma unroll
-            for (uint32_t i = 0; i < CLS_WAVES; ++i) tc += spec_ws[i];
-            if (tc != a.tile_frames)
-                atomicMax(&a.spec_nonfull[tile % UDPDK_SPEC_WORDS],
-                          ((unsigned long long)a.spec_epoch << 32) | (0xFFFFFFFFu - tile));
-        }
+        if (tid == 0 && tile + 1u < a.n_tiles && tcount != a.tile_frames)
+            atomicMax(&a.spec_nonfull[tile % UDPDK_SPEC_WORDS],
+                      ((unsigned long long)a.spec_epoch << 32) | (0xFFFFFFFFu - tile));
         const uint32_t f = t0 + j0;
-        if (d == 0xFu && (pos & 3u) == 0u && pos + 4u <= a.spec_cap) {
+        if (fuse) {
+            // written through: the completing workgroup may rewrite these words (no stale dirty
+            // copy may stay behind in this XCD's L2) -- range-checked by the resource
+            const __amdgpu_buffer_rsrc_t sr = make_rsrc(a.spec_pkt, a.spec_cap * 4u);
+            if (d == 0xFu && (pos & 3u) == 0u) {
+                const __attribute__((ext_vector_type(4))) uint32_t x = {f, f + 1u, f + 2u, f + 3u};
+                __builtin_amdgcn_raw_buffer_store_b128(x, sr, (int)(4u * pos), 0, 16);
+            } else {
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if ((d >> j) & 1u) {
+                        __builtin_amdgcn_raw_buffer_store_b32(f + j, sr, (int)(4u * pos), 0, 16);
+                        ++pos;
+                    }
+            }
+        } else if (d == 0xFu && (pos & 3u) == 0u && pos + 4u <= a.spec_cap) {
             *reinterpret_cast<uint4 *>(a.spec_pkt + pos) = make_uint4(f, f + 1u, f + 2u, f + 3u);
         } else {
 #pragma unroll
@@ -733,7 +876,26 @@ rx_classify(RxArgs a)
     if (nbuf == 1u) {
         const uint32_t nv = t1 - t0;
         uint32_t *dst = a.meta + t0;
-        if (nv == a.tile_frames && ((uintptr_t)dst & 15u) == 0) {
+        if (fuse) {
+            // verdict words written through (the completing workgroup reads them back when a
+            // tile was not full)
+            const __amdgpu_buffer_rsrc_t mr = make_rsrc(dst, nv * 4u);
+            if (((uintptr_t)dst & 15u) == 0) {
+                const uint4 *s4 = reinterpret_cast<const uint4 *>(mstage);
+                for (uint32_t i = tid; i < (nv + 3u) / 4u; i += CLS_BLOCK) {
+                    const uint4 v = s4[i];
+                    const __attribute__((ext_vector_type(4))) uint32_t x = {v.x, v.y, v.z, v.w};
+                    if (4u * i + 4u <= nv)
+                        __builtin_amdgcn_raw_buffer_store_b128(x, mr, (int)(16u * i), 0, 16);
+                    else
+                        for (uint32_t j = 4u * i; j < nv; ++j)
+                            __builtin_amdgcn_raw_buffer_store_b32(mstage[j], mr, (int)(4u * j), 0, 16);
+                }
+            } else {
+                for (uint32_t i = tid; i < nv; i += CLS_BLOCK)
+                    __builtin_amdgcn_raw_buffer_store_b32(mstage[i], mr, (int)(4u * i), 0, 16);
+            }
+        } else if (nv == a.tile_frames && ((uintptr_t)dst & 15u) == 0) {
             uint4 *d4 = reinterpret_cast<uint4 *>(dst);
             const uint4 *s4 = reinterpret_cast<const uint4 *>(mstage);
             for (uint32_t i = tid; i < nv / 4; i += CLS_BLOCK) d4[i] = s4[i];
@@ -746,7 +908,12 @@ rx_classify(RxArgs a)
     if (a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
 #endif
     if (a.n_lanes == 1u) {
-        if (tid == 0) a.hist[tile] = tile_counter(UDPDK_C_DELIVERIES);
+        if (tid == 0) {
+            if (fuse)
+                __hip_atomic_store(&a.hist[tile], tcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                a.hist[tile] = tile_counter(UDPDK_C_DELIVERIES);
+        }
     } else {
         if (a.hist16) {           // u16 row of n_lanes (rounded up to even) counts
             const uint32_t hw = (a.n_lanes + 1u) >> 1;
@@ -757,7 +924,18 @@ rx_classify(RxArgs a)
         }
     }
     if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = tile_counter(tid);
+    // the host's kernel choice for its next calls: this call needed tail passes. Sampled (every
+    // 64th tile, one lane): a store to host memory per wave cost IMIX classify 91 -> 544 us.
+    if (a.hint && (tile & 63u) == 0u && tid == 0) {
+        if (tail_any)
+            __hip_atomic_store(&a.hint[UDPDK_HINT_TAIL], a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tile == 0u)
+            __hip_atomic_store(&a.hint[UDPDK_HINT_DONE], a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (fuse) classify_complete(a, tile, tcount, tid, lane, w);
 }
+template __global__ void rx_classify<1>(RxArgs a);
+template __global__ void rx_classify<2>(RxArgs a);
 
 
 // ------------------------------------------------------------------------------------------
@@ -848,6 +1026,8 @@ rx_compact1(Compact1Args a)
         uint32_t first = (uint32_t)(nf >> 32) == a.spec_epoch ? 0xFFFFFFFFu - (uint32_t)nf : 0xFFFFFFFFu;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) first = min(first, (uint32_t)__shfl_xor((int)first, d, 64));
+        if (first < tl && blockIdx.x == 0 && tid == 0 && a.hint)
+            __hip_atomic_store(&a.hint[UDPDK_HINT_NONFULL], a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (first >= tl) {
             if (blockIdx.x == 0 && tid == 0) {
                 const uint32_t total = tl * a.tile_frames + a.tile_count[tl];

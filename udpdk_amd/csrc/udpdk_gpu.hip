@@ -8,6 +8,7 @@
 
 #include <errno.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -58,6 +59,7 @@ struct Pipe {
     uint32_t *ticket = nullptr;               // rx_scan_cols lane-block tickets
     uint32_t epoch = 0;                       // rx_scan_cols calls on this pipe (look-back tag)
     uint32_t spec_epoch = 0;                  // speculative compaction calls (DevResult::nonfull tag)
+    unsigned long long *fuse = nullptr;       // rx_classify fused-completion fan-in words (zeroed)
     uint32_t *tile_cnt = nullptr;
     DevResult *res = nullptr;                 // counters, total (device)
     DevResult *h_res = nullptr;               // pinned mirror, filled by udpdk_gpu_rx_stats
@@ -76,6 +78,12 @@ struct Pipe {
     const uint32_t *staged_meta = nullptr;    // and its verdict words
 };
 constexpr int MAX_PIPES = 4;
+constexpr size_t FUSE_BYTES = 128u * (UDPDK_FUSE_SHARDS + 1u);   // one 128-B line per fan-in word
+constexpr size_t HINT_BYTES = 192u;
+#ifndef UDPDK_HINT_WINDOW
+#define UDPDK_HINT_WINDOW 8u       // calls (as far as the GPU got) a tail pass / a not-full tile
+                                   // keeps the other form on
+#endif
 
 } // namespace
 
@@ -93,6 +101,15 @@ struct udpdk_gpu_ctx {
     uint32_t slots_cap = 0, n_slots = 0;
     uint32_t n_lanes = 1, lane_mask = 0xFFFFFFFFu, key_bits = 0, max_fanout = 0;
     uint32_t one_lane_tile = 0;    // UDPDK_ONE_LANE_TILE (diagnostic): single-lane tile override
+    // Kernel hints (pinned host memory the kernels write, RxArgs::hint): the call sequence number
+    // of the last call that ran a tail pass / had a tile before the last not full. The single-lane
+    // path takes rx_classify<1> and the fused completion while neither was seen in the last
+    // UDPDK_HINT_WINDOW calls; both forms are exact for any batch, the hint only picks the faster.
+    uint32_t *hint = nullptr;
+    uint32_t rx_seq = 0;
+    int force_fuse = -1;           // UDPDK_RX_FUSE=0/1 (tests, A/B): fused completion off / always
+    int force_tailg = 0;           // UDPDK_RX_TAILG=1/2 (tests, A/B): rx_classify<G> always
+    bool trace = false;            // UDPDK_RX_TRACE (diagnostic): the form of every call on stderr
     bool have_snapshot = false;
 
     // RX workspace, one set per pipe
@@ -272,6 +289,12 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
         const uint32_t t = (uint32_t)atoi(e);
         if (t >= RX_TILE_MIN && t <= RX_TILE_MAX && (t & (t - 1)) == 0) c->one_lane_tile = t;
     }
+    if (const char *e = getenv("UDPDK_RX_FUSE")) c->force_fuse = atoi(e) ? 1 : 0;
+    c->trace = getenv("UDPDK_RX_TRACE") != nullptr;
+    if (const char *e = getenv("UDPDK_RX_TAILG")) {
+        const int g = atoi(e);
+        if (g == 1 || g == 2) c->force_tailg = g;
+    }
     int rc = -EIO;
     do {
         if (hipSetDevice(device) != hipSuccess) break;
@@ -301,10 +324,22 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
             ok = ok && hipMalloc((void **)&P.res, sizeof(DevResult)) == hipSuccess;
             ok = ok && hipMemset(P.res, 0, sizeof(DevResult)) == hipSuccess;
             ok = ok && hipHostMalloc((void **)&P.h_res, sizeof(DevResult), hipHostMallocDefault) == hipSuccess;
+            ok = ok && hipMalloc((void **)&P.fuse, FUSE_BYTES) == hipSuccess;
+            ok = ok && hipMemset(P.fuse, 0, FUSE_BYTES) == hipSuccess;
+        }
+        // fine-grained (coherent) host memory: the kernels' hint stores go straight to it
+        ok = ok && hipHostMalloc((void **)&c->hint, HINT_BYTES, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess;
+        if (ok) {
+            // a fresh context starts on the two-launch form (as if call 1 had a tile not full):
+            // the fused completion's rewrite of a not-full call is one workgroup's work
+            memset(c->hint, 0, HINT_BYTES);
+            c->hint[UDPDK_HINT_NONFULL] = 1u;
         }
         if (!ok) break;
         // rx_classify needs up to 141 KiB of dynamic LDS (16384 lanes, 8192-frame tiles)
-        if (hipFuncSetAttribute((const void *)rx_classify, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void *)rx_classify<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)classify_lds_bytes(UDPDK_GPU_MAX_LANES, RX_TILE_MAX)) != hipSuccess) break;
+        if (hipFuncSetAttribute((const void *)rx_classify<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)classify_lds_bytes(UDPDK_GPU_MAX_LANES, RX_TILE_MAX)) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)scatter1_lds_bytes(UDPDK_GPU_MAX_LANES)) != hipSuccess) break;
@@ -341,7 +376,7 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
         void *ph[] = {P.st_frames_h, P.st_desc_h};
         for (void *p : ph) if (p) (void)hipHostFree(p);
         void *pd[] = {P.hist, P.partial, P.base, P.agg, P.ticket, P.tile_cnt, P.res, P.st_frames_d,
-                      P.st_desc_d, P.st_out_d};
+                      P.st_desc_d, P.st_out_d, P.fuse};
         for (void *p : pd) if (p) (void)hipFree(p);
         if (P.h_res) (void)hipHostFree(P.h_res);
         if (P.tail) (void)hipEventDestroy(P.tail);
@@ -351,6 +386,7 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
             for (int k = 0; k < 2 * TIMED_KERNELS; ++k) (void)hipEventDestroy(c->sets[i].ev[k]);
         delete[] c->sets;
     }
+    if (c->hint) (void)hipHostFree(c->hint);
     for (Pipe &P : c->pipes)
         if (P.stream) (void)hipStreamDestroy(P.stream);
     delete c;
@@ -608,10 +644,31 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     if (spec && ++P.spec_epoch == 0) P.spec_epoch = 1;       // 0: the zeroed word's tag
     ra.spec_nonfull = spec ? P.res->nonfull : nullptr;
     ra.spec_epoch = P.spec_epoch;
+    // kernel form from the hints of the recent calls (RxArgs::hint)
+    if (++c->rx_seq == 0) c->rx_seq = 1;
+    const uint32_t seq = c->rx_seq;
+    // measured against the latest call the GPU has reached (the host may run tens of calls ahead)
+    const uint32_t done = __atomic_load_n(&c->hint[UDPDK_HINT_DONE], __ATOMIC_RELAXED);
+    auto recent = [&](int k) {
+        const uint32_t v = __atomic_load_n(&c->hint[k], __ATOMIC_RELAXED);
+        return v != 0u && (int32_t)(done - v) <= (int32_t)UDPDK_HINT_WINDOW;
+    };
+    ra.hint = c->hint;
+    ra.seq = seq;
+    const bool fuse = spec && tiles <= UDPDK_FUSE_MAX_TILES &&
+                      (c->force_fuse >= 0 ? c->force_fuse == 1 : !recent(UDPDK_HINT_NONFULL));
+    const int tailg = c->force_tailg ? c->force_tailg : (one_lane && !recent(UDPDK_HINT_TAIL)) ? 1 : 2;
+    if (c->trace)
+        fprintf(stderr, "udpdk_gpu_rx seq %u done %u hint tail %u nonfull %u -> classify<%d>%s\n", seq,
+                done, c->hint[UDPDK_HINT_TAIL], c->hint[UDPDK_HINT_NONFULL], tailg, fuse ? " fused" : "");
+    ra.fuse = fuse ? P.fuse : nullptr;
+    ra.lane_off = o->lane_off_dev;
+    ra.total = &P.res->total;
 
     if (ts) for (int k = 0; k < TIMED_KERNELS; ++k) ts->used[k] = false;
-    HIPC(c, launch(st, ts, 0, true, true, rx_classify, dim3(tiles), dim3(CLS_BLOCK),
-                       classify_lds_bytes(S, T), ra));
+    HIPC(c, launch(st, ts, 0, true, true, tailg == 1 ? rx_classify<1> : rx_classify<2>, dim3(tiles),
+                   dim3(CLS_BLOCK), classify_lds_bytes(S, T), ra));
+    if (fuse) return 0;                        // the last workgroup completed the lane
     if (one_lane) {
         Compact1Args ca;
         ca.meta = o->meta_dev;
@@ -627,6 +684,8 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
         ca.spec = spec ? 1u : 0u;
         ca.spec_nonfull = P.res->nonfull;
         ca.spec_epoch = P.spec_epoch;
+        ca.hint = c->hint;
+        ca.seq = seq;
         if (tiles > COMPACT1_DIRECT_TILES && tiles <= c->partial_cap) {
             // past a few thousand tiles each workgroup's sum over its predecessors costs more
             // than one extra launch scanning the counts once
