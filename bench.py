@@ -58,6 +58,11 @@ def parse():
     p.add_argument("--strong-total", type=int, default=None,
                    help="strong scaling: this many frames in total, split into contiguous equal "
                         "shards over the ranks (SURVEY.md 8(e): one 32 M batch)")
+    p.add_argument("--no-strong", action="store_true",
+                   help="skip the `strong` object (one 32 M-frame config-5 batch over the ranks)")
+    p.add_argument("--strong-pieces", type=int, default=8,
+                   help="`strong`: the batch is this many config-5 shards of --strong-piece frames")
+    p.add_argument("--strong-piece", type=int, default=1 << 22, help="frames per strong-batch piece")
     p.add_argument("--rotate-mib", type=int, default=640, help="device bytes cycled by the loop")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the 1500 B / IMIX side lines")
@@ -711,6 +716,68 @@ def socket_path_lines(specs=((1 << 20, 64, 1024, 5), (1 << 20, 0, 1024, 3), (1 <
     return out
 
 
+def strong_pieces(world: int, rank: int, pieces: int) -> range:
+    """The pieces of the one strong-scaling batch rank `rank` of `world` takes: a contiguous run,
+    pieces split as evenly as they go (8 pieces: 8 / 4 / 2 / 1 per rank at N = 1 / 2 / 4 / 8)."""
+    return range(rank * pieces // world, (rank + 1) * pieces // world)
+
+
+def strong_workload(world: int, rank: int, pieces: int, piece: int) -> F.Workload:
+    """SURVEY.md §8(e)'s strong-scaling batch: ONE batch of pieces x piece 64 B frames (default
+    8 x 4 M = 32 M) over 4096 ports, Zipf-0.99, defined as the concatenation of config 5's shards
+    0..pieces-1 in order (piece p = config_batch(5, shard=p)), so rank r's contiguous part is built
+    from its own pieces alone. At N = 8 every rank's part is config 5's shard: the weak point."""
+    parts = [F.config_batch(5, n=piece, shard=p) for p in strong_pieces(world, rank, pieces)]
+    if len(parts) == 1:
+        w = parts[0]
+    else:
+        nb = sum(x.batch.frames_bytes for x in parts)
+        flat = np.zeros((nb + 255) // 256 * 256 + 256, np.uint8)
+        off, ln, pos = [], [], 0
+        for x in parts:
+            b = x.batch
+            flat[pos:pos + b.frames_bytes] = b.frames[:b.frames_bytes]
+            off.append(b.offset.astype(np.uint64) + pos)
+            ln.append(b.length)
+            pos += b.frames_bytes
+        w = F.Workload(parts[0].name, F.Batch(flat, np.concatenate(off).astype(np.uint32),
+                                              np.concatenate(ln), nb), 4096, 10000)
+    total = pieces * piece
+    w.name = f"{F._nlabel(total)}-64B-4096ports-zipf0.99 ({pieces} x {F._nlabel(piece)} pieces)"
+    return w
+
+
+def strong_line(ctx, world: int, rank: int, barrier, dist, steps: int, warmup: int, pieces: int, piece: int):
+    """Strong scaling: one batch of pieces x piece frames split into contiguous
+    parts over the N ranks (no collective: each part's lanes are the batch's lanes for its frames,
+    shard.merge_lanes), each rank's part processed as one udpdk_gpu_rx call per step, pipelined;
+    the steps bracketed by a barrier + device sync, the MAX wall over ranks; value = the whole
+    batch's frames / that time. Fixed total work, so scaling is "strong"."""
+    w = strong_workload(world, rank, pieces, piece)
+    rx = Rx(ctx, w, 0)
+    depth = auto_depth(w)
+    ctx.pipeline(depth)
+    wall, gpu_step, _, _ = time_loop(rx, steps, warmup, barrier, 0)
+    ctx.pipeline(1)
+    mine = rx.n * steps / wall / 1e6
+    if dist is not None:
+        import torch
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    total = pieces * piece
+    out = {"workload": w.name, "baseline_config": 5, "scaling": "strong", "n_gpus": world,
+           "frames_total": total, "frames_rank0": rx.n, "pieces_rank0": list(strong_pieces(world, rank, pieces)),
+           "value": round(total * steps / wall / 1e6, 2), "unit": "Mpkt/s", "steps": steps,
+           "ms_per_step": round(1e3 * wall / steps, 5), "pipeline_depth": depth,
+           "gbps_pipeline": round(rx.pipeline_bytes() * world * steps / wall / 1e9, 1),
+           "rank0_mpkt_s": round(mine, 2), "rank0_gpu_us_per_step": round(1e3 * gpu_step, 3)}
+    for a in rx.args:
+        a[4].frames.free(); a[4].offset.free(); a[4].length.free()
+        a[5].meta.free(); a[5].lane_off.free(); a[5].lane_pkt.free()
+    return out
+
+
 def scale_line(ctx, world: int, rank: int, barrier, dist, steps: int, warmup: int, rotate: int):
     """The scaling workload (BASELINE.json configs[4], config 5) at this N: each rank its own
     independent 4 M x 64 B shard over 4096 ports, Zipf-0.99 (seed 1000 + rank), pipelined, the K
@@ -782,7 +849,9 @@ def main():
     if args.strong_total:
         frames = -(-args.strong_total // world)          # this rank's contiguous shard
     w = F.config_batch(args.config, n=frames, shard=rank)
-    ctx = abi.GpuContext(device, max_frames=max(w.batch.n, 1 << 22), max_lanes=4096)
+    strong_n = 0 if (args.no_strong or args.strong_total) else \
+        len(strong_pieces(world, rank, args.strong_pieces)) * args.strong_piece
+    ctx = abi.GpuContext(device, max_frames=max(w.batch.n, 1 << 22, strong_n), max_lanes=4096)
     rx = Rx(ctx, w, args.rotate_mib << 20)
     # the timed region (value): consecutive batches pipelined over several streams, no events inside
     if args.pipeline is None:
@@ -827,6 +896,10 @@ def main():
         scale = scale_line(ctx, world, rank, barrier, dist, max(10, args.steps // 4), 5,
                            args.rotate_mib << 20)
         scale["distinct_gpus"] = distinct
+    strong = None
+    if strong_n:
+        strong = strong_line(ctx, world, rank, barrier, dist, max(5, args.steps // 8), 3,
+                             args.strong_pieces, args.strong_piece)
     total_pkts = rx.n * args.steps * world
     mpkt_s = total_pkts / wall / 1e6
     ms_step = 1e3 * wall / args.steps
@@ -877,6 +950,8 @@ def main():
     line["distinct_gpus"] = distinct
     if scale is not None:
         line["scale"] = scale
+    if strong is not None:
+        line["strong"] = strong
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         gdig = gpu_digest(ctx, rx.args[0][5], rx.n, w.n_sockets) if rx.n <= (1 << 22) else None
         res, cores = cpu_baseline(w, args.cpu_seconds, gdig)
@@ -982,6 +1057,20 @@ def dry_run(args, world, rank, dist):
         mine["scale_workload"] = w5.name
         mine["scale_frames"] = w5.batch.n
         mine["scale_digest"] = _digest(w5.batch.frames[:w5.batch.frames_bytes], w5.batch.length)
+        mine["scale_digest_rebased"] = _digest(w5.batch.frames[:w5.batch.frames_bytes], w5.batch.length,
+                                               w5.batch.offset)
+    if not args.no_strong and not args.strong_total:
+        ws = strong_workload(world, rank, args.strong_pieces, args.strong_piece)
+        mine["strong_workload"] = ws.name
+        mine["strong_pieces"] = list(strong_pieces(world, rank, args.strong_pieces))
+        mine["strong_frames"] = ws.batch.n
+        # each piece's bytes, lengths and rebased offsets, cut back out of the rank's batch
+        pd, k = [], args.strong_piece
+        for j in range(len(mine["strong_pieces"])):
+            o = ws.batch.offset[j * k:(j + 1) * k].astype(np.int64)
+            a, b = int(o[0]), int(o[-1]) + int(ws.batch.length[(j + 1) * k - 1])
+            pd.append(_digest(ws.batch.frames[a:b], ws.batch.length[j * k:(j + 1) * k], (o - a).astype(np.uint32)))
+        mine["strong_piece_digests"] = pd
     per_rank = [mine]
     wall = 1.0 + rank
     if dist is not None:

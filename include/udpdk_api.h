@@ -150,6 +150,11 @@ udpdk_gpu_ctx *udpdk_gpu_context(void);
  * to max device ids and returns how many there are (1 without "devices", 0 before udpdk_init). */
 int udpdk_shard_devices(int *devices, int max);
 
+/* The same device list read from a config file without creating any context (no GPU needed):
+ * what udpdk_init(-c cfg_path) would bind, in shard order. Returns the count (1 for a single
+ * "[gpu] device"), -EINVAL for a malformed list, -ENOENT for a missing file. */
+int udpdk_shard_plan(const char *cfg_path, int *devices, int max);
+
 /* With "[gpu] dispatch = rss" (and two or more devices) a poll sends each frame to the shard of
  * its RSS queue instead: one RX queue per device, queue = reta[Toeplitz hash] with
  * udpdk_gpu_rss's hash definition, default key and redirection table (the NIC's ETH_MQ_RX_RSS

@@ -24,10 +24,13 @@ def _run(args, env=None, timeout=240):
                           timeout=timeout, env=e, cwd=ROOT)
 
 
+SMALL = ["--frames", "2048", "--strong-piece", "1024"]
+
+
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_gpus_n_spawns_ranks(n):
-    r = _run(["--gpus", str(n), "--dry-run", "--frames", "2048"])
+    r = _run(["--gpus", str(n), "--dry-run"] + SMALL, timeout=280)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == n and line["baseline_config"] == 2 and line["scaling"] == "weak"
@@ -40,6 +43,35 @@ def test_gpus_n_spawns_ranks(n):
     assert len({p["digest"] for p in ranks}) == n          # independent shards
     assert len({p["scale_digest"] for p in ranks}) == n
     assert line["max_wall"] == float(n)                     # MAX over ranks (rank r reports 1 + r)
+    # strong: the ranks' pieces tile the one 8-piece batch in order
+    assert sum((p["strong_pieces"] for p in ranks), []) == list(range(8))
+    assert sum(p["strong_frames"] for p in ranks) == 8 * 1024
+
+
+@pytest.mark.timeout(400)
+def test_strong_batch_same_at_one_two_and_eight_gpus():
+    """The strong-scaling object measures ONE 8-piece batch at every N: the pieces cut back out of
+    each rank's part (bytes, lengths, rebased offsets) are the same pieces in the same order at
+    N = 1, 2 and 8, and at N = 8 each rank's part is config 5's shard of that rank (the weak
+    point of the curve)."""
+    lines = {}
+    for n in (1, 2, 8):
+        r = _run(["--gpus", str(n), "--dry-run"] + SMALL, timeout=280)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines[n] = json.loads(r.stdout.strip().splitlines()[-1])
+    pieces = {n: sum((p["strong_piece_digests"] for p in l["per_rank"]), []) for n, l in lines.items()}
+    assert len(pieces[1]) == 8 and len(set(pieces[1])) == 8
+    assert pieces[1] == pieces[2] == pieces[8]
+    one = lines[1]["per_rank"][0]
+    assert one["strong_frames"] == 8 * 1024 and one["strong_pieces"] == list(range(8))
+    assert one["strong_workload"].startswith("8192-64B-4096ports-zipf0.99")
+    for p in lines[8]["per_rank"]:
+        assert p["strong_frames"] == 1024
+    # --frames 2048 vs --strong-piece 1024: a piece is config 5 at 1024 frames, seeded by its index
+    r = _run(["--gpus", "8", "--dry-run", "--frames", "1024", "--strong-piece", "1024"], timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for p in json.loads(r.stdout.strip().splitlines()[-1])["per_rank"]:
+        assert p["strong_piece_digests"] == [p["scale_digest_rebased"]]
 
 
 def test_same_workloads_at_one_and_two_gpus():
@@ -56,7 +88,7 @@ def test_same_workloads_at_one_and_two_gpus():
 
 
 def test_strong_scaling_shards():
-    r = _run(["--gpus", "2", "--dry-run", "--strong-total", "5000", "--config", "2"])
+    r = _run(["--gpus", "2", "--dry-run", "--strong-total", "5000", "--config", "2", "--no-strong"])
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["scaling"] == "strong"

@@ -200,6 +200,7 @@ _PROTOS = {
     "udpdk_btable_snapshot": (C.c_int, [C.POINTER(BindSnapshot), C.c_int]),
     "udpdk_gpu_context": (_P, []),
     "udpdk_shard_devices": (C.c_int, [_P, C.c_int]),
+    "udpdk_shard_plan": (C.c_int, [C.c_char_p, _P, C.c_int]),
     "udpdk_shard_frames": (C.c_int, [_P, C.c_int]),
     "udpdk_config_set": (C.c_int, [_P, _P, C.c_uint32]),
     "udpdk_config_get": (C.c_int, [_P, _P, C.POINTER(C.c_uint32)]),

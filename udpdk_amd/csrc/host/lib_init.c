@@ -91,8 +91,9 @@ static char *h_trim(char *s)
 }
 
 /* "[gpu] devices = 0-3,5,5": the RX shard contexts, one per entry, in shard order (a device
- * may repeat: several contexts on one GPU). The first entry is also the main context's device. */
-static int h_parse_devices(const char *v)
+ * may repeat: several contexts on one GPU). The first entry is also the main context's device.
+ * Parsed into dev[H_MAX_DEVS]; returns the count, or -1. */
+static int h_parse_device_list(const char *v, int *dev)
 {
     uint32_t n = 0;
     const char *p = v;
@@ -109,17 +110,63 @@ static int h_parse_devices(const char *v)
         }
         for (long d = a; d <= b; d++) {
             if (n == H_MAX_DEVS) return -1;
-            g_udpdk.shard_dev[n++] = (int)d;
+            dev[n++] = (int)d;
         }
         while (*p == ' ' || *p == '\t') p++;
         if (*p == ',') p++;
         else if (*p) return -1;
         while (*p == ' ' || *p == '\t') p++;
     }
-    if (!n) return -1;
-    g_udpdk.n_shards = n;
+    return n ? (int)n : -1;
+}
+
+static int h_parse_devices(const char *v)
+{
+    const int n = h_parse_device_list(v, g_udpdk.shard_dev);
+    if (n < 0) return -1;
+    g_udpdk.n_shards = (uint32_t)n;
     g_udpdk.gpu_device = g_udpdk.shard_dev[0];
     return 0;
+}
+
+/* The device plan udpdk_init would build from the config file, without touching a GPU: the
+ * contexts in shard order ("[gpu] devices", two or more entries) or the one context of
+ * "[gpu] device" (default 0). Every context of the plan binds its device (hipSetDevice) on each
+ * C-ABI call, so each shard's pool thread allocates, copies and launches on its own GPU. */
+int udpdk_shard_plan(const char *cfg_path, int *devices, int max)
+{
+    if (!cfg_path || max < 0 || (max && !devices)) return -EINVAL;
+    FILE *f = fopen(cfg_path, "r");
+    if (!f) return -ENOENT;
+    char line[512], section[64] = "";
+    int dev[H_MAX_DEVS], n = 1, rc = 0;
+    dev[0] = 0;
+    while (fgets(line, sizeof(line), f)) {
+        char *s = h_trim(line);
+        if (!*s || *s == '#' || *s == ';') continue;
+        if (*s == '[') {
+            char *e = strchr(s, ']');
+            if (!e) { rc = -EINVAL; break; }
+            *e = 0;
+            snprintf(section, sizeof(section), "%s", s + 1);
+            continue;
+        }
+        char *eq = strchr(s, '=');
+        if (!eq || strcmp(section, "gpu")) continue;
+        *eq = 0;
+        const char *k = h_trim(s), *v = h_trim(eq + 1);
+        if (!strcmp(k, "device")) {
+            dev[0] = atoi(v);
+            n = 1;
+        } else if (!strcmp(k, "devices")) {
+            n = h_parse_device_list(v, dev);
+            if (n < 0) { rc = -EINVAL; break; }
+        }
+    }
+    fclose(f);
+    if (rc) return rc;
+    for (int k = 0; k < n && k < max; k++) devices[k] = dev[k];
+    return n;
 }
 
 /* Minimal INI reader for the keys the reference understands plus a [gpu] section. */
