@@ -2,7 +2,8 @@
 context creation) and compared with the oracle bit for bit: the fused completion (the last
 workgroup writes lane_off and the total; with a tile before the last not full it rewrites the
 later tiles' entries from the verdict words) against rx_classify + rx_compact1, and
-rx_classify<1> (one tail chunk group in flight) against <2>. The automatic choice between them
+rx_classify<1> (one tail chunk group in flight) against <2>, and a bind table of at most 8 ports
+passed in the kernel arguments against the port-table loads. The automatic choice between them
 (kernel hints, udpdk_gpu.hip) only picks the faster of two exact forms."""
 import os
 
@@ -14,17 +15,23 @@ from udpdk_amd import abi, frames as F
 
 pytestmark = pytest.mark.gpu
 
-FORMS = [(1, 1), (1, 2), (0, 1), (0, 2)]
+# (fused completion, tail chunk groups, bind table of <= 8 ports in the kernel arguments)
+FORMS = [(1, 1, 1), (1, 2, 1), (0, 1, 1), (0, 2, 1), (1, 1, 0), (0, 2, 0)]
+ENV = ("UDPDK_RX_FUSE", "UDPDK_RX_TAILG", "UDPDK_RX_NO_INLINE")
 
 
-@pytest.fixture(scope="module", params=FORMS, ids=lambda f: f"fuse{f[0]}-g{f[1]}")
+@pytest.fixture(scope="module", params=FORMS, ids=lambda f: f"fuse{f[0]}-g{f[1]}-inl{f[2]}")
 def form_ctx(request):
-    fuse, g = request.param
-    old = {k: os.environ.get(k) for k in ("UDPDK_RX_FUSE", "UDPDK_RX_TAILG")}
+    fuse, g, inl = request.param
+    old = {k: os.environ.get(k) for k in ENV}
     os.environ["UDPDK_RX_FUSE"] = str(fuse)
     os.environ["UDPDK_RX_TAILG"] = str(g)
+    if not inl:
+        os.environ["UDPDK_RX_NO_INLINE"] = "1"
+    else:
+        os.environ.pop("UDPDK_RX_NO_INLINE", None)
     try:
-        ctx = abi.GpuContext(0, max_frames=1 << 21, max_lanes=16)
+        ctx = abi.GpuContext(0, max_frames=1 << 21, max_lanes=64)
     finally:
         for k, v in old.items():
             if v is None:
@@ -131,6 +138,30 @@ def test_tail_forms(form_ctx, seed):
     lists = {abi.raw_port(10001): [(0, 0, 0)], abi.raw_port(10002): [(0, 1, 0)]}
     want, got = _run(form_ctx, m, lists, 8)
     _same(want, got, f"mixed seed={seed}")
+
+
+IP1, IP9 = "172.31.100.1", "172.31.100.9"
+
+
+@pytest.mark.parametrize("nports", [5, 8, 9])
+def test_bind_table_sizes(form_ctx, nports):
+    """Ports with fan-out (REUSEPORT pairs), a specific address that does not match, ANY ahead of
+    a specific binding, on 5, 8 (both in the arguments) and 9 (the port table) bound ports."""
+    ports = [10001 + i for i in range(nports)]
+    lists = {}
+    for i, p in enumerate(ports):
+        kind = i % 4
+        if kind == 0:
+            lists[abi.raw_port(p)] = [(0, i, 0)]
+        elif kind == 1:
+            lists[abi.raw_port(p)] = [(abi.raw_ip(IP1), i, 1), (abi.raw_ip(IP1), 20 + i, 1)]
+        elif kind == 2:
+            lists[abi.raw_port(p)] = [(abi.raw_ip(IP9), i, 0)]
+        else:
+            lists[abi.raw_port(p)] = [(0, i, 1), (abi.raw_ip(IP1), 20 + i, 1)]
+    m = F.mixed_batch(50 + nports, 4000, ports, [9, 20000, 65535], [IP1, IP9])
+    want, got = _run(form_ctx, m, lists, 32)
+    _same(want, got, f"ports={nports}")
 
 
 @pytest.mark.parametrize("cfg", [1, 2, 3])

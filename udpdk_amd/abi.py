@@ -226,7 +226,13 @@ def lib() -> C.CDLL:
             raise RuntimeError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build())")
         L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
         for name, (res, args) in _PROTOS.items():
-            f = getattr(L, name)
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                # an A/B build of an older tree (tools/ab.py) may predate a newer entry point
+                if os.environ.get("UDPDK_LIB_OVERRIDE"):
+                    continue
+                raise
             f.restype = res
             f.argtypes = args
         _lib = L

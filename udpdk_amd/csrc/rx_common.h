@@ -110,7 +110,15 @@ struct RxArgs {
     // call ran a tail pass, hint[UDPDK_HINT_NONFULL] = seq when a tile before the last was not full
     uint32_t *hint;
     uint32_t seq;
+    // a bind table of at most UDPDK_INLINE_PORTS bound ports rides in the arguments (inl != 0):
+    // the demux compares the frame's raw dst port with inl_port[0 .. n_inl) and takes that port's
+    // 16-byte entry from inl_ent, no port-table load (the bindings list still comes from binds)
+    uint32_t inl;
+    uint32_t n_inl;
+    uint32_t inl_port[8];
+    uint4 inl_ent[8];
 };
+#define UDPDK_INLINE_PORTS 8u
 #define UDPDK_FUSE_SHARDS 8u
 #define UDPDK_FUSE_MAX_TILES 65535u          // fan-in fields: 16-bit arrival and not-full counts
 #define UDPDK_HINT_TAIL 0

@@ -437,6 +437,9 @@ rx_classify(RxArgs a)
 
     __shared__ uint32_t tail_any;           // some wave of the tile ran a tail pass (kernel hint)
     if (tid == 0) tail_any = 0u;            // (ordered by the staging barrier)
+    __shared__ uint4 inl_tab[UDPDK_INLINE_PORTS + 1];   // RxArgs::inl entries + a zero slot
+    if (a.inl && tid <= UDPDK_INLINE_PORTS)
+        inl_tab[tid] = tid < a.n_inl ? a.inl_ent[tid] : make_uint4(0, 0, 0, 0);
     stage(0);
     __syncthreads();
     uint32_t st = __builtin_amdgcn_readfirstlane(w);             // wave-uniform step (SGPR)
@@ -707,8 +710,23 @@ rx_classify(RxArgs a)
             uint2 S[SPR];
 #pragma unroll
             for (uint32_t j = 0; j < SPR; ++j) S[j] = dstash[((st - RSTEPS + CLS_WAVES * j) * 64 + lane) & (RX_ROUND - 1u)];
+            if (a.inl) {
+                // few bound ports: their entries came with the arguments and sit in LDS (slot
+                // n_inl is zero: an unbound port), so the lookup is an LDS read, not a dependent
+                // global load
 #pragma unroll
-            for (uint32_t j = 0; j < SPR; ++j) E[j] = a.port_tab[S[j].x & 0xFFFFu];
+                for (uint32_t j = 0; j < SPR; ++j) {
+                    const uint32_t pt = S[j].x & 0xFFFFu;
+                    uint32_t k = a.n_inl;
+#pragma unroll
+                    for (uint32_t q = 0; q < UDPDK_INLINE_PORTS; ++q)
+                        k = q < a.n_inl && pt == a.inl_port[q] ? q : k;
+                    E[j] = inl_tab[k];
+                }
+            } else {
+#pragma unroll
+                for (uint32_t j = 0; j < SPR; ++j) E[j] = a.port_tab[S[j].x & 0xFFFFu];
+            }
 #pragma unroll
             for (uint32_t j = 0; j < SPR; ++j) {
                 const uint32_t i = (st - RSTEPS + CLS_WAVES * j) * 64 + lane;

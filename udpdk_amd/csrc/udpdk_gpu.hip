@@ -100,6 +100,9 @@ struct udpdk_gpu_ctx {
     uint4 *slots = nullptr;
     uint32_t slots_cap = 0, n_slots = 0;
     uint32_t n_lanes = 1, lane_mask = 0xFFFFFFFFu, key_bits = 0, max_fanout = 0;
+    // the bound ports when there are at most UDPDK_INLINE_PORTS (RxArgs::inl)
+    uint32_t inl = 0, n_inl = 0, inl_port[UDPDK_INLINE_PORTS] = {};
+    uint4 inl_ent[UDPDK_INLINE_PORTS] = {};
     uint32_t one_lane_tile = 0;    // UDPDK_ONE_LANE_TILE (diagnostic): single-lane tile override
     // Kernel hints (pinned host memory the kernels write, RxArgs::hint): the call sequence number
     // of the last call that ran a tail pass / had a tile before the last not full. The single-lane
@@ -110,6 +113,7 @@ struct udpdk_gpu_ctx {
     int force_fuse = -1;           // UDPDK_RX_FUSE=0/1 (tests, A/B): fused completion off / always
     int force_tailg = 0;           // UDPDK_RX_TAILG=1/2 (tests, A/B): rx_classify<G> always
     bool trace = false;            // UDPDK_RX_TRACE (diagnostic): the form of every call on stderr
+    bool no_inline = false;        // UDPDK_RX_NO_INLINE (tests, A/B): always the port-table loads
     bool have_snapshot = false;
 
     // RX workspace, one set per pipe
@@ -291,6 +295,7 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
     }
     if (const char *e = getenv("UDPDK_RX_FUSE")) c->force_fuse = atoi(e) ? 1 : 0;
     c->trace = getenv("UDPDK_RX_TRACE") != nullptr;
+    c->no_inline = getenv("UDPDK_RX_NO_INLINE") != nullptr;
     if (const char *e = getenv("UDPDK_RX_TAILG")) {
         const int g = atoi(e);
         if (g == 1 || g == 2) c->force_tailg = g;
@@ -484,7 +489,8 @@ int udpdk_gpu_bind_snapshot_upload(udpdk_gpu_ctx *c, const udpdk_bind_snapshot_t
     if (s->n_lanes == 0 || s->n_lanes > c->max_lanes || s->n_binds > UDPDK_GPU_MAX_BINDS) return -EINVAL;
     if (s->n_slots && !s->slots) return -EINVAL;
     std::vector<uint4> tab(UDPDK_UDP_PORTS, make_uint4(0, 0, 0, 0));
-    uint32_t maxfan = 0;
+    uint32_t maxfan = 0, nports = 0, iport[UDPDK_INLINE_PORTS] = {};
+    uint4 ient[UDPDK_INLINE_PORTS] = {};
     for (uint32_t p = 0; p < UDPDK_UDP_PORTS; ++p) {
         const uint32_t cnt = s->port_count[p];
         if (!cnt) continue;
@@ -493,6 +499,11 @@ int udpdk_gpu_bind_snapshot_upload(udpdk_gpu_ctx *c, const udpdk_bind_snapshot_t
         const udpdk_binding_t &b0 = s->binds[first];
         tab[p] = make_uint4(cnt, first, b0.ip, (uint32_t)b0.sockfd | (b0.reuse ? 0x80000000u : 0u));
         maxfan = std::max(maxfan, cnt);
+        if (nports < UDPDK_INLINE_PORTS) {
+            iport[nports] = p;
+            ient[nports] = tab[p];
+        }
+        ++nports;
     }
     std::vector<uint2> b(s->n_binds ? s->n_binds : 1);
     for (uint32_t i = 0; i < s->n_binds; ++i) {
@@ -536,6 +547,12 @@ int udpdk_gpu_bind_snapshot_upload(udpdk_gpu_ctx *c, const udpdk_bind_snapshot_t
     while ((1u << kb) < s->n_lanes) ++kb;
     c->key_bits = kb;
     c->max_fanout = maxfan;
+    c->inl = nports <= UDPDK_INLINE_PORTS && !c->no_inline ? 1u : 0u;
+    c->n_inl = c->inl ? nports : 0u;
+    for (uint32_t k = 0; k < UDPDK_INLINE_PORTS; ++k) {
+        c->inl_port[k] = iport[k];
+        c->inl_ent[k] = ient[k];
+    }
     c->have_snapshot = true;
     return 0;
 }
@@ -637,6 +654,12 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     ra.n_tiles = tiles;
     ra.lane_mask = c->lane_mask;
     ra.n_lanes = S;
+    ra.inl = c->inl;
+    ra.n_inl = c->n_inl;
+    for (uint32_t k = 0; k < UDPDK_INLINE_PORTS; ++k) {
+        ra.inl_port[k] = c->inl_port[k];
+        ra.inl_ent[k] = c->inl_ent[k];
+    }
     // speculative single-lane entries from classify (see RxArgs::spec_pkt)
     const bool spec = UDPDK_SPEC_COMPACT && one_lane && T == (uint32_t)RX_ROUND && CLS_BLOCK * 4 == RX_ROUND;
     ra.spec_pkt = spec ? o->lane_pkt_dev : nullptr;
