@@ -87,6 +87,21 @@ def test_rss_config4(gpu_ctx, nq, n):
     assert go[-1] == w.batch.n and np.all(np.diff(go.astype(np.int64)) > 0)
 
 
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_rss_base_forms(gpu_ctx, monkeypatch, fuse):
+    """The queue bases from the last rss_hash workgroup (fused, the default) and from the separate
+    rss_base launch (UDPDK_RSS_FUSE=0, read by udpdk_gpu_rss_config), on a ragged IMIX batch, a
+    small mixed one and a single frame, alternating on one context (the fan-in words reset)."""
+    monkeypatch.setenv("UDPDK_RSS_FUSE", fuse)
+    w = F.config_batch(4, n=300001)
+    small = F.mixed_batch(13, 2500, [10001, 10002], [9], ["172.31.100.1"])
+    one = F.mixed_batch(1, 1, [10001], [9], ["172.31.100.1"])
+    for b, nq in ((w.batch, 8), (small, 5), (one, 2), (w.batch, 3), (small, 64)):
+        (wh, wo, wp), (gh, go, gp) = _both(gpu_ctx, b, abi.rss_conf(nq))
+        assert np.array_equal(wh, gh) and np.array_equal(wo, go) and np.array_equal(wp, gp)
+        assert go[-1] == b.n
+
+
 def test_rss_edges(gpu_ctx):
     """Empty batch, bad configurations, a single frame; the RSS call needs a configuration."""
     import ctypes as C

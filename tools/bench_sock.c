@@ -8,9 +8,17 @@
  *
  * Sockets 0..S-1 are bound ANY to ports 10000..10000+S-1; frame i goes to port 10000 + i % S
  * (uniform), so each ring receives n / S datagrams per poll (n / S must stay <= 2047, the ring).
- * Prints one JSON object: poll and recvfrom time per batch, datagrams/s of each and end to end.
+ * Prints one JSON object: poll and recvfrom time per batch, datagrams/s of each and end to end
+ * (the two one after the other on one thread), then the reference's own arrangement (a poller
+ * running beside the application, udpdk_poller.c:443-446 vs the app's recvfrom loop): a poller
+ * thread polls batch k + 1 while the application thread drains batch k, at most two batches in
+ * the rings (each holds n / S <= 1023 datagrams per batch of a 2047-entry ring), and the rate is
+ * the datagrams the application received over the wall time of all reps ("overlap_mdgram_s").
  */
 #include <arpa/inet.h>
+#include <errno.h>
+#include <pthread.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -58,6 +66,34 @@ static void make_frame(uint8_t *f, uint32_t len, uint16_t dport, uint32_t seq)
     u[4] = (uint8_t)(ul >> 8); u[5] = (uint8_t)ul;
     u[6] = u[7] = 0;
     for (uint32_t i = 42; i < len; i++) f[i] = (uint8_t)(seq * 31u + i);
+}
+
+struct poller {
+    const uint8_t *fr;
+    uint64_t bytes;
+    const uint32_t *off;
+    const uint16_t *len;
+    uint32_t n;
+    int reps;
+    atomic_int posted;       /* batches admitted to the rings */
+    atomic_int consumed;     /* batches the application drained */
+    int err;
+};
+
+static void *poller_main(void *arg)
+{
+    struct poller *P = arg;
+    for (int r = 0; r < P->reps; r++) {
+        while (atomic_load(&P->consumed) < r - 1) ;          /* at most two batches in the rings */
+        udpdk_rx_stats_t st;
+        if (udpdk_poll_rx(P->fr, P->bytes, P->off, P->len, NULL, P->n, &st) < 0) {
+            P->err = errno;
+            atomic_store(&P->posted, P->reps + 1);
+            return NULL;
+        }
+        atomic_store(&P->posted, r + 1);
+    }
+    return NULL;
 }
 
 int main(int argc, char **argv)
@@ -124,12 +160,34 @@ int main(int argc, char **argv)
             pbytes += pb;
         }
     }
+    /* the reference's arrangement: poller beside the application */
+    const int oreps = 2 * reps + 2;
+    struct poller P = {fr, bytes, off, len, n, oreps, 0, 0, 0};
+    pthread_t th;
+    uint64_t ogot = 0;
+    const double o0 = now();
+    if (pthread_create(&th, NULL, poller_main, &P)) { perror("pthread_create"); return 1; }
+    for (int r = 0; r < oreps; r++) {
+        while (atomic_load(&P.posted) <= r) ;
+        if (P.err) { errno = P.err; perror("udpdk_poll_rx (poller thread)"); return 1; }
+        const uint32_t per = n / (uint32_t)S;
+        for (int s = 0; s < S; s++) {
+            const uint32_t want = per + ((uint32_t)s < n % (uint32_t)S ? 1u : 0u);
+            for (uint32_t k = 0; k < want; k++) {
+                if (udpdk_recvfrom(s, buf, sizeof(buf), 0, NULL, NULL) < 0) { perror("udpdk_recvfrom"); return 1; }
+                ogot++;
+            }
+        }
+        atomic_store(&P.consumed, r + 1);
+    }
+    const double o1 = now();
+    pthread_join(th, NULL);
     const double dg = (double)got / reps;
-    printf("{\"frames\": %u, \"frame_bytes\": %s, \"sockets\": %d, \"reps\": %d, "
+    printf("{\"overlap_mdgram_s\": %.2f, \"overlap_batches\": %d, \"frames\": %u, \"frame_bytes\": %s, \"sockets\": %d, \"reps\": %d, "
            "\"poll_ms\": %.3f, \"recv_ms\": %.3f, \"poll_mdgram_s\": %.2f, \"recv_mdgram_s\": %.2f, "
            "\"end_to_end_mdgram_s\": %.2f, \"end_to_end_frame_gbps\": %.2f, \"delivered_per_batch\": %.0f, "
            "\"payload_bytes_per_batch\": %.0f}\n",
-           n, fsz ? argv[3] : "\"IMIX\"", S, reps, 1e3 * t_poll / reps, 1e3 * t_recv / reps,
+           (double)ogot / (o1 - o0) / 1e6, oreps, n, fsz ? argv[3] : "\"IMIX\"", S, reps, 1e3 * t_poll / reps, 1e3 * t_recv / reps,
            dg / (t_poll / reps) / 1e6, dg / (t_recv / reps) / 1e6, dg / ((t_poll + t_recv) / reps) / 1e6,
            (double)bytes / ((t_poll + t_recv) / reps) / 1e9, dg, (double)pbytes / reps);
     udpdk_gpu_host_free(udpdk_gpu_context(), fr);

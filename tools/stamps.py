@@ -10,7 +10,7 @@ sys.path.insert(0, ROOT)
 import numpy as np
 from udpdk_amd import abi, frames as F
 
-PH = ["prologue", "window wait+fields", "header sums", "demux pass", "-", "descriptor staging+barrier",
+PH = ["prologue", "window wait+fields", "header sums", "demux pass", "fused completion", "descriptor staging+barrier",
       "state+stash+tail+next window", "counters+tile end"]
 L = abi.lib()
 L.udpdk_gpu_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]

@@ -120,6 +120,34 @@ struct RxArgs {
 };
 #define UDPDK_INLINE_PORTS 8u
 #define UDPDK_FUSE_SHARDS 8u
+
+// Launch completion by the last workgroup (rx_classify's fused single-lane completion, rss_hash's
+// fused queue bases): called by ONE thread of each workgroup after every wave of it drained its
+// written-through stores behind a barrier (cdna_hip_programming.md Guideline 16). Adds
+// {1 arrival << 48 | payload} to the fan-in word of its shard (tile mod 8, fuse[16 s], 128 B
+// apart: 1024 arrivals on one word serialise, tools/probe/ticket_probe.hip); the shard's last
+// arrival adds the shard's payload sum to the top word fuse[16 x 8]; the top's last arrival
+// returns true with the launch's payload sum (< 2^48) in *fin. Each word is zeroed again by its
+// last arrival, so the next launch on the same words starts from zeros.
+__device__ __forceinline__ bool fanin_arrive(unsigned long long *fuse, uint32_t tile, uint32_t n_tiles,
+                                             unsigned long long payload, unsigned long long *fin)
+{
+    constexpr unsigned long long LOW = (1ull << 48) - 1ull;
+    const uint32_t s = tile & (UDPDK_FUSE_SHARDS - 1u);
+    const uint32_t ns = (n_tiles - 1u - s) / UDPDK_FUSE_SHARDS + 1u;     // tiles of shard s
+    const unsigned long long mine = (1ull << 48) | payload;
+    unsigned long long *sw = fuse + 16u * s;
+    const unsigned long long now = __hip_atomic_fetch_add(sw, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + mine;
+    if ((uint32_t)(now >> 48) != ns) return false;
+    __hip_atomic_store(sw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long m2 = (1ull << 48) | (now & LOW);
+    unsigned long long *tw = fuse + 16u * UDPDK_FUSE_SHARDS;
+    const unsigned long long now2 = __hip_atomic_fetch_add(tw, m2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + m2;
+    if ((uint32_t)(now2 >> 48) != (n_tiles < UDPDK_FUSE_SHARDS ? n_tiles : UDPDK_FUSE_SHARDS)) return false;
+    __hip_atomic_store(tw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *fin = now2 & LOW;
+    return true;
+}
 #define UDPDK_FUSE_MAX_TILES 65535u          // fan-in fields: 16-bit arrival and not-full counts
 #define UDPDK_HINT_TAIL 0
 #define UDPDK_HINT_NONFULL 16                // its own 64-byte line
@@ -287,6 +315,11 @@ struct RssArgs {
     uint32_t hash_types;      // bit 0: IPv4 2-tuple, bit 1: unfragmented IPv4 UDP 4-tuple
     uint32_t n_tiles;
     uint32_t qmajor;
+    // fused queue bases (qmajor): the last rss_hash workgroup scans the histogram into
+    // queue_off / total / the scatter's bases (fan-in words, zero between calls); null: rss_base
+    unsigned long long *fuse;
+    uint32_t *queue_off;
+    uint32_t *total;
 };
 __global__ void rss_hash(RssArgs a);
 __global__ void rss_scatter(RssArgs a);

@@ -230,28 +230,11 @@ __device__ __forceinline__ void classify_complete(const RxArgs &a, uint32_t tile
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every wave: its stores written through
     __syncthreads();
     if (tid == 0) {
-        const uint32_t s = tile & (UDPDK_FUSE_SHARDS - 1u);
-        const uint32_t ns = (a.n_tiles - 1u - s) / UDPDK_FUSE_SHARDS + 1u;   // tiles of shard s
+        // payload: {tiles before the last that were not full << 32 | deliveries}
         const bool nonfull = tile + 1u < a.n_tiles && tcount != a.tile_frames;
-        const unsigned long long mine = (1ull << 48) | (nonfull ? 1ull << 32 : 0ull) | tcount;
-        unsigned long long *sw = a.fuse + 16u * s;
-        const unsigned long long now =
-            __hip_atomic_fetch_add(sw, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + mine;
-        uint32_t last = 0;
         unsigned long long fin = 0;
-        if ((uint32_t)(now >> 48) == ns) {
-            __hip_atomic_store(sw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long m2 = (1ull << 48) | (now & 0xFFFFFFFFFFFFull);
-            unsigned long long *tw = a.fuse + 16u * UDPDK_FUSE_SHARDS;
-            const unsigned long long now2 =
-                __hip_atomic_fetch_add(tw, m2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + m2;
-            if ((uint32_t)(now2 >> 48) == min(a.n_tiles, (uint32_t)UDPDK_FUSE_SHARDS)) {
-                __hip_atomic_store(tw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                last = 1;
-                fin = now2;
-            }
-        }
-        fz[0] = last;
+        const bool last = fanin_arrive(a.fuse, tile, a.n_tiles, (nonfull ? 1ull << 32 : 0ull) | tcount, &fin);
+        fz[0] = last ? 1u : 0u;
         fz[1] = (uint32_t)fin;                              // deliveries of the call
         fz[2] = (uint32_t)(fin >> 32) & 0xFFFFu;            // tiles (not the last) not full
     }
@@ -921,10 +904,6 @@ rx_classify(RxArgs a)
             for (uint32_t i = tid; i < nv; i += CLS_BLOCK) dst[i] = mstage[i];
         }
     }
-#ifdef UDPDK_STAMPS
-    STAMP_END();
-    if (a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
-#endif
     if (a.n_lanes == 1u) {
         if (tid == 0) {
             if (fuse)
@@ -951,6 +930,11 @@ rx_classify(RxArgs a)
             __hip_atomic_store(&a.hint[UDPDK_HINT_DONE], a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (fuse) classify_complete(a, tile, tcount, tid, lane, w);
+#ifdef UDPDK_STAMPS
+    STAMP(4);                                              // slot 4: fused completion
+    STAMP_END();
+    if (a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
+#endif
 }
 template __global__ void rx_classify<1>(RxArgs a);
 template __global__ void rx_classify<2>(RxArgs a);

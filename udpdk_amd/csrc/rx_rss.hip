@@ -46,6 +46,67 @@ __device__ __forceinline__ unsigned long long peers_of(uint32_t key, uint32_t bi
     return peers;
 }
 
+// The fused form of rss_base, run by the last rss_hash workgroup (RssArgs::fuse): the same
+// exclusive scan of the queue-major histogram as one array, in passes of 32 entries per thread
+// (8 x 16-byte sc1 loads, written through by the other workgroups), a running carry between
+// passes; queue_off[q] = the scanned value at q * T, queue_off[Q] = total.
+__device__ void rss_scan_last(uint32_t *hist, uint32_t n, uint32_t T, uint32_t *queue_off, uint32_t *total)
+{
+    __shared__ uint32_t wsum[RSS_BLOCK / 64];
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+    const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(hist, (short)0, (int)(4u * n), 0x00020000);
+    constexpr uint32_t PER = 32;
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += PER * RSS_BLOCK) {
+        const uint32_t k0 = b0 + PER * tid;
+        uint32_t v[PER];
+#pragma unroll
+        for (uint32_t i = 0; i < PER / 4u; ++i) {
+            const uint4 q = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(hr, (int)(4u * k0 + 16u * i), 0, 16));
+            v[4 * i] = q.x; v[4 * i + 1] = q.y; v[4 * i + 2] = q.z; v[4 * i + 3] = q.w;
+        }
+        uint32_t sum = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; ++i) sum += v[i];
+        uint32_t incl = sum;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t u = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += u;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t run = carry + incl - sum, grand = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < RSS_BLOCK / 64; ++i) {
+            run += i < w ? wsum[i] : 0u;
+            grand += wsum[i];
+        }
+        uint32_t next = k0 < n ? ((k0 + T - 1u) / T) * T : 0xFFFFFFFFu;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; ++i) {
+            if (k0 + i == next) {
+                queue_off[next / T] = run;
+                next += T;
+            }
+            const uint32_t x = v[i];
+            v[i] = run;
+            run += x;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < PER / 4u; ++i)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, make_uint4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3])),
+                hr, (int)(4u * k0 + 16u * i), 0, 0);
+        carry += grand;
+        __syncthreads();                                   // wsum read by every wave
+    }
+    if (tid == 0) {
+        queue_off[n / T] = carry;
+        *total = carry;
+    }
+}
+
 } // namespace
 
 __global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
@@ -135,8 +196,28 @@ __global__ void __launch_bounds__(RSS_BLOCK) rss_hash(RssArgs a)
             atomicAdd(&hist[q], (uint32_t)__popcll(peers));
     }
     __syncthreads();
+    if (!a.fuse) {
+        for (uint32_t q = tid; q < a.n_queues; q += RSS_BLOCK)
+            a.hist[a.qmajor ? (size_t)q * a.n_tiles + tile : (size_t)tile * a.n_queues + q] = hist[q];
+        return;
+    }
+    // fused queue bases (queue-major histogram): the row written through and drained, then the
+    // launch's last workgroup scans the histogram (rss_base's work, no third launch)
+    __shared__ uint32_t last;
     for (uint32_t q = tid; q < a.n_queues; q += RSS_BLOCK)
-        a.hist[a.qmajor ? (size_t)q * a.n_tiles + tile : (size_t)tile * a.n_queues + q] = hist[q];
+        __hip_atomic_store(&a.hist[(size_t)q * a.n_tiles + tile], hist[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long fin;
+        last = fanin_arrive(a.fuse, tile, a.n_tiles, 0ull, &fin) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last) return;
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    rss_scan_last(a.hist, a.n_queues * a.n_tiles, a.n_tiles, a.queue_off, a.total);
 }
 
 // The scan between rss_hash and rss_scatter for up to RSS_BASE_MAX histogram entries, in one

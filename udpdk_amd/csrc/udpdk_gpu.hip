@@ -136,6 +136,8 @@ struct udpdk_gpu_ctx {
     uint32_t *rss_ktab = nullptr;             // [12][256] key windows
     uint8_t *rss_qid = nullptr;
     uint32_t *rss_hist = nullptr, *rss_partial = nullptr, *rss_total = nullptr;
+    unsigned long long *rss_fuse = nullptr;   // rss_hash fan-in words (fused queue bases)
+    bool rss_no_fuse = false;                 // UDPDK_RSS_FUSE=0 (tests, A/B): the rss_base launch
 
     // timing
     uint32_t timing_every = 0;                // 0 off, N: events on every Nth call
@@ -342,10 +344,12 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
         }
         if (!ok) break;
         // rx_classify needs up to 141 KiB of dynamic LDS (16384 lanes, 8192-frame tiles)
+        const int cls_lds = (int)std::min<uint32_t>(classify_lds_bytes(UDPDK_GPU_MAX_LANES, RX_TILE_MAX),
+                                                    160u * 1024u - 1024u);   // static LDS besides
         if (hipFuncSetAttribute((const void *)rx_classify<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)classify_lds_bytes(UDPDK_GPU_MAX_LANES, RX_TILE_MAX)) != hipSuccess) break;
+                                cls_lds) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_classify<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)classify_lds_bytes(UDPDK_GPU_MAX_LANES, RX_TILE_MAX)) != hipSuccess) break;
+                                cls_lds) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)scatter1_lds_bytes(UDPDK_GPU_MAX_LANES)) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatterw, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -373,7 +377,7 @@ int udpdk_gpu_ctx_destroy(udpdk_gpu_ctx *c)
     reasm_destroy(c->reasm);
     c->reasm = nullptr;
     for (void *p : {(void *)c->rss_reta, (void *)c->rss_ktab, (void *)c->rss_qid, (void *)c->rss_hist,
-                    (void *)c->rss_partial, (void *)c->rss_total})
+                    (void *)c->rss_partial, (void *)c->rss_total, (void *)c->rss_fuse})
         if (p) (void)hipFree(p);
     void *dev[] = {c->port_tab, c->binds, c->slots};
     for (void *p : dev) if (p) (void)hipFree(p);
@@ -1091,6 +1095,12 @@ int udpdk_gpu_rss_config(udpdk_gpu_ctx *c, const udpdk_rss_conf_t *conf)
         HIPC(c, hipMalloc((void **)&c->rss_hist, (size_t)tiles * RSS_MAX_QUEUES * 4));
         HIPC(c, hipMalloc((void **)&c->rss_partial, (size_t)ceil_div(tiles, SCAN_COL_CHUNK) * RSS_MAX_QUEUES * 4));
         HIPC(c, hipMalloc((void **)&c->rss_total, 64));
+        HIPC(c, hipMalloc((void **)&c->rss_fuse, FUSE_BYTES));
+        HIPC(c, hipMemset(c->rss_fuse, 0, FUSE_BYTES));
+    }
+    {
+        const char *e = getenv("UDPDK_RSS_FUSE");
+        c->rss_no_fuse = e && atoi(e) == 0;
     }
     HIPC(c, hipMemcpy(c->rss_reta, conf->reta, conf->reta_size * sizeof(uint16_t), hipMemcpyHostToDevice));
     // Toeplitz key windows per (input byte position, byte value): win(b) = key bits [b, b + 32)
@@ -1156,6 +1166,11 @@ int udpdk_gpu_rss(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rss_
     const uint32_t tiles = ceil_div(bt->n, RSS_TILE);
     a.n_tiles = tiles;
     a.qmajor = tiles * S <= RSS_BASE_MAX ? 1u : 0u;
+    // queue-major histogram: the last rss_hash workgroup scans it (no rss_base launch)
+    const bool fuse = a.qmajor && !c->rss_no_fuse && tiles <= UDPDK_FUSE_MAX_TILES;
+    a.fuse = fuse ? c->rss_fuse : nullptr;
+    a.queue_off = o->queue_off_dev;
+    a.total = c->rss_total;
     hipLaunchKernelGGL(rss_hash, dim3(tiles), dim3(RSS_BLOCK), 0, st, a);
     HIPC(c, hipGetLastError());
     ScanArgs sa;
@@ -1167,7 +1182,9 @@ int udpdk_gpu_rss(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rss_
     sa.n_elems = tiles * S;
     sa.n_tiles = tiles;
     sa.n_lanes = S;
-    if (a.qmajor) {
+    if (fuse) {
+        // (the bases were written by rss_hash's last workgroup)
+    } else if (a.qmajor) {
         hipLaunchKernelGGL(rss_base, dim3(1), dim3(1024), 0, st, c->rss_hist, tiles * S, tiles,
                            o->queue_off_dev, c->rss_total);
     } else {
