@@ -12,7 +12,8 @@
  * (the two one after the other on one thread), then the reference's own arrangement (a poller
  * running beside the application, udpdk_poller.c:443-446 vs the app's recvfrom loop): a poller
  * thread polls batch k + 1 while the application thread drains batch k, at most two batches in
- * the rings (each holds n / S <= 1023 datagrams per batch of a 2047-entry ring), and the rate is
+ * the rings (the first 1023 x S frames: <= 1023 datagrams per socket per batch, two batches fit a
+ * 2047-entry ring), and the rate is
  * the datagrams the application received over the wall time of all reps ("overlap_mdgram_s").
  */
 #include <arpa/inet.h>
@@ -23,6 +24,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "udpdk_api.h"
 
@@ -96,6 +98,14 @@ static void *poller_main(void *arg)
     return NULL;
 }
 
+/* a run that stops receiving (a burst dropped somewhere) ends with EINTR instead of spinning */
+static void *watchdog_main(void *arg)
+{
+    sleep(*(unsigned *)arg);
+    udpdk_interrupt(2);
+    return NULL;
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 6) {
@@ -161,18 +171,25 @@ int main(int argc, char **argv)
         }
     }
     /* the reference's arrangement: poller beside the application */
+    /* two batches share a socket's 2047-entry ring: at most 1023 datagrams per socket per batch
+     * (a burst that does not fit is dropped whole, as flush_rx_queue does, and would never come) */
     const int oreps = 2 * reps + 2;
-    struct poller P = {fr, bytes, off, len, n, oreps, 0, 0, 0};
-    pthread_t th;
+    const uint32_t n_ov = n < 1023u * (uint32_t)S ? n : 1023u * (uint32_t)S;
+    const uint64_t bytes_ov = n_ov < n ? off[n_ov] : bytes;
+    struct poller P = {fr, bytes_ov, off, len, n_ov, oreps, 0, 0, 0};
+    pthread_t th, wd;
+    static unsigned wd_s = 100;
+    if (pthread_create(&wd, NULL, watchdog_main, &wd_s)) { perror("pthread_create"); return 1; }
+    pthread_detach(wd);
     uint64_t ogot = 0;
     const double o0 = now();
     if (pthread_create(&th, NULL, poller_main, &P)) { perror("pthread_create"); return 1; }
     for (int r = 0; r < oreps; r++) {
         while (atomic_load(&P.posted) <= r) ;
         if (P.err) { errno = P.err; perror("udpdk_poll_rx (poller thread)"); return 1; }
-        const uint32_t per = n / (uint32_t)S;
+        const uint32_t per = n_ov / (uint32_t)S;
         for (int s = 0; s < S; s++) {
-            const uint32_t want = per + ((uint32_t)s < n % (uint32_t)S ? 1u : 0u);
+            const uint32_t want = per + ((uint32_t)s < n_ov % (uint32_t)S ? 1u : 0u);
             for (uint32_t k = 0; k < want; k++) {
                 if (udpdk_recvfrom(s, buf, sizeof(buf), 0, NULL, NULL) < 0) { perror("udpdk_recvfrom"); return 1; }
                 ogot++;

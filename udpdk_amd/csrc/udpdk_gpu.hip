@@ -80,6 +80,7 @@ struct Pipe {
 constexpr int MAX_PIPES = 4;
 constexpr size_t FUSE_BYTES = 128u * (UDPDK_FUSE_SHARDS + 1u);   // one 128-B line per fan-in word
 constexpr size_t HINT_BYTES = 192u;
+constexpr uint32_t RSS_FUSE_MAX_ENTRIES = 8192u;   // rss_hash's last workgroup scans <= this many
 #ifndef UDPDK_HINT_WINDOW
 #define UDPDK_HINT_WINDOW 8u       // calls (as far as the GPU got) a tail pass / a not-full tile
                                    // keeps the other form on
@@ -1167,7 +1168,10 @@ int udpdk_gpu_rss(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const udpdk_rss_
     a.n_tiles = tiles;
     a.qmajor = tiles * S <= RSS_BASE_MAX ? 1u : 0u;
     // queue-major histogram: the last rss_hash workgroup scans it (no rss_base launch)
-    const bool fuse = a.qmajor && !c->rss_no_fuse && tiles <= UDPDK_FUSE_MAX_TILES;
+    // (only for small histograms: at 4 M frames x 8 queues the one-workgroup tail scan of 32 K
+    // entries cost more than the 1024-thread rss_base launch, 90.7 vs 84.7 us per call; at 1 M
+    // frames 25.5 vs 26.0, same-box A/B)
+    const bool fuse = a.qmajor && !c->rss_no_fuse && tiles * S <= RSS_FUSE_MAX_ENTRIES;
     a.fuse = fuse ? c->rss_fuse : nullptr;
     a.queue_off = o->queue_off_dev;
     a.total = c->rss_total;
