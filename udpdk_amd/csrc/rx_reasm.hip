@@ -1511,8 +1511,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
     }
 }
 
-// In place (one wave per datagram, the next one's loads in flight while this one stores): the
-// first fragment's frame is extended over its followers.
+// In place (one wave per datagram): the first fragment's frame is extended over its followers.
 // Fragment k (data order, k >= 1) moves 34 k bytes back, over the headers before it, as aligned
 // 16-byte chunk rounds in ascending address order: a round's stores land below every byte a later
 // round (or fragment k itself) still reads, and fragment k + 1 starts only after fragment k's
@@ -1529,173 +1528,108 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit_inplace(EmitArgs a, uint8
     constexpr uint32_t OOR = 0x80000000u;
     const uint32_t stride = gridDim.x * RS_WAVES;
     uint32_t k = blockIdx.x * RS_WAVES + w;
-    if (k >= C) return;
+    // Software pipeline over the wave's datagrams: the next datagram's fragment offsets (which
+    // need its record) are loaded while this one moves, and the record after it is loaded then.
     auto offsets = [&](const ReasmDone &x, uint32_t (&o)[RS_MAX_FRAG], uint32_t (&sx)[RS_MAX_FRAG]) -> uint32_t {
         const uint32_t mx = data_order(x, sx);
 #pragma unroll
         for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) o[f] = f < mx ? a.offset[pick4(x.where, sx[f])] : 0u;
         return mx;
     };
-    // One fragment's move: bytes [dst, dst + len) <- [src, src + len), dst < src, as
-    // destination-aligned 16-byte chunks (lane = chunk, 64 per round): loads of two rounds
-    // (load16 + the funnel's fifth dword), then their stores; the partial end chunks store only
-    // their own bytes. A round's stores land below every byte a later round reads.
-    struct Move {
-        uint32_t D0, dst, De, shift, nch;
-        uint4 x[2];
-        uint32_t hi[2];
-        uint4 head;            // destination bytes [D0, dst) of the first chunk (lane 0)
-    };
-    auto frag_geom = [&](const ReasmDone &r, const uint32_t (&fo)[RS_MAX_FRAG], const uint32_t (&sl)[RS_MAX_FRAG],
-                         uint32_t f, Move &mv) {
-        const uint32_t fq = pick4(r.fr, pick4(sl, f));
-        const uint32_t len = fq >> 16, ofs = fq & 0xFFFFu;
-        const uint32_t src = pick4(fo, f) + 34u;
-        mv.dst = fo[0] + 34u + ofs;
-        mv.D0 = mv.dst & ~15u;
-        mv.De = mv.dst + len;
-        mv.shift = src - mv.dst;
-        mv.nch = (mv.De - mv.D0 + 15u) >> 4;
-    };
-    auto load_round = [&](Move &mv, uint32_t c0) {
-#pragma unroll
-        for (uint32_t u = 0; u < 2; ++u) {
-            const uint32_t c = c0 + 64u * u + lane;
-            const uint32_t S = mv.D0 + 16u * c + mv.shift, sa = S & ~3u, sh = S & 3u;
-            mv.x[u] = load16(fr, c < mv.nch ? sa : OOR);
-            mv.hi[u] = ld32(fr, c < mv.nch && sh ? sa + 16u : OOR);
-        }
-        mv.head = load16(fr, c0 == 0u && lane == 0u && mv.dst != mv.D0 ? mv.D0 : OOR);
-    };
-    auto store_round = [&](const Move &mv, uint32_t c0) {
-#pragma unroll
-        for (uint32_t u = 0; u < 2; ++u) {
-            const uint32_t c = c0 + 64u * u + lane;
-            if (c >= mv.nch) continue;
-            const uint32_t D = mv.D0 + 16u * c;
-            uint4 v = funnel4(mv.x[u], mv.hi[u], (D + mv.shift) & 3u);
-            // Whole 16-byte stores only. The first chunk's bytes before dst are the datagram's
-            // own bytes already in place (read back from the destination, lane 0 = chunk 0); the
-            // last chunk's bytes past De (< 16) lie in the moved fragment's old last 34 bytes:
-            // dead after the move, or the next fragment's destination, written after this one.
-            // (Masked single-byte stores were up to 32 store instructions per datagram.)
-            if (D < mv.dst) {
-                const uint32_t k = mv.dst - D;                          // 1..15 head bytes
-                const uint32_t hv[4] = {mv.head.x, mv.head.y, mv.head.z, mv.head.w};
-                uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (uint32_t d = 0; d < 4; ++d) {
-                    const uint32_t keep = min(max((int)k - 4 * (int)d, 0), 4);   // head bytes in dword d
-                    const uint32_t hm = keep >= 4u ? 0xFFFFFFFFu : ((1u << (8u * keep)) - 1u);
-                    vv[d] = (hv[d] & hm) | (vv[d] & ~hm);
-                }
-                v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
-            }
-            store16(fr, D, v);
-        }
-    };
-    // header bytes 14..33: six dwords from the one at or below, lane 0 (the moves never touch them)
-    auto load_header = [&](uint32_t o0, uint32_t (&hw)[6]) {
-        const uint32_t ha = (o0 + 14u) & ~3u, hs = (o0 + 14u) & 3u;
-#pragma unroll
-        for (uint32_t j = 0; j < 6; ++j) hw[j] = ld32(fr, lane == 0u && (j < 5u || hs) ? ha + 4u * j : OOR);
-    };
-    // total length (16-17), fragment field DF only (20-21), checksum (24-25) over bytes 14..33,
-    // and the output record
-    auto finish = [&](const ReasmDone &r, uint32_t o0, const uint32_t (&hw)[6], uint32_t kk) {
-        if (lane != 0) return;
-        const uint32_t hs = (o0 + 14u) & 3u;
-        uint32_t h[5];
-#pragma unroll
-        for (uint32_t j = 0; j < 5; ++j) h[j] = __builtin_amdgcn_alignbyte(hw[j + 1], hw[j], hs);
-        // h[0] = bytes 14-17, h[1] = 18-21, h[2] = 22-25, h[3] = 26-29, h[4] = 30-33
-        const uint32_t tl = r.total + 20u;
-        h[0] = (h[0] & 0x0000FFFFu) | ((tl >> 8) & 0xFFu) << 16 | (tl & 0xFFu) << 24;
-        h[1] = (h[1] & 0x0000FFFFu) | (h[1] & 0x00400000u);
-        h[2] = h[2] & 0x0000FFFFu;
-        uint32_t sum = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 5; ++j) sum += (h[j] & 0xFFFFu) + (h[j] >> 16);
-        sum = (sum >> 16) + (sum & 0xFFFFu);
-        sum = (sum >> 16) + (sum & 0xFFFFu);
-        const uint32_t ck = a.cksum_zero ? 0u : ~sum & 0xFFFFu;
-        const uint8_t pb[6] = {(uint8_t)(h[0] >> 16), (uint8_t)(h[0] >> 24), (uint8_t)(h[1] >> 16),
-                               (uint8_t)(h[1] >> 24), (uint8_t)ck, (uint8_t)(ck >> 8)};
-        const uint32_t po[6] = {16, 17, 20, 21, 24, 25};
-#pragma unroll
-        for (uint32_t j = 0; j < 6; ++j) __builtin_amdgcn_raw_buffer_store_b8(pb[j], fr, (int)(o0 + po[j]), 0, 0);
-        a.out_off[kk] = o0;
-        a.out_len[kk] = (uint16_t)(34u + r.total);
-        a.out_ptype[kk] = 0x211u;
-        a.out_origin[kk] = r.origin;
-    };
-    // Two datagrams in flight per wave: the common datagram (two fragments, the second's data in
-    // at most 128 chunks: one pair of rounds) has its loads issued one datagram ahead, so they are
-    // in flight while the datagram before it stores (datagrams are disjoint regions of the frame
-    // buffer). Any other datagram moves fragment by fragment, loads then stores, as it comes.
-    // Records two ahead and fragment offsets one ahead, as before.
-    ReasmDone r = a.done[a.perm[k]], rn{};
-    uint32_t fo[RS_MAX_FRAG], sl[RS_MAX_FRAG];
-    uint32_t m = offsets(r, fo, sl);
+    ReasmDone r{}, rn{};
+    uint32_t fo[RS_MAX_FRAG] = {0, 0, 0, 0}, sl[RS_MAX_FRAG] = {0, 0, 0, 0}, m = 0;
+    if (k < C) {
+        r = a.done[a.perm[k]];
+        m = offsets(r, fo, sl);
+    }
     if (k + stride < C) rn = a.done[a.perm[k + stride]];
-    Move A{};
-    uint32_t hwA[6];
-    bool fastA = false;
-    if (m == 2u) {
-        frag_geom(r, fo, sl, 1u, A);
-        fastA = A.nch <= 128u;
-    }
-    if (fastA) {
-        load_round(A, 0u);
-        load_header(fo[0], hwA);
-    }
     for (; k < C; k += stride) {
         uint32_t fon[RS_MAX_FRAG] = {0, 0, 0, 0}, sln[RS_MAX_FRAG] = {0, 0, 0, 0}, mn = 0;
         ReasmDone rnn{};
-        Move B{};
-        uint32_t hwB[6] = {0, 0, 0, 0, 0, 0};
-        bool fastB = false;
-        if (k + stride < C) {
-            mn = offsets(rn, fon, sln);
-            if (mn == 2u) {
-                frag_geom(rn, fon, sln, 1u, B);
-                fastB = B.nch <= 128u;
-            }
-            if (fastB) {                                      // the next datagram's loads, now
-                load_round(B, 0u);
-                load_header(fon[0], hwB);
+        if (k + stride < C) mn = offsets(rn, fon, sln);
+        if (k + 2u * stride < C) rnn = a.done[a.perm[k + 2u * stride]];
+        const uint32_t o0 = fo[0];
+        // header bytes 14..33: six dwords from the one at or below, lane 0 (issued with the first
+        // fragment's chunk loads; the moves never touch them)
+        const uint32_t ha = (o0 + 14u) & ~3u, hs = (o0 + 14u) & 3u;
+        uint32_t hw[6];
+#pragma unroll
+        for (uint32_t j = 0; j < 6; ++j) hw[j] = ld32(fr, lane == 0u && (j < 5u || hs) ? ha + 4u * j : OOR);
+#pragma unroll
+        for (uint32_t f = 1; f < RS_MAX_FRAG; ++f) {            // static indices: no scratch
+            if (f >= m) break;
+            const uint32_t q = sl[f];
+            const uint32_t fq = pick4(r.fr, q);
+            const uint32_t len = fq >> 16, ofs = fq & 0xFFFFu;
+            const uint32_t src = fo[f] + 34u, dst = o0 + 34u + ofs;
+            // bytes [dst, dst + len) <- [src, src + len), dst < src: destination-aligned 16-byte
+            // chunks (lane = chunk), two rounds' loads in flight before their stores (a round's
+            // stores land below every byte a later round reads); the two partial end chunks store
+            // only their own bytes
+            const uint32_t D0 = dst & ~15u, De = dst + len, shift = src - dst;
+            const uint32_t nch = (De - D0 + 15u) >> 4;
+            for (uint32_t c0 = 0; c0 < nch; c0 += 128u) {
+                uint4 v[2];
+                uint32_t Dv[2];
+                bool inv[2];
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u) {
+                    const uint32_t c = c0 + 64u * u + lane;
+                    inv[u] = c < nch;
+                    Dv[u] = D0 + 16u * c;
+                    const uint32_t S = Dv[u] + shift, sa = S & ~3u, sh = S & 3u;
+                    const uint4 x = load16(fr, inv[u] ? sa : OOR);
+                    const uint32_t hi = ld32(fr, inv[u] && sh ? sa + 16u : OOR);
+                    v[u] = funnel4(x, hi, sh);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u) {
+                    const uint32_t D = Dv[u];
+                    if (inv[u] && D >= dst && D + 16u <= De) {
+                        store16(fr, D, v[u]);
+                    } else if (inv[u]) {
+                        const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (uint32_t j = 0; j < 16; ++j)
+                            if (D + j >= dst && D + j < De)
+                                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(vv[j >> 2] >> (8u * (j & 3u))), fr,
+                                                                     (int)(D + j), 0, 0);
+                    }
+                }
             }
         }
-        if (k + 2u * stride < C) rnn = a.done[a.perm[k + 2u * stride]];
-        if (fastA) {
-            store_round(A, 0u);
-            finish(r, fo[0], hwA, k);
-        } else {
-            uint32_t hw[6];
-            load_header(fo[0], hw);
+        // header: total length (16-17), fragment field DF only (20-21), checksum (24-25) over
+        // bytes 14..33
+        if (lane == 0) {
+            uint32_t h[5];
 #pragma unroll
-            for (uint32_t f = 1; f < RS_MAX_FRAG; ++f) {        // static indices: no scratch
-                if (f >= m) break;
-                Move mv;
-                frag_geom(r, fo, sl, f, mv);
-                for (uint32_t c0 = 0; c0 < mv.nch; c0 += 128u) {
-                    load_round(mv, c0);
-                    store_round(mv, c0);
-                }
-                // the next fragment's first chunk reads this one's last bytes back: stores done
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            finish(r, fo[0], hw, k);
+            for (uint32_t j = 0; j < 5; ++j) h[j] = __builtin_amdgcn_alignbyte(hw[j + 1], hw[j], hs);
+            // h[0] = bytes 14-17, h[1] = 18-21, h[2] = 22-25, h[3] = 26-29, h[4] = 30-33
+            const uint32_t tl = r.total + 20u;
+            h[0] = (h[0] & 0x0000FFFFu) | ((tl >> 8) & 0xFFu) << 16 | (tl & 0xFFu) << 24;
+            h[1] = (h[1] & 0x0000FFFFu) | (h[1] & 0x00400000u);
+            h[2] = h[2] & 0x0000FFFFu;
+            uint32_t sum = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 5; ++j) sum += (h[j] & 0xFFFFu) + (h[j] >> 16);
+            sum = (sum >> 16) + (sum & 0xFFFFu);
+            sum = (sum >> 16) + (sum & 0xFFFFu);
+            const uint32_t ck = a.cksum_zero ? 0u : ~sum & 0xFFFFu;
+            const uint8_t pb[6] = {(uint8_t)(h[0] >> 16), (uint8_t)(h[0] >> 24), (uint8_t)(h[1] >> 16),
+                                   (uint8_t)(h[1] >> 24), (uint8_t)ck, (uint8_t)(ck >> 8)};
+            const uint32_t po[6] = {16, 17, 20, 21, 24, 25};
+#pragma unroll
+            for (uint32_t j = 0; j < 6; ++j) __builtin_amdgcn_raw_buffer_store_b8(pb[j], fr, (int)(o0 + po[j]), 0, 0);
+            a.out_off[k] = o0;
+            a.out_len[k] = (uint16_t)(34u + r.total);
+            a.out_ptype[k] = 0x211u;
+            a.out_origin[k] = r.origin;
         }
         r = rn;
         rn = rnn;
         m = mn;
 #pragma unroll
         for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) { fo[f] = fon[f]; sl[f] = sln[f]; }
-        A = B;
-        fastA = fastB;
-#pragma unroll
-        for (uint32_t j = 0; j < 6; ++j) hwA[j] = hwB[j];
     }
 }
 
