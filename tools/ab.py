@@ -103,7 +103,7 @@ def main():
                 res = run([sys.executable, os.path.abspath(__file__), "--_line", a.line], env, a.timeout, log)
             else:
                 extra = (a.bench or "").split()
-                dflt = ["--steps", "200", "--warmup", "20", "--no-cpu-baseline", "--no-extra"]
+                dflt = ["--steps", "200", "--warmup", "20", "--no-cpu-baseline", "--no-extra", "--no-strong"]
                 res = run([sys.executable, "bench.py", *dflt, *extra], env, a.timeout, log)
             for d in res:
                 print(f"r{rep} {n:10s} {summary(d)}", flush=True)

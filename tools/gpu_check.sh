@@ -19,9 +19,9 @@ if [ $rc -le 1 ]; then case ",$STEPS," in *,pytest,*) run pytest_gpu 1100 python
 if [ $rc -le 1 ]; then case ",$STEPS," in *,bench,*) run bench 600 python bench.py ${BENCH_ARGS};; esac; fi
 if [ $rc -le 1 ]; then case ",$STEPS," in *,prof,*)
   export TMPDIR=/tmp
-  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o rx -- python3 "$R/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-extra --no-scale --pipeline 1
+  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o rx -- python3 "$R/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-extra --no-scale --no-strong --pipeline 1
   if [ $rc -le 1 ]; then
-    run prof5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof5" -o rx -- python3 "$R/bench.py" --config 5 --steps 50 --warmup 5 --no-cpu-baseline --no-extra --no-scale --pipeline 1
+    run prof5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof5" -o rx -- python3 "$R/bench.py" --config 5 --steps 50 --warmup 5 --no-cpu-baseline --no-extra --no-scale --no-strong --pipeline 1
   fi
 ;; esac; fi
 exit $rc

@@ -9,7 +9,7 @@ mkdir -p gpurun_out/pmc
 for cfg in ${PMC_CONFIGS:-2 3}; do
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$PWD/gpurun_out/pmc/${ctr}_c$cfg" -o p \
-      -- python3 "$PWD/bench.py" --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --no-extra --no-scale \
+      -- python3 "$PWD/bench.py" --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --no-extra --no-scale --no-strong \
       > "gpurun_out/pmc/${ctr}_c$cfg.log" 2>&1 || exit 1
   done
 done
