@@ -7,6 +7,6 @@ import sys
 agg = collections.defaultdict(list)
 for f in sys.argv[1:]:
     for r in csv.DictReader(open(f)):
-        agg[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append(float(r["Counter_Value"]))
+        agg[(r["Kernel_Name"].split("(")[0].replace("void ", ""), r["Counter_Name"])].append(float(r["Counter_Value"]))
 for (k, c), v in sorted(agg.items()):
     print(f"{k:40s} {c:28s} {sum(v) / len(v):16.1f}  (n={len(v)})")

@@ -24,7 +24,9 @@ for cfg in (1, 2, 3, 4, 5):
             continue
         agg = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
-            agg[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+            # "void udpdk::rx_classify<1>(udpdk::RxArgs)" -> "udpdk::rx_classify" (both forms)
+            kn = r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0]
+            agg[kn].append(float(r["Counter_Value"]))
         vals[ctr] = {k: sum(v) / len(v) for k, v in agg.items()}
     if len(vals) < 2:
         continue
