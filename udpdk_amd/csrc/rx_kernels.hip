@@ -580,8 +580,18 @@ rx_classify(RxArgs a)
                                     W.c.x, W.c.y, W.c.z, W.c.w, W.d.x, W.d.y};
             const uint32_t sh = off & 3u;     // lanes whose window was not loaded: unused words
             uint32_t g[13];                   // g[i] = frame bytes 12+4i ..
+#ifdef UDPDK_EXP_ALIGNED
+            if (__ballot(sh != 0u) == 0ull) { // every frame of the step at a dword offset
+#pragma unroll
+                for (int i = 0; i < 13; ++i) g[i] = D[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 13; ++i) g[i] = __builtin_amdgcn_alignbyte(D[i + 1], D[i], sh);
+            }
+#else
 #pragma unroll
             for (int i = 0; i < 13; ++i) g[i] = __builtin_amdgcn_alignbyte(D[i + 1], D[i], sh);
+#endif
             // IPv4 gate (udpdk_poller.c:334): the ptype array's L3_IPV4 bit when given, else derived
             // from ether_type (frames shorter than an Ethernet header are not IPv4)
             const uint32_t eth_ip = (len >= 14u && (g[0] & 0xFFFFu) == 0x0008u) ? 0x10u : 0u;
@@ -701,9 +711,15 @@ rx_classify(RxArgs a)
                 for (uint32_t j = 0; j < SPR; ++j) {
                     const uint32_t pt = S[j].x & 0xFFFFu;
                     uint32_t k = a.n_inl;
+#ifdef UDPDK_EXP_INLOOP
+#pragma unroll 1
+                    for (uint32_t q = 0; q < a.n_inl; ++q)     // uniform trip count (<= 8)
+                        k = pt == a.inl_port[q] ? q : k;
+#else
 #pragma unroll
                     for (uint32_t q = 0; q < UDPDK_INLINE_PORTS; ++q)
                         k = q < a.n_inl && pt == a.inl_port[q] ? q : k;
+#endif
                     E[j] = inl_tab[k];
                 }
             } else {
