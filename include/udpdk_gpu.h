@@ -201,9 +201,13 @@ typedef struct {
     uint32_t overflow;       /* deliveries > lane_cap: lane_pkt holds only the first lane_cap  */
 } udpdk_rx_stats_t;
 
-/* Enqueue the RX pipeline for one batch on the context stream (async): rx_classify, then either
- * rx_compact1 (one lane and no fan-out in the snapshot) or rx_scan + rx_scatter. meta, lane_off
- * and lane_pkt are complete when the stream reaches the end of the sequence.
+/* Enqueue the RX pipeline for one batch on the context stream (async): rx_classify, then, with
+ * one lane and no fan-out in the snapshot, nothing more (the last classify workgroup completes
+ * the lane) or rx_compact1, else rx_scan + rx_scatter. meta, lane_off and lane_pkt are complete
+ * when the stream reaches the end of the sequence. Which single-lane form runs (and how many
+ * tail chunk groups classify keeps in flight) follows hints the kernels leave in pinned host
+ * memory about the context's recent calls; every form gives the same results for any batch.
+ * A fresh context starts on the two-launch form.
  *
  * Tailroom contract: batch->frames_dev must be readable for frames_bytes +
  * UDPDK_GPU_FRAMES_TAILROOM bytes. The kernels read frame bytes with byte-aligned dword loads
