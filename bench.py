@@ -893,7 +893,7 @@ def main():
                          "(set UDPDK_BENCH_SHARED_DEVICE=1 for a one-GPU rehearsal)")
     scale = None
     if not args.no_scale and not args.strong_total:
-        scale = scale_line(ctx, world, rank, barrier, dist, max(10, args.steps // 4), 5,
+        scale = scale_line(ctx, world, rank, barrier, dist, max(20, args.steps // 4), 5,
                            args.rotate_mib << 20)
         scale["distinct_gpus"] = distinct
     strong = None
