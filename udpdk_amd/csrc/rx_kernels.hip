@@ -369,13 +369,6 @@ rx_classify(RxArgs a)
     // counters: per-lane packed 8-bit fields (verdicts 0-3 / 4-7, flag counters), deliveries
     // and bytes; reduced across the wave once per tile
     uint32_t acc_v0 = 0, acc_v1 = 0, acc_f0 = 0, acc_f1 = 0, acc_fan = 0, lane_bytes = 0;
-#ifdef UDPDK_EXP_TILECNT
-    // a one-round tile counts its verdicts, flags and bytes once at the tile end from the staged
-    // verdict words (every field is in them); a tile of several rounds counts per step
-    const bool perstep = classify_dsc_bufs(a.tile_frames) > 1u;
-#else
-    constexpr bool perstep = true;
-#endif
 
     // Loads are unconditional (clamped index / range-checked buffer offsets): a load under a
     // lane condition makes the compiler wait for it at the end of the branch, which would drain
@@ -568,7 +561,7 @@ rx_classify(RxArgs a)
                 if (fo & 1u) t = ((t & 0xFFu) << 8) | (t >> 8);   // buffer-aligned words: swap back
                 const bool ok = fold32(t + (dw >> 16)) == 0xFFFFu;
                 mstage[i & (RX_ROUND - 1u)] = (m & ~0x60u) | ((ok ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD) << 5);
-                if (perstep) acc_f0 += ok ? 0x10000u : 0x1000000u;
+                acc_f0 += ok ? 0x10000u : 0x1000000u;
             }
     };
 
@@ -587,18 +580,8 @@ rx_classify(RxArgs a)
                                     W.c.x, W.c.y, W.c.z, W.c.w, W.d.x, W.d.y};
             const uint32_t sh = off & 3u;     // lanes whose window was not loaded: unused words
             uint32_t g[13];                   // g[i] = frame bytes 12+4i ..
-#ifdef UDPDK_EXP_ALIGNED
-            if (__ballot(sh != 0u) == 0ull) { // every frame of the step at a dword offset
-#pragma unroll
-                for (int i = 0; i < 13; ++i) g[i] = D[i];
-            } else {
-#pragma unroll
-                for (int i = 0; i < 13; ++i) g[i] = __builtin_amdgcn_alignbyte(D[i + 1], D[i], sh);
-            }
-#else
 #pragma unroll
             for (int i = 0; i < 13; ++i) g[i] = __builtin_amdgcn_alignbyte(D[i + 1], D[i], sh);
-#endif
             // IPv4 gate (udpdk_poller.c:334): the ptype array's L3_IPV4 bit when given, else derived
             // from ether_type (frames shorter than an Ethernet header are not IPv4)
             const uint32_t eth_ip = (len >= 14u && (g[0] & 0xFFFFu) == 0x0008u) ? 0x10u : 0u;
@@ -672,13 +655,11 @@ rx_classify(RxArgs a)
             const uint32_t l3f = l3 ? ((ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8) : 0u;
             const uint32_t udpf = is_udp ? (state << 5 | (len_bad ? 1u : 0u) << 7) : 0u;
             // (pending frames count their UDP state in the tail pass)
-            if (perstep) {
-                acc_f0 += (l3 && !ip_ok ? 1u : 0u) | (l3 && ihl_ne5 ? 0x100u : 0u) |
-                          (is_udp && state == UDPDK_UDP_CSUM_OK ? 0x10000u : 0u) |
-                          (is_udp && state == UDPDK_UDP_CSUM_BAD ? 0x1000000u : 0u);
-                acc_f1 += (is_udp && state == UDPDK_UDP_CSUM_NONE ? 1u : 0u) | (is_udp && len_bad ? 0x100u : 0u);
-                if (good) lane_bytes += len;
-            }
+            acc_f0 += (l3 && !ip_ok ? 1u : 0u) | (l3 && ihl_ne5 ? 0x100u : 0u) |
+                      (is_udp && state == UDPDK_UDP_CSUM_OK ? 0x10000u : 0u) |
+                      (is_udp && state == UDPDK_UDP_CSUM_BAD ? 0x1000000u : 0u);
+            acc_f1 += (is_udp && state == UDPDK_UDP_CSUM_NONE ? 1u : 0u) | (is_udp && len_bad ? 0x100u : 0u);
+            if (good) lane_bytes += len;
 
             // the port-table lookup waits for the round's demux pass: verdict field 0xF until then
             mstage[(st * 64 + lane) & (RX_ROUND - 1u)] = (pre == 0xFFu ? 0xFu : pre) | l3f | udpf;
@@ -720,15 +701,9 @@ rx_classify(RxArgs a)
                 for (uint32_t j = 0; j < SPR; ++j) {
                     const uint32_t pt = S[j].x & 0xFFFFu;
                     uint32_t k = a.n_inl;
-#ifdef UDPDK_EXP_INLOOP
-#pragma unroll 1
-                    for (uint32_t q = 0; q < a.n_inl; ++q)     // uniform trip count (<= 8)
-                        k = pt == a.inl_port[q] ? q : k;
-#else
 #pragma unroll
                     for (uint32_t q = 0; q < UDPDK_INLINE_PORTS; ++q)
                         k = q < a.n_inl && pt == a.inl_port[q] ? q : k;
-#endif
                     E[j] = inl_tab[k];
                 }
             } else {
@@ -771,11 +746,9 @@ rx_classify(RxArgs a)
                 // one round, so three workgroups fit a CU at 4096 lanes instead of two)
                 if (nbuf > 1u && valid) a.meta[t0 + i] = fin;
                 // per-lane packed counters (8-bit fields; a lane sees <= 64 frames per tile)
-                if (perstep) {
-                    const uint32_t vinc = valid ? 1u << (8u * (verdict & 3u)) : 0u;
-                    acc_v0 += verdict < 4u ? vinc : 0u;
-                    acc_v1 += verdict < 4u ? 0u : vinc;
-                }
+                const uint32_t vinc = valid ? 1u << (8u * (verdict & 3u)) : 0u;
+                acc_v0 += verdict < 4u ? vinc : 0u;
+                acc_v1 += verdict < 4u ? 0u : vinc;
                 acc_fan += fan;
                 const bool delivered = valid && fan > 0u;
                 // first delivery of every frame into the tile histogram; small key spaces are
@@ -804,36 +777,6 @@ rx_classify(RxArgs a)
         STAMP(3);
     }
 
-#ifdef UDPDK_EXP_TILECNT
-    if (!perstep) {
-        // one-round tile: frames 4 tid .. 4 tid + 3 from the staged verdict words (demux and tail
-        // pass done: every wave passed the round's LDS ordering) and the staged lengths
-        __syncthreads();
-        const uint32_t nv = t1 - t0, j0 = 4u * tid;
-        if (j0 < nv) {
-            const uint4 v4 = reinterpret_cast<const uint4 *>(mstage)[tid];
-            const uint32_t mv[4] = {v4.x, v4.y, v4.z, v4.w};
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                if (j0 + j >= nv) break;
-                const uint32_t m = mv[j], verdict = m & 0xFu;
-                const uint32_t vinc = 1u << (8u * (verdict & 3u));
-                acc_v0 += verdict < 4u ? vinc : 0u;
-                acc_v1 += verdict < 4u ? 0u : vinc;
-                // l3: FRAG, NOT_UDP and the UDP verdicts; UDP: DELIVERED, NO_BIND, NO_MATCH
-                const bool l3 = verdict != UDPDK_V_NOT_IPV4 && verdict < UDPDK_V_TRUNC;
-                const bool udp = verdict == UDPDK_V_DELIVERED || verdict == UDPDK_V_NO_BIND ||
-                                 verdict == UDPDK_V_NO_MATCH;
-                const uint32_t st = (m >> 5) & 3u;
-                acc_f0 += (l3 && !((m >> 4) & 1u) ? 1u : 0u) | (l3 && ((m >> 8) & 1u) ? 0x100u : 0u) |
-                          (udp && st == UDPDK_UDP_CSUM_OK ? 0x10000u : 0u) |
-                          (udp && st == UDPDK_UDP_CSUM_BAD ? 0x1000000u : 0u);
-                acc_f1 += (udp && st == UDPDK_UDP_CSUM_NONE ? 1u : 0u) | (udp && ((m >> 7) & 1u) ? 0x100u : 0u);
-                if (verdict != UDPDK_V_BAD_DESC) lane_bytes += d_lp[j0 + j] & 0xFFFFu;
-            }
-        }
-    }
-#endif
     // ---- tile counters: one row per wave (lanes 0-15), summed by the readers ----
     uint32_t sc[UDPDK_N_COUNTERS];
     {
@@ -908,7 +851,8 @@ rx_classify(RxArgs a)
         if (fuse) {
             // written through: the completing workgroup may rewrite these words (no stale dirty
             // copy may stay behind in this XCD's L2) -- range-checked by the resource
-            const __amdgpu_buffer_rsrc_t sr = make_rsrc(a.spec_pkt, a.spec_cap * 4u);
+            const __amdgpu_buffer_rsrc_t sr =
+                make_rsrc(a.spec_pkt, a.spec_cap >= 0x40000000u ? 0xFFFFFFFCu : a.spec_cap * 4u);
             if (d == 0xFu && (pos & 3u) == 0u) {
                 const __attribute__((ext_vector_type(4))) uint32_t x = {f, f + 1u, f + 2u, f + 3u};
                 __builtin_amdgcn_raw_buffer_store_b128(x, sr, (int)(4u * pos), 0, 16);
