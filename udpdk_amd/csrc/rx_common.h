@@ -63,11 +63,17 @@ __host__ __device__ constexpr uint32_t classify_stage_frames(uint32_t tile_frame
     return tile_frames > RX_ROUND ? RX_ROUND : tile_frames;
 }
 
-__host__ __device__ constexpr uint32_t classify_lds_bytes(uint32_t n_lanes, uint32_t tile_frames)
+// LDS words of the tile histogram: n_lanes, or half as many u16 pairs (hist16), rounded up to 4
+__host__ __device__ constexpr uint32_t classify_hist_words(uint32_t n_lanes, bool hist16)
+{
+    return ((hist16 ? (n_lanes + 1u) >> 1 : n_lanes) + 3u) & ~3u;
+}
+
+__host__ __device__ constexpr uint32_t classify_lds_bytes(uint32_t n_lanes, uint32_t tile_frames, bool hist16 = false)
 {
     return (uint32_t)DSC_OFF + 8u * RX_ROUND * classify_dsc_bufs(tile_frames) +
-           4u * ((n_lanes + 3u) & ~3u) + 4u * classify_stage_frames(tile_frames) + 4u * RX_ROUND +
-           8u * RX_ROUND;
+           4u * classify_hist_words(n_lanes, hist16) + 4u * classify_stage_frames(tile_frames) +
+           4u * RX_ROUND + 8u * RX_ROUND;
 }
 
 // Port table entry (16 B per raw port): x = bindings on the port, y = index of the first in the
@@ -272,7 +278,10 @@ __global__ void rx_scan_top(ScanArgs a, uint32_t n_part);
 __global__ void rx_scan_down(ScanArgs a);
 __global__ void rx_scatter(ScatterArgs a);
 __global__ void rx_scatterw(ScatterArgs a);
-constexpr uint32_t SCATTER_WAVES = 8;           // rx_scatterw workgroup: 8 waves per tile
+#ifndef UDPDK_SCATTER_WAVES
+#define UDPDK_SCATTER_WAVES 8
+#endif
+constexpr uint32_t SCATTER_WAVES = UDPDK_SCATTER_WAVES;   // rx_scatterw workgroup: waves per tile
 constexpr uint32_t SCATTERW_MAX_LANES = 4096;   // rx_scatterw LDS: (4 + 2 x 8) x lanes bytes
 __host__ __device__ constexpr uint32_t scatterw_lds_bytes(uint32_t n_lanes)
 {

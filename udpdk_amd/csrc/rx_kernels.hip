@@ -343,7 +343,7 @@ rx_classify(RxArgs a)
     // The tile's verdict words are staged in LDS and stored once per tile (16 B per lane): no
     // global store inside the step loop, so no s_waitcnt there ever waits for a store (on gfx9
     // stores count in vmcnt, in order with the loads).
-    uint32_t *mstage = hist + ((a.n_lanes + 3u) & ~3u);              // [stage frames], index & SMASK
+    uint32_t *mstage = hist + classify_hist_words(a.n_lanes, a.hist16 != 0u);   // [stage frames]
     // datagram end (34 + UDP length) of the frames whose checksum the tail pass completes
     // pending frames' datagram end | folded window part of the UDP sum << 16
     uint32_t *dgl = mstage + classify_stage_frames(a.tile_frames);   // [RX_ROUND]

@@ -105,6 +105,7 @@ struct udpdk_gpu_ctx {
     uint32_t inl = 0, n_inl = 0, inl_port[UDPDK_INLINE_PORTS] = {};
     uint4 inl_ent[UDPDK_INLINE_PORTS] = {};
     uint32_t one_lane_tile = 0;    // UDPDK_ONE_LANE_TILE (diagnostic): single-lane tile override
+    uint64_t geo_cap = RX_HIST_CAP; // UDPDK_RX_HIST_CAP (diagnostic): lanes x tiles bound of the geometry
     // Kernel hints (pinned host memory the kernels write, RxArgs::hint): the call sequence number
     // of the last call that ran a tail pass / had a tile before the last not full. The single-lane
     // path takes rx_classify<1> and the fused completion while neither was seen in the last
@@ -173,10 +174,10 @@ uint32_t frames_rsrc_bytes(uint64_t frames_bytes)
     return (uint32_t)std::min<uint64_t>((frames_bytes + 3 + 3) & ~3ull, 0xFFFFFFFCull);
 }
 
-void geometry(uint32_t n, uint32_t lanes, uint32_t *T, uint32_t *tiles)
+void geometry(uint32_t n, uint32_t lanes, uint32_t *T, uint32_t *tiles, uint64_t cap = RX_HIST_CAP)
 {
     uint32_t t = RX_TILE_MIN;
-    while (t < RX_TILE_MAX && (uint64_t)ceil_div(n, t) * lanes > RX_HIST_CAP) t *= 2;
+    while (t < RX_TILE_MAX && (uint64_t)ceil_div(n, t) * lanes > cap) t *= 2;
     *T = t;
     *tiles = std::max<uint32_t>(1u, ceil_div(n, t));
 }
@@ -296,6 +297,10 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
         const uint32_t t = (uint32_t)atoi(e);
         if (t >= RX_TILE_MIN && t <= RX_TILE_MAX && (t & (t - 1)) == 0) c->one_lane_tile = t;
     }
+    if (const char *e = getenv("UDPDK_RX_HIST_CAP")) {
+        const uint64_t v = strtoull(e, nullptr, 0);
+        if (v >= (1u << 16) && v <= (1u << 26)) c->geo_cap = v;
+    }
     if (const char *e = getenv("UDPDK_RX_FUSE")) c->force_fuse = atoi(e) ? 1 : 0;
     c->trace = getenv("UDPDK_RX_TRACE") != nullptr;
     c->no_inline = getenv("UDPDK_RX_NO_INLINE") != nullptr;
@@ -315,7 +320,7 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
         c->stream = c->pipes[0].stream;
         if (hipMalloc((void **)&c->port_tab, UDPDK_UDP_PORTS * sizeof(uint4)) != hipSuccess) break;
         if (hipMemset(c->port_tab, 0, UDPDK_UDP_PORTS * sizeof(uint4)) != hipSuccess) break;
-        const uint64_t e_cap = std::max<uint64_t>((uint64_t)RX_HIST_CAP + max_lanes,
+        const uint64_t e_cap = std::max<uint64_t>(std::max<uint64_t>(RX_HIST_CAP, c->geo_cap) + max_lanes,
                                                   (uint64_t)ceil_div(max_frames, RX_TILE_MAX) * max_lanes);
         c->hist_cap = e_cap;
         c->partial_cap = e_cap / SCAN_COL_CHUNK + max_lanes + 1;   // chunks x lanes
@@ -621,7 +626,7 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
         return 0;
     }
     uint32_t T, tiles;
-    geometry(bt->n, S, &T, &tiles);
+    geometry(bt->n, S, &T, &tiles, c->geo_cap);
     if (S == 1 && c->max_fanout <= 1 && c->one_lane_tile) {   // diagnostic override
         T = c->one_lane_tile;
         tiles = std::max<uint32_t>(1u, ceil_div(bt->n, T));
@@ -695,7 +700,7 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
 
     if (ts) for (int k = 0; k < TIMED_KERNELS; ++k) ts->used[k] = false;
     HIPC(c, launch(st, ts, 0, true, true, tailg == 1 ? rx_classify<1> : rx_classify<2>, dim3(tiles),
-                   dim3(CLS_BLOCK), classify_lds_bytes(S, T), ra));
+                   dim3(CLS_BLOCK), classify_lds_bytes(S, T, hist16), ra));
     if (fuse) return 0;                        // the last workgroup completed the lane
     if (one_lane) {
         Compact1Args ca;
