@@ -1511,6 +1511,33 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
     }
 }
 
+// Bytes [lo, hi) of the 16-byte chunk v at buffer offset D (16-byte aligned; 0 <= lo < hi <= 16):
+// the whole dwords as dword stores, the at most three bytes at either end as a byte store and a
+// 2-byte store. At most 10 store instructions per wave for any ranges of its lanes, where a store
+// per byte took 16 (in place, the texture address unit was 72 % busy, mostly with byte stores).
+__device__ __forceinline__ void store_part(__amdgpu_buffer_rsrc_t r, uint32_t D, const uint4 v, uint32_t lo, uint32_t hi)
+{
+    const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d)
+        if (4u * d >= lo && 4u * d + 4u <= hi) __builtin_amdgcn_raw_buffer_store_b32(vv[d], r, (int)(D + 4u * d), 0, 0);
+    auto word = [&](uint32_t x) { return x < 4u ? vv[0] : x < 8u ? vv[1] : x < 12u ? vv[2] : vv[3]; };
+    auto bytes = [&](uint32_t a, uint32_t b) {            // [a, b) inside one dword, b - a <= 3
+        if (a < b && (a & 1u)) {
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(word(a) >> (8u * (a & 3u))), r, (int)(D + a), 0, 0);
+            ++a;
+        }
+        if (a + 2u <= b) {
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(word(a) >> (8u * (a & 2u))), r, (int)(D + a), 0, 0);
+            a += 2u;
+        }
+        if (a < b) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(word(a) >> (8u * (a & 3u))), r, (int)(D + a), 0, 0);
+    };
+    const uint32_t ha = (lo & 3u) ? min(hi, (lo + 3u) & ~3u) : lo;
+    bytes(lo, ha);
+    bytes((hi & 3u) ? max(ha, hi & ~3u) : hi, hi);
+}
+
 // In place (one wave per datagram): the first fragment's frame is extended over its followers.
 // Fragment k (data order, k >= 1) moves 34 k bytes back, over the headers before it, as aligned
 // 16-byte chunk rounds in ascending address order: a round's stores land below every byte a later
@@ -1553,8 +1580,11 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit_inplace(EmitArgs a, uint8
         // fragment's chunk loads; the moves never touch them)
         const uint32_t ha = (o0 + 14u) & ~3u, hs = (o0 + 14u) & 3u;
         uint32_t hw[6];
-#pragma unroll
-        for (uint32_t j = 0; j < 6; ++j) hw[j] = ld32(fr, lane == 0u && (j < 5u || hs) ? ha + 4u * j : OOR);
+        {
+            const uint4 h4 = load16(fr, lane == 0u ? ha : OOR);
+            const auto h2 = __builtin_amdgcn_raw_buffer_load_b64(fr, (int)(lane == 0u ? ha + 16u : OOR), 0, 0);
+            hw[0] = h4.x; hw[1] = h4.y; hw[2] = h4.z; hw[3] = h4.w; hw[4] = h2[0]; hw[5] = h2[1];
+        }
 #pragma unroll
         for (uint32_t f = 1; f < RS_MAX_FRAG; ++f) {            // static indices: no scratch
             if (f >= m) break;
@@ -1585,16 +1615,10 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit_inplace(EmitArgs a, uint8
 #pragma unroll
                 for (uint32_t u = 0; u < 2; ++u) {
                     const uint32_t D = Dv[u];
-                    if (inv[u] && D >= dst && D + 16u <= De) {
+                    if (inv[u] && D >= dst && D + 16u <= De)
                         store16(fr, D, v[u]);
-                    } else if (inv[u]) {
-                        const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                        for (uint32_t j = 0; j < 16; ++j)
-                            if (D + j >= dst && D + j < De)
-                                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(vv[j >> 2] >> (8u * (j & 3u))), fr,
-                                                                     (int)(D + j), 0, 0);
-                    }
+                    else if (inv[u])
+                        store_part(fr, D, v[u], D >= dst ? 0u : dst - D, min(De - D, 16u));
                 }
             }
         }
@@ -1615,11 +1639,18 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit_inplace(EmitArgs a, uint8
             sum = (sum >> 16) + (sum & 0xFFFFu);
             sum = (sum >> 16) + (sum & 0xFFFFu);
             const uint32_t ck = a.cksum_zero ? 0u : ~sum & 0xFFFFu;
-            const uint8_t pb[6] = {(uint8_t)(h[0] >> 16), (uint8_t)(h[0] >> 24), (uint8_t)(h[1] >> 16),
-                                   (uint8_t)(h[1] >> 24), (uint8_t)ck, (uint8_t)(ck >> 8)};
-            const uint32_t po[6] = {16, 17, 20, 21, 24, 25};
+            const uint16_t pw[3] = {(uint16_t)(h[0] >> 16), (uint16_t)(h[1] >> 16), (uint16_t)ck};
+            const uint32_t po[3] = {16, 20, 24};
+            if ((o0 & 1u) == 0u) {
 #pragma unroll
-            for (uint32_t j = 0; j < 6; ++j) __builtin_amdgcn_raw_buffer_store_b8(pb[j], fr, (int)(o0 + po[j]), 0, 0);
+                for (uint32_t j = 0; j < 3; ++j) __builtin_amdgcn_raw_buffer_store_b16(pw[j], fr, (int)(o0 + po[j]), 0, 0);
+            } else {
+#pragma unroll
+                for (uint32_t j = 0; j < 3; ++j) {
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)pw[j], fr, (int)(o0 + po[j]), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pw[j] >> 8), fr, (int)(o0 + po[j] + 1u), 0, 0);
+                }
+            }
             a.out_off[k] = o0;
             a.out_len[k] = (uint16_t)(34u + r.total);
             a.out_ptype[k] = 0x211u;
