@@ -1152,8 +1152,8 @@ struct SpecTail {
     unsigned long long out_cap;
     // in place (udpdk_gpu_rx_reassemble_inplace): reasm_clist_count checks every completion's
     // fragments (back to back in the frame buffer, in data order, no padding) and raises refuse
-    // (counts[5]) for one that is not; reasm_emit_inplace then runs only if none did, and
-    // reasm_emit only if one did
+    // (counts[5]) for one that is not; reasm_emit_either then moves in place if none did, and
+    // copies if one did
     uint32_t inplace;
     uint32_t *refuse;
     const uint32_t *offset;                      // the batch's descriptors
@@ -1369,15 +1369,13 @@ __device__ __forceinline__ uint4 merge_at(const uint4 x, const uint4 y, uint32_t
                       (x.z & m2) | (y.z & ~m2), (x.w & m3) | (y.w & ~m3));
 }
 
-__global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
+// the copying emit of C datagrams (reasm_emit; reasm_emit_either when in place was refused)
+__device__ __forceinline__ void emit_copy(const EmitArgs &a, uint32_t C)
 {
     // the wave index as a scalar: the datagram record and everything derived from it are
     // wave-uniform scalar loads and SGPRs, not per-lane copies
     const uint32_t lane = __lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
-    uint32_t F_unused, C = a.C;
-    if (!spec_tail_go(a.g, F_unused, C) || !spec_copy_fits(a.g)) return;
-    if (a.g.inplace && !__hip_atomic_load(a.g.refuse, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     // The next datagram's record and output offset are loaded while this one is copied.
     const uint32_t stride = gridDim.x * RS_WAVES;
     uint32_t k = blockIdx.x * RS_WAVES + w;
@@ -1545,12 +1543,9 @@ __device__ __forceinline__ void store_part(__amdgpu_buffer_rsrc_t r, uint32_t D,
 // last round (its destination covers the tail of fragment k's source). Then the header's total
 // length, fragment field (DF only) and checksum are patched. Datagrams are disjoint regions (the
 // caller's frames do not overlap), so waves never touch each other's bytes.
-__global__ void __launch_bounds__(RS_BLOCK) reasm_emit_inplace(EmitArgs a, uint8_t *frames)
+__device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames, uint32_t C)
 {
     const uint32_t lane = __lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t F_unused, C = a.C;
-    if (!spec_tail_go(a.g, F_unused, C)) return;
-    if (!a.g.inplace || __hip_atomic_load(a.g.refuse, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     const __amdgpu_buffer_rsrc_t fr = rsrc(frames, a.rsrc_bytes);
     constexpr uint32_t OOR = 0x80000000u;
     const uint32_t stride = gridDim.x * RS_WAVES;
@@ -1662,6 +1657,30 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit_inplace(EmitArgs a, uint8
 #pragma unroll
         for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) { fo[f] = fon[f]; sl[f] = sln[f]; }
     }
+}
+
+__global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
+{
+    uint32_t F_unused, C = a.C;
+    if (!spec_tail_go(a.g, F_unused, C) || !spec_copy_fits(a.g)) return;
+    emit_copy(a, C);
+}
+
+// A call that may reassemble in place: one launch takes whichever emit the device-side check
+// chose (in place unless reasm_clist_count refused it, then the copy when its buffer fits), so
+// the call has no second, empty emit launch.
+#ifndef UDPDK_EMIT_WPE
+#define UDPDK_EMIT_WPE 8
+#endif
+__global__ void __launch_bounds__(RS_BLOCK) __attribute__((amdgpu_waves_per_eu(UDPDK_EMIT_WPE, 8)))
+reasm_emit_either(EmitArgs a, uint8_t *frames)
+{
+    uint32_t F_unused, C = a.C;
+    if (!spec_tail_go(a.g, F_unused, C)) return;
+    if (!__hip_atomic_load(a.g.refuse, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        emit_inplace(a, frames, C);
+    else if (spec_copy_fits(a.g))
+        emit_copy(a, C);
 }
 
 struct StoreArgs {
@@ -1980,13 +1999,12 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         ea.g = g;
         ea.cksum_zero = (r->flags & UDPDK_FRAG_CKSUM_DPDK) ? 1u : 0u;
         const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_WAVES - 1) / RS_WAVES, 8192));
-        hipLaunchKernelGGL(reasm_emit, dim3(ge), dim3(RS_BLOCK), 0, st, ea);
-        RS_HIP(hipGetLastError());
-        if (g.inplace) {
-            hipLaunchKernelGGL(reasm_emit_inplace, dim3(ge), dim3(RS_BLOCK), 0, st, ea,
+        if (g.inplace)
+            hipLaunchKernelGGL(reasm_emit_either, dim3(ge), dim3(RS_BLOCK), 0, st, ea,
                                const_cast<uint8_t *>(bt->frames_dev));
-            RS_HIP(hipGetLastError());
-        }
+        else
+            hipLaunchKernelGGL(reasm_emit, dim3(ge), dim3(RS_BLOCK), 0, st, ea);
+        RS_HIP(hipGetLastError());
         return 0;
     };
     auto analysis = [&](uint32_t Fk, uint32_t Fgrid, bool grp) -> int {
