@@ -15,5 +15,6 @@ print('value', d['value'], 'ms', d['ms_per_step'], 'd1', d['depth1']['gpu_us_per
 print('scale', d['scale']['value'], 'strong', d['strong']['value'], 'cpu', d['cpu_baseline']['value'])"
 step prof2; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o rx -- python3 "$PWD/bench.py" --steps 100 --warmup 10 --no-cpu-baseline --no-extra --no-scale --no-strong --pipeline 1 > gpurun_out/prof.log 2>&1 || { tail gpurun_out/prof.log; exit 1; }
 step prof5; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof5" -o rx -- python3 "$PWD/bench.py" --config 5 --steps 50 --warmup 5 --no-cpu-baseline --no-extra --no-scale --no-strong --pipeline 1 > gpurun_out/prof5.log 2>&1 || { tail gpurun_out/prof5.log; exit 1; }
+step profreasm; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/profr" -o rx -- python3 "$PWD/tools/ab.py" --_line reasmip > gpurun_out/profr.log 2>&1 || { tail gpurun_out/profr.log; exit 1; }
 step pmc; PMC_CONFIGS="1 2 3 4 5" bash tools/pmc_traffic.sh || exit 1
 step done
