@@ -1659,7 +1659,11 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
     }
 }
 
-__global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
+// Both emits at 8 waves per SIMD: their SGPR budget alone allows 7 (106 SGPRs), and the move is
+// latency-bound, so the eighth wave is worth its SGPR spills to VGPR lanes (copy 514-521 -> 474-480
+// us per call, in place 447-472 -> 402-408 us; same-box A/Bs)
+__global__ void __launch_bounds__(RS_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8)))
+reasm_emit(EmitArgs a)
 {
     uint32_t F_unused, C = a.C;
     if (!spec_tail_go(a.g, F_unused, C) || !spec_copy_fits(a.g)) return;
@@ -1669,10 +1673,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_emit(EmitArgs a)
 // A call that may reassemble in place: one launch takes whichever emit the device-side check
 // chose (in place unless reasm_clist_count refused it, then the copy when its buffer fits), so
 // the call has no second, empty emit launch.
-#ifndef UDPDK_EMIT_WPE
-#define UDPDK_EMIT_WPE 8
-#endif
-__global__ void __launch_bounds__(RS_BLOCK) __attribute__((amdgpu_waves_per_eu(UDPDK_EMIT_WPE, 8)))
+__global__ void __launch_bounds__(RS_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8)))
 reasm_emit_either(EmitArgs a, uint8_t *frames)
 {
     uint32_t F_unused, C = a.C;
