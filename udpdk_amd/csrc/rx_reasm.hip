@@ -185,29 +185,25 @@ __device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, uint32_t off, 
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
-// crc32c (reflected, poly 0x82F63B78) of one dword from four 256-entry tables in LDS
-// (crc_table_init, slicing by 4: table k = a byte followed by k zero bytes), so a dword's four
-// lookups are independent instead of a chain of four (three dwords per fragment: 3 dependent LDS
-// round trips instead of 12; the bit-serial form was ~450 VALU instructions per fragment).
+// crc32c (reflected, poly 0x82F63B78) of one dword, a byte at a time from a 256-entry table of
+// the byte steps in LDS (crc_table_init): 4 lookups instead of 32 dependent bit steps (the
+// bit-serial form was ~450 VALU instructions per fragment, a sixth of reasm_runs).
 __device__ __forceinline__ uint32_t crc32c_u32(const uint32_t *tab, uint32_t crc, uint32_t v)
 {
     crc ^= v;
-    return tab[768u + (crc & 0xFFu)] ^ tab[512u + ((crc >> 8) & 0xFFu)] ^ tab[256u + ((crc >> 16) & 0xFFu)] ^
-           tab[crc >> 24];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) crc = (crc >> 8) ^ tab[crc & 0xFFu];
+    return crc;
 }
 
-// The block's four crc32c tables, 1024 words (RS_BLOCK >= 256 threads, one byte value each, every
-// table by further bit steps in registers); the caller syncs.
+// The block's crc32c byte table (RS_BLOCK >= 256 threads, one entry each); the caller syncs.
 __device__ __forceinline__ void crc_table_init(uint32_t *tab)
 {
     if (threadIdx.x < 256u) {
         uint32_t c = threadIdx.x;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
-            tab[256u * k + threadIdx.x] = c;
-        }
+        for (int i = 0; i < 8; ++i) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+        tab[threadIdx.x] = c;
     }
 }
 
@@ -406,7 +402,7 @@ __device__ __forceinline__ void prep_record(const ReasmArgs &a, const uint32_t *
 
 __global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
 {
-    __shared__ uint32_t crc_tab[1024];
+    __shared__ uint32_t crc_tab[256];
     crc_table_init(crc_tab);
     __syncthreads();
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
@@ -425,7 +421,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
 // another run, or two keys share a fingerprint) sets counts[4] and the batch takes the sorts.
 __global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned long long *hset, uint32_t hmask)
 {
-    __shared__ uint32_t crc_tab[1024];
+    __shared__ uint32_t crc_tab[256];
     crc_table_init(crc_tab);
     __syncthreads();
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
@@ -437,18 +433,15 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned lon
         const uint32_t p = pb + lane;
         const bool valid = p < F;
         const uint32_t i = valid ? a.frag_list[p] : 0u;
-        // the key of the position before the wave's first (lane 0's predecessor): the same loads
-        // in every lane (one line each), issued beside the lane's own chain instead of after it
-        const uint32_t op = a.offset[a.frag_list[pb > 0u ? pb - 1u : 0u]];
-        const uint32_t pw16 = ld32(fr, op + 16), ps0 = ld32(fr, op + 26), pd0 = ld32(fr, op + 30);
         const FragHdr h = frag_hdr(a, fr, i);
         const uint32_t id = h.id, src = h.src, dst = h.dst;
         if (valid) prep_record(a, crc_tab, p, i, h, false);
         uint32_t pid = __shfl_up(id, 1, 64), psrc = __shfl_up(src, 1, 64), pdst = __shfl_up(dst, 1, 64);
-        if (lane == 0u) {
-            pid = pw16 >> 16;
-            psrc = ps0;
-            pdst = pd0;
+        if (lane == 0u && valid && p > 0u) {
+            const uint32_t op = a.offset[a.frag_list[p - 1]];
+            pid = ld32(fr, op + 16) >> 16;
+            psrc = ld32(fr, op + 26);
+            pdst = ld32(fr, op + 30);
         }
         const bool start = p == 0u || pid != id || psrc != src || pdst != dst;
         if (!valid || !start) continue;
