@@ -1558,6 +1558,38 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
         for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) o[f] = f < mx ? a.offset[pick4(x.where, sx[f])] : 0u;
         return mx;
     };
+    // Quick moves: a datagram of two fragments whose move is one round (<= 128 chunks, the
+    // MTU-sized case) has its loads issued one datagram ahead, before the previous datagram's
+    // stores, so the wait for a datagram's bytes leaves the next one's in flight (two per wave at
+    // 8 waves per SIMD; the move is latency-bound) and never waits for the previous stores (gfx9
+    // counts stores in vmcnt, in order). The loads are unconditional (out-of-range offsets when
+    // there is nothing to load) so that wait stays a counted one. Other datagrams take the round
+    // loop.
+    struct Quick {
+        uint32_t D0, dst, De, shift, nch;
+        uint4 x[2];
+        uint32_t hi[2];
+    };
+    auto quick_geom = [&](const ReasmDone &x, const uint32_t (&o)[RS_MAX_FRAG], const uint32_t (&sx)[RS_MAX_FRAG],
+                          uint32_t mx, bool have, Quick &g) -> bool {
+        const uint32_t fq = pick4(x.fr, sx[1]);
+        g.dst = o[0] + 34u + (fq & 0xFFFFu);
+        g.D0 = g.dst & ~15u;
+        g.De = g.dst + (fq >> 16);
+        g.shift = o[1] + 34u - g.dst;
+        g.nch = (g.De - g.D0 + 15u) >> 4;
+        return have && mx == 2u && g.nch <= 128u;
+    };
+    auto quick_load = [&](Quick &g, bool on) {
+#pragma unroll
+        for (uint32_t u = 0; u < 2; ++u) {
+            const uint32_t c = 64u * u + lane;
+            const bool in = on && c < g.nch;
+            const uint32_t S = g.D0 + 16u * c + g.shift, sa = S & ~3u;
+            g.x[u] = load16(fr, in ? sa : OOR);
+            g.hi[u] = ld32(fr, in && (S & 3u) ? sa + 16u : OOR);
+        }
+    };
     ReasmDone r{}, rn{};
     uint32_t fo[RS_MAX_FRAG] = {0, 0, 0, 0}, sl[RS_MAX_FRAG] = {0, 0, 0, 0}, m = 0;
     if (k < C) {
@@ -1565,6 +1597,9 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
         m = offsets(r, fo, sl);
     }
     if (k + stride < C) rn = a.done[a.perm[k + stride]];
+    Quick qc, qn;
+    bool qc_on = quick_geom(r, fo, sl, m, k < C, qc);
+    quick_load(qc, qc_on);
     for (; k < C; k += stride) {
         uint32_t fon[RS_MAX_FRAG] = {0, 0, 0, 0}, sln[RS_MAX_FRAG] = {0, 0, 0, 0}, mn = 0;
         ReasmDone rnn{};
@@ -1580,9 +1615,25 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
             const auto h2 = __builtin_amdgcn_raw_buffer_load_b64(fr, (int)(lane == 0u ? ha + 16u : OOR), 0, 0);
             hw[0] = h4.x; hw[1] = h4.y; hw[2] = h4.z; hw[3] = h4.w; hw[4] = h2[0]; hw[5] = h2[1];
         }
+        const bool qn_on = quick_geom(rn, fon, sln, mn, k + stride < C, qn);
+        quick_load(qn, qn_on);                                   // the next datagram in flight
+        if (qc_on) {
+#pragma unroll
+            for (uint32_t u = 0; u < 2; ++u) {
+                const uint32_t c = 64u * u + lane;
+                if (c < qc.nch) {
+                    const uint32_t D = qc.D0 + 16u * c;
+                    const uint4 v = funnel4(qc.x[u], qc.hi[u], (D + qc.shift) & 3u);
+                    if (D >= qc.dst && D + 16u <= qc.De)
+                        store16(fr, D, v);
+                    else
+                        store_part(fr, D, v, D >= qc.dst ? 0u : qc.dst - D, min(qc.De - D, 16u));
+                }
+            }
+        }
 #pragma unroll
         for (uint32_t f = 1; f < RS_MAX_FRAG; ++f) {            // static indices: no scratch
-            if (f >= m) break;
+            if (qc_on || f >= m) break;
             const uint32_t q = sl[f];
             const uint32_t fq = pick4(r.fr, q);
             const uint32_t len = fq >> 16, ofs = fq & 0xFFFFu;
@@ -1656,6 +1707,8 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
         m = mn;
 #pragma unroll
         for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) { fo[f] = fon[f]; sl[f] = sln[f]; }
+        qc = qn;
+        qc_on = qn_on;
     }
 }
 
