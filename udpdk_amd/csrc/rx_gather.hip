@@ -22,11 +22,7 @@
 
 namespace udpdk {
 
-#ifndef UDPDK_GATHER_WPE
-#define UDPDK_GATHER_WPE 1
-#endif
-__global__ void __launch_bounds__(GATHER_BLOCK) __attribute__((amdgpu_waves_per_eu(UDPDK_GATHER_WPE, 8)))
-rx_gather(GatherArgs a)
+__global__ void __launch_bounds__(GATHER_BLOCK) rx_gather(GatherArgs a)
 {
     const __amdgpu_buffer_rsrc_t fr =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.frames), (short)0, (int)a.rsrc_bytes, 0x00020000);
@@ -93,76 +89,59 @@ rx_gather(GatherArgs a)
                     if (c + 16u * u < n) *reinterpret_cast<uint4 *>(dst + c + 16u * u) = v[u];
             }
         } else {
-            // long payloads: the wave copies its entries one at a time, every wave-load a
-            // contiguous KiB of one payload (lane i: bytes 16 i .. 16 i + 15 of each KiB). Sources
-            // are read from the dword-aligned offset at or below each piece (byte-aligned 16-byte
-            // loads run the vector memory path ~15-25 % slower, tools/probe/align_probe.hip) and
-            // funnelled by the payload's offset & 3 with the next lane's first dword; lane 63 loads
-            // its own next dword. The first 2 KiB of entry j + 1 are loaded before entry j's
-            // stores, so the wait for an entry's bytes leaves the next entry's in flight and never
-            // waits for the stores before them (gfx9 counts stores in vmcnt, in order); bytes past
-            // 2 KiB (reassembled datagrams) are copied after, one 2 KiB round at a time.
-            struct Piece {
-                uint4 v[2];
-                uint32_t e[2];
-            };
-            auto entry = [&](uint32_t j, uint32_t &nj, uint32_t &oj, uint64_t &dj) {
-                const uint32_t jj = min(j, 63u);
-                nj = j < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)n, (int)jj) : 0u;
-                oj = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)jj);
-                dj = a.slot_off ? (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)so32, (int)jj)
-                                : (uint64_t)(kw + jj) * a.slot_bytes;
-            };
-            auto load_round = [&](uint32_t nj, uint32_t oj, uint32_t c, Piece &p) {
-                const uint32_t shj = (oj + 42u) & 3u;
+            // long payloads: the wave copies its entries one pair at a time, every wave-load a
+            // contiguous KiB of one payload (lane i: bytes 16 i .. 16 i + 15 of each KiB)
+            for (uint32_t j = 0; j < 64u; j += 2u) {
+                uint32_t nj[2], oj[2];
+                uint64_t dj[2];
 #pragma unroll
-                for (uint32_t h2 = 0; h2 < 2; ++h2) {
-                    const uint32_t b = c + 1024u * h2 + 16u * lane;
-                    const uint32_t sa = (oj + 42u + b) & ~3u;
-                    // (a piece just past the payload still loads when the piece before it needs
-                    // its first dword)
-                    const auto x = __builtin_amdgcn_raw_buffer_load_b128(
-                        fr, (int)(b < nj + (shj != 0u ? 16u : 0u) ? sa : 0x80000000u), 0, 0);
-                    p.v[h2] = make_uint4(x[0], x[1], x[2], x[3]);
-                    p.e[h2] = __builtin_amdgcn_raw_buffer_load_b32(
-                        fr, (int)(lane == 63u && shj != 0u && b < nj ? sa + 16u : 0x80000000u), 0, 0);
+                for (uint32_t u = 0; u < 2; ++u) {
+                    nj[u] = (uint32_t)__builtin_amdgcn_readlane((int)n, (int)(j + u));
+                    oj[u] = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)(j + u));
+                    dj[u] = a.slot_off ? (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)so32, (int)(j + u))
+                                       : (uint64_t)(kw + j + u) * a.slot_bytes;
                 }
-            };
-            auto store_round = [&](uint32_t nj, uint32_t oj, uint64_t dj, uint32_t c, const Piece &p) {
-                const uint32_t shj = (oj + 42u) & 3u;
+                const uint32_t m = max(nj[0], nj[1]);
+                // Sources are read from the dword-aligned offset at or below each piece (byte-
+                // aligned 16-byte loads run the vector memory path ~15-25 % slower,
+                // tools/probe/align_probe.hip) and funnelled by the payload's offset & 3 with the
+                // next lane's first dword; lane 63 loads its own next dword. Shift 0: identity.
+                uint32_t sh[2];
 #pragma unroll
-                for (uint32_t h2 = 0; h2 < 2; ++h2) {
-                    const uint32_t b = c + 1024u * h2 + 16u * lane;
-                    const uint4 x = p.v[h2];
-                    const uint32_t nx = __shfl_down(x.x, 1, 64);
-                    const uint32_t hi = lane == 63u ? p.e[h2] : nx;
-                    const uint4 y = make_uint4(__builtin_amdgcn_alignbyte(x.y, x.x, shj),
-                                               __builtin_amdgcn_alignbyte(x.z, x.y, shj),
-                                               __builtin_amdgcn_alignbyte(x.w, x.z, shj),
-                                               __builtin_amdgcn_alignbyte(hi, x.w, shj));
-                    if (b < nj) *reinterpret_cast<uint4 *>(a.payload + dj + b) = y;
+                for (uint32_t u = 0; u < 2; ++u) sh[u] = (oj[u] + 42u) & 3u;
+                for (uint32_t c = 0; c < m; c += 2048u) {
+                    uint4 v[2][2];
+                    uint32_t e[2][2];
+#pragma unroll
+                    for (uint32_t u = 0; u < 2; ++u)
+#pragma unroll
+                        for (uint32_t h2 = 0; h2 < 2; ++h2) {
+                            const uint32_t b = c + 1024u * h2 + 16u * lane;
+                            const uint32_t sa = (oj[u] + 42u + b) & ~3u;
+                            // (a piece just past the payload still loads when the piece before
+                            // it needs its first dword)
+                            const auto x = __builtin_amdgcn_raw_buffer_load_b128(
+                                fr, (int)(b < nj[u] + (sh[u] != 0u ? 16u : 0u) ? sa : 0x80000000u), 0, 0);
+                            v[u][h2] = make_uint4(x[0], x[1], x[2], x[3]);
+                            e[u][h2] = __builtin_amdgcn_raw_buffer_load_b32(
+                                fr, (int)(lane == 63u && sh[u] != 0u && b < nj[u] ? sa + 16u : 0x80000000u), 0, 0);
+                        }
+#pragma unroll
+                    for (uint32_t u = 0; u < 2; ++u)
+#pragma unroll
+                        for (uint32_t h2 = 0; h2 < 2; ++h2) {
+                            const uint32_t b = c + 1024u * h2 + 16u * lane;
+                            const uint4 x = v[u][h2];
+                            const uint32_t nx = __shfl_down(x.x, 1, 64);
+                            const uint32_t hi = lane == 63u ? e[u][h2] : nx;
+                            const uint4 y = make_uint4(__builtin_amdgcn_alignbyte(x.y, x.x, sh[u]),
+                                                       __builtin_amdgcn_alignbyte(x.z, x.y, sh[u]),
+                                                       __builtin_amdgcn_alignbyte(x.w, x.z, sh[u]),
+                                                       __builtin_amdgcn_alignbyte(hi, x.w, sh[u]));
+                            if (b < nj[u])
+                                *reinterpret_cast<uint4 *>(a.payload + dj[u] + b) = y;
+                        }
                 }
-            };
-            uint32_t nc, oc;
-            uint64_t dc;
-            entry(0u, nc, oc, dc);
-            Piece pc, pn;
-            load_round(nc, oc, 0u, pc);
-            for (uint32_t j = 0; j < 64u; ++j) {
-                uint32_t nn, on;
-                uint64_t dn;
-                entry(j + 1u, nn, on, dn);                        // nn = 0 past the wave's last
-                load_round(nn, on, 0u, pn);
-                store_round(nc, oc, dc, 0u, pc);
-                for (uint32_t c = 2048u; c < nc; c += 2048u) {   // reassembled datagrams only
-                    Piece px;
-                    load_round(nc, oc, c, px);
-                    store_round(nc, oc, dc, c, px);
-                }
-                nc = nn;
-                oc = on;
-                dc = dn;
-                pc = pn;
             }
         }
     }
