@@ -857,62 +857,80 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_process(ReasmArgs a, uint32_t 
     const bool fallback = a.counts[3] != 0;
     const uint32_t step = gridDim.x * RS_BLOCK;
     unsigned long long c_len = 0, c_short = 0, c_done = 0, c_holes = 0, c_err = 0, c_bytes = 0;
-    for (uint32_t p0 = blockIdx.x * RS_BLOCK + (threadIdx.x & ~63u); p0 < F; p0 += step) {
-        const uint32_t p = p0 + __lane_id();
-        uint32_t nser = 0;
-        bool serial = false;
-        const uint32_t f = p < F ? a.pflag[p] : 0u;
-        const uint32_t oc = (f & PF_START) ? a.oc[p] : 0u;
-        serial = (f & PF_TOUCH) && (fallback || (f & (PF_COMPLEX | PF_SHARED)));
-        if ((f & PF_START) && !serial && !(oc & OC_OVF)) {
-            // reasm_flows walked this flow on its own and wrote its completions: add up
-            c_len += oc & 63u;
-            c_short += (oc >> 6) & 63u;
-            c_done += (oc >> 12) & 63u;
-            c_holes += (oc >> 18) & 63u;
-            c_err += (oc >> 24) & 63u;
-            c_bytes += a.ob[p];
-        } else if (f & PF_START) {
-            bool live = false;
-            for (uint32_t q = p; q < F && (q == p || same_key(a, p, q)); ++q) {
-                const uint32_t m = a.s_meta[q], cls = m >> 30;
-                if (cls) {
-                    if (cls == 1) ++c_len;
-                    else ++c_short;
-                    continue;
-                }
-                if (serial) {
-                    ++nser;
-                    a.dk[q] = RS_NONE;                 // reasm_flows' completion, if any, is void
-                    continue;
-                }
-                const uint32_t i = a.s_i[q];
-                if (!live) state_reset(st, 0, 0, 0, 0, 0);
-                uint32_t idx;
-                const uint32_t r = frag_apply(st, m & 0xFFFFu, ((m >> 16) & 0x1FFFu) * 8u, (m >> 29) & 1u, i, &idx);
-                live = r == FA_KEEP;
-                if (r == FA_DONE) {
-                    write_done(a, st, q, i, RS_NONE);
-                    ++c_done;
-                    c_bytes += (34u + st[E_TOTAL] + 15u) & ~15u;
-                } else if (r == FA_HOLE) {
-                    ++c_holes;
-                } else if (r != FA_KEEP) {
-                    ++c_err;
+    // The wave's positions are taken PF grid strides at a time with every flag and outcome word of
+    // the batch loaded at once (clamped indices, unconditional): the per-position loads were one
+    // dependent round trip per grid stride (8 strides per wave at 512 K fragments).
+    constexpr uint32_t PF = 8;
+    const uint32_t fl = F ? F - 1u : 0u;
+    for (uint32_t pb = blockIdx.x * RS_BLOCK + (threadIdx.x & ~63u); pb < F; pb += step * PF) {
+        uint32_t fv[PF], ocv[PF], obv[PF];
+#pragma unroll
+        for (uint32_t it = 0; it < PF; ++it) {
+            const uint32_t p = pb + it * step + __lane_id();
+            fv[it] = p < F ? a.pflag[min(p, fl)] : 0u;
+            ocv[it] = a.oc[min(p, fl)];
+            obv[it] = a.ob[min(p, fl)];
+        }
+#pragma unroll 1
+        for (uint32_t it = 0; it < PF; ++it) {
+            const uint32_t p0 = pb + it * step;
+            if (p0 >= F) break;                                      // wave-uniform
+            const uint32_t p = p0 + __lane_id();
+            uint32_t nser = 0;
+            bool serial = false;
+            const uint32_t f = fv[it];
+            const uint32_t oc = (f & PF_START) ? ocv[it] : 0u;
+            serial = (f & PF_TOUCH) && (fallback || (f & (PF_COMPLEX | PF_SHARED)));
+            if ((f & PF_START) && !serial && !(oc & OC_OVF)) {
+                // reasm_flows walked this flow on its own and wrote its completions: add up
+                c_len += oc & 63u;
+                c_short += (oc >> 6) & 63u;
+                c_done += (oc >> 12) & 63u;
+                c_holes += (oc >> 18) & 63u;
+                c_err += (oc >> 24) & 63u;
+                c_bytes += obv[it];
+            } else if (f & PF_START) {
+                bool live = false;
+                for (uint32_t q = p; q < F && (q == p || same_key(a, p, q)); ++q) {
+                    const uint32_t m = a.s_meta[q], cls = m >> 30;
+                    if (cls) {
+                        if (cls == 1) ++c_len;
+                        else ++c_short;
+                        continue;
+                    }
+                    if (serial) {
+                        ++nser;
+                        a.dk[q] = RS_NONE;                 // reasm_flows' completion, if any, is void
+                        continue;
+                    }
+                    const uint32_t i = a.s_i[q];
+                    if (!live) state_reset(st, 0, 0, 0, 0, 0);
+                    uint32_t idx;
+                    const uint32_t r = frag_apply(st, m & 0xFFFFu, ((m >> 16) & 0x1FFFu) * 8u, (m >> 29) & 1u, i, &idx);
+                    live = r == FA_KEEP;
+                    if (r == FA_DONE) {
+                        write_done(a, st, q, i, RS_NONE);
+                        ++c_done;
+                        c_bytes += (34u + st[E_TOTAL] + 15u) & ~15u;
+                    } else if (r == FA_HOLE) {
+                        ++c_holes;
+                    } else if (r != FA_KEEP) {
+                        ++c_err;
+                    }
                 }
             }
-        }
-        uint32_t total;
-        const uint32_t off = wave_excl_scan(nser, &total);
-        uint32_t base = 0;
-        if (__lane_id() == 0 && total) base = atomicAdd(&a.counts[2], total);
-        base = __shfl(base, 0, 64) + off;
-        if (nser) {
-            for (uint32_t q = p; q < F && (q == p || same_key(a, p, q)); ++q) {
-                if (a.s_meta[q] >> 30) continue;
-                a.sl_k[base] = a.s_i[q];
-                a.sl_v[base] = q;
-                ++base;
+            uint32_t total;
+            const uint32_t off = wave_excl_scan(nser, &total);
+            uint32_t base = 0;
+            if (__lane_id() == 0 && total) base = atomicAdd(&a.counts[2], total);
+            base = __shfl(base, 0, 64) + off;
+            if (nser) {
+                for (uint32_t q = p; q < F && (q == p || same_key(a, p, q)); ++q) {
+                    if (a.s_meta[q] >> 30) continue;
+                    a.sl_k[base] = a.s_i[q];
+                    a.sl_v[base] = q;
+                    ++base;
+                }
             }
         }
     }
