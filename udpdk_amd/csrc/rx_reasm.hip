@@ -1156,7 +1156,10 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_sizes(const ReasmDone *done, c
 // launches (per 2048-position block: count and bytes; then each block's base from its
 // predecessors' totals and a block scan), instead of a rocPRIM select, a size pass and a rocPRIM
 // scan (three passes, six launches with the scans' state initialisation).
-constexpr uint32_t RS_CL = 2048;                 // positions per block, 8 per thread
+#ifndef UDPDK_RS_CL
+#define UDPDK_RS_CL 512
+#endif
+constexpr uint32_t RS_CL = UDPDK_RS_CL;           // positions per block, 2 per thread (8: +6 us per call)
 
 // The grouped path's tail (completion list, offsets, emit) launched right behind reasm_process,
 // before the host has read the call's counts back (counts == nullptr: an ordinary launch). It runs
