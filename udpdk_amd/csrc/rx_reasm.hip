@@ -64,7 +64,10 @@ constexpr uint32_t RS_NONE = 0xFFFFFFFFu;
 // per-call device block: stats [UDPDK_RS_N], out_bytes [1], counts [8 x u32] (u64 words)
 constexpr uint32_t RS_ZERO_WORDS = UDPDK_RS_N + 1 + 4;
 constexpr uint32_t RS_MAX_FRAG = 4;             // RTE_LIBRTE_IP_FRAG_MAX_FRAG
-constexpr uint32_t RS_FLOW_CHUNK = 1024;        // sorted positions per reasm_flows block step
+#ifndef UDPDK_RS_FLOW_CHUNK
+#define UDPDK_RS_FLOW_CHUNK 512
+#endif
+constexpr uint32_t RS_FLOW_CHUNK = UDPDK_RS_FLOW_CHUNK;   // sorted positions per reasm_flows block step (1024: +7 us per call)
 
 // Bits to hold every value in [0, v]
 inline uint32_t bits_for(uint32_t v) { return v ? 32u - (uint32_t)__builtin_clz(v) : 1u; }
