@@ -2076,6 +2076,8 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         ea.C = Cn;
         ea.g = g;
         ea.cksum_zero = (r->flags & UDPDK_FRAG_CKSUM_DPDK) ? 1u : 0u;
+        // (a grid of 2048 or 4096 workgroups, one resident generation with longer per-wave
+        // pipelines, measured even or slower: same-box A/B, 4 pairs)
         const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_WAVES - 1) / RS_WAVES, 8192));
         if (g.inplace)
             hipLaunchKernelGGL(reasm_emit_either, dim3(ge), dim3(RS_BLOCK), 0, st, ea,
