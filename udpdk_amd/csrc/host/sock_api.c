@@ -460,7 +460,8 @@ ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
     const uint32_t t = atomic_load_explicit(&r->tail, memory_order_acquire);
     if (t != h + 1) {
         /* the next datagram's bytes are fetched while this one is copied: recvfrom at 1500 B is
-         * one memcpy out of host memory per call, bound by the core's cache misses */
+         * one memcpy out of host memory per call, bound by the core's cache misses (two entries
+         * ahead measured even at 1500 B and 8 % slower at IMIX) */
         const struct h_dgram *nx = &r->e[(h + 1) % UDPDK_RX_RING_SIZE];
         const char *np = (const char *)nx->data;
         for (uint32_t o = 0; o < nx->len; o += 64) __builtin_prefetch(np + o);
