@@ -266,6 +266,29 @@ def pci_bus_id(device: int) -> str:
     return buf.value.decode() if rc == 0 else f"unknown(rc={rc})"
 
 
+def effective_cpus() -> int:
+    """The CPUs the process can actually use at once: its affinity mask, capped by the cgroup
+    CPU quota (the GPU boxes show 256 CPUs in the mask under a 16-CPU quota; threads beyond
+    the quota time-slice). The count the CPU baseline's "cores" states."""
+    n = host_cores()
+    for f in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(f).read().split()[:2]
+            if q != "max":
+                n = min(n, max(1, math.ceil(int(q) / int(per))))
+            return n
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            n = min(n, max(1, math.ceil(q / per)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_quota() -> str:
     """The cgroup CPU limit of this process (v2 cpu.max, else v1 cfs quota/period): the share of
     the host cores the affinity mask may not show."""
@@ -319,7 +342,8 @@ def cpu_baseline(w: F.Workload, target_s: float, gpu_dig: str | None = None, swe
         parity["match"] = parity["oracle"] == parity["gpu"]
     res = {"parity": parity, "sweep": {}}
     cores = host_cores()
-    counts = sorted({t for t in (1, 16, 32, 64, 128, 256) if t <= cores} | {cores}) if sweep else [1, cores]
+    eff = effective_cpus()
+    counts = sorted({t for t in (1, 16, 32, 64, 128, 256) if t <= cores} | {cores, eff}) if sweep else [1, cores]
 
     def leg(th, csum):
         # calibrate reps so the timed leg takes ~target_s (every rep: th x n frames)
@@ -685,7 +709,8 @@ def end_to_end(ctx, cfg: int, reps: int):
             "path": "pinned host frames -> H2D -> rx pipeline -> D2H meta+lanes, synchronous"}
 
 
-def socket_path_lines(specs=((1 << 20, 64, 1024, 5), (1 << 20, 0, 1024, 3), (1 << 20, 1500, 1024, 3)),
+def socket_path_lines(specs=((1 << 20, 64, 1024, 5), (1 << 20, 0, 1024, 3), (1 << 20, 1500, 1024, 3),
+                             (1 << 13, 65000, 64, 3)),
                       gpu_extra: str = ""):
     """The reference-API path end to end: tools/bin/bench_sock, a C program
     written against include/udpdk_api.h like the reference's apps, times udpdk_poll_rx (frames in
@@ -714,6 +739,20 @@ def socket_path_lines(specs=((1 << 20, 64, 1024, 5), (1 << 20, 0, 1024, 3), (1 <
     finally:
         os.unlink(ini)
     return out
+
+
+def rank_parity(ctx, rx: Rx, dist) -> dict:
+    """Parity of this rank's measured batch (outside the timed region): the digest of the GPU's
+    verdict words and lanes for one call against the oracle's for the same frames (SURVEY.md
+    §8(d) parity mode), gathered over the ranks so a multi-GPU run verifies every shard."""
+    mine = {"gpu": gpu_digest(ctx, rx.args[0][5], rx.n, rx.w.n_sockets), "oracle": oracle_digest(rx.w)}
+    mine["match"] = mine["gpu"] == mine["oracle"]
+    ranks = [mine]
+    if dist is not None:
+        ranks = [None] * dist.get_world_size()
+        dist.all_gather_object(ranks, mine)
+    return {"rank0": mine, "all_ranks_match": all(r["match"] for r in ranks),
+            "per_rank_match": [r["match"] for r in ranks]}
 
 
 def strong_pieces(world: int, rank: int, pieces: int) -> range:
@@ -772,6 +811,7 @@ def strong_line(ctx, world: int, rank: int, barrier, dist, steps: int, warmup: i
            "ms_per_step": round(1e3 * wall / steps, 5), "pipeline_depth": depth,
            "gbps_pipeline": round(rx.pipeline_bytes() * world * steps / wall / 1e9, 1),
            "rank0_mpkt_s": round(mine, 2), "rank0_gpu_us_per_step": round(1e3 * gpu_step, 3)}
+    out["parity"] = rank_parity(ctx, rx, dist)
     for a in rx.args:
         a[4].frames.free(); a[4].offset.free(); a[4].length.free()
         a[5].meta.free(); a[5].lane_off.free(); a[5].lane_pkt.free()
@@ -802,6 +842,7 @@ def scale_line(ctx, world: int, rank: int, barrier, dist, steps: int, warmup: in
            "ms_per_step": round(1e3 * wall / steps, 5), "scaling": "weak", "pipeline_depth": depth,
            "gbps_pipeline": round(gbps, 1), "frac_hbm_pipeline_per_gpu": round(gbps / world / HBM_PEAK_GBS, 4),
            "rank0_mpkt_s": round(mine, 2), "rank0_gpu_us_per_step": round(1e3 * gpu_step, 3)}
+    out["parity"] = rank_parity(ctx, rx5, dist)
     for a in rx5.args:
         a[4].frames.free(); a[4].offset.free(); a[4].length.free()
         a[5].meta.free(); a[5].lane_off.free(); a[5].lane_pkt.free()
@@ -915,6 +956,19 @@ def main():
         except Exception:
             traffic = None
 
+    rocprof = None
+    rf = os.path.join(ROOT, "profiles", "rocprof_classify.json")
+    if os.path.exists(rf):
+        try:
+            with open(rf) as f:
+                r = json.load(f)["workloads"].get(w.name)
+            if r:
+                rocprof = {"kernel_us": r["mean_us"], "source": r["source"],
+                           "achieved": round(cls_bytes / r["mean_us"] / 1e3, 1),
+                           "frac": round(cls_bytes / r["mean_us"] / 1e3 / HBM_PEAK_GBS, 4)}
+        except Exception:
+            rocprof = None
+
     line = {
         "metric": "device-resident Mpkt/s + GB/s, RX parse+cksum+port-demux, 64B & 1500B frames",
         "value": round(mpkt_s, 2),
@@ -943,7 +997,9 @@ def main():
                      "traffic": traffic, "kernel": "rx_classify",
                      "traffic_source": "profiles/traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                                        "passes of this workload (tools/pmc_traffic.sh)",
-                     "algorithmic_bytes_per_launch": cls_bytes},
+                     "algorithmic_bytes_per_launch": cls_bytes,
+                     "kernel_us_events": round(cls_us, 3),
+                     "rocprof": rocprof},
         "cpu_baseline": None,
     }
     line["per_rank"] = per_rank
@@ -957,11 +1013,14 @@ def main():
         res, cores = cpu_baseline(w, args.cpu_seconds, gdig)
         best = res["best"]
         v, reps, secs = res["sweep"][best]
+        eff = effective_cpus()
         line["cpu_baseline"] = {
-            "value": round(v, 2), "unit": "Mpkt/s", "cores": best, "kind": "port",
-            "sample": f"{best} pinned threads (the best of the sweep), each running the poller "
-                      f"restatement over its own NUMA-local copy of the {rx.n}-frame {w.name} batch "
-                      f"x {reps} passes ({secs:.1f} s), RX checksum verification on",
+            "value": round(v, 2), "unit": "Mpkt/s", "cores": min(best, eff), "kind": "port",
+            "sample": f"{best} pinned threads (the best of the sweep) on {min(best, eff)} effective "
+                      f"CPUs (affinity {cores}, cgroup quota {cpu_quota()}), each thread running the "
+                      f"poller restatement over its own NUMA-local copy of the {rx.n}-frame {w.name} "
+                      f"batch x {reps} passes ({secs:.1f} s), RX checksum verification on",
+            "threads": best, "effective_cpus": eff,
             "threads_sweep_mpkt_s": {str(t): round(x[0], 2) for t, x in res["sweep"].items()},
             "all_cores": {"threads": cores, "mpkt_s": round(res["sweep"][cores][0], 2)},
             "affinity_cores": cores, "cgroup_cpu_quota": cpu_quota(),

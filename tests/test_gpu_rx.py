@@ -166,6 +166,15 @@ def test_zipf_4096_full(gpu_ctx):
     assert np.all(d[mask] > 0)
 
 
+@pytest.mark.parametrize("shard", range(1, 8))
+def test_zipf_4096_other_shards(gpu_ctx, shard):
+    """Config 5's other shards (seeds 1001-1007: the frames each rank of an 8-GPU run gets),
+    at a quarter of the full size: exact against the oracle."""
+    w = F.config_batch(5, n=1 << 20, shard=shard)
+    want, got = _rx_both(gpu_ctx, w.batch, w.port_lists(), w.n_sockets)
+    _assert_same(want, got, f"{w.name} shard {shard}")
+
+
 @pytest.mark.parametrize("seed", [21, 22])
 def test_tail_checksums_every_alignment(gpu_ctx, seed):
     """rx_classify sums a datagram's tail (frame bytes [64, end)) from the dword-aligned buffer

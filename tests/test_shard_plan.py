@@ -47,3 +47,17 @@ def test_bad_lists(tmp_path):
 def test_plan_truncates_to_max(tmp_path):
     n, dev = _plan(tmp_path, "[gpu]\ndevices = 0-7\n", max_=3)
     assert n == 8 and dev == [0, 1, 2]
+
+
+@pytest.mark.parametrize("body,want", [
+    # a later single device moves only the main context: the shard list stays (as udpdk_init)
+    ("devices = 0-3\ndevice = 5\n", [0, 1, 2, 3]),
+    ("device = 5\ndevices = 0-3\n", [0, 1, 2, 3]),
+    # a one-entry list is no shard list: one context, on the last device named
+    ("devices = 2\n", [2]),
+    ("devices = 2\ndevice = 5\n", [5]),
+    ("device = 5\ndevices = 2\n", [2]),
+])
+def test_device_and_devices_key_order(tmp_path, body, want):
+    n, dev = _plan(tmp_path, "[gpu]\n" + body)
+    assert n == len(want) and dev == want

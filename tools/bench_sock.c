@@ -143,7 +143,7 @@ int main(int argc, char **argv)
     uint8_t *fr = NULL;
     if (udpdk_gpu_host_alloc(udpdk_gpu_context(), bytes + 64, (void **)&fr)) { perror("host_alloc"); return 1; }
     for (uint32_t i = 0; i < n; i++) make_frame(fr + off[i], len[i], (uint16_t)(10000 + i % (uint32_t)S), i);
-    static char buf[2048];
+    static char buf[65536];                    /* up to the largest UDP payload */
     double t_poll = 0, t_recv = 0;
     uint64_t got = 0, pbytes = 0;
     for (int r = 0; r < reps + 1; r++) {                        /* rep 0 warms up */

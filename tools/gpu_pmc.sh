@@ -1,5 +1,6 @@
-# Before/after PMC passes of rx_classify at config 2 (and config 5): the round-3 library
-# (tools/var/old.so) against the current one, one counter group per rocprofv3 run.
+# Before/after PMC passes of rx_classify at config 2 (and config 5): an earlier revision's library
+# against the current one, one counter group per rocprofv3 run. Build the earlier one first:
+#   tools/build_rev.sh <rev> old          # -> tools/var/old.so
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

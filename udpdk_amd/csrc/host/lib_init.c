@@ -139,8 +139,9 @@ int udpdk_shard_plan(const char *cfg_path, int *devices, int max)
     FILE *f = fopen(cfg_path, "r");
     if (!f) return -ENOENT;
     char line[512], section[64] = "";
-    int dev[H_MAX_DEVS], n = 1, rc = 0;
-    dev[0] = 0;
+    /* the two keys tracked apart, as h_load_ini does: "devices" sets the shard list and the main
+     * context's device; a later "device" moves only the main context's device */
+    int dev[H_MAX_DEVS], n = 0, single = 0, rc = 0;
     while (fgets(line, sizeof(line), f)) {
         char *s = h_trim(line);
         if (!*s || *s == '#' || *s == ';') continue;
@@ -156,15 +157,19 @@ int udpdk_shard_plan(const char *cfg_path, int *devices, int max)
         *eq = 0;
         const char *k = h_trim(s), *v = h_trim(eq + 1);
         if (!strcmp(k, "device")) {
-            dev[0] = atoi(v);
-            n = 1;
+            single = atoi(v);
         } else if (!strcmp(k, "devices")) {
             n = h_parse_device_list(v, dev);
             if (n < 0) { rc = -EINVAL; break; }
+            single = dev[0];
         }
     }
     fclose(f);
     if (rc) return rc;
+    if (n < 2) {                        /* no shard list: the one context of gpu_device */
+        n = 1;
+        dev[0] = single;
+    }
     for (int k = 0; k < n && k < max; k++) devices[k] = dev[k];
     return n;
 }

@@ -21,6 +21,10 @@
 
 #include "host_state.h"
 
+#ifndef UDPDK_RECV_PREFETCH
+#define UDPDK_RECV_PREFETCH 4096u      /* bytes of the next datagram prefetched by recvfrom */
+#endif
+
 struct h_state g_udpdk;
 
 static int h_valid_fd(int s) { return s >= 0 && s < UDPDK_MAX_SOCKETS; }
@@ -461,10 +465,14 @@ ssize_t udpdk_recvfrom(int s, void *buf, size_t len, int flags,
     if (t != h + 1) {
         /* the next datagram's bytes are fetched while this one is copied: recvfrom at 1500 B is
          * one memcpy out of host memory per call, bound by the core's cache misses (two entries
-         * ahead measured even at 1500 B and 8 % slower at IMIX) */
+         * ahead measured even at 1500 B and 8 % slower at IMIX). Only the first
+         * UDPDK_RECV_PREFETCH bytes: a 64 KiB datagram would otherwise issue 1024 prefetches
+         * competing with this call's own copy (the hardware prefetcher follows the memcpy's
+         * stream past them) */
         const struct h_dgram *nx = &r->e[(h + 1) % UDPDK_RX_RING_SIZE];
         const char *np = (const char *)nx->data;
-        for (uint32_t o = 0; o < nx->len; o += 64) __builtin_prefetch(np + o);
+        const uint32_t pf = nx->len < UDPDK_RECV_PREFETCH ? nx->len : UDPDK_RECV_PREFETCH;
+        for (uint32_t o = 0; o < pf; o += 64) __builtin_prefetch(np + o);
     }
     const size_t n = d.len < len ? d.len : len;
     if (n) memcpy(buf, d.data, n);
