@@ -65,7 +65,10 @@ int main()
         printf("%-8s G=%5d lds=%6zu  entry spread us p10 %.2f p50 %.2f p90 %.2f max %.2f\n", name, G, lds,
                pc(0.1), pc(0.5), pc(0.9), pc(1.0));
     };
-    for (size_t l : {15872, 17920, 20480, 32768, 40000})
+    run("light", k_light, 1024, 0);
+    run("light", k_light, 2048, 0);
+    run("vgpr", k_vgpr, 1024, 28160);
+    for (size_t l : {15872, 17920, 20480, 28160, 32768, 40000})
         run("lds", k_lds, 1024, l);
     run("lds", k_lds, 512, 40000);
     run("lds", k_lds, 512, 65536);

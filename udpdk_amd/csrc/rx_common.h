@@ -24,6 +24,9 @@ constexpr uint32_t RX_HIST_CAP = UDPDK_RX_HIST_CAP;  // target bound on lanes x 
 #ifndef UDPDK_CLS_BLOCK
 #define UDPDK_CLS_BLOCK 256
 #endif
+#ifndef UDPDK_CLS_EARLY
+#define UDPDK_CLS_EARLY 0                    // rx_classify<1>: next window issued at the step's top
+#endif
 #ifndef UDPDK_CLS_WPE
 #define UDPDK_CLS_WPE 4                      // rx_classify minimum waves per SIMD (VGPR budget)
 #endif

@@ -355,8 +355,6 @@ rx_classify(RxArgs a)
     // deliveries per lane, <= 8192 without fan-out), stored as a u16 row
     const uint32_t hsh = a.hist16 ? 1u : 0u;
     auto hist_add = [&](uint32_t k, uint32_t v) { atomicAdd(&hist[k >> hsh], v << ((k & hsh) << 4)); };
-    if (a.n_lanes > 1u)
-        for (uint32_t s = tid; s < ((a.n_lanes + hsh) >> hsh); s += CLS_BLOCK) hist[s] = 0;
     // Tiles in dispatch order (consecutive tiles on different XCDs). An XCD-contiguous remap
     // (each XCD's L2 streaming one contiguous eighth of the batch) measured 1.7 us slower per
     // 1 M x 64 B launch (tools/probe/stream_probe.hip, feat4).
@@ -376,21 +374,32 @@ rx_classify(RxArgs a)
     const uint32_t plast = a.n - 1u;
     // round r's descriptors (frames t0 + RX_ROUND r + [0, RX_ROUND)) into buffer r & 1; the
     // ptype array, when given, only contributes its L3_IPV4 bit (udpdk_poller.c:334)
-    auto stage = [&](uint32_t r) {
-        uint32_t o[RX_ROUND / CLS_BLOCK], l[RX_ROUND / CLS_BLOCK], t[RX_ROUND / CLS_BLOCK];
+    // (the ptype word is loaded unconditionally, from the offset array when there is no ptype
+    // array, and masked: a load under a condition makes the compiler wait for it in the branch)
+    const bool has_ptype = a.ptype != nullptr;
+    const uint32_t *ptw = has_ptype ? a.ptype : a.offset;
+    constexpr uint32_t SPT = RX_ROUND / CLS_BLOCK;          // descriptors staged per thread
+    auto stage_load = [&](uint32_t r, uint32_t (&o)[SPT], uint32_t (&l)[SPT], uint32_t (&t)[SPT]) {
 #pragma unroll
-        for (uint32_t i = 0; i < RX_ROUND / CLS_BLOCK; ++i) {
+        for (uint32_t i = 0; i < SPT; ++i) {
             const uint32_t pc = min(t0 + r * RX_ROUND + i * CLS_BLOCK + tid, plast);
             o[i] = a.offset[pc];
             l[i] = a.length[pc];
-            t[i] = a.ptype ? a.ptype[pc] : 0u;
+            t[i] = ptw[pc];
         }
+    };
+    auto stage_store = [&](uint32_t r, const uint32_t (&o)[SPT], const uint32_t (&l)[SPT], const uint32_t (&t)[SPT]) {
         const uint32_t b = (r & (nbuf - 1u)) * RX_ROUND;
 #pragma unroll
-        for (uint32_t i = 0; i < RX_ROUND / CLS_BLOCK; ++i) {
+        for (uint32_t i = 0; i < SPT; ++i) {
             d_off[b + i * CLS_BLOCK + tid] = o[i];
-            d_lp[b + i * CLS_BLOCK + tid] = l[i] | ((t[i] & 0x10u) << 12);
+            d_lp[b + i * CLS_BLOCK + tid] = l[i] | (has_ptype ? (t[i] & 0x10u) << 12 : 0u);
         }
+    };
+    auto stage = [&](uint32_t r) {
+        uint32_t o[SPT], l[SPT], t[SPT];
+        stage_load(r, o, l, t);
+        stage_store(r, o, l, t);
     };
     // step s's descriptor for this lane (the index wraps inside the buffers for s >= steps)
     auto read_desc = [&](uint32_t s, uint32_t &o, uint32_t &lp) {
@@ -418,18 +427,33 @@ rx_classify(RxArgs a)
         return r;
     };
 
+    // Prologue, shortest chain first: the round's descriptor loads go out before anything else,
+    // and the first window (step w: frames t0 + tid, this thread's own first descriptor) before
+    // the descriptors are staged and the workgroup waits at the barrier. The argument-borne bind
+    // table (a vector load from the kernel-argument segment) and the LDS initialisation follow,
+    // off that chain (each used to cost a dependent round trip ahead of the descriptor loads).
     __shared__ uint32_t tail_any;           // some wave of the tile ran a tail pass (kernel hint)
-    if (tid == 0) tail_any = 0u;            // (ordered by the staging barrier)
     __shared__ uint4 inl_tab[UDPDK_INLINE_PORTS + 1];   // RxArgs::inl entries + a zero slot
-    if (a.inl && tid <= UDPDK_INLINE_PORTS)
-        inl_tab[tid] = tid < a.n_inl ? a.inl_ent[tid] : make_uint4(0, 0, 0, 0);
-    stage(0);
-    __syncthreads();
     uint32_t st = __builtin_amdgcn_readfirstlane(w);             // wave-uniform step (SGPR)
-    const bool has_ptype = a.ptype != nullptr;
     uint32_t c_off, c_lp;
-    read_desc(st, c_off, c_lp);
-    Win W = load_win(st, c_off, c_lp & 0xFFFFu);
+    Win W;
+    {
+        uint32_t o[SPT], l[SPT], t[SPT];
+        stage_load(0, o, l, t);
+        // (issued before the window: its wait then leaves the window loads in flight)
+        const uint4 ie = a.inl_ent[min(tid, UDPDK_INLINE_PORTS - 1u)];
+        c_off = o[0];
+        c_lp = l[0] | (has_ptype ? (t[0] & 0x10u) << 12 : 0u);
+        W = load_win(st, c_off, c_lp & 0xFFFFu);
+        __builtin_amdgcn_sched_barrier(0);
+        const bool inl = a.inl && tid <= UDPDK_INLINE_PORTS;
+        if (tid == 0) tail_any = 0u;        // (ordered by the staging barrier)
+        if (a.n_lanes > 1u)
+            for (uint32_t s = tid; s < ((a.n_lanes + hsh) >> hsh); s += CLS_BLOCK) hist[s] = 0;
+        stage_store(0, o, l, t);
+        if (inl) inl_tab[tid] = tid < a.n_inl ? ie : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
     STAMP(0);
 
     // ---- tail pass: UDP checksums of the datagrams that extend past the header window ----
@@ -574,6 +598,21 @@ rx_classify(RxArgs a)
             const bool valid = p < t1;
             const uint32_t off = c_off, len = c_lp & 0xFFFFu;
             const bool good = valid && len <= a.frames_bytes && off <= a.frames_bytes - len;
+            // Early issue (G = 1, a step of the round with a successor in the same round): the
+            // next step's window goes out before this step's arithmetic, so its load overlaps the
+            // whole step instead of the last quarter; the scheduler barriers keep the compiler
+            // from sinking the loads back to their use (it does, to hold occupancy:
+            // tools/probe/chain_probe.hip). A step that needs a tail pass then runs it with that
+            // window in flight.
+            const uint32_t nst = st + CLS_WAVES;
+            uint32_t n_off, n_lp;
+            Win NW;
+            const bool early = UDPDK_CLS_EARLY && G == 1 && jstep + 1u < SPR;
+            if (early) {
+                read_desc(nst, n_off, n_lp);
+                NW = load_win(nst, n_off, n_lp & 0xFFFFu);
+                __builtin_amdgcn_sched_barrier(0);
+            }
 
             // ---- header fields from the window registers (lane = frame) ----
             const uint32_t D[14] = {W.a.x, W.a.y, W.a.z, W.a.w, W.b.x, W.b.y, W.b.z, W.b.w,
@@ -635,12 +674,10 @@ rx_classify(RxArgs a)
             // (the one it shares with the frame's first tail chunk, and the one the previous
             // frame's tail ends in) are then still in L2 when that step's tail reads them, where a
             // window loaded a whole step earlier had left L2 by then (IMIX fetched 1.29x its bytes).
-            const uint32_t nst = st + CLS_WAVES;
-            uint32_t n_off, n_lp;
-            read_desc(nst, n_off, n_lp);      // in range of the buffers for any s (unused past the tile)
+            if (!early)
+                read_desc(nst, n_off, n_lp);  // in range of the buffers for any s (unused past the tile)
             const bool tail_now = __ballot(pend) != 0ull;
-            Win NW;
-            if (!tail_now) NW = load_win(nst, n_off, n_lp & 0xFFFFu);
+            if (!early && !tail_now) NW = load_win(nst, n_off, n_lp & 0xFFFFu);
 
             // ---- what does not need the port entry: UDP state, flags, flag counters ----
             const uint32_t state = ucks == 0u ? UDPDK_UDP_CSUM_NONE
@@ -666,7 +703,7 @@ rx_classify(RxArgs a)
             dstash[(st * 64 + lane) & (RX_ROUND - 1u)] = make_uint2(dport | (is_udp ? 0x10000u : 0u), dip);
             if (tail_now) {
                 tail_step(st);
-                NW = load_win(nst, n_off, n_lp & 0xFFFFu);
+                if (!early) NW = load_win(nst, n_off, n_lp & 0xFFFFu);
             }
             STAMP(6);
             // next round's descriptors into the other buffer at the wave's next-to-last step of a
