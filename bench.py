@@ -408,6 +408,66 @@ def side_config(ctx, cfg: int, steps: int, rotate: int):
     return out
 
 
+class SporadicRx:
+    """Config 2's single-socket stream where every `period`-th call carries one stray frame (a
+    datagram to an unbound port, NO_BIND, at a seeded position): the call's tiles are not all
+    full, so its fused completion repairs the lane in the same launch."""
+
+    def __init__(self, ctx, rotate: int, period: int = 9):
+        w = F.config_batch(2)
+        wd = F.config_batch(2)
+        pos = int(np.random.default_rng(99).integers(0, wd.batch.n))
+        v = wd.batch.frames[:wd.batch.n * 64].reshape(wd.batch.n, 64)
+        v[pos, 36], v[pos, 37] = 0x4E, 0x20                        # dst port 20000
+        self.clean, self.drop = Rx(ctx, w, rotate), Rx(ctx, wd, rotate // 4)
+        self.period, self.pos, self.n = period, pos, w.batch.n
+
+    def step(self, i: int):
+        (self.drop if i % self.period == self.period - 1 else self.clean).step(i)
+
+
+def sporadic_line(ctx, steps: int, rotate: int):
+    """Per-call time of a single-socket stream with a stray frame every 9th call against the
+    clean stream (same pipeline depth, same number of calls, GPU events around the calls), and
+    the stray call alone at depth 1 against a clean call; parity of the stray call's outputs."""
+    sp = SporadicRx(ctx, rotate)
+    depth = auto_depth(sp.clean.w)
+    steps = max(steps // 9, 2) * 9
+
+    def run(step, k, d):
+        ctx.pipeline(d)
+        for i in range(18):
+            step(i)
+        ctx.sync()
+        ev = HipEvents(ctx)
+        ev.record(0)
+        for i in range(k):
+            step(18 + i)
+        ctx.join()
+        ev.record(1)
+        ms = ev.elapsed_ms()
+        ev.close()
+        ctx.pipeline(1)
+        return 1e3 * ms / k
+    clean_us = run(sp.clean.step, steps, depth)
+    spor_us = run(sp.step, steps, depth)
+    clean1 = run(sp.clean.step, 36, 1)
+    drop1 = run(sp.drop.step, 36, 1)
+    dg = gpu_digest(ctx, sp.drop.args[0][5], sp.n, 1)
+    od = oracle_digest(sp.drop.w)
+    out = {"workload": f"{sp.clean.w.name}, one NO_BIND frame every {sp.period}th call (frame {sp.pos})",
+           "pipeline_depth": depth, "calls": steps,
+           "clean_us_per_call": round(clean_us, 3), "sporadic_us_per_call": round(spor_us, 3),
+           "sporadic_over_clean": round(spor_us / clean_us, 4),
+           "depth1_clean_us": round(clean1, 3), "depth1_stray_call_us": round(drop1, 3),
+           "parity": {"gpu": dg, "oracle": od, "match": dg == od}}
+    for r in (sp.clean, sp.drop):
+        for a in r.args:
+            a[4].frames.free(); a[4].offset.free(); a[4].length.free()
+            a[5].meta.free(); a[5].lane_off.free(); a[5].lane_pkt.free()
+    return out
+
+
 def tx_line(ctx, payload_len: int, n: int, steps: int, mtu: int = 0):
     """udpdk_gpu_tx_build over n datagrams of payload_len bytes (one bound socket, ANY:10000 ->
     172.31.100.1:10001, frames back to back): device-resident TX header build + rte_ipv4_cksum +
@@ -1054,6 +1114,10 @@ def main():
             except Exception as e:
                 e2e.append({"config": cfg, "async": True, "error": repr(e)})
         line["end_to_end"] = e2e
+        try:
+            line["sporadic_drop"] = sporadic_line(ctx, max(90, args.steps), args.rotate_mib << 20)
+        except Exception as e:
+            line["sporadic_drop"] = {"error": repr(e)}
         try:
             line["socket_path"] = socket_path_lines()
         except Exception as e:

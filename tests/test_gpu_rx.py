@@ -240,6 +240,68 @@ def test_single_lane_speculation(gpu_ctx, drops):
         _assert_same(want, got, f"drops={drops} call={k}")
 
 
+def _drop(b, rows):
+    v = b.frames[:b.n * 64].reshape(b.n, 64)
+    v[rows, 36] = 0x4E                                          # dst port 20000: not bound
+    v[rows, 37] = 0x20
+
+
+@pytest.mark.parametrize("case", ["first", "middle", "last_but_one", "whole_tile", "many", "every_other",
+                                  "cap_4096_tiles"])
+def test_fused_repair(gpu_ctx, case):
+    """A single-lane call whose tiles are not all full is repaired inside the same launch: the
+    last arrival opens the repair and the shards' last arrivals that saw the call's short-tile flag
+    join it (full tiles written as frame-index runs, short ones from their verdict words). Exact
+    against the oracle for short tiles at the start, middle and end, a whole dropped tile, many
+    short tiles, every other tile short, and the 4096-tile cap of the fused form; each case runs
+    between clean calls on the same context, so a stale flag, work or done word would show."""
+    lists = {abi.raw_port(10001): [(0, 0, 0)]}
+    n = (4096 if case == "cap_4096_tiles" else 1024) * 1024 - 77
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    for k in range(3):
+        b = F.build_frames(np.full(n, 64, np.uint32), np.full(n, 10001, np.uint32), 60 + k)
+        if k == 1:
+            nt = -(-n // 1024)
+            if case == "first":
+                rows = [5]
+            elif case == "middle":
+                rows = [500 * 1024 + 3]
+            elif case == "last_but_one":
+                rows = [(nt - 2) * 1024 + 1023]
+            elif case == "whole_tile":
+                rows = np.arange(300 * 1024, 301 * 1024)
+            elif case == "many":
+                rows = rng.choice(n, 3000, replace=False)
+            elif case == "every_other":
+                rows = np.arange(0, n, 2048)
+            else:
+                rows = rng.choice(n, 50, replace=False)
+            _drop(b, rows)
+        want, got = _rx_both(gpu_ctx, b, lists, 1)
+        _assert_same(want, got, f"{case} call={k}")
+
+
+def test_fused_repair_lane_overflow(gpu_ctx):
+    """The repair of a call whose lane overflows its capacity: entries past the capacity are not
+    written, the ones below it are exact, and the call reports ENOSPC with the true total."""
+    lists = {abi.raw_port(10001): [(0, 0, 0)]}
+    n = 64 * 1024
+    b = F.build_frames(np.full(n, 64, np.uint32), np.full(n, 10001, np.uint32), 9)
+    _drop(b, [100, 20000, 20001])
+    hs = abi.snapshot_from_lists(lists, 1)
+    gpu_ctx.upload_snapshot(hs)
+    bt = O.bindtable_from_lists(lists)
+    wm, wl, wp, wc = O.rx(bt, b.frames, b.frames_bytes, b.offset, b.length, None, 1)
+    db = abi.rx_upload(gpu_ctx, b.frames, b.offset, b.length)
+    db.frames_bytes = b.frames_bytes
+    cap = 40000
+    out = abi.rx_alloc_out(gpu_ctx, n, 1, cap)
+    meta, loff, pkt, cnt, rc = abi.rx_run(gpu_ctx, db, out)
+    assert rc == -errno.ENOSPC
+    assert loff[1] == n - 3 and np.array_equal(meta, wm)
+    assert np.array_equal(pkt, wp[:cap])
+
+
 def test_empty_batch(gpu_ctx):
     lists = {abi.raw_port(10001): [(0, 0, 0)]}
     hs = abi.snapshot_from_lists(lists, 3)

@@ -30,6 +30,7 @@ LINES = {
     "reasmip": "out(bench.reasm_inplace_line(ctx, 1 << 18, 2952, 10))",
     "gather": "for cfg in (2, 3): out(bench.gather_line(ctx, cfg, 50))\n"
               "out(bench.gather_line(ctx, 2, 50, slot=0))",
+    "sporadic": "out(bench.sporadic_line(ctx, 180, 640 << 20))",
     "cfg": "import os\nfor c in os.environ.get('CFGS', '4 5').split(): out(bench.side_config(ctx, int(c), 50, 640 << 20))",
 }
 
@@ -66,7 +67,8 @@ def summary(d: dict) -> str:
         return (f"value {d['value']:.0f}  step {d.get('gpu_us_per_step')}  d1 {d['depth1']['gpu_us_per_step']}  "
                 f"k {d.get('kernel_us')}")
     keys = [k for k in ("us_per_launch", "us_per_call", "gpu_us_per_step", "kernel_us", "frac_hbm",
-                        "frac_hbm_pipeline", "mpkt_s") if k in d]
+                        "frac_hbm_pipeline", "mpkt_s", "clean_us_per_call", "sporadic_us_per_call",
+                        "sporadic_over_clean", "depth1_clean_us", "depth1_stray_call_us") if k in d]
     return f"{d.get('workload', '')[:40]:40s} " + "  ".join(f"{k} {d[k]}" for k in keys)
 
 
@@ -98,7 +100,7 @@ def main():
     for rep in range(a.reps):
         for n in libs:
             env = dict(os.environ, UDPDK_LIB_OVERRIDE=lib_path(n))
-            log = os.path.join(ROOT, "gpurun_out", f"ab_{n}.log")
+            log = os.path.join(ROOT, "gpurun_out", f"ab_{n}_r{rep}.log")
             if a.line:
                 res = run([sys.executable, os.path.abspath(__file__), "--_line", a.line], env, a.timeout, log)
             else:

@@ -138,8 +138,10 @@ struct RxArgs {
 // arrival adds the shard's payload sum to the top word fuse[16 x 8]; the top's last arrival
 // returns true with the launch's payload sum (< 2^48) in *fin. Each word is zeroed again by its
 // last arrival, so the next launch on the same words starts from zeros.
+// *left (optional): how many of the shard's workgroups arrive after this one.
 __device__ __forceinline__ bool fanin_arrive(unsigned long long *fuse, uint32_t tile, uint32_t n_tiles,
-                                             unsigned long long payload, unsigned long long *fin)
+                                             unsigned long long payload, unsigned long long *fin,
+                                             uint32_t *left = nullptr)
 {
     constexpr unsigned long long LOW = (1ull << 48) - 1ull;
     const uint32_t s = tile & (UDPDK_FUSE_SHARDS - 1u);
@@ -147,6 +149,7 @@ __device__ __forceinline__ bool fanin_arrive(unsigned long long *fuse, uint32_t 
     const unsigned long long mine = (1ull << 48) | payload;
     unsigned long long *sw = fuse + 16u * s;
     const unsigned long long now = __hip_atomic_fetch_add(sw, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + mine;
+    if (left) *left = ns - (uint32_t)(now >> 48);
     if ((uint32_t)(now >> 48) != ns) return false;
     __hip_atomic_store(sw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long m2 = (1ull << 48) | (now & LOW);
@@ -157,7 +160,19 @@ __device__ __forceinline__ bool fanin_arrive(unsigned long long *fuse, uint32_t 
     *fin = now2 & LOW;
     return true;
 }
-#define UDPDK_FUSE_MAX_TILES 65535u          // fan-in fields: 16-bit arrival and not-full counts
+#define UDPDK_FUSE_MAX_TILES 4096u           // fused single-lane calls (the repair's LDS tile bases)
+// Words after the fan-in lines (fuse[16 k], one 128-byte line each): the repair of a fused call
+// with a short tile (rx_classify's classify_complete). FLAG = max of the call epochs that had a
+// short tile, DONE = epoch of the latest call whose repair opened, WORK = epoch << 32 | next chunk.
+#define UDPDK_FUSE_FLAG (16u * (UDPDK_FUSE_SHARDS + 1u))
+#define UDPDK_FUSE_DONE (16u * (UDPDK_FUSE_SHARDS + 2u))
+#define UDPDK_FUSE_WORK (16u * (UDPDK_FUSE_SHARDS + 3u))
+#define UDPDK_FUSE_LINES (UDPDK_FUSE_SHARDS + 4u)
+#ifndef UDPDK_FIX_HELPERS
+#define UDPDK_FIX_HELPERS 8u                // repair helpers: a shard's last arrivals that may join
+#endif
+#define UDPDK_FIX_CHUNK 4u                   // tiles per repair work item
+#define UDPDK_FIX_SPIN 200000u               // a helper's bounded wait for the call's last arrival
 #define UDPDK_HINT_TAIL 0
 #define UDPDK_HINT_NONFULL 16                // its own 64-byte line
 #define UDPDK_HINT_DONE 32                   // seq of the latest call whose first tile ran

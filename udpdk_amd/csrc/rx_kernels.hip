@@ -218,83 +218,186 @@ __device__ __forceinline__ uint32_t max_scan_dpp(uint32_t v)
 // (a.fuse[128]) and the top's last arrival completes the call. Every word is reset by its last
 // arrival, so the pipe's next call starts from zeros. When every tile before the last delivered
 // all its frames (the common case of a port-bound stream) the speculative entries are the lane
-// already and the completion writes lane_off and the total only. Otherwise it rewrites the
-// entries after the first tile that was not full from the verdict words (sc1 loads behind an
-// agent acquire; one workgroup, 4096 frames per pass) -- slow, so the host goes back to the
-// two-launch form for its next calls (a.hint).
+// already and the completion writes lane_off and the total only.
+//
+// Repair (a tile before the last not full: a stray frame, a drop): every later tile's entries sit
+// at tile x T + rank instead of their base + rank. A short tile raises the call's FLAG word
+// (before its arrival); every workgroup loads FLAG beside its store drain, so the value costs no
+// round trip. The last UDPDK_FIX_HELPERS arrivals of each shard that saw FLAG wait for the call's
+// last arrival, which opens the repair (WORK = epoch << 32, then DONE = epoch) and joins it. Each
+// participant takes every tile's delivery count (sc1 loads behind an agent acquire), their
+// exclusive prefix in LDS, and then chunks of UDPDK_FIX_CHUNK tiles after the first short tile
+// from WORK: a full tile's entries are its frame indices in order (stores only), a short tile's
+// come from its verdict words. Helpers are optional (a helper that waits past UDPDK_FIX_SPIN
+// leaves; the last arrival works through every chunk itself if it must), so the repair is exact
+// whoever joins; with helpers it costs a few microseconds instead of a one-workgroup rewrite.
+// No workgroup waits unless a tile of its call was short, and at most UDPDK_FIX_HELPERS x 8 wait,
+// far fewer than the workgroups resident at once, so no workgroup waits on one that cannot start.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void classify_complete(const RxArgs &a, uint32_t tile, uint32_t tcount,
-                                                  uint32_t tid, uint32_t lane, uint32_t w)
+__device__ __forceinline__ uint32_t block_scan4(uint32_t v, uint32_t *ws, uint32_t lane, uint32_t w,
+                                                uint32_t *total)
 {
-    __shared__ uint32_t fz[4 + CLS_WAVES];
+    // exclusive scan over the CLS_WAVES x 64 threads (ws: CLS_WAVES words of LDS)
+    const uint32_t incl = scan_dpp(v);
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t pre = incl - v, tot = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < CLS_WAVES; ++i) {
+        pre += i < w ? ws[i] : 0u;
+        tot += ws[i];
+    }
+    __syncthreads();
+    *total = tot;
+    return pre;
+}
+
+__device__ __forceinline__ void classify_complete(const RxArgs &a, uint32_t tile, uint32_t tcount,
+                                                  uint32_t tid, uint32_t lane, uint32_t w, uint8_t *smem)
+{
+    __shared__ uint32_t fz[8 + CLS_WAVES];
+    const uint32_t T = a.tile_frames;
+    const bool nonfull = tile + 1u < a.n_tiles && tcount != T;
+    unsigned long long flag = 0;
+    if (tid == 0) {
+        if (nonfull) atomicMax(&a.fuse[UDPDK_FUSE_FLAG], (unsigned long long)a.spec_epoch);
+        flag = __hip_atomic_load(&a.fuse[UDPDK_FUSE_FLAG], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every wave: its stores written through
     __syncthreads();
     if (tid == 0) {
         // payload: {tiles before the last that were not full << 32 | deliveries}
-        const bool nonfull = tile + 1u < a.n_tiles && tcount != a.tile_frames;
         unsigned long long fin = 0;
-        const bool last = fanin_arrive(a.fuse, tile, a.n_tiles, (nonfull ? 1ull << 32 : 0ull) | tcount, &fin);
+        uint32_t left = 0;
+        const bool last = fanin_arrive(a.fuse, tile, a.n_tiles, (nonfull ? 1ull << 32 : 0ull) | tcount, &fin, &left);
         fz[0] = last ? 1u : 0u;
         fz[1] = (uint32_t)fin;                              // deliveries of the call
         fz[2] = (uint32_t)(fin >> 32) & 0xFFFFu;            // tiles (not the last) not full
+        fz[3] = !last && (uint32_t)flag == a.spec_epoch && left < UDPDK_FIX_HELPERS ? 1u : 0u;
     }
     __syncthreads();
-    if (!fz[0]) return;
-    const uint32_t total = fz[1];
-    if (fz[2] != 0u) {
-        // the other workgroups' tile counts and verdict words: one acquire, then sc1 loads
-        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool last = fz[0] != 0u;
+    if (last) {
+        if (tid == 0) {
+            a.lane_off[0] = 0u;
+            a.lane_off[1] = fz[1];
+            *a.total = fz[1];
+            if (fz[2] != 0u) {                             // open the repair
+                __hip_atomic_store(&a.fuse[UDPDK_FUSE_WORK], (unsigned long long)a.spec_epoch << 32,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&a.fuse[UDPDK_FUSE_DONE], (unsigned long long)a.spec_epoch,
+                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (fz[2] == 0u) return;
+    } else {
+        if (fz[3] == 0u) return;
+        if (tid == 0) {
+            uint32_t ok = 0;
+            for (uint32_t it = 0; it < UDPDK_FIX_SPIN; ++it) {
+                if (__hip_atomic_load(&a.fuse[UDPDK_FUSE_DONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                    (unsigned long long)a.spec_epoch) {
+                    ok = 1u;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            fz[4] = ok;
+        }
         __syncthreads();
-        const uint32_t T = a.tile_frames;
-        const __amdgpu_buffer_rsrc_t hr = make_rsrc(a.hist, a.n_tiles * 4u);
-        uint32_t f = 0xFFFFFFFFu;
-        for (uint32_t t = tid; t + 1u < a.n_tiles; t += CLS_BLOCK)
-            if (__builtin_amdgcn_raw_buffer_load_b32(hr, (int)(4u * t), 0, 16) != T) f = min(f, t);
+        if (fz[4] == 0u) return;
+    }
+    // the other workgroups' tile counts and verdict words: one acquire, then sc1 loads
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint32_t nt = a.n_tiles;
+    uint32_t *base = reinterpret_cast<uint32_t *>(smem + DSC_OFF);   // [nt + 1] tile bases
+    uint32_t *ws = fz + 8;
+    {
+        // thread tid holds tiles [k0, k0 + per): counts, their exclusive prefix, the first
+        // short tile (not the last)
+        const __amdgpu_buffer_rsrc_t hr = make_rsrc(a.hist, nt * 4u);
+        const uint32_t per = (nt + CLS_BLOCK - 1u) / CLS_BLOCK, k0 = tid * per;
+        uint32_t sum = 0, f = 0xFFFFFFFFu;
+        for (uint32_t k = 0; k < per; ++k) {
+            const uint32_t t = k0 + k;
+            const uint32_t c = t < nt ? __builtin_amdgcn_raw_buffer_load_b32(hr, (int)(4u * t), 0, 16) : 0u;
+            if (t < nt) base[t] = c;                        // counts first, prefix below
+            if (t + 1u < nt && c != T) f = min(f, t);
+            sum += c;
+        }
+        uint32_t tot;
+        uint32_t run = block_scan4(sum, ws, lane, w, &tot);
+        for (uint32_t k = 0; k < per; ++k) {
+            const uint32_t t = k0 + k;
+            if (t < nt) {
+                const uint32_t c = base[t];
+                base[t] = run;
+                run += c;
+            }
+        }
+        if (tid == 0) base[nt] = tot;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) f = min(f, (uint32_t)__shfl_xor((int)f, d, 64));
-        if (lane == 0) fz[4 + w] = f;
+        if (lane == 0) ws[w] = f;
         __syncthreads();
+        f = ws[0];
 #pragma unroll
-        for (uint32_t i = 0; i < CLS_WAVES; ++i) f = min(f, fz[4 + i]);
-        // tiles up to f hold their entries already (every tile before f was full)
-        uint32_t run = f * T + __builtin_amdgcn_raw_buffer_load_b32(hr, (int)(4u * f), 0, 16);
-        const __amdgpu_buffer_rsrc_t mr = make_rsrc(a.meta, a.n * 4u);
-        for (uint32_t c0 = (f + 1u) * T; c0 < a.n; c0 += 16u * CLS_BLOCK) {
-            const uint32_t fb = c0 + 16u * tid;
-            uint32_t bits = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(mr, (int)(4u * (fb + 4u * k)), 0, 16);
-#pragma unroll
-                for (uint32_t j = 0; j < 4; ++j)
-                    if ((v[j] & 0xFu) == UDPDK_V_DELIVERED && fb + 4u * k + j < a.n) bits |= 1u << (4u * k + j);
-            }
-            const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
-            const uint32_t incl = scan_dpp(cnt);
-            __syncthreads();                                // fz[4..] of the previous pass read
-            if (lane == 63) fz[4 + w] = incl;
-            __syncthreads();
-            uint32_t pos = run + incl - cnt, pass = 0;
-#pragma unroll
-            for (uint32_t i = 0; i < CLS_WAVES; ++i) {
-                pos += i < w ? fz[4 + i] : 0u;
-                pass += fz[4 + i];
-            }
-            for (uint32_t j = 0; j < 16; ++j)
-                if ((bits >> j) & 1u) {
-                    if (pos < a.spec_cap) a.spec_pkt[pos] = fb + j;
-                    ++pos;
-                }
-            run += pass;
-        }
-        if (tid == 0 && a.hint)
-            __hip_atomic_store(&a.hint[UDPDK_HINT_NONFULL], a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (uint32_t i = 1; i < CLS_WAVES; ++i) f = min(f, ws[i]);
+        __syncthreads();
+        if (tid == 0) fz[6] = f;
+        __syncthreads();
     }
-    if (tid == 0) {
-        a.lane_off[0] = 0u;
-        a.lane_off[1] = total;
-        *a.total = total;
+    const uint32_t first = fz[6];                           // tiles up to it hold their entries
+    const __amdgpu_buffer_rsrc_t sr =
+        make_rsrc(a.spec_pkt, a.spec_cap >= 0x40000000u ? 0xFFFFFFFCu : a.spec_cap * 4u);
+    const __amdgpu_buffer_rsrc_t mr = make_rsrc(a.meta, a.n * 4u);
+    for (;;) {
+        __syncthreads();                                    // fz[5] of the previous chunk read
+        if (tid == 0) {
+            const unsigned long long k = __hip_atomic_fetch_add(&a.fuse[UDPDK_FUSE_WORK], 1ull,
+                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            fz[5] = (uint32_t)(k >> 32) == a.spec_epoch ? (uint32_t)k : 0xFFFFFFFFu;
+        }
+        __syncthreads();
+        const uint32_t k = fz[5];
+        if (first == 0xFFFFFFFFu || k == 0xFFFFFFFFu || k >= nt) break;
+        const uint32_t ta = first + 1u + k * UDPDK_FIX_CHUNK;
+        if (ta >= nt) break;
+        const uint32_t tb = min(nt, ta + UDPDK_FIX_CHUNK);
+        for (uint32_t t = ta; t < tb; ++t) {
+            const uint32_t b = base[t], c = base[t + 1u] - b, f0 = t * T;
+            if (c == T) {
+                // a full tile: its frames in order (stores only)
+                const uint32_t j = 4u * tid, pos = b + j;
+                const __attribute__((ext_vector_type(4))) uint32_t x = {f0 + j, f0 + j + 1u, f0 + j + 2u, f0 + j + 3u};
+                if ((pos & 3u) == 0u) {
+                    __builtin_amdgcn_raw_buffer_store_b128(x, sr, (int)(4u * pos), 0, 0);
+                } else {
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i)
+                        __builtin_amdgcn_raw_buffer_store_b32(f0 + j + i, sr, (int)(4u * (pos + i)), 0, 0);
+                }
+            } else {
+                // a short (or the last) tile: its delivered frames from its verdict words
+                const uint32_t fb = f0 + 4u * tid;
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(mr, (int)(4u * fb), 0, 16);
+                uint32_t bits = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i)
+                    if ((v[i] & 0xFu) == UDPDK_V_DELIVERED && fb + i < a.n && 4u * tid + i < T) bits |= 1u << i;
+                const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
+                uint32_t tot;
+                uint32_t pos = b + block_scan4(cnt, ws, lane, w, &tot);
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i)
+                    if ((bits >> i) & 1u) {
+                        __builtin_amdgcn_raw_buffer_store_b32(fb + i, sr, (int)(4u * pos), 0, 0);
+                        ++pos;
+                    }
+            }
+        }
     }
 }
 
@@ -967,7 +1070,7 @@ rx_classify(RxArgs a)
         if (tile == 0u)
             __hip_atomic_store(&a.hint[UDPDK_HINT_DONE], a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (fuse) classify_complete(a, tile, tcount, tid, lane, w);
+    if (fuse) classify_complete(a, tile, tcount, tid, lane, w, smem);
 #ifdef UDPDK_STAMPS
     STAMP(4);                                              // slot 4: fused completion
     STAMP_END();

@@ -78,7 +78,7 @@ struct Pipe {
     const uint32_t *staged_meta = nullptr;    // and its verdict words
 };
 constexpr int MAX_PIPES = 4;
-constexpr size_t FUSE_BYTES = 128u * (UDPDK_FUSE_SHARDS + 1u);   // one 128-B line per fan-in word
+constexpr size_t FUSE_BYTES = 128u * UDPDK_FUSE_LINES;   // one 128-B line per fan-in / repair word
 constexpr size_t HINT_BYTES = 192u;
 constexpr uint32_t RSS_FUSE_MAX_ENTRIES = 8192u;   // rss_hash's last workgroup scans <= this many
 #ifndef UDPDK_HINT_WINDOW
@@ -688,8 +688,9 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     };
     ra.hint = c->hint;
     ra.seq = seq;
-    const bool fuse = spec && tiles <= UDPDK_FUSE_MAX_TILES &&
-                      (c->force_fuse >= 0 ? c->force_fuse == 1 : !recent(UDPDK_HINT_NONFULL));
+    // fused completion whenever it applies: a call with a short tile repairs its lane inside the
+    // same launch (classify_complete), so no form switching follows a stray frame
+    const bool fuse = spec && tiles <= UDPDK_FUSE_MAX_TILES && c->force_fuse != 0;
     const int tailg = c->force_tailg ? c->force_tailg : (one_lane && !recent(UDPDK_HINT_TAIL)) ? 1 : 2;
     if (c->trace)
         fprintf(stderr, "udpdk_gpu_rx seq %u done %u hint tail %u nonfull %u -> classify<%d>%s\n", seq,
