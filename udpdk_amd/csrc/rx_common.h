@@ -27,6 +27,9 @@ constexpr uint32_t RX_HIST_CAP = UDPDK_RX_HIST_CAP;  // target bound on lanes x 
 #ifndef UDPDK_CLS_EARLY
 #define UDPDK_CLS_EARLY 0                    // rx_classify<1>: next window issued at the step's top
 #endif
+#ifndef UDPDK_CLS_K2
+#define UDPDK_CLS_K2 0                       // rx_classify<1>: two windows ahead (W, W1 + one in flight)
+#endif
 #ifndef UDPDK_CLS_WPE
 #define UDPDK_CLS_WPE 4                      // rx_classify minimum waves per SIMD (VGPR budget)
 #endif
@@ -288,7 +291,9 @@ struct GatherArgs {
     const uint32_t *slot_off;   // [count + 1] packed slots (udpdk_gpu_rx_gather_packed), or null
 };
 
-template <int G> __global__ void rx_classify(RxArgs a);   // G: tail chunk groups in flight (1, 2)
+// G: tail chunk groups in flight (1, 2); MR: tiles of several rounds, whose next round's
+// descriptors are loaded a round ahead (in registers) instead of when they are staged
+template <int G, int MR> __global__ void rx_classify(RxArgs a);
 __global__ void rx_gather(GatherArgs a);
 __global__ void rx_scan_cols(ScanArgs a, uint32_t lb);
 __global__ void rx_scan_reduce(ScanArgs a);

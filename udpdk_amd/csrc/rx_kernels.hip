@@ -419,8 +419,9 @@ struct Win {
 // batches overlapping on several streams want (config 2, --steps 20, same-box A/B with the
 // compaction launch gone: 57.1 -> 63.0 Gpkt/s; config 1 (106 B, one tail chunk per frame) is
 // 8 % slower at G = 1, so the host picks G by whether recent calls had tail passes).
-template <int G>
-__global__ void __launch_bounds__(CLS_BLOCK) __attribute__((amdgpu_waves_per_eu(G == 1 ? 5 : UDPDK_CLS_WPE, 8)))
+template <int G, int MR>
+__global__ void __launch_bounds__(CLS_BLOCK)
+__attribute__((amdgpu_waves_per_eu(MR ? 2 : G == 1 && !UDPDK_CLS_K2 ? 5 : UDPDK_CLS_WPE, 8)))
 rx_classify(RxArgs a)
 {
     static_assert(G == 1 || G == 2, "one or two tail chunk groups in flight");
@@ -430,6 +431,7 @@ rx_classify(RxArgs a)
     constexpr uint32_t RSTEPS = RX_ROUND / 64;              // steps per staging round
     constexpr uint32_t SPR = RSTEPS / CLS_WAVES;            // steps per wave per staging round
     static_assert(SPR >= 2, "round staging needs two steps per wave per round");
+    static_assert(!(G == 1 && UDPDK_CLS_K2) || SPR >= 3, "two windows ahead stage the next round a step earlier");
 #ifdef UDPDK_STAMPS
     unsigned long long st_acc[16] = {0}, st_last = __builtin_amdgcn_s_memtime();
     st_acc[12] = __builtin_amdgcn_s_memrealtime();
@@ -540,6 +542,11 @@ rx_classify(RxArgs a)
     uint32_t st = __builtin_amdgcn_readfirstlane(w);             // wave-uniform step (SGPR)
     uint32_t c_off, c_lp;
     Win W;
+    // K2 (G = 1, UDPDK_CLS_K2): two windows ahead; W1 / c1_* hold the next step's window and
+    // descriptor while the step after it is in flight
+    constexpr bool K2 = G == 1 && UDPDK_CLS_K2;
+    Win W1;
+    uint32_t c1_off = 0, c1_lp = 0;
     {
         uint32_t o[SPT], l[SPT], t[SPT];
         stage_load(0, o, l, t);
@@ -548,6 +555,11 @@ rx_classify(RxArgs a)
         c_off = o[0];
         c_lp = l[0] | (has_ptype ? (t[0] & 0x10u) << 12 : 0u);
         W = load_win(st, c_off, c_lp & 0xFFFFu);
+        if constexpr (K2) {                 // step w + 4: this thread's second staged descriptor
+            c1_off = o[1];
+            c1_lp = l[1] | (has_ptype ? (t[1] & 0x10u) << 12 : 0u);
+            W1 = load_win(st + CLS_WAVES, c1_off, c1_lp & 0xFFFFu);
+        }
         __builtin_amdgcn_sched_barrier(0);
         const bool inl = a.inl && tid <= UDPDK_INLINE_PORTS;
         if (tid == 0) tail_any = 0u;        // (ordered by the staging barrier)
@@ -692,6 +704,7 @@ rx_classify(RxArgs a)
             }
     };
 
+    uint32_t pf_o[SPT], pf_l[SPT], pf_t[SPT];             // MR: the next round's descriptors
     // rounds of RX_ROUND frames: SPR steps per wave (each followed by its tail pass when a frame
     // of the step is pending), then the round's demux pass
     for (uint32_t rnd = 0; rnd < steps / RSTEPS; ++rnd) {
@@ -707,11 +720,24 @@ rx_classify(RxArgs a)
             // from sinking the loads back to their use (it does, to hold occupancy:
             // tools/probe/chain_probe.hip). A step that needs a tail pass then runs it with that
             // window in flight.
+            // MR: the next round's descriptors go out at the round's first step, into registers,
+            // and are stored to LDS at its staging step: the staging no longer waits a round trip
+            // (config 5: a descriptor round trip per round was a fifth of each workgroup's time)
+            if (MR && jstep == 0u && rnd + 1u < steps / RSTEPS) {
+                stage_load(rnd + 1u, pf_o, pf_l, pf_t);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             const uint32_t nst = st + CLS_WAVES;
             uint32_t n_off, n_lp;
             Win NW;
-            const bool early = UDPDK_CLS_EARLY && G == 1 && jstep + 1u < SPR;
-            if (early) {
+            const bool early = K2 || (UDPDK_CLS_EARLY && G == 1 && jstep + 1u < SPR);
+            if (K2) {
+                // the window two steps ahead (its round's descriptors are staged by then: the
+                // next round is staged at the round's second step, below)
+                read_desc(nst + CLS_WAVES, n_off, n_lp);
+                NW = load_win(nst + CLS_WAVES, n_off, n_lp & 0xFFFFu);
+                __builtin_amdgcn_sched_barrier(0);
+            } else if (early) {
                 read_desc(nst, n_off, n_lp);
                 NW = load_win(nst, n_off, n_lp & 0xFFFFu);
                 __builtin_amdgcn_sched_barrier(0);
@@ -814,14 +840,29 @@ rx_classify(RxArgs a)
             // buffer were before the previous round's barrier, and the next round is first read at
             // j = SPR - 1.
             // Uniform across the workgroup (every wave has steps / 4 steps).
-            if ((st / CLS_WAVES) % SPR == SPR - 2u && st / RSTEPS + 1u < steps / RSTEPS) {
-                stage(st / RSTEPS + 1u);
+            // With K2 the next round is staged one step earlier (its first step is read two steps
+            // ahead, at the round's third step); the buffer's last reads were then at the
+            // previous round's second step, before that round's barrier.
+            if ((st / CLS_WAVES) % SPR == SPR - (K2 ? 3u : 2u) && st / RSTEPS + 1u < steps / RSTEPS) {
+                if constexpr (MR != 0)
+                    stage_store(st / RSTEPS + 1u, pf_o, pf_l, pf_t);
+                else
+                    stage(st / RSTEPS + 1u);
                 __syncthreads();
                 STAMP(5);
             }
-            W = NW;
-            c_off = n_off;
-            c_lp = n_lp;
+            if constexpr (K2) {
+                W = W1;
+                W1 = NW;
+                c_off = c1_off;
+                c_lp = c1_lp;
+                c1_off = n_off;
+                c1_lp = n_lp;
+            } else {
+                W = NW;
+                c_off = n_off;
+                c_lp = n_lp;
+            }
             st = nst;
         }
         // ---- demux pass: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
@@ -1077,8 +1118,10 @@ rx_classify(RxArgs a)
     if (a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
 #endif
 }
-template __global__ void rx_classify<1>(RxArgs a);
-template __global__ void rx_classify<2>(RxArgs a);
+template __global__ void rx_classify<1, 0>(RxArgs a);
+template __global__ void rx_classify<2, 0>(RxArgs a);
+template __global__ void rx_classify<1, 1>(RxArgs a);
+template __global__ void rx_classify<2, 1>(RxArgs a);
 
 
 // ------------------------------------------------------------------------------------------

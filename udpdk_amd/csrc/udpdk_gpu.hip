@@ -114,6 +114,7 @@ struct udpdk_gpu_ctx {
     uint32_t rx_seq = 0;
     int force_fuse = -1;           // UDPDK_RX_FUSE=0/1 (tests, A/B): fused completion off / always
     int force_tailg = 0;           // UDPDK_RX_TAILG=1/2 (tests, A/B): rx_classify<G> always
+    int force_mr = -1;             // UDPDK_RX_MR=0/1 (tests, A/B): the round-ahead descriptor form
     bool trace = false;            // UDPDK_RX_TRACE (diagnostic): the form of every call on stderr
     bool no_inline = false;        // UDPDK_RX_NO_INLINE (tests, A/B): always the port-table loads
     bool have_snapshot = false;
@@ -304,6 +305,7 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
     if (const char *e = getenv("UDPDK_RX_FUSE")) c->force_fuse = atoi(e) ? 1 : 0;
     c->trace = getenv("UDPDK_RX_TRACE") != nullptr;
     c->no_inline = getenv("UDPDK_RX_NO_INLINE") != nullptr;
+    if (const char *e = getenv("UDPDK_RX_MR")) c->force_mr = atoi(e) ? 1 : 0;
     if (const char *e = getenv("UDPDK_RX_TAILG")) {
         const int g = atoi(e);
         if (g == 1 || g == 2) c->force_tailg = g;
@@ -352,9 +354,13 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
         // rx_classify needs up to 141 KiB of dynamic LDS (16384 lanes, 8192-frame tiles)
         const int cls_lds = (int)std::min<uint32_t>(classify_lds_bytes(UDPDK_GPU_MAX_LANES, RX_TILE_MAX),
                                                     160u * 1024u - 1024u);   // static LDS besides
-        if (hipFuncSetAttribute((const void *)rx_classify<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void *)rx_classify<2, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 cls_lds) != hipSuccess) break;
-        if (hipFuncSetAttribute((const void *)rx_classify<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void *)rx_classify<1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                cls_lds) != hipSuccess) break;
+        if (hipFuncSetAttribute((const void *)rx_classify<2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                cls_lds) != hipSuccess) break;
+        if (hipFuncSetAttribute((const void *)rx_classify<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 cls_lds) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)scatter1_lds_bytes(UDPDK_GPU_MAX_LANES)) != hipSuccess) break;
@@ -700,7 +706,11 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     ra.total = &P.res->total;
 
     if (ts) for (int k = 0; k < TIMED_KERNELS; ++k) ts->used[k] = false;
-    HIPC(c, launch(st, ts, 0, true, true, tailg == 1 ? rx_classify<1> : rx_classify<2>, dim3(tiles),
+    // tiles of several rounds (many lanes: config 5's 8192-frame tiles) take the form that loads
+    // each next round's descriptors a round ahead
+    const bool mr = c->force_mr >= 0 ? c->force_mr == 1 : T > (uint32_t)RX_ROUND;
+    auto cls = tailg == 1 ? (mr ? rx_classify<1, 1> : rx_classify<1, 0>) : (mr ? rx_classify<2, 1> : rx_classify<2, 0>);
+    HIPC(c, launch(st, ts, 0, true, true, cls, dim3(tiles),
                    dim3(CLS_BLOCK), classify_lds_bytes(S, T, hist16), ra));
     if (fuse) return 0;                        // the last workgroup completed the lane
     if (one_lane) {
