@@ -704,6 +704,86 @@ rx_classify(RxArgs a)
             }
     };
 
+    // ---- demux of one frame: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
+    // i: the frame's index in the tile, m: its verdict word so far (verdict field 0xF: UDP, port
+    // lookup pending), Sv: {raw dst port | is-UDP << 16, raw dst IPv4}, Ev: the port's 16-byte
+    // entry (first binding inline; the binding list is walked only for ports with several).
+    // Returns the final verdict word; counts the frame and adds it to the tile histogram.
+    auto demux_frame = [&](uint32_t i, uint32_t m, uint2 Sv, uint4 Ev) -> uint32_t {
+        const bool valid = t0 + i < t1;
+        const uint4 e = (Sv.x >> 16) ? Ev : make_uint4(0, 0, 0, 0);
+        const uint32_t dip = Sv.y;
+        const bool match0 = e.x != 0u && (dip == e.z || e.z == 0u);     // poller.c:391
+        uint32_t fan = match0 ? 1u : 0u;
+        uint32_t first = match0 ? (e.w & 0x7FFFFFFFu) : 0u;
+        const bool walk = e.x > 1u && !(match0 && !(e.w >> 31));        // poller.c:396-403
+        if (__ballot(walk)) {
+            if (walk) {
+                for (uint32_t b = 1; b < e.x; ++b) {
+                    const uint2 bd = a.binds[e.y + b];
+                    if (dip == bd.x || bd.x == 0u) {
+                        const uint32_t sock = bd.y & 0x7FFFFFFFu;
+                        if (fan > 0 && a.n_lanes > 1u)
+                            hist_add(sock & a.lane_mask, 1u);           // clones (rare)
+                        if (fan == 0) first = sock;
+                        ++fan;
+                        if (!(bd.y >> 31)) break;
+                    }
+                }
+            }
+        }
+        const uint32_t pre = m & 0xFu;
+        const uint32_t verdict = pre != 0xFu ? pre
+                               : e.x == 0u ? UDPDK_V_NO_BIND
+                               : fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
+        const uint32_t fin = (m & ~0xFu) | verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
+        // per-lane packed counters (8-bit fields; a lane sees <= 64 frames per tile)
+        const uint32_t vinc = valid ? 1u << (8u * (verdict & 3u)) : 0u;
+        acc_v0 += verdict < 4u ? vinc : 0u;
+        acc_v1 += verdict < 4u ? 0u : vinc;
+        acc_fan += fan;
+        const bool delivered = valid && fan > 0u;
+        // first delivery of every frame into the tile histogram; small key spaces are
+        // aggregated with a wave multi-split first (all 64 lanes may share one lane)
+        // (one lane: the tile's count is its delivery counter, written at the tile end)
+        const uint32_t key = first & a.lane_mask;
+#ifdef UDPDK_DIAG_NO_HIST
+        if (true) {                           // timing only: histogram skipped
+#else
+        if (a.n_lanes == 1u) {
+#endif
+        } else if (a.key_bits <= 4u) {
+            unsigned long long peers = __ballot(delivered);
+            for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
+                const bool kb = (key >> bit) & 1u;
+                const unsigned long long bal = __ballot(kb);
+                peers &= kb ? bal : ~bal;
+            }
+            if (delivered && lane == (uint32_t)__ffsll((long long)peers) - 1u)
+                hist_add(key, (uint32_t)__popcll(peers));
+        } else if (delivered) {
+            hist_add(key, 1u);
+        }
+        return fin;
+    };
+    // the argument-borne bind table (few bound ports): the port's entry from LDS (slot n_inl is
+    // zero: an unbound port); one bound port, the pktgen case, is one compare
+    auto inl_entry = [&](uint32_t pt) -> uint4 {
+        uint32_t k = a.n_inl;
+        if (a.n_inl == 1u) {
+            k = pt == a.inl_port[0] ? 0u : 1u;
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < UDPDK_INLINE_PORTS; ++q)
+                k = q < a.n_inl && pt == a.inl_port[q] ? q : k;
+        }
+        return inl_tab[k];
+    };
+    // One-round tiles with the argument-borne table demux each frame in its step (an LDS lookup,
+    // no global load to batch): the tile's end no longer waits for a demux pass over the round.
+    // Several rounds keep the round's pass (their verdict words are stored by it, after the
+    // round's tail passes).
+    const bool step_demux = a.inl && nbuf == 1u;
     uint32_t pf_o[SPT], pf_l[SPT], pf_t[SPT];             // MR: the next round's descriptors
     // rounds of RX_ROUND frames: SPR steps per wave (each followed by its tail pass when a frame
     // of the step is pending), then the round's demux pass
@@ -827,9 +907,19 @@ rx_classify(RxArgs a)
             acc_f1 += (is_udp && state == UDPDK_UDP_CSUM_NONE ? 1u : 0u) | (is_udp && len_bad ? 0x100u : 0u);
             if (good) lane_bytes += len;
 
-            // the port-table lookup waits for the round's demux pass: verdict field 0xF until then
-            mstage[(st * 64 + lane) & (RX_ROUND - 1u)] = (pre == 0xFFu ? 0xFu : pre) | l3f | udpf;
-            dstash[(st * 64 + lane) & (RX_ROUND - 1u)] = make_uint2(dport | (is_udp ? 0x10000u : 0u), dip);
+            // the port-table lookup: now (step_demux), else in the round's demux pass (verdict
+            // field 0xF until then)
+            {
+                const uint32_t w0 = (pre == 0xFFu ? 0xFu : pre) | l3f | udpf;
+                const uint2 sv = make_uint2(dport | (is_udp ? 0x10000u : 0u), dip);
+                const uint32_t si = (st * 64 + lane) & (RX_ROUND - 1u);
+                if (step_demux) {
+                    mstage[si] = demux_frame(st * 64 + lane, w0, sv, inl_entry(dport));
+                } else {
+                    mstage[si] = w0;
+                    dstash[si] = sv;
+                }
+            }
             if (tail_now) {
                 tail_step(st);
                 if (!early) NW = load_win(nst, n_off, n_lp & 0xFFFFu);
@@ -865,28 +955,17 @@ rx_classify(RxArgs a)
             }
             st = nst;
         }
-        // ---- demux pass: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
-        // The round's port-table lookups of this wave, all SPR steps' 16-byte entries in flight at
-        // once (one round trip per round instead of one exposed per step). The entry carries the
-        // port's first binding; the binding list is walked only for ports with several.
-        {
+        // ---- demux pass (not step_demux): the round's port-table lookups of this wave, all SPR
+        // steps' 16-byte entries in flight at once (one round trip per round instead of one
+        // exposed per step) ----
+        if (!step_demux) {
             uint4 E[SPR];
             uint2 S[SPR];
 #pragma unroll
             for (uint32_t j = 0; j < SPR; ++j) S[j] = dstash[((st - RSTEPS + CLS_WAVES * j) * 64 + lane) & (RX_ROUND - 1u)];
             if (a.inl) {
-                // few bound ports: their entries came with the arguments and sit in LDS (slot
-                // n_inl is zero: an unbound port), so the lookup is an LDS read, not a dependent
-                // global load
 #pragma unroll
-                for (uint32_t j = 0; j < SPR; ++j) {
-                    const uint32_t pt = S[j].x & 0xFFFFu;
-                    uint32_t k = a.n_inl;
-#pragma unroll
-                    for (uint32_t q = 0; q < UDPDK_INLINE_PORTS; ++q)
-                        k = q < a.n_inl && pt == a.inl_port[q] ? q : k;
-                    E[j] = inl_tab[k];
-                }
+                for (uint32_t j = 0; j < SPR; ++j) E[j] = inl_entry(S[j].x & 0xFFFFu);
             } else {
 #pragma unroll
                 for (uint32_t j = 0; j < SPR; ++j) E[j] = a.port_tab[S[j].x & 0xFFFFu];
@@ -894,65 +973,11 @@ rx_classify(RxArgs a)
 #pragma unroll
             for (uint32_t j = 0; j < SPR; ++j) {
                 const uint32_t i = (st - RSTEPS + CLS_WAVES * j) * 64 + lane;
-                const uint32_t m = mstage[i & (RX_ROUND - 1u)];
-                const bool valid = t0 + i < t1;
-                const uint4 e = (S[j].x >> 16) ? E[j] : make_uint4(0, 0, 0, 0);
-                const uint32_t dip = S[j].y;
-                const bool match0 = e.x != 0u && (dip == e.z || e.z == 0u);     // poller.c:391
-                uint32_t fan = match0 ? 1u : 0u;
-                uint32_t first = match0 ? (e.w & 0x7FFFFFFFu) : 0u;
-                const bool walk = e.x > 1u && !(match0 && !(e.w >> 31));        // poller.c:396-403
-                if (__ballot(walk)) {
-                    if (walk) {
-                        for (uint32_t b = 1; b < e.x; ++b) {
-                            const uint2 bd = a.binds[e.y + b];
-                            if (dip == bd.x || bd.x == 0u) {
-                                const uint32_t sock = bd.y & 0x7FFFFFFFu;
-                                if (fan > 0 && a.n_lanes > 1u)
-                                    hist_add(sock & a.lane_mask, 1u);           // clones (rare)
-                                if (fan == 0) first = sock;
-                                ++fan;
-                                if (!(bd.y >> 31)) break;
-                            }
-                        }
-                    }
-                }
-                const uint32_t pre = m & 0xFu;
-                const uint32_t verdict = pre != 0xFu ? pre
-                                       : e.x == 0u ? UDPDK_V_NO_BIND
-                                       : fan ? UDPDK_V_DELIVERED : UDPDK_V_NO_MATCH;
-                const uint32_t fin = (m & ~0xFu) | verdict | (min(fan, 127u) << 9) | ((first & 0xFFFFu) << 16);
+                const uint32_t fin = demux_frame(i, mstage[i & (RX_ROUND - 1u)], S[j], E[j]);
                 mstage[i & (RX_ROUND - 1u)] = fin;
                 // a tile of several rounds stores each round's verdict words here (its LDS holds
                 // one round, so three workgroups fit a CU at 4096 lanes instead of two)
-                if (nbuf > 1u && valid) a.meta[t0 + i] = fin;
-                // per-lane packed counters (8-bit fields; a lane sees <= 64 frames per tile)
-                const uint32_t vinc = valid ? 1u << (8u * (verdict & 3u)) : 0u;
-                acc_v0 += verdict < 4u ? vinc : 0u;
-                acc_v1 += verdict < 4u ? 0u : vinc;
-                acc_fan += fan;
-                const bool delivered = valid && fan > 0u;
-                // first delivery of every frame into the tile histogram; small key spaces are
-                // aggregated with a wave multi-split first (all 64 lanes may share one lane)
-                // (one lane: the tile's count is its delivery counter, written at the tile end)
-                const uint32_t key = first & a.lane_mask;
-#ifdef UDPDK_DIAG_NO_HIST
-                if (true) {                           // timing only: histogram skipped
-#else
-                if (a.n_lanes == 1u) {
-#endif
-                } else if (a.key_bits <= 4u) {
-                    unsigned long long peers = __ballot(delivered);
-                    for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
-                        const bool kb = (key >> bit) & 1u;
-                        const unsigned long long bal = __ballot(kb);
-                        peers &= kb ? bal : ~bal;
-                    }
-                    if (delivered && lane == (uint32_t)__ffsll((long long)peers) - 1u)
-                        hist_add(key, (uint32_t)__popcll(peers));
-                } else if (delivered) {
-                    hist_add(key, 1u);
-                }
+                if (nbuf > 1u && t0 + i < t1) a.meta[t0 + i] = fin;
             }
         }
         STAMP(3);
