@@ -122,7 +122,7 @@ __device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
     do {                                                                         \
         if (w == 0) {                                                            \
             const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
-            st_acc[k] += t_ - st_last;                                           \
+            if (lane == 0) st_acc[k] += t_ - st_last;                            \
             st_last = t_;                                                        \
         }                                                                        \
     } while (0)
@@ -133,6 +133,7 @@ __device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t r, uint32_t off)
 #ifdef UDPDK_STAMPS
 #define STAMP_END()                                                                   \
     do {                                                                              \
+        if (tid != 0) break;                                                          \
         st_acc[13] = __builtin_amdgcn_s_memrealtime();                                \
         st_acc[14] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |  \
                      ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32); \
@@ -433,8 +434,12 @@ rx_classify(RxArgs a)
     static_assert(SPR >= 2, "round staging needs two steps per wave per round");
     static_assert(!(G == 1 && UDPDK_CLS_K2) || SPR >= 3, "two windows ahead stage the next round a step earlier");
 #ifdef UDPDK_STAMPS
-    unsigned long long st_acc[16] = {0}, st_last = __builtin_amdgcn_s_memtime();
-    st_acc[12] = __builtin_amdgcn_s_memrealtime();
+    // (in LDS: a register array indexed by lane at the end went to scratch, and the scratch
+    // allocation held workgroups back from starting)
+    __shared__ unsigned long long st_acc[16];
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+    if (tid < 16) st_acc[tid] = 0;
+    if (tid == 0) st_acc[12] = __builtin_amdgcn_s_memrealtime();
 #endif
 
     uint32_t *cntw = reinterpret_cast<uint32_t *>(smem + CNT_OFF);    // [wave][counter]
@@ -983,35 +988,9 @@ rx_classify(RxArgs a)
         STAMP(3);
     }
 
-    // ---- tile counters: one row per wave (lanes 0-15), summed by the readers ----
-    uint32_t sc[UDPDK_N_COUNTERS];
-    {
-        auto wsum = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)scan_dpp(v), 63); };
-        const uint32_t packed[4] = {acc_v0, acc_v1, acc_f0, acc_f1};
-        const int field[4][4] = {{0, 1, 2, 3}, {4, 5, 6, 7},
-                                 {UDPDK_C_IP_BAD, UDPDK_C_IHL_NE5, UDPDK_C_UDP_OK, UDPDK_C_UDP_BAD},
-                                 {UDPDK_C_UDP_NONE, UDPDK_C_LEN_BAD, -1, -1}};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t ev = wsum(packed[k] & 0x00FF00FFu);        // 16-bit sums: no carry
-            const uint32_t od = wsum((packed[k] >> 8) & 0x00FF00FFu);
-            if (field[k][0] >= 0) sc[field[k][0]] = ev & 0xFFFFu;
-            if (field[k][1] >= 0) sc[field[k][1]] = od & 0xFFFFu;
-            if (field[k][2] >= 0) sc[field[k][2]] = ev >> 16;
-            if (field[k][3] >= 0) sc[field[k][3]] = od >> 16;
-        }
-        sc[UDPDK_C_DELIVERIES] = wsum(acc_fan);
-        sc[UDPDK_C_BYTES] = wsum(lane_bytes);
-    }
-    {
-        uint32_t row = 0;
-#pragma unroll
-        for (int c = 0; c < UDPDK_N_COUNTERS; ++c) row = lane == (uint32_t)c ? sc[c] : row;
-        if (lane < UDPDK_N_COUNTERS) cntw[w * 16 + lane] = row;
-        if (tailed && lane == 0) tail_any = 1u;
-    }
+    // The tile's stores go out first (its verdict words are all in LDS after this barrier), the
+    // counter reduction after them: the fused completion's drain then finds them written.
     __syncthreads();
-    STAMP(7);
     auto tile_counter = [&](uint32_t c) -> uint32_t {
         uint32_t v = 0;
 #pragma unroll
@@ -1111,6 +1090,35 @@ rx_classify(RxArgs a)
             for (uint32_t i = tid; i < nv; i += CLS_BLOCK) dst[i] = mstage[i];
         }
     }
+    // ---- tile counters: one row per wave (lanes 0-15), summed by the readers ----
+    uint32_t sc[UDPDK_N_COUNTERS];
+    {
+        auto wsum = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)scan_dpp(v), 63); };
+        const uint32_t packed[4] = {acc_v0, acc_v1, acc_f0, acc_f1};
+        const int field[4][4] = {{0, 1, 2, 3}, {4, 5, 6, 7},
+                                 {UDPDK_C_IP_BAD, UDPDK_C_IHL_NE5, UDPDK_C_UDP_OK, UDPDK_C_UDP_BAD},
+                                 {UDPDK_C_UDP_NONE, UDPDK_C_LEN_BAD, -1, -1}};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t ev = wsum(packed[k] & 0x00FF00FFu);        // 16-bit sums: no carry
+            const uint32_t od = wsum((packed[k] >> 8) & 0x00FF00FFu);
+            if (field[k][0] >= 0) sc[field[k][0]] = ev & 0xFFFFu;
+            if (field[k][1] >= 0) sc[field[k][1]] = od & 0xFFFFu;
+            if (field[k][2] >= 0) sc[field[k][2]] = ev >> 16;
+            if (field[k][3] >= 0) sc[field[k][3]] = od >> 16;
+        }
+        sc[UDPDK_C_DELIVERIES] = wsum(acc_fan);
+        sc[UDPDK_C_BYTES] = wsum(lane_bytes);
+    }
+    {
+        uint32_t row = 0;
+#pragma unroll
+        for (int c = 0; c < UDPDK_N_COUNTERS; ++c) row = lane == (uint32_t)c ? sc[c] : row;
+        if (lane < UDPDK_N_COUNTERS) cntw[w * 16 + lane] = row;
+        if (tailed && lane == 0) tail_any = 1u;
+    }
+    __syncthreads();
+    STAMP(7);
     if (a.n_lanes == 1u) {
         if (tid == 0) {
             if (fuse)
@@ -1129,17 +1137,21 @@ rx_classify(RxArgs a)
     }
     if (tid < UDPDK_N_COUNTERS) a.tile_cnt[(size_t)tile * UDPDK_N_COUNTERS + tid] = tile_counter(tid);
     // the host's kernel choice for its next calls: this call needed tail passes. Sampled (every
-    // 64th tile, one lane): a store to host memory per wave cost IMIX classify 91 -> 544 us.
-    if (a.hint && (tile & 63u) == 0u && tid == 0) {
-        if (tail_any)
+    // 64th tile, one lane): a store to host memory per wave cost IMIX classify 91 -> 544 us. After
+    // the fused completion: its drain would otherwise wait for these stores to cross PCIe.
+    const bool hint = a.hint && (tile & 63u) == 0u && tid == 0;
+    const bool tail_seen = tail_any != 0u;
+    if (fuse) classify_complete(a, tile, tcount, tid, lane, w, smem);
+    if (hint) {
+        if (tail_seen)
             __hip_atomic_store(&a.hint[UDPDK_HINT_TAIL], a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (tile == 0u)
             __hip_atomic_store(&a.hint[UDPDK_HINT_DONE], a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (fuse) classify_complete(a, tile, tcount, tid, lane, w, smem);
 #ifdef UDPDK_STAMPS
     STAMP(4);                                              // slot 4: fused completion
     STAMP_END();
+    __syncthreads();
     if (a.dbg && w == 0 && lane < 16) a.dbg[blockIdx.x * 16 + lane] = st_acc[lane];
 #endif
 }
