@@ -264,6 +264,26 @@ int udpdk_gpu_rx_host_async(udpdk_gpu_ctx *ctx,
 /* Complete every outstanding udpdk_gpu_rx_host_async call (oldest first). */
 int udpdk_gpu_rx_host_wait(udpdk_gpu_ctx *ctx);
 
+/* Poller internals, for udpdk_poll_rx's pipelined form (a large host batch cut into chunks at
+ * burst boundaries, each chunk's RX, gather and payload copy on its own pipe): the same host RX
+ * as udpdk_gpu_rx_host_async on an explicit pipe (1 .. 3), and the device view, gather and
+ * copies of that chunk on that pipe's stream with no joins across pipes, so one chunk's payload
+ * D2H overlaps the next chunk's frame H2D. udpdk_gpu_pipe_wait completes the pipe's stream and
+ * the stats of its RX. offset_base: subtracted from every offset_host entry (a chunk of a larger
+ * buffer whose frames_host points offset_base bytes into it). Not needed by an application;
+ * reference: udpdk_poller.c:516-545 (the burst loop these chunks stand for). */
+int udpdk_gpu_pipe_rx_host(udpdk_gpu_ctx *ctx, int pipe,
+                           const uint8_t *frames_host, uint64_t frames_bytes,
+                           const uint32_t *offset_host, uint32_t offset_base,
+                           const uint16_t *length_host,
+                           const uint32_t *ptype_host, uint32_t n,
+                           uint32_t *meta_host, uint32_t *lane_off_host,
+                           uint32_t *lane_pkt_host, uint32_t lane_cap,
+                           udpdk_rx_stats_t *stats);
+int udpdk_gpu_pipe_wait(udpdk_gpu_ctx *ctx, int pipe);
+int udpdk_gpu_pipe_batch(udpdk_gpu_ctx *ctx, int pipe, udpdk_rx_batch_t *batch, const uint32_t **meta_dev);
+int udpdk_gpu_pipe_copy(udpdk_gpu_ctx *ctx, int pipe, void *dst, const void *src, size_t bytes);
+
 /* ---------------------------------------------------------------------------------------------
  * RX payload delivery: the batch form of udpdk_recvfrom (udpdk_syscall.c:401-488) over the lane
  * entries [first, first + count) of an RX output (e.g. one socket's lane, lane_off[s] ..
@@ -293,6 +313,10 @@ int udpdk_gpu_rx_gather(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch,
 int udpdk_gpu_rx_gather_packed(udpdk_gpu_ctx *ctx, const udpdk_rx_batch_t *batch,
                                const uint32_t *lane_pkt_dev, uint32_t first, uint32_t count,
                                const uint32_t *slot_off_dev, const udpdk_rx_gather_t *out);
+/* The packed gather on pipe `pipe`'s stream (poller internals, above). */
+int udpdk_gpu_pipe_gather_packed(udpdk_gpu_ctx *ctx, int pipe, const udpdk_rx_batch_t *batch,
+                                 const uint32_t *lane_pkt_dev, uint32_t first, uint32_t count,
+                                 const uint32_t *slot_off_dev, const udpdk_rx_gather_t *out);
 
 /* ---------------------------------------------------------------------------------------------
  * RX reassembly of IPv4 fragments (udpdk_poller.c:338-361: FRAG frames go through

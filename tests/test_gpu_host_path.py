@@ -107,3 +107,65 @@ def test_poll_rx_inplace_reassembly_keeps_aliased_frames(tmp_path, host_api):
                     assert addr == ("10.9.8.7", 4000)
     finally:
         L.udpdk_cleanup()
+
+
+def _poll_and_drain(tmp_path, host_api, frames, extra):
+    """udpdk_init (+ the [gpu] lines `extra`), one udpdk_poll_rx over the packed frames (after a
+    pre-fill of socket 1's ring), then every socket drained: ([(len, data, addr)] per socket,
+    the poll's counters)."""
+    ini = tmp_path / "udpdk.ini"
+    ini.write_text("[port0]\nmac_addr = 68:05:ca:95:f8:ec\nip_addr = 172.31.100.1\n"
+                   "[port0_dst]\nmac_addr = 68:05:ca:95:fa:64\n"
+                   "[gpu]\ndevice = 0\nmax_frames = 131072\nmax_lanes = 16\n"
+                   "frag_buckets = 1024\nfrag_bucket_entries = 16\nfrag_max_dgram = 16384\n" + extra)
+    L = abi.lib()
+    argv = (C.c_char_p * 4)(b"prog", b"-c", str(ini).encode(), None)
+    assert L.udpdk_init(3, argv) == 0
+    try:
+        socks = [host_api.socket() for _ in range(4)]
+        for k, s in enumerate(socks):
+            assert host_api.bind(s, "0.0.0.0", 10000 + k) == 0
+        src, dst = raw_ip("10.9.8.7"), raw_ip("172.31.100.1")
+        pre = [ip_frame(src, dst, k, 0, udp_datagram(_port(4000), _port(10001), b"P" * 30), False)
+               for k in range(900)]
+        stats = []
+        for fr in (pre, frames):
+            buf, off, ln = batch(fr)
+            st = abi.RxStats()
+            assert L.udpdk_poll_rx(buf.ctypes.data, len(buf) - 64, off.ctypes.data, ln.ctypes.data,
+                                   None, len(off), C.byref(st)) == 0
+            stats.append((list(st.counters), st.deliveries))
+        L.udpdk_interrupt(0)                    # recvfrom on an empty ring: -1 instead of waiting
+        got = []
+        for s in socks:
+            q = []
+            while True:
+                n, data, addr = host_api.recvfrom(s, 70000)
+                if n < 0:
+                    break
+                q.append((n, data, addr))
+            got.append(q)
+        return got, stats
+    finally:
+        L.udpdk_cleanup()
+
+
+def test_poll_rx_chunked_equals_one_piece(tmp_path, host_api):
+    """The pipelined poll ([gpu] poll_chunk_mb: a large batch cut into chunks at burst boundaries,
+    chunk k + 1's RX overlapping chunk k - 1's payload copy) gives every ring exactly what the
+    one-piece poll gives it: the same datagrams in the same order, reassembled datagrams whose
+    fragments straddle chunk cuts included, and the same bursts dropped where a ring fills (every
+    socket gets more than its 2047 entries). poll_chunk_mb = 1 cuts this ~9 MB batch into 8+
+    chunks; the default (128) polls it in one piece."""
+    from reasm_util import scenario
+    frames = [f for fs, _ in scenario(11, n_batches=10, flows_per_batch=300, normal_per_batch=1800)
+              for f in fs]
+    one, st_one = _poll_and_drain(tmp_path, host_api, frames, "")
+    chk, st_chk = _poll_and_drain(tmp_path, host_api, frames, "poll_chunk_mb = 1\n")
+    assert st_chk == st_one
+    assert [len(q) for q in chk] == [len(q) for q in one]
+    assert sum(len(q) for q in one) > 4000 and all(len(q) >= 1000 for q in one)
+    for k, (a, b) in enumerate(zip(one, chk)):
+        assert a == b, k
+    # the rings did fill: fewer datagrams than deliveries
+    assert sum(len(q) for q in one) < st_one[1][1] + 900

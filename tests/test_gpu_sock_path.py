@@ -176,13 +176,13 @@ def _admitted(idx, room):
     return acc
 
 
-@pytest.mark.parametrize("api", [1, 3, 8, 32], indirect=True)
+@pytest.mark.parametrize("api", [1, 3, 8, 32, "poll_threads = 3\npoll_chunk_mb = 1\n"], indirect=True)
 def test_rx_many_sockets_over_poll_threads(api):
     """40 sockets, Zipf-skewed destination ports, some rings partly full before the poll: the
     admission and ring publication split the sockets over 1, 3, 8 or 32 threads (sockets
     straddle the parts' boundaries; at 32 most parts hold one socket or none, the Zipf head
     filling several parts' share alone) and every socket still gets exactly its admitted
-    bursts, in order."""
+    bursts, in order. (poll_chunk_mb = 1: the pipelined poll, the batch cut into chunks.)"""
     ns = 40
     socks = [api.socket() for _ in range(ns)]
     for k, s in enumerate(socks):

@@ -165,6 +165,14 @@ _PROTOS = {
                                           C.c_uint32, C.POINTER(RxStats)]),
     "udpdk_gpu_rx_host_wait": (C.c_int, [_P]),
     "udpdk_gpu_rx_host_batch": (C.c_int, [_P, C.POINTER(RxBatch), C.POINTER(_P)]),
+    # poller internals (udpdk_poll_rx's pipelined form)
+    "udpdk_gpu_pipe_rx_host": (C.c_int, [_P, C.c_int, _P, C.c_uint64, _P, C.c_uint32, _P, _P, C.c_uint32,
+                                         _P, _P, _P, C.c_uint32, C.POINTER(RxStats)]),
+    "udpdk_gpu_pipe_wait": (C.c_int, [_P, C.c_int]),
+    "udpdk_gpu_pipe_batch": (C.c_int, [_P, C.c_int, C.POINTER(RxBatch), C.POINTER(_P)]),
+    "udpdk_gpu_pipe_copy": (C.c_int, [_P, C.c_int, _P, _P, C.c_size_t]),
+    "udpdk_gpu_pipe_gather_packed": (C.c_int, [_P, C.c_int, C.POINTER(RxBatch), _P, C.c_uint32, C.c_uint32,
+                                               _P, C.POINTER(RxGather)]),
     "udpdk_gpu_rx_gather": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint32, C.c_uint32,
                                       C.POINTER(RxGather)]),
     "udpdk_gpu_rx_gather_packed": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint32, C.c_uint32, _P,

@@ -166,6 +166,11 @@ struct h_state {
     uint32_t *acc_sock;                          /* per accepted entry: socket | from-frag<<31 */
     uint64_t  acc_d_cap, acc_f_cap, acc_do_cap, acc_fo_cap, acc_sock_cap;
     struct h_gbuf gb;                            /* device: gather list + outputs (context 0)  */
+    /* udpdk_poll_rx's pipelined form (h_poll_chunked): pinned verdict words, per-chunk lanes and
+     * the gather lists of the chunk in flight; [gpu] poll_chunk_mb = chunk size (0: one piece) */
+    uint32_t *pc_meta, *pc_loff, *pc_lpkt, *pc_acc;
+    uint64_t  pc_meta_cap, pc_loff_cap, pc_lpkt_cap, pc_acc_cap;
+    uint32_t  poll_chunk_mb;
     /* multi-device RX ([gpu] devices): n_shards > 1 splits every poll into contiguous shards over
      * the shard contexts; the context above (g_udpdk.gpu) keeps TX and the reassembly table */
     uint32_t  n_shards;
@@ -223,6 +228,9 @@ void h_btable_reset(void);
 int  h_btable_add(int sockfd, uint32_t ip, uint32_t port, int opts);
 void h_btable_del(int sockfd, uint32_t port);
 int  h_btable_free_port(void);
+
+/* tx_drain.c: grow-only pinned host buffer (g_udpdk.gpu's allocator) */
+int  h_grow_pinned(void **p, uint64_t *cap, uint64_t need);
 
 /* sock_api.c */
 void h_sockets_reset(void);

@@ -123,6 +123,14 @@ void h_rx_buffers_free(void)
         *dcap[k] = 0;
     }
     h_gbuf_free(g_udpdk.gpu, &g_udpdk.gb);
+    void **pin[] = {(void **)&g_udpdk.pc_meta, (void **)&g_udpdk.pc_loff, (void **)&g_udpdk.pc_lpkt,
+                    (void **)&g_udpdk.pc_acc};
+    uint64_t *pcap[] = {&g_udpdk.pc_meta_cap, &g_udpdk.pc_loff_cap, &g_udpdk.pc_lpkt_cap, &g_udpdk.pc_acc_cap};
+    for (unsigned k = 0; k < sizeof(pin) / sizeof(pin[0]); k++) {
+        if (*pin[k] && g_udpdk.gpu) udpdk_gpu_host_free(g_udpdk.gpu, *pin[k]);
+        *pin[k] = NULL;
+        *pcap[k] = 0;
+    }
 }
 
 /* The shard contexts and their buffers (udpdk_cleanup). */
@@ -944,6 +952,231 @@ static int h_shards_gather(uint32_t nad)
     return 0;
 }
 
+/* ---- pipelined form of an unsharded poll over a large host batch ----
+ * The poller takes its bursts one after another (udpdk_poller.c:516-545); here a batch of at
+ * least two [gpu] poll_chunk_mb chunks is cut into K chunks at burst boundaries and each chunk
+ * runs the one-piece steps (RX, FRAG pass, admission, gather, publication) in order, on pipe
+ * 1 + k % 3 of the context: chunk k + 1's RX (frames H2D, classify, verdicts and lanes D2H) is
+ * enqueued before chunk k's admission and runs while chunk k - 1's payload slab comes back,
+ * so the two PCIe directions overlap instead of following each other (58.8 ms for 1 M x 1500 B
+ * in one piece: 30 ms of frames in, 29 ms of payloads out). A chunk is admitted only after the
+ * chunk before it is published, so every burst's decision reads the room its ring has after
+ * the bursts before it, as in the one-piece poll and the reference's burst loop. Chunks need
+ * the batch's descriptors in range, ascending and disjoint (the network order a NIC ring gives);
+ * others take the one-piece path. */
+#define H_CHUNKS_MAX 16u
+
+struct h_chunk {
+    uint32_t f0, n;              /* frames [f0, f0 + n) of the poll                              */
+    uint64_t lo, bytes;          /* the frame bytes they span (lo 16-byte aligned)               */
+    udpdk_rx_stats_t st;
+};
+
+/* descriptors in range, ascending and disjoint (each frame ends at or before the next starts) */
+static int h_desc_sorted(const uint32_t *offset, const uint16_t *length, uint32_t n, uint64_t frames_bytes)
+{
+    uint64_t end = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t o = offset[i], l = length[i];
+        if (l > frames_bytes || o > frames_bytes - l || o < end) return 0;
+        end = o + l;
+    }
+    return 1;
+}
+
+static inline int h_pipe_of(uint32_t k) { return 1 + (int)(k % 3u); }
+
+/* The direct and reassembled payload gathers of one chunk on its pipe's stream: gather lists
+ * H2D from pinned memory, the packed gather, the slabs' D2H. Both gathers share the device
+ * buffers, in stream order. *ad / *af: the slabs (NULL when that count is 0). */
+static int h_gather_chunk(udpdk_gpu_ctx *g, int pipe, const udpdk_rx_batch_t *b, uint32_t nad,
+                          const udpdk_rx_batch_t *rb, uint32_t naf, struct h_arena **ad, struct h_arena **af)
+{
+    *ad = *af = NULL;
+    const uint64_t bd = g_udpdk.acc_do[nad] ? g_udpdk.acc_do[nad] : 16u;
+    const uint64_t bf = g_udpdk.acc_fo[naf] ? g_udpdk.acc_fo[naf] : 16u;
+    const uint32_t cmax = nad > naf ? nad : naf;
+    const uint64_t bmax = bd > bf ? bd : bf;
+    struct h_gbuf *gb = &g_udpdk.gb;
+    if (h_grow_pinned((void **)&g_udpdk.pc_acc, &g_udpdk.pc_acc_cap, 8ull * (nad + naf) + 8) ||
+        h_grow_dev_on(g, &gb->acc, &gb->acc_cap, 8ull * cmax + 4) ||
+        h_grow_dev_on(g, &gb->pay, &gb->pay_cap, bmax) ||
+        h_grow_dev_on(g, &gb->len, &gb->len_cap, 4ull * cmax) ||
+        h_grow_dev_on(g, &gb->sip, &gb->sip_cap, 4ull * cmax) ||
+        h_grow_dev_on(g, &gb->spt, &gb->spt_cap, 2ull * cmax))
+        return -1;
+    const udpdk_rx_gather_t go = {gb->pay, 16u, gb->len, gb->sip, gb->spt};
+    uint32_t *dacc = gb->acc;
+    uint32_t *hl = g_udpdk.pc_acc;
+    for (int part = 0; part < 2; part++) {
+        const uint32_t cnt = part ? naf : nad;
+        if (!cnt) continue;
+        const uint32_t *acc = part ? g_udpdk.acc_f : g_udpdk.acc_d, *offs = part ? g_udpdk.acc_fo : g_udpdk.acc_do;
+        const uint64_t bytes = part ? bf : bd;
+        struct h_arena *a = h_arena_get(cnt, bytes);
+        if (!a) return -1;                             /* ENOBUFS (budget) or ENOMEM */
+        *(part ? af : ad) = a;
+        memcpy(hl, acc, 4ull * cnt);
+        memcpy(hl + cnt, offs, 4ull * cnt + 4);
+        int rc;
+        if ((rc = udpdk_gpu_pipe_copy(g, pipe, dacc, hl, 8ull * cnt + 4)) ||
+            (rc = udpdk_gpu_pipe_gather_packed(g, pipe, part ? rb : b, dacc, 0, cnt, dacc + cnt, &go)) ||
+            (rc = udpdk_gpu_pipe_copy(g, pipe, a->payload, gb->pay, bytes)) ||
+            (rc = udpdk_gpu_pipe_copy(g, pipe, a->len, gb->len, 4ull * cnt)) ||
+            (rc = udpdk_gpu_pipe_copy(g, pipe, a->src_ip, gb->sip, 4ull * cnt)) ||
+            (rc = udpdk_gpu_pipe_copy(g, pipe, a->src_port, gb->spt, 2ull * cnt))) {
+            errno = -rc;
+            return -1;
+        }
+        hl += 2 * cnt + 1;
+    }
+    return 0;
+}
+
+/* 1: not taken (the caller polls in one piece); 0: done; -1: error (errno). */
+static int h_poll_chunked(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *offset,
+                          const uint16_t *length, const uint32_t *ptype, uint32_t n, uint32_t lanes,
+                          uint32_t maxfan, udpdk_rx_stats_t *stats_out)
+{
+    const uint64_t chunk = (uint64_t)g_udpdk.poll_chunk_mb << 20;
+    if (!chunk || g_udpdk.host_copy_min || frames_bytes < 2 * chunk || frames_bytes >= (1ull << 32) ||
+        n < 2u * H_BURST_SIZE || (uint64_t)n * maxfan > (1ull << 28) ||
+        !h_desc_sorted(offset, length, n, frames_bytes))
+        return 1;
+    udpdk_gpu_ctx *g = g_udpdk.gpu;
+    uint64_t kk = frames_bytes / chunk;
+    const uint32_t want = kk > H_CHUNKS_MAX ? H_CHUNKS_MAX : (uint32_t)kk;
+    struct h_chunk ck[H_CHUNKS_MAX];
+    uint32_t K = 0, f = 0;
+    for (uint32_t k = 1; k <= want; k++) {             /* byte-balanced cuts at burst boundaries */
+        uint32_t e = n;
+        if (k < want) {
+            const uint64_t target = frames_bytes * k / want;
+            uint32_t a = f, b = n;
+            while (a < b) {
+                const uint32_t m = a + (b - a) / 2;
+                if (offset[m] < target) a = m + 1; else b = m;
+            }
+            e = a - a % H_BURST_SIZE;
+            if (e <= f) continue;
+        }
+        const uint64_t lo = offset[f] & ~(uint64_t)15u, hi = (uint64_t)offset[e - 1] + length[e - 1];
+        ck[K].f0 = f;
+        ck[K].n = e - f;
+        ck[K].lo = lo;
+        ck[K].bytes = hi > lo ? hi - lo : 0;
+        K++;
+        f = e;
+    }
+    if (K < 2) return 1;
+    const uint32_t L1 = lanes + 1, SL = lanes < UDPDK_MAX_SOCKETS ? lanes : UDPDK_MAX_SOCKETS;
+    if (h_grow_pinned((void **)&g_udpdk.pc_meta, &g_udpdk.pc_meta_cap, 4ull * n + 4) ||
+        h_grow_pinned((void **)&g_udpdk.pc_loff, &g_udpdk.pc_loff_cap, 4ull * L1 * K) ||
+        h_grow_pinned((void **)&g_udpdk.pc_lpkt, &g_udpdk.pc_lpkt_cap, 4ull * n * maxfan + 4))
+        return -1;
+    int rc, err = 0;
+    struct h_arena *ad = NULL, *af = NULL;       /* slabs of the chunk whose gather is in flight */
+    uint32_t pnad = 0, pnaf = 0;
+    int pend = -1;
+    struct h_adm A;
+    udpdk_rx_stats_t tot;
+    memset(&tot, 0, sizeof(tot));
+#define CK_ISSUE(k) udpdk_gpu_pipe_rx_host(g, h_pipe_of(k), frames + ck[k].lo, ck[k].bytes, offset + ck[k].f0,     \
+                                           (uint32_t)ck[k].lo, length + ck[k].f0, ptype ? ptype + ck[k].f0 : NULL, \
+                                           ck[k].n, g_udpdk.pc_meta + ck[k].f0, g_udpdk.pc_loff + (uint64_t)L1 * (k), \
+                                           g_udpdk.pc_lpkt + (uint64_t)ck[k].f0 * maxfan, ck[k].n * maxfan, &ck[k].st)
+    if ((rc = CK_ISSUE(0))) { errno = -rc; return -1; }
+    for (uint32_t k = 0; k < K && !err; k++) {
+        if (k + 1 < K && (rc = CK_ISSUE(k + 1))) { err = -rc; break; }
+        rc = udpdk_gpu_pipe_wait(g, h_pipe_of(k));
+        if (rc && rc != -ENOSPC) { err = -rc; break; }
+        /* chunk k - 1: its payloads are home, publish them */
+        if (pend >= 0) {
+            if ((rc = udpdk_gpu_pipe_wait(g, h_pipe_of((uint32_t)pend)))) { err = -rc; break; }
+            if (ad) atomic_store_explicit(&ad->refs, pnad, memory_order_relaxed);
+            if (af) atomic_store_explicit(&af->refs, pnaf, memory_order_relaxed);
+            struct h_pub P = {&A, ad, af, 0};
+            h_pool_run(h_pub_job, &P);
+            ad = af = NULL;
+            pend = -1;
+        }
+        const struct h_chunk *C = &ck[k];
+        const uint32_t *loff = g_udpdk.pc_loff + (uint64_t)L1 * k, *lpkt = g_udpdk.pc_lpkt + (uint64_t)C->f0 * maxfan;
+        for (uint32_t v = 0; v < UDPDK_N_COUNTERS; v++) tot.counters[v] += C->st.counters[v];
+        tot.deliveries += C->st.deliveries;
+        tot.overflow |= C->st.overflow;
+        udpdk_rx_batch_t staged, rb;
+        const uint32_t *meta_dev = NULL;
+        if ((rc = udpdk_gpu_pipe_batch(g, h_pipe_of(k), &staged, &meta_dev))) { err = -rc; break; }
+        uint32_t nd = 0;
+        const uint64_t nfrag = C->st.counters[UDPDK_V_FRAG];
+        if (h_frag_pass(&staged, meta_dev, nfrag, lanes, maxfan, 1, &rb, &nd)) { err = errno; break; }
+        const uint32_t *floff = nd ? g_udpdk.fr_loff : NULL;
+        const uint32_t cap = C->n * maxfan, D = loff[lanes], DF = nd ? floff[lanes] : 0u;
+        int lanes_ok = loff[0] == 0u && D <= cap;
+        for (uint32_t s = 0; lanes_ok && s < lanes; s++) lanes_ok = loff[s] <= loff[s + 1];
+        if (!lanes_ok) { err = EIO; break; }
+        if (h_grow_host((void **)&g_udpdk.acc_d, &g_udpdk.acc_d_cap, 4ull * D + 4) ||
+            h_grow_host((void **)&g_udpdk.acc_f, &g_udpdk.acc_f_cap, 4ull * DF + 4) ||
+            h_grow_host((void **)&g_udpdk.acc_do, &g_udpdk.acc_do_cap, 4ull * D + 8) ||
+            h_grow_host((void **)&g_udpdk.acc_fo, &g_udpdk.acc_fo_cap, 4ull * DF + 8) ||
+            h_grow_host((void **)&g_udpdk.acc_sock, &g_udpdk.acc_sock_cap, 4ull * (D + DF) + 4)) {
+            err = errno;
+            break;
+        }
+        /* admission of the chunk's bursts (frame indices chunk-local; cuts at burst boundaries
+         * keep the bursts the one-piece poll would form) */
+        A.loff = loff; A.lpkt = lpkt; A.floff = floff; A.flpkt = g_udpdk.fr_lpkt; A.forg = g_udpdk.fr_org;
+        A.length = length + C->f0; A.lanes = SL; A.fill = 0; A.n = C->n;
+        atomic_init(&A.bad, 0);
+        h_adm_split(&A, h_pool_parts());
+        h_pool_run(h_adm_job, &A);
+        if (atomic_load(&A.bad)) { err = EIO; break; }
+        uint32_t nad = 0, naf = 0;
+        uint64_t offd = 0, offf = 0;
+        for (uint32_t s = 0; s < A.lanes; s++) {
+            s_kd[s] = nad; s_kf[s] = naf; s_od[s] = offd; s_of[s] = offf;
+            nad += s_nd[s]; naf += s_nf[s]; offd += s_bd[s]; offf += s_bf[s];
+        }
+        if (offd > 0xFFFFFFF0ull || offf > 0xFFFFFFF0ull) { err = ENOBUFS; break; }
+        A.fill = 1;
+        h_pool_run(h_adm_job, &A);
+        g_udpdk.acc_do[nad] = (uint32_t)offd;
+        g_udpdk.acc_fo[naf] = (uint32_t)offf;
+        if (nad + naf && h_gather_chunk(g, h_pipe_of(k), &staged, nad, &rb, naf, &ad, &af)) {
+            if (errno != ENOBUFS) { err = errno; break; }
+            /* slab budget exhausted by datagrams still queued: this chunk's bursts are dropped */
+            if (ad) h_arena_put(ad);
+            if (af) h_arena_put(af);
+            ad = af = NULL;
+            __atomic_fetch_add(&g_udpdk.rx_nobufs, (uint64_t)nad + naf, __ATOMIC_RELAXED);
+            continue;
+        }
+        if (nad + naf) { pend = (int)k; pnad = nad; pnaf = naf; }
+    }
+#undef CK_ISSUE
+    if (!err && pend >= 0) {
+        if ((rc = udpdk_gpu_pipe_wait(g, h_pipe_of((uint32_t)pend)))) {
+            err = -rc;
+        } else {
+            if (ad) atomic_store_explicit(&ad->refs, pnad, memory_order_relaxed);
+            if (af) atomic_store_explicit(&af->refs, pnaf, memory_order_relaxed);
+            struct h_pub P = {&A, ad, af, 0};
+            h_pool_run(h_pub_job, &P);
+            ad = af = NULL;
+        }
+    }
+    if (err) {                                   /* nothing of ours left in flight */
+        for (uint32_t k = 0; k < 3; k++) (void)udpdk_gpu_pipe_wait(g, h_pipe_of(k));
+        if (ad) h_arena_put(ad);
+        if (af) h_arena_put(af);
+        errno = err;
+        return -1;
+    }
+    if (stats_out) *stats_out = tot;
+    return 0;
+}
+
 int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *offset,
                   const uint16_t *length, const uint32_t *ptype, uint32_t n,
                   udpdk_rx_stats_t *stats_out)
@@ -958,6 +1191,10 @@ int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *
     if (h_snapshot_refresh()) goto out;
     PROF_T(p1);
     const uint32_t lanes = g_udpdk.snap_lanes, maxfan = g_udpdk.snap_maxfan;
+    if (g_udpdk.n_shards <= 1) {
+        const int r = h_poll_chunked(frames, frames_bytes, offset, length, ptype, n, lanes, maxfan, stats_out);
+        if (r <= 0) { ret = r; goto out; }
+    }
     const uint64_t cap64 = (uint64_t)n * maxfan;
     const uint32_t cap = cap64 > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)cap64;
     if (h_grow_host((void **)&g_udpdk.rx_meta, &g_udpdk.rx_meta_cap, 4ull * n + 4) ||

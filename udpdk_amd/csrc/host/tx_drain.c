@@ -27,7 +27,7 @@ void h_tx_buffers_free(void)
     g_udpdk.tx_sel_cap = 0;
 }
 
-static int h_grow_pinned(void **p, uint64_t *cap, uint64_t need)
+int h_grow_pinned(void **p, uint64_t *cap, uint64_t need)
 {
     if (*p && *cap >= need) return 0;
     if (*p) udpdk_gpu_host_free(g_udpdk.gpu, *p);

@@ -875,7 +875,7 @@ int enqueue_host(udpdk_gpu_ctx *c, int pipe, const uint8_t *frames_host, uint64_
                  const uint32_t *offset_host, const uint16_t *length_host,
                  const uint32_t *ptype_host, uint32_t n, uint32_t *meta_host,
                  uint32_t *lane_off_host, uint32_t *lane_pkt_host, uint32_t lane_cap,
-                 udpdk_rx_stats_t *stats, bool copy_lanes = true)
+                 udpdk_rx_stats_t *stats, bool copy_lanes = true, uint32_t offset_base = 0)
 {
     if (!stats || !lane_off_host || n > c->max_frames) return -EINVAL;
     if (n && (!frames_host || !offset_host || !length_host || !meta_host)) return -EINVAL;
@@ -907,7 +907,12 @@ int enqueue_host(udpdk_gpu_ctx *c, int pipe, const uint8_t *frames_host, uint64_
         src = P.st_frames_h;
     }
     uint8_t *dh = P.st_desc_h;
-    memcpy(dh, offset_host, (size_t)n * 4);
+    if (offset_base) {                          // a chunk of a larger batch: offsets rebased
+        uint32_t *o = (uint32_t *)dh;
+        for (uint32_t i = 0; i < n; ++i) o[i] = offset_host[i] - offset_base;
+    } else {
+        memcpy(dh, offset_host, (size_t)n * 4);
+    }
     memcpy(dh + (size_t)n * 4, length_host, (size_t)n * 2);
     const size_t pt_off = ((size_t)n * 6 + 15) & ~(size_t)15;
     if (ptype_host) memcpy(dh + pt_off, ptype_host, (size_t)n * 4);
@@ -1012,7 +1017,7 @@ namespace {
 
 static int rx_gather_launch(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const uint32_t *lane_pkt_dev,
                      uint32_t first, uint32_t count, const uint32_t *slot_off_dev,
-                     const udpdk_rx_gather_t *o)
+                     const udpdk_rx_gather_t *o, int pipe = -1)
 {
     if (!c || !bt || !o) return -EINVAL;
     if (!count) return 0;
@@ -1022,7 +1027,10 @@ static int rx_gather_launch(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const 
     if ((uintptr_t)o->payload_dev & 15u) return -EINVAL;
     if (bt->frames_bytes >= (1ull << 32) || (uint64_t)first + count > 0xFFFFFFFFull) return -EINVAL;
     HIPC(c, hipSetDevice(c->device));
-    if (c->depth > 1) { int r = join_pipes(c); if (r) return r; }
+    // pipe >= 0: on that pipe's stream, after its own work only (udpdk_gpu_pipe_gather_packed)
+    if (pipe < 0 && c->depth > 1) { int r = join_pipes(c); if (r) return r; }
+    const hipStream_t gst = pipe < 0 ? c->stream : c->pipes[pipe].stream;
+    if (pipe >= 0) c->pipes[pipe].dirty = true;
     GatherArgs ga;
     ga.frames = bt->frames_dev;
     ga.offset = bt->offset_dev;
@@ -1043,12 +1051,12 @@ static int rx_gather_launch(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, const 
     if (c->timing_every) {
         HIPC(c, hipEventCreate(&e0));
         HIPC(c, hipEventCreate(&e1));
-        HIPC(c, hipEventRecord(e0, c->stream));
+        HIPC(c, hipEventRecord(e0, gst));
     }
-    hipLaunchKernelGGL(rx_gather, dim3(grid), dim3(GATHER_BLOCK), 0, c->stream, ga);
+    hipLaunchKernelGGL(rx_gather, dim3(grid), dim3(GATHER_BLOCK), 0, gst, ga);
     HIPC(c, hipGetLastError());
     if (c->timing_every) {
-        HIPC(c, hipEventRecord(e1, c->stream));
+        HIPC(c, hipEventRecord(e1, gst));
         HIPC(c, hipEventSynchronize(e1));
         float ms = 0;
         HIPC(c, hipEventElapsedTime(&ms, e0, e1));
@@ -1074,6 +1082,58 @@ int udpdk_gpu_rx_gather_packed(udpdk_gpu_ctx *c, const udpdk_rx_batch_t *bt, con
 {
     if (count && !slot_off_dev) return -EINVAL;
     return rx_gather_launch(c, bt, lane_pkt_dev, first, count, slot_off_dev, o);
+}
+
+// ---- poller internals: udpdk_poll_rx's pipelined form (explicit pipes, no cross-pipe joins) ----
+int udpdk_gpu_pipe_rx_host(udpdk_gpu_ctx *c, int pipe, const uint8_t *frames_host, uint64_t frames_bytes,
+                           const uint32_t *offset_host, uint32_t offset_base, const uint16_t *length_host,
+                           const uint32_t *ptype_host, uint32_t n, uint32_t *meta_host,
+                           uint32_t *lane_off_host, uint32_t *lane_pkt_host, uint32_t lane_cap,
+                           udpdk_rx_stats_t *stats)
+{
+    if (!c || pipe < 1 || pipe >= MAX_PIPES) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    int rc = finish_host(c, c->pipes[pipe]);
+    if (rc && rc != -ENOSPC) return rc;
+    return enqueue_host(c, pipe, frames_host, frames_bytes, offset_host, length_host, ptype_host, n,
+                        meta_host, lane_off_host, lane_pkt_host, lane_cap, stats, true, offset_base);
+}
+
+int udpdk_gpu_pipe_wait(udpdk_gpu_ctx *c, int pipe)
+{
+    if (!c || pipe < 1 || pipe >= MAX_PIPES) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    Pipe &P = c->pipes[pipe];
+    const int rc = finish_host(c, P);
+    HIPC(c, hipStreamSynchronize(P.stream));
+    return rc;
+}
+
+int udpdk_gpu_pipe_batch(udpdk_gpu_ctx *c, int pipe, udpdk_rx_batch_t *batch, const uint32_t **meta_dev)
+{
+    if (!c || !batch || pipe < 1 || pipe >= MAX_PIPES) return -EINVAL;
+    const Pipe &P = c->pipes[pipe];
+    if (!P.staged_meta) return -ENOENT;
+    *batch = P.staged;
+    if (meta_dev) *meta_dev = P.staged_meta;
+    return 0;
+}
+
+int udpdk_gpu_pipe_copy(udpdk_gpu_ctx *c, int pipe, void *dst, const void *src, size_t bytes)
+{
+    if (!c || pipe < 1 || pipe >= MAX_PIPES || ((!dst || !src) && bytes)) return -EINVAL;
+    HIPC(c, hipSetDevice(c->device));
+    c->pipes[pipe].dirty = true;
+    if (bytes) HIPC(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, c->pipes[pipe].stream));
+    return 0;
+}
+
+int udpdk_gpu_pipe_gather_packed(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt,
+                                 const uint32_t *lane_pkt_dev, uint32_t first, uint32_t count,
+                                 const uint32_t *slot_off_dev, const udpdk_rx_gather_t *o)
+{
+    if (!c || pipe < 1 || pipe >= MAX_PIPES || (count && !slot_off_dev)) return -EINVAL;
+    return rx_gather_launch(c, bt, lane_pkt_dev, first, count, slot_off_dev, o, pipe);
 }
 
 int udpdk_gpu_rss_default_conf(udpdk_rss_conf_t *conf, uint32_t n_queues)
