@@ -17,12 +17,13 @@
 //  * every other flow's fragments go through the table in arrival order on one wave
 //    (reasm_serial), which is then exactly the reference's sequence of ip_frag_find calls.
 // Launch sequence (udpdk_gpu_rx_reassemble, synchronous):
-//   reasm_fsel_*    FRAG verdicts -> fragment list in arrival order (+ the stats block zeroed)
+//   reasm_fsel_*    FRAG verdicts -> fragment list in arrival order (+ the stats block zeroed);
+//                   the count launch's extra blocks make the bucket summary: valid entries per
+//                   bucket, any expired (the table is unchanged until the analysis reads it)
 //   reasm_runs      (id << ib | index) sort keys; does every flow key form one run? (grouped)
 //   [not grouped]   radix sort 1 by (id, index); reasm_keys: src|dst keys in that order; radix
 //                   sort 2 (stable). Grouped batches skip both: the list is already grouped
 //   reasm_prep      per sorted position: frame, key, crc32c signature, length class
-//   reasm_bsum      per bucket: valid entries, any expired
 //   reasm_flows     per flow: span, pending or not, key in the table, overlap records
 //   [not grouped]   radix sort 4 + max scan + reasm_overlap: flows whose spans overlap on a
 //                   shared bucket (grouped: no two spans overlap)
@@ -309,13 +310,13 @@ __device__ __forceinline__ uint32_t frag_bits8(const uint32_t *meta, uint32_t i0
     return m;
 }
 
-__global__ void __launch_bounds__(RS_BLOCK) reasm_fsel_count(const uint32_t *meta, uint32_t n, uint32_t *blk,
-                                                            unsigned long long *stats_block)
+__device__ __forceinline__ void fsel_count_block(const uint32_t *meta, uint32_t n, uint32_t *blk,
+                                                 unsigned long long *stats_block, uint32_t b)
 {
     __shared__ uint32_t red[RS_WAVES];
     const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
-    if (blockIdx.x == 0 && tid < RS_ZERO_WORDS) stats_block[tid] = 0ull;
-    uint32_t c = (uint32_t)__builtin_popcount(frag_bits8(meta, blockIdx.x * RS_FS + 8u * tid, n));
+    if (b == 0 && tid < RS_ZERO_WORDS) stats_block[tid] = 0ull;
+    uint32_t c = (uint32_t)__builtin_popcount(frag_bits8(meta, b * RS_FS + 8u * tid, n));
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
     if (lane == 0) red[w] = c;
@@ -324,8 +325,14 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_fsel_count(const uint32_t *met
         uint32_t t = 0;
 #pragma unroll
         for (uint32_t i = 0; i < RS_WAVES; ++i) t += red[i];
-        blk[blockIdx.x] = t;
+        blk[b] = t;
     }
+}
+
+__global__ void __launch_bounds__(RS_BLOCK) reasm_fsel_count(const uint32_t *meta, uint32_t n, uint32_t *blk,
+                                                            unsigned long long *stats_block)
+{
+    fsel_count_block(meta, n, blk, stats_block, blockIdx.x);
 }
 
 __global__ void __launch_bounds__(RS_BLOCK) reasm_fsel_write(const uint32_t *meta, uint32_t n, const uint32_t *blk,
@@ -618,13 +625,13 @@ __device__ __forceinline__ uint32_t bucket2_of(const ReasmArgs &a, uint32_t sig)
 
 // Per bucket of the table at call start: valid entries | (an expired valid entry) << 31; the
 // bucket's count of complex flows (below) is reset. One lane per entry, assoc lanes per bucket.
-__global__ void __launch_bounds__(RS_BLOCK) reasm_bsum(ReasmArgs a)
+__device__ __forceinline__ void bsum_rows(const ReasmArgs &a, uint32_t blk, uint32_t nblk)
 {
     const uint32_t lane = __lane_id();
     const uint32_t g0 = lane & ~(a.assoc - 1u);                  // the bucket's first lane
     const unsigned long long gm = (a.assoc == 64u ? ~0ull : ((1ull << a.assoc) - 1ull)) << g0;
     const uint32_t ne = a.nbuckets * a.assoc;
-    for (uint32_t x0 = blockIdx.x * RS_BLOCK + (threadIdx.x & ~63u); x0 < ne; x0 += gridDim.x * RS_BLOCK) {
+    for (uint32_t x0 = blk * RS_BLOCK + (threadIdx.x & ~63u); x0 < ne; x0 += nblk * RS_BLOCK) {
         const uint32_t x = x0 + lane;
         bool v = false, old = false;
         if (x < ne) {
@@ -643,6 +650,17 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_bsum(ReasmArgs a)
             a.cplx[b] = 0;
         }
     }
+}
+
+// The fragment count per select block (blocks [0, nfs)) and, in the blocks after them, the
+// bucket summary (reasm_bsum's rows): one launch at the start of a call, the table being
+// unchanged until the flow analysis reads the summary.
+__global__ void __launch_bounds__(RS_BLOCK) reasm_fsel_count_bsum(ReasmArgs a, uint32_t *blk, uint32_t nfs)
+{
+    if (blockIdx.x < nfs)
+        fsel_count_block(a.meta, a.n, blk, a.stats, blockIdx.x);
+    else
+        bsum_rows(a, blockIdx.x - nfs, gridDim.x - nfs);
 }
 
 // One thread per flow segment (at its first sorted position p). The flow is walked on its own,
@@ -948,13 +966,30 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_process(ReasmArgs a, uint32_t 
     if (threadIdx.x == UDPDK_RS_N && s_cnt[UDPDK_RS_N]) atomicAdd(a.out_bytes, s_cnt[UDPDK_RS_N]);
 }
 
-// TAILQ_FIRST(&tbl->lru): the valid entry with the smallest (E_LRU_CALL, E_LRU_IDX), by the
-// whole wave (eight entries per lane in flight per round); RS_NONE when the table is empty.
-__device__ uint32_t lru_head(const ReasmArgs &a)
+// TAILQ_FIRST(&tbl->lru): the valid entry with the smallest (E_LRU_CALL, E_LRU_IDX). The wave keeps
+// one minimum per lane, over the entries x with x % 64 == lane (its partition), built by one scan
+// of the table (eight entries per lane in flight per round) the first time a call needs the head.
+// A lane's minimum can only go stale one way: the entry it names is invalidated or moved to the
+// list's tail (a new key is larger than every key in the table, so no entry can appear below it).
+// A cached minimum is therefore never above its partition's true one, and the head is the
+// smallest cached minimum once that one is checked against its entry; a stale one costs a scan
+// of its own partition (entries / 64, spread over the wave), not of the table.
+struct LruMin {
+    unsigned long long key;                  // this lane's partition minimum, ~0 when none
+    uint32_t idx;
+};
+
+__device__ __forceinline__ unsigned long long lru_key(const ReasmArgs &a, uint32_t x, bool *valid)
+{
+    const uint32_t *e = a.tab + (size_t)x * E_WORDS;
+    *valid = ld_a(e + E_VALID) != 0;
+    return ((unsigned long long)ld_a(e + E_LRU_CALL) << 32) | ld_a(e + E_LRU_IDX);
+}
+
+__device__ LruMin lru_scan_all(const ReasmArgs &a)
 {
     const uint32_t lane = __lane_id();
-    unsigned long long best = ~0ull;
-    uint32_t bi = RS_NONE;
+    LruMin m{~0ull, RS_NONE};
     for (uint32_t x0 = 0; x0 < a.entries; x0 += 512u) {
         uint32_t v[8], hi[8], lo[8];
 #pragma unroll
@@ -968,10 +1003,27 @@ __device__ uint32_t lru_head(const ReasmArgs &a)
 #pragma unroll
         for (uint32_t u = 0; u < 8; ++u) {
             const unsigned long long key = ((unsigned long long)hi[u] << 32) | lo[u];
-            if (v[u] && key < best) {
-                best = key;
-                bi = x0 + 64u * u + lane;
+            if (v[u] && key < m.key) {
+                m.key = key;
+                m.idx = x0 + 64u * u + lane;
             }
+        }
+    }
+    return m;
+}
+
+// the minimum of partition `part` (entries part, part + 64, ...), by the whole wave; wave-uniform
+__device__ LruMin lru_scan_part(const ReasmArgs &a, uint32_t part)
+{
+    const uint32_t lane = __lane_id();
+    unsigned long long best = ~0ull;
+    uint32_t bi = RS_NONE;
+    for (uint32_t x = part + 64u * lane; x < a.entries; x += 64u * 64u) {
+        bool v;
+        const unsigned long long key = lru_key(a, x, &v);
+        if (v && key < best) {
+            best = key;
+            bi = x;
         }
     }
 #pragma unroll
@@ -983,7 +1035,34 @@ __device__ uint32_t lru_head(const ReasmArgs &a)
             bi = oi;
         }
     }
-    return bi;
+    return LruMin{best, bi};
+}
+
+// The head from the lanes' cached minima (refreshing the stale ones it meets); RS_NONE when the
+// table is empty. Wave-uniform.
+__device__ uint32_t lru_head(const ReasmArgs &a, LruMin &mine)
+{
+    const uint32_t lane = __lane_id();
+    for (;;) {
+        unsigned long long best = mine.key;
+        uint32_t bi = mine.idx, owner = lane;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const unsigned long long ob = __shfl_xor(best, d, 64);
+            const uint32_t oi = __shfl_xor(bi, d, 64), oo = __shfl_xor(owner, d, 64);
+            if (ob < best || (ob == best && oi < bi)) {
+                best = ob;
+                bi = oi;
+                owner = oo;
+            }
+        }
+        if (bi == RS_NONE) return RS_NONE;
+        bool v;
+        const unsigned long long key = lru_key(a, bi, &v);
+        if (v && key == best) return bi;
+        const LruMin fresh = lru_scan_part(a, owner);      // that partition's minimum had gone
+        if (lane == owner) mine = fresh;
+    }
 }
 
 // The serial path: one wave takes the listed fragments in arrival order, exactly as the
@@ -1004,7 +1083,8 @@ __global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *
     const bool limit = a.counts[6] != 0u;
     uint32_t use = ld_a(a.tab_used);
     uint32_t head = RS_NONE;                 // the LRU head, while head_ok
-    bool head_ok = false;
+    bool head_ok = false, lru_built = false;
+    LruMin lru{~0ull, RS_NONE};              // this lane's partition minimum (lru_head)
     for (uint32_t k = 0; k < K; ++k) {
         const uint32_t q = list[k];
         const uint32_t i = a.s_i[q], m = a.s_meta[q];
@@ -1033,7 +1113,11 @@ __global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *
             // a free entry, but max_entries in use: the LRU head goes if it has expired, else
             // the fragment is dropped (ip_frag_find's fail_nospace)
             if (!head_ok) {
-                head = lru_head(a);
+                if (!lru_built) {
+                    lru = lru_scan_all(a);
+                    lru_built = true;
+                }
+                head = lru_head(a, lru);
                 head_ok = true;
             }
             bool del = false;
@@ -2016,8 +2100,9 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     size_t tb = r->tmp_bytes;
     if (n) {
         const uint32_t nfs = (n + RS_FS - 1) / RS_FS;   // blocks of the fragment select (their
-        hipLaunchKernelGGL(reasm_fsel_count, dim3(nfs), dim3(RS_BLOCK), 0, st, meta_dev, n, r->sizes,
-                           r->stats);            // counts sit in sizes, dead until the completion list)
+        const uint32_t gb = std::max<uint32_t>(1, std::min<uint32_t>((r->entries + RS_BLOCK - 1) / RS_BLOCK, 4096));
+        hipLaunchKernelGGL(reasm_fsel_count_bsum, dim3(nfs + gb), dim3(RS_BLOCK), 0, st, a, r->sizes,
+                           nfs);                 // counts sit in sizes, dead until the completion list)
         hipLaunchKernelGGL(reasm_fsel_write, dim3(nfs), dim3(RS_BLOCK), 0, st, meta_dev, n,
                            (const uint32_t *)r->sizes, r->frag_list, r->counts);
         RS_HIP(hipGetLastError());
@@ -2089,9 +2174,9 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     };
     auto analysis = [&](uint32_t Fk, uint32_t Fgrid, bool grp) -> int {
         const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((Fgrid + RS_BLOCK - 1) / RS_BLOCK, 4096));
-        const uint32_t gb = std::max<uint32_t>(1, std::min<uint32_t>((r->entries + RS_BLOCK - 1) / RS_BLOCK, 4096));
-        hipLaunchKernelGGL(reasm_bsum, dim3(gb), dim3(RS_BLOCK), 0, st, a);
-        RS_HIP(hipGetLastError());
+        // (the bucket summary: made by reasm_fsel_count_bsum at the call's start; the table and
+        // the complex-flow counts are untouched until here, a speculative grouped analysis that
+        // found the batch not grouped having returned at once)
         const uint32_t gfl = std::max<uint32_t>(1, std::min<uint32_t>((Fgrid + RS_FLOW_CHUNK - 1) / RS_FLOW_CHUNK, 2048));
         hipLaunchKernelGGL(reasm_flows, dim3(gfl), dim3(RS_BLOCK), 0, st, a, Fk);
         RS_HIP(hipGetLastError());
