@@ -1268,6 +1268,29 @@ struct SpecTail {
     const uint16_t *length;
 };
 
+// In-place emit: the header dwords of the next datagram loaded with its bytes (1), or in its own
+// step (0: 8 VGPRs fewer); waves per SIMD of the emit launches.
+#ifndef UDPDK_RS_HWPF
+#define UDPDK_RS_HWPF 1
+#endif
+#ifndef UDPDK_RS_EMIT_WPE
+#define UDPDK_RS_EMIT_WPE 7
+#endif
+
+// A load through the constant address space: with a wave-uniform address it is a scalar load
+// (s_load, counted by lgkmcnt), so waiting for it does not wait for the wave's older vector
+// stores, which vmcnt counts in order with vector loads. For data no launch writes while it runs
+// (the completion records, their order, the batch's descriptors).
+template <typename T>
+__device__ __forceinline__ T cload(const T *p)
+{
+#if __HIP_DEVICE_COMPILE__
+    return *(const __attribute__((address_space(4))) T *)(uintptr_t)p;
+#else
+    return *p;                                   // (host pass: never called)
+#endif
+}
+
 // x[i] for a runtime i without indexing a register array (which would go to scratch)
 __device__ __forceinline__ uint32_t pick4(const uint32_t (&x)[RS_MAX_FRAG], uint32_t i)
 {
@@ -1490,16 +1513,16 @@ __device__ __forceinline__ void emit_copy(const EmitArgs &a, uint32_t C)
     ReasmDone rn{};
     uint32_t oon = 0;
     if (k < C) {
-        rn = a.done[a.perm[k]];
-        oon = a.out_off_in[k];
+        rn = cload(&a.done[cload(&a.perm[k])]);
+        oon = cload(&a.out_off_in[k]);
     }
     constexpr uint32_t OOR = 0x80000000u;         // out of any buffer's range: no access, zeros
     for (; k < C; k += stride) {
         const ReasmDone r = rn;
         const uint32_t oo = oon;
         if (k + stride < C) {
-            rn = a.done[a.perm[k + stride]];
-            oon = a.out_off_in[k + stride];
+            rn = cload(&a.done[cload(&a.perm[k + stride])]);
+            oon = cload(&a.out_off_in[k + stride]);
         }
         const uint32_t L = 34u + r.total;
         const uint8_t *eb = a.ebuf + (size_t)r.entry * a.stride;
@@ -1517,7 +1540,7 @@ __device__ __forceinline__ void emit_copy(const EmitArgs &a, uint32_t C)
             // the fragment at offset 0 carries the header: its segment starts at byte 0
             d0[q] = !use ? 0xFFFFFFFFu : ofs == 0u ? 0u : 34u + ofs;
             d1[q] = !use ? 0xFFFFFFFFu : 34u + ofs + ln;
-            const uint32_t fo = use && !held[q] ? a.offset[r.where[q]] : 0u;
+            const uint32_t fo = use && !held[q] ? cload(&a.offset[r.where[q]]) : 0u;
             s0[q] = held[q] ? d0[q] : fo + (ofs == 0u ? 0u : 34u);
             if (use) {
                 any_held = any_held || held[q];
@@ -1663,20 +1686,30 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
     auto offsets = [&](const ReasmDone &x, uint32_t (&o)[RS_MAX_FRAG], uint32_t (&sx)[RS_MAX_FRAG]) -> uint32_t {
         const uint32_t mx = data_order(x, sx);
 #pragma unroll
-        for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) o[f] = f < mx ? a.offset[pick4(x.where, sx[f])] : 0u;
+        for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) o[f] = f < mx ? cload(&a.offset[pick4(x.where, sx[f])]) : 0u;
         return mx;
     };
     // Quick moves: a datagram of two fragments whose move is one round (<= 128 chunks, the
-    // MTU-sized case) has its loads issued one datagram ahead, before the previous datagram's
-    // stores, so the wait for a datagram's bytes leaves the next one's in flight (two per wave at
-    // 8 waves per SIMD; the move is latency-bound) and never waits for the previous stores (gfx9
-    // counts stores in vmcnt, in order). The loads are unconditional (out-of-range offsets when
-    // there is nothing to load) so that wait stays a counted one. Other datagrams take the round
-    // loop.
+    // MTU-sized case) has its bytes and its header dwords loaded one datagram ahead, before the
+    // previous datagram's stores, so the wait for them leaves the next datagram's loads in flight
+    // (two datagrams per wave at 8 waves per SIMD). gfx9 counts stores in vmcnt with the loads, in
+    // order, so that wait must not also wait for the previous datagram's stores: a quick step
+    // issues the same VMEM instructions whatever its geometry (loads at out-of-range offsets when
+    // there is nothing to load; every chunk one 16-byte store, dropped out of range; the header
+    // patch six byte stores; the outputs stored by every lane), and quick steps run in a loop of
+    // their own entered with nothing outstanding, so the compiler's count for that wait (the
+    // step's 12 stores and the next datagram's 7 loads younger than it) holds on every path. The first chunk's bytes below the destination (the first
+    // fragment's data) are loaded with the move's bytes and stored back merged; the last chunk's
+    // bytes past the datagram's end land in the second fragment's old frame (its 34 header bytes
+    // are more than a chunk), which nothing reads again. Other datagrams take the round loop.
     struct Quick {
         uint32_t D0, dst, De, shift, nch;
         uint4 x[2];
         uint32_t hi[2];
+        uint4 orig;                          // lane 0: the 16 bytes at D0 before the move
+#if UDPDK_RS_HWPF
+        uint32_t hw[6];                      // lane 0: header dwords from the one at or below byte 14
+#endif
     };
     auto quick_geom = [&](const ReasmDone &x, const uint32_t (&o)[RS_MAX_FRAG], const uint32_t (&sx)[RS_MAX_FRAG],
                           uint32_t mx, bool have, Quick &g) -> bool {
@@ -1688,7 +1721,21 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
         g.nch = (g.De - g.D0 + 15u) >> 4;
         return have && mx == 2u && g.nch <= 128u;
     };
-    auto quick_load = [&](Quick &g, bool on) {
+    // header dwords of the datagram whose first frame is at o0 (any datagram: the patch needs
+    // them), then the move's bytes when quick
+    auto header_load = [&](uint32_t (&hw)[6], bool have, uint32_t o0) {
+        const uint32_t ha = (o0 + 14u) & ~3u;
+        const uint4 h4 = load16(fr, have && lane == 0u ? ha : OOR);
+        const auto h2 = __builtin_amdgcn_raw_buffer_load_b64(fr, (int)(have && lane == 0u ? ha + 16u : OOR), 0, 0);
+        hw[0] = h4.x; hw[1] = h4.y; hw[2] = h4.z; hw[3] = h4.w; hw[4] = h2[0]; hw[5] = h2[1];
+    };
+    auto quick_load = [&](Quick &g, bool on, bool have, uint32_t o0) {
+#if UDPDK_RS_HWPF
+        header_load(g.hw, have, o0);
+#else
+        (void)have;
+        (void)o0;
+#endif
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t c = 64u * u + lane;
@@ -1697,88 +1744,98 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
             g.x[u] = load16(fr, in ? sa : OOR);
             g.hi[u] = ld32(fr, in && (S & 3u) ? sa + 16u : OOR);
         }
+        g.orig = load16(fr, on && lane == 0u ? g.D0 : OOR);
     };
     ReasmDone r{}, rn{};
     uint32_t fo[RS_MAX_FRAG] = {0, 0, 0, 0}, sl[RS_MAX_FRAG] = {0, 0, 0, 0}, m = 0;
     if (k < C) {
-        r = a.done[a.perm[k]];
+        r = cload(&a.done[cload(&a.perm[k])]);
         m = offsets(r, fo, sl);
     }
-    if (k + stride < C) rn = a.done[a.perm[k + stride]];
-    Quick qc, qn;
-    bool qc_on = quick_geom(r, fo, sl, m, k < C, qc);
-    quick_load(qc, qc_on);
-    for (; k < C; k += stride) {
+    if (k + stride < C) rn = cload(&a.done[cload(&a.perm[k + stride])]);
+    // the current datagram's loads sit in one of two register sets and the next one's go to the
+    // other (a quick run alternates them: a copy from the next set to the current one would wait
+    // for the next datagram's loads to land)
+    Quick q0, q1;
+    bool qc_on = quick_geom(r, fo, sl, m, k < C, q0);
+    quick_load(q0, qc_on, k < C, fo[0]);
+    // one datagram (k): the next one's loads, this one's move, header patch and outputs; then the
+    // pipeline advances
+    auto step = [&](bool quick, Quick &qc, Quick &qn) {
         uint32_t fon[RS_MAX_FRAG] = {0, 0, 0, 0}, sln[RS_MAX_FRAG] = {0, 0, 0, 0}, mn = 0;
         ReasmDone rnn{};
         if (k + stride < C) mn = offsets(rn, fon, sln);
-        if (k + 2u * stride < C) rnn = a.done[a.perm[k + 2u * stride]];
-        const uint32_t o0 = fo[0];
-        // header bytes 14..33: six dwords from the one at or below, lane 0 (issued with the first
-        // fragment's chunk loads; the moves never touch them)
-        const uint32_t ha = (o0 + 14u) & ~3u, hs = (o0 + 14u) & 3u;
-        uint32_t hw[6];
-        {
-            const uint4 h4 = load16(fr, lane == 0u ? ha : OOR);
-            const auto h2 = __builtin_amdgcn_raw_buffer_load_b64(fr, (int)(lane == 0u ? ha + 16u : OOR), 0, 0);
-            hw[0] = h4.x; hw[1] = h4.y; hw[2] = h4.z; hw[3] = h4.w; hw[4] = h2[0]; hw[5] = h2[1];
-        }
+        if (k + 2u * stride < C) rnn = cload(&a.done[cload(&a.perm[k + 2u * stride])]);
+        const uint32_t o0 = fo[0], hs = (o0 + 14u) & 3u;
+#if UDPDK_RS_HWPF
+        const uint32_t (&hw)[6] = qc.hw;
+#else
+        uint32_t hw[6];                                          // issued with this step's loads
+        header_load(hw, true, o0);
+#endif
         const bool qn_on = quick_geom(rn, fon, sln, mn, k + stride < C, qn);
-        quick_load(qn, qn_on);                                   // the next datagram in flight
-        if (qc_on) {
+        quick_load(qn, qn_on, k + stride < C, fon[0]);             // the next datagram in flight
+        // (pinned: the scheduler otherwise hoists this datagram's first uses, and their waits,
+        // above the next datagram's loads, which then issue only once these bytes have landed)
+        __builtin_amdgcn_sched_barrier(0);
+        if (quick) {
 #pragma unroll
             for (uint32_t u = 0; u < 2; ++u) {
                 const uint32_t c = 64u * u + lane;
-                if (c < qc.nch) {
-                    const uint32_t D = qc.D0 + 16u * c;
-                    const uint4 v = funnel4(qc.x[u], qc.hi[u], (D + qc.shift) & 3u);
-                    if (D >= qc.dst && D + 16u <= qc.De)
-                        store16(fr, D, v);
-                    else
-                        store_part(fr, D, v, D >= qc.dst ? 0u : qc.dst - D, min(qc.De - D, 16u));
+                const uint32_t D = qc.D0 + 16u * c;
+                uint4 v = funnel4(qc.x[u], qc.hi[u], (D + qc.shift) & 3u);
+                if (u == 0u) {                   // (per component: a uint4 select went through scratch)
+                    const uint4 mv = merge_at(qc.orig, v, qc.dst - qc.D0);
+                    const bool l0 = lane == 0u;
+                    v.x = l0 ? mv.x : v.x;
+                    v.y = l0 ? mv.y : v.y;
+                    v.z = l0 ? mv.z : v.z;
+                    v.w = l0 ? mv.w : v.w;
                 }
+                store16(fr, c < qc.nch ? D : OOR, v);
             }
-        }
+        } else {
 #pragma unroll
-        for (uint32_t f = 1; f < RS_MAX_FRAG; ++f) {            // static indices: no scratch
-            if (qc_on || f >= m) break;
-            const uint32_t q = sl[f];
-            const uint32_t fq = pick4(r.fr, q);
-            const uint32_t len = fq >> 16, ofs = fq & 0xFFFFu;
-            const uint32_t src = fo[f] + 34u, dst = o0 + 34u + ofs;
-            // bytes [dst, dst + len) <- [src, src + len), dst < src: destination-aligned 16-byte
-            // chunks (lane = chunk), two rounds' loads in flight before their stores (a round's
-            // stores land below every byte a later round reads); the two partial end chunks store
-            // only their own bytes
-            const uint32_t D0 = dst & ~15u, De = dst + len, shift = src - dst;
-            const uint32_t nch = (De - D0 + 15u) >> 4;
-            for (uint32_t c0 = 0; c0 < nch; c0 += 128u) {
-                uint4 v[2];
-                uint32_t Dv[2];
-                bool inv[2];
+            for (uint32_t f = 1; f < RS_MAX_FRAG; ++f) {            // static indices: no scratch
+                if (f >= m) break;
+                const uint32_t q = sl[f];
+                const uint32_t fq = pick4(r.fr, q);
+                const uint32_t len = fq >> 16, ofs = fq & 0xFFFFu;
+                const uint32_t src = fo[f] + 34u, dst = o0 + 34u + ofs;
+                // bytes [dst, dst + len) <- [src, src + len), dst < src: destination-aligned
+                // 16-byte chunks (lane = chunk), two rounds' loads in flight before their stores (a
+                // round's stores land below every byte a later round reads); the two partial end
+                // chunks store only their own bytes
+                const uint32_t D0 = dst & ~15u, De = dst + len, shift = src - dst;
+                const uint32_t nch = (De - D0 + 15u) >> 4;
+                for (uint32_t c0 = 0; c0 < nch; c0 += 128u) {
+                    uint4 v[2];
+                    uint32_t Dv[2];
+                    bool inv[2];
 #pragma unroll
-                for (uint32_t u = 0; u < 2; ++u) {
-                    const uint32_t c = c0 + 64u * u + lane;
-                    inv[u] = c < nch;
-                    Dv[u] = D0 + 16u * c;
-                    const uint32_t S = Dv[u] + shift, sa = S & ~3u, sh = S & 3u;
-                    const uint4 x = load16(fr, inv[u] ? sa : OOR);
-                    const uint32_t hi = ld32(fr, inv[u] && sh ? sa + 16u : OOR);
-                    v[u] = funnel4(x, hi, sh);
-                }
+                    for (uint32_t u = 0; u < 2; ++u) {
+                        const uint32_t c = c0 + 64u * u + lane;
+                        inv[u] = c < nch;
+                        Dv[u] = D0 + 16u * c;
+                        const uint32_t S = Dv[u] + shift, sa = S & ~3u, sh = S & 3u;
+                        const uint4 x = load16(fr, inv[u] ? sa : OOR);
+                        const uint32_t hi = ld32(fr, inv[u] && sh ? sa + 16u : OOR);
+                        v[u] = funnel4(x, hi, sh);
+                    }
 #pragma unroll
-                for (uint32_t u = 0; u < 2; ++u) {
-                    const uint32_t D = Dv[u];
-                    if (inv[u] && D >= dst && D + 16u <= De)
-                        store16(fr, D, v[u]);
-                    else if (inv[u])
-                        store_part(fr, D, v[u], D >= dst ? 0u : dst - D, min(De - D, 16u));
+                    for (uint32_t u = 0; u < 2; ++u) {
+                        const uint32_t D = Dv[u];
+                        if (inv[u] && D >= dst && D + 16u <= De)
+                            store16(fr, D, v[u]);
+                        else if (inv[u])
+                            store_part(fr, D, v[u], D >= dst ? 0u : dst - D, min(De - D, 16u));
+                    }
                 }
             }
         }
         // header: total length (16-17), fragment field DF only (20-21), checksum (24-25) over
-        // bytes 14..33
-        if (lane == 0) {
+        // bytes 14..33 (lane 0's values; the other lanes' stores drop)
+        {
             uint32_t h[5];
 #pragma unroll
             for (uint32_t j = 0; j < 5; ++j) h[j] = __builtin_amdgcn_alignbyte(hw[j + 1], hw[j], hs);
@@ -1795,15 +1852,11 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
             const uint32_t ck = a.cksum_zero ? 0u : ~sum & 0xFFFFu;
             const uint16_t pw[3] = {(uint16_t)(h[0] >> 16), (uint16_t)(h[1] >> 16), (uint16_t)ck};
             const uint32_t po[3] = {16, 20, 24};
-            if ((o0 & 1u) == 0u) {
 #pragma unroll
-                for (uint32_t j = 0; j < 3; ++j) __builtin_amdgcn_raw_buffer_store_b16(pw[j], fr, (int)(o0 + po[j]), 0, 0);
-            } else {
-#pragma unroll
-                for (uint32_t j = 0; j < 3; ++j) {
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)pw[j], fr, (int)(o0 + po[j]), 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pw[j] >> 8), fr, (int)(o0 + po[j] + 1u), 0, 0);
-                }
+            for (uint32_t j = 0; j < 3; ++j) {
+                const uint32_t at = lane == 0u ? o0 + po[j] : OOR;
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)pw[j], fr, (int)at, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pw[j] >> 8), fr, (int)(at + 1u), 0, 0);
             }
             a.out_off[k] = o0;
             a.out_len[k] = (uint16_t)(34u + r.total);
@@ -1815,8 +1868,27 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
         m = mn;
 #pragma unroll
         for (uint32_t f = 0; f < RS_MAX_FRAG; ++f) { fo[f] = fon[f]; sl[f] = sln[f]; }
-        qc = qn;
         qc_on = qn_on;
+        k += stride;
+    };
+    while (k < C) {
+        if (qc_on) {
+            // the run's first datagram's loads land here (vmcnt(0)), so on entry nothing the
+            // loop's waits count is outstanding and they follow the loop's own steady state
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+            for (;;) {
+                step(true, q0, q1);
+                if (!(k < C && qc_on)) {
+                    q0 = q1;
+                    break;
+                }
+                step(true, q1, q0);
+                if (!(k < C && qc_on)) break;
+            }
+        } else {
+            step(false, q0, q1);
+            q0 = q1;
+        }
     }
 }
 
@@ -1834,7 +1906,7 @@ reasm_emit(EmitArgs a)
 // A call that may reassemble in place: one launch takes whichever emit the device-side check
 // chose (in place unless reasm_clist_count refused it, then the copy when its buffer fits), so
 // the call has no second, empty emit launch.
-__global__ void __launch_bounds__(RS_BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8)))
+__global__ void __launch_bounds__(RS_BLOCK) __attribute__((amdgpu_waves_per_eu(UDPDK_RS_EMIT_WPE, 8)))
 reasm_emit_either(EmitArgs a, uint8_t *frames)
 {
     uint32_t F_unused, C = a.C;
