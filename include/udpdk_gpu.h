@@ -282,7 +282,8 @@ int udpdk_gpu_pipe_rx_host(udpdk_gpu_ctx *ctx, int pipe,
                            udpdk_rx_stats_t *stats);
 int udpdk_gpu_pipe_wait(udpdk_gpu_ctx *ctx, int pipe);
 int udpdk_gpu_pipe_batch(udpdk_gpu_ctx *ctx, int pipe, udpdk_rx_batch_t *batch, const uint32_t **meta_dev);
-int udpdk_gpu_pipe_copy(udpdk_gpu_ctx *ctx, int pipe, void *dst, const void *src, size_t bytes);
+int udpdk_gpu_pipe_h2d(udpdk_gpu_ctx *ctx, int pipe, void *dev, const void *host, size_t bytes);
+int udpdk_gpu_pipe_d2h(udpdk_gpu_ctx *ctx, int pipe, void *host, const void *dev, size_t bytes);
 
 /* ---------------------------------------------------------------------------------------------
  * RX payload delivery: the batch form of udpdk_recvfrom (udpdk_syscall.c:401-488) over the lane

@@ -155,13 +155,13 @@ def test_poll_rx_chunked_equals_one_piece(tmp_path, host_api):
     chunk k + 1's RX overlapping chunk k - 1's payload copy) gives every ring exactly what the
     one-piece poll gives it: the same datagrams in the same order, reassembled datagrams whose
     fragments straddle chunk cuts included, and the same bursts dropped where a ring fills (every
-    socket gets more than its 2047 entries). poll_chunk_mb = 1 cuts this ~9 MB batch into 8+
-    chunks; the default (128) polls it in one piece."""
+    socket gets more than its 2047 entries). poll_chunk_mb = 1 (and poll_chunk_min_avg = 0: its
+    frames are short) cuts this ~9 MB batch into 9 chunks; the default polls it in one piece."""
     from reasm_util import scenario
     frames = [f for fs, _ in scenario(11, n_batches=10, flows_per_batch=300, normal_per_batch=1800)
               for f in fs]
     one, st_one = _poll_and_drain(tmp_path, host_api, frames, "")
-    chk, st_chk = _poll_and_drain(tmp_path, host_api, frames, "poll_chunk_mb = 1\n")
+    chk, st_chk = _poll_and_drain(tmp_path, host_api, frames, "poll_chunk_mb = 1\npoll_chunk_min_avg = 0\n")
     assert st_chk == st_one
     assert [len(q) for q in chk] == [len(q) for q in one]
     assert sum(len(q) for q in one) > 4000 and all(len(q) >= 1000 for q in one)

@@ -176,7 +176,7 @@ def _admitted(idx, room):
     return acc
 
 
-@pytest.mark.parametrize("api", [1, 3, 8, 32, "poll_threads = 3\npoll_chunk_mb = 1\n"], indirect=True)
+@pytest.mark.parametrize("api", [1, 3, 8, 32, "poll_threads = 3\npoll_chunk_mb = 1\npoll_chunk_min_avg = 0\n"], indirect=True)
 def test_rx_many_sockets_over_poll_threads(api):
     """40 sockets, Zipf-skewed destination ports, some rings partly full before the poll: the
     admission and ring publication split the sockets over 1, 3, 8 or 32 threads (sockets

@@ -173,7 +173,9 @@ int main(int argc, char **argv)
     /* the reference's arrangement: poller beside the application */
     /* two batches share a socket's 2047-entry ring: at most 1023 datagrams per socket per batch
      * (a burst that does not fit is dropped whole, as flush_rx_queue does, and would never come) */
-    const int oreps = 2 * reps + 2;
+    /* BENCH_SOCK_OVERLAP=0: the sequential part only (a poll profile of it alone) */
+    const char *ov = getenv("BENCH_SOCK_OVERLAP");
+    const int oreps = ov && !atoi(ov) ? 0 : 2 * reps + 2;
     const uint32_t n_ov = n < 1023u * (uint32_t)S ? n : 1023u * (uint32_t)S;
     const uint64_t bytes_ov = n_ov < n ? off[n_ov] : bytes;
     struct poller P = {fr, bytes_ov, off, len, n_ov, oreps, 0, 0, 0};
@@ -204,7 +206,7 @@ int main(int argc, char **argv)
            "\"poll_ms\": %.3f, \"recv_ms\": %.3f, \"poll_mdgram_s\": %.2f, \"recv_mdgram_s\": %.2f, "
            "\"end_to_end_mdgram_s\": %.2f, \"end_to_end_frame_gbps\": %.2f, \"delivered_per_batch\": %.0f, "
            "\"payload_bytes_per_batch\": %.0f}\n",
-           (double)ogot / (o1 - o0) / 1e6, oreps, n, fsz ? argv[3] : "\"IMIX\"", S, reps, 1e3 * t_poll / reps, 1e3 * t_recv / reps,
+           oreps ? (double)ogot / (o1 - o0) / 1e6 : 0.0, oreps, n, fsz ? argv[3] : "\"IMIX\"", S, reps, 1e3 * t_poll / reps, 1e3 * t_recv / reps,
            dg / (t_poll / reps) / 1e6, dg / (t_recv / reps) / 1e6, dg / ((t_poll + t_recv) / reps) / 1e6,
            (double)bytes / ((t_poll + t_recv) / reps) / 1e9, dg, (double)pbytes / reps);
     udpdk_gpu_host_free(udpdk_gpu_context(), fr);

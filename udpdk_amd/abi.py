@@ -170,7 +170,8 @@ _PROTOS = {
                                          _P, _P, _P, C.c_uint32, C.POINTER(RxStats)]),
     "udpdk_gpu_pipe_wait": (C.c_int, [_P, C.c_int]),
     "udpdk_gpu_pipe_batch": (C.c_int, [_P, C.c_int, C.POINTER(RxBatch), C.POINTER(_P)]),
-    "udpdk_gpu_pipe_copy": (C.c_int, [_P, C.c_int, _P, _P, C.c_size_t]),
+    "udpdk_gpu_pipe_h2d": (C.c_int, [_P, C.c_int, _P, _P, C.c_size_t]),
+    "udpdk_gpu_pipe_d2h": (C.c_int, [_P, C.c_int, _P, _P, C.c_size_t]),
     "udpdk_gpu_pipe_gather_packed": (C.c_int, [_P, C.c_int, C.POINTER(RxBatch), _P, C.c_uint32, C.c_uint32,
                                                _P, C.POINTER(RxGather)]),
     "udpdk_gpu_rx_gather": (C.c_int, [_P, C.POINTER(RxBatch), _P, C.c_uint32, C.c_uint32,

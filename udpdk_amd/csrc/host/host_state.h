@@ -171,6 +171,7 @@ struct h_state {
     uint32_t *pc_meta, *pc_loff, *pc_lpkt, *pc_acc;
     uint64_t  pc_meta_cap, pc_loff_cap, pc_lpkt_cap, pc_acc_cap;
     uint32_t  poll_chunk_mb;
+    uint32_t  poll_chunk_min_avg;                /* ... for batches of at least this mean frame size */
     /* multi-device RX ([gpu] devices): n_shards > 1 splits every poll into contiguous shards over
      * the shard contexts; the context above (g_udpdk.gpu) keeps TX and the reassembly table */
     uint32_t  n_shards;

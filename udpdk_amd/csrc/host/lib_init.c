@@ -30,6 +30,7 @@ static void h_config_defaults(void)
     g_udpdk.poll_threads = 0;
     g_udpdk.host_copy_min = 0;         /* off: the GPU gather (tools/sock_tune.py) */
     g_udpdk.poll_chunk_mb = 128;       /* pipelined polls from 256 MB of frames (rx_poll.c) */
+    g_udpdk.poll_chunk_min_avg = 1024; /* ... of 1 KiB frames on average */
     g_udpdk.gpu_max_frames = 1u << 20;
     g_udpdk.gpu_max_lanes = UDPDK_MAX_SOCKETS;
     g_udpdk.frag_buckets = 0x1000;     /* NUM_FLOWS_DEF, udpdk_constants.h:32 */
@@ -220,6 +221,8 @@ static int h_load_ini(const char *path)
             g_udpdk.poll_threads = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "poll_chunk_mb")) {
             g_udpdk.poll_chunk_mb = (uint32_t)strtoul(v, NULL, 0);
+        } else if (!strcmp(section, "gpu") && !strcmp(k, "poll_chunk_min_avg")) {
+            g_udpdk.poll_chunk_min_avg = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "host_copy_min")) {
             g_udpdk.host_copy_min = (uint32_t)strtoul(v, NULL, 0);
         } else if (!strcmp(section, "gpu") && !strcmp(k, "frag_buckets")) {

@@ -45,16 +45,30 @@ static double h_prof_now(void)
 }
 #define PROF_T(v) const double v = h_prof_now()
 #define PROF_ADD(k, a, b) (g_prof[k] += (b) - (a))
+/* the pipelined form's phases, summed over its chunks */
+static double g_cprof[8];
+static const char *g_cprof_name[8] = {"rx_issue", "rx_wait", "gather_wait", "publish", "frag_pass",
+                                      "admission", "gather_issue", "calls"};
+#define CPROF_T(v) v = h_prof_now()
+#define CPROF_ADD(k, a, b) (g_cprof[k] += (b) - (a))
 __attribute__((visibility("hidden"))) void udpdk_poll_profile_dump(void)
 {
-    if (!g_prof[7]) return;
-    fprintf(stderr, "{\"udpdk_poll_profile_ms_per_call\": {");
-    for (int k = 0; k < 7; k++) fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", g_prof_name[k], g_prof[k] / g_prof[7]);
-    fprintf(stderr, "}, \"calls\": %.0f}\n", g_prof[7]);
+    if (g_prof[7]) {
+        fprintf(stderr, "{\"udpdk_poll_profile_ms_per_call\": {");
+        for (int k = 0; k < 7; k++) fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", g_prof_name[k], g_prof[k] / g_prof[7]);
+        fprintf(stderr, "}, \"calls\": %.0f}\n", g_prof[7]);
+    }
+    if (g_cprof[7]) {
+        fprintf(stderr, "{\"udpdk_poll_chunked_profile_ms_per_call\": {");
+        for (int k = 0; k < 7; k++) fprintf(stderr, "%s\"%s\": %.3f", k ? ", " : "", g_cprof_name[k], g_cprof[k] / g_cprof[7]);
+        fprintf(stderr, "}, \"calls\": %.0f}\n", g_cprof[7]);
+    }
 }
 #else
 #define PROF_T(v) do {} while (0)
 #define PROF_ADD(k, a, b) do {} while (0)
+#define CPROF_T(v) (void)(v)
+#define CPROF_ADD(k, a, b) do {} while (0)
 void udpdk_poll_profile_dump(void) {}
 #endif
 
@@ -964,7 +978,7 @@ static int h_shards_gather(uint32_t nad)
  * the bursts before it, as in the one-piece poll and the reference's burst loop. Chunks need
  * the batch's descriptors in range, ascending and disjoint (the network order a NIC ring gives);
  * others take the one-piece path. */
-#define H_CHUNKS_MAX 16u
+#define H_CHUNKS_MAX 32u
 
 struct h_chunk {
     uint32_t f0, n;              /* frames [f0, f0 + n) of the poll                              */
@@ -1019,12 +1033,12 @@ static int h_gather_chunk(udpdk_gpu_ctx *g, int pipe, const udpdk_rx_batch_t *b,
         memcpy(hl, acc, 4ull * cnt);
         memcpy(hl + cnt, offs, 4ull * cnt + 4);
         int rc;
-        if ((rc = udpdk_gpu_pipe_copy(g, pipe, dacc, hl, 8ull * cnt + 4)) ||
+        if ((rc = udpdk_gpu_pipe_h2d(g, pipe, dacc, hl, 8ull * cnt + 4)) ||
             (rc = udpdk_gpu_pipe_gather_packed(g, pipe, part ? rb : b, dacc, 0, cnt, dacc + cnt, &go)) ||
-            (rc = udpdk_gpu_pipe_copy(g, pipe, a->payload, gb->pay, bytes)) ||
-            (rc = udpdk_gpu_pipe_copy(g, pipe, a->len, gb->len, 4ull * cnt)) ||
-            (rc = udpdk_gpu_pipe_copy(g, pipe, a->src_ip, gb->sip, 4ull * cnt)) ||
-            (rc = udpdk_gpu_pipe_copy(g, pipe, a->src_port, gb->spt, 2ull * cnt))) {
+            (rc = udpdk_gpu_pipe_d2h(g, pipe, a->payload, gb->pay, bytes)) ||
+            (rc = udpdk_gpu_pipe_d2h(g, pipe, a->len, gb->len, 4ull * cnt)) ||
+            (rc = udpdk_gpu_pipe_d2h(g, pipe, a->src_ip, gb->sip, 4ull * cnt)) ||
+            (rc = udpdk_gpu_pipe_d2h(g, pipe, a->src_port, gb->spt, 2ull * cnt))) {
             errno = -rc;
             return -1;
         }
@@ -1038,8 +1052,14 @@ static int h_poll_chunked(const uint8_t *frames, uint64_t frames_bytes, const ui
                           const uint16_t *length, const uint32_t *ptype, uint32_t n, uint32_t lanes,
                           uint32_t maxfan, udpdk_rx_stats_t *stats_out)
 {
+    /* only batches of long frames ([gpu] poll_chunk_min_avg, default 1 KiB on average): there
+     * the poll is the two PCIe legs and overlapping them pays (1 M x 1500 B: 60 -> 40 ms); with
+     * short frames each socket's
+     * datagrams end up in one slab region per chunk, and recvfrom's loop over them lost more than
+     * the poll gained (1 M IMIX: poll 15.9 -> 12.7 ms, recvfrom 16.1 -> 24.0 ms) */
     const uint64_t chunk = (uint64_t)g_udpdk.poll_chunk_mb << 20;
     if (!chunk || g_udpdk.host_copy_min || frames_bytes < 2 * chunk || frames_bytes >= (1ull << 32) ||
+        frames_bytes < (uint64_t)n * g_udpdk.poll_chunk_min_avg ||
         n < 2u * H_BURST_SIZE || (uint64_t)n * maxfan > (1ull << 28) ||
         !h_desc_sorted(offset, length, n, frames_bytes))
         return 1;
@@ -1085,20 +1105,27 @@ static int h_poll_chunked(const uint8_t *frames, uint64_t frames_bytes, const ui
                                            (uint32_t)ck[k].lo, length + ck[k].f0, ptype ? ptype + ck[k].f0 : NULL, \
                                            ck[k].n, g_udpdk.pc_meta + ck[k].f0, g_udpdk.pc_loff + (uint64_t)L1 * (k), \
                                            g_udpdk.pc_lpkt + (uint64_t)ck[k].f0 * maxfan, ck[k].n * maxfan, &ck[k].st)
+    double t0 = 0, t1 = 0;
+    (void)t0; (void)t1;
     if ((rc = CK_ISSUE(0))) { errno = -rc; return -1; }
     for (uint32_t k = 0; k < K && !err; k++) {
+        CPROF_T(t0);
         if (k + 1 < K && (rc = CK_ISSUE(k + 1))) { err = -rc; break; }
+        CPROF_T(t1); CPROF_ADD(0, t0, t1);
         rc = udpdk_gpu_pipe_wait(g, h_pipe_of(k));
         if (rc && rc != -ENOSPC) { err = -rc; break; }
+        CPROF_T(t0); CPROF_ADD(1, t1, t0);
         /* chunk k - 1: its payloads are home, publish them */
         if (pend >= 0) {
             if ((rc = udpdk_gpu_pipe_wait(g, h_pipe_of((uint32_t)pend)))) { err = -rc; break; }
+            CPROF_T(t1); CPROF_ADD(2, t0, t1); t0 = t1;
             if (ad) atomic_store_explicit(&ad->refs, pnad, memory_order_relaxed);
             if (af) atomic_store_explicit(&af->refs, pnaf, memory_order_relaxed);
             struct h_pub P = {&A, ad, af, 0};
             h_pool_run(h_pub_job, &P);
             ad = af = NULL;
             pend = -1;
+            CPROF_T(t1); CPROF_ADD(3, t0, t1); t0 = t1;
         }
         const struct h_chunk *C = &ck[k];
         const uint32_t *loff = g_udpdk.pc_loff + (uint64_t)L1 * k, *lpkt = g_udpdk.pc_lpkt + (uint64_t)C->f0 * maxfan;
@@ -1111,6 +1138,7 @@ static int h_poll_chunked(const uint8_t *frames, uint64_t frames_bytes, const ui
         uint32_t nd = 0;
         const uint64_t nfrag = C->st.counters[UDPDK_V_FRAG];
         if (h_frag_pass(&staged, meta_dev, nfrag, lanes, maxfan, 1, &rb, &nd)) { err = errno; break; }
+        CPROF_T(t1); CPROF_ADD(4, t0, t1); t0 = t1;
         const uint32_t *floff = nd ? g_udpdk.fr_loff : NULL;
         const uint32_t cap = C->n * maxfan, D = loff[lanes], DF = nd ? floff[lanes] : 0u;
         int lanes_ok = loff[0] == 0u && D <= cap;
@@ -1143,6 +1171,7 @@ static int h_poll_chunked(const uint8_t *frames, uint64_t frames_bytes, const ui
         h_pool_run(h_adm_job, &A);
         g_udpdk.acc_do[nad] = (uint32_t)offd;
         g_udpdk.acc_fo[naf] = (uint32_t)offf;
+        CPROF_T(t1); CPROF_ADD(5, t0, t1); t0 = t1;
         if (nad + naf && h_gather_chunk(g, h_pipe_of(k), &staged, nad, &rb, naf, &ad, &af)) {
             if (errno != ENOBUFS) { err = errno; break; }
             /* slab budget exhausted by datagrams still queued: this chunk's bursts are dropped */
@@ -1153,6 +1182,7 @@ static int h_poll_chunked(const uint8_t *frames, uint64_t frames_bytes, const ui
             continue;
         }
         if (nad + naf) { pend = (int)k; pnad = nad; pnaf = naf; }
+        CPROF_T(t1); CPROF_ADD(6, t0, t1);
     }
 #undef CK_ISSUE
     if (!err && pend >= 0) {
@@ -1174,6 +1204,14 @@ static int h_poll_chunked(const uint8_t *frames, uint64_t frames_bytes, const ui
         return -1;
     }
     if (stats_out) *stats_out = tot;
+#ifdef UDPDK_POLL_PROFILE
+    {   /* the first call (allocations) is left out */
+        static int first = 1;
+        if (first) memset(g_cprof, 0, sizeof(g_cprof));
+        else g_cprof[7] += 1;
+        first = 0;
+    }
+#endif
     return 0;
 }
 

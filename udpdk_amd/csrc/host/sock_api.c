@@ -70,7 +70,9 @@ int h_ring_push_bulk(struct h_ring *r, const struct h_dgram *d, uint32_t n)
 }
 
 /* ---- payload slabs ------------------------------------------------------------------------ */
-#define H_ARENA_FREE_KEEP 8      /* free slabs kept for reuse; the rest go back to the runtime */
+#define H_ARENA_FREE_KEEP 32     /* free slabs kept for reuse; the rest go back to the runtime
+                                  * (a pipelined poll makes a slab per chunk: with 8 kept, every
+                                  * 1 M x 1500 B poll freed and re-pinned three 140 MB slabs) */
 
 /* frees a slab's memory; the budget accounting is the caller's */
 static void h_arena_destroy(struct h_arena *a)
@@ -92,16 +94,28 @@ static uint64_t h_arena_footprint(uint64_t cb, uint32_t cn) { return cb + 10ull 
 struct h_arena *h_arena_get(uint32_t n, uint64_t need)
 {
     pthread_mutex_lock(&g_udpdk.arena_lock);
-    struct h_arena **pp = &g_udpdk.arena_free, *a = NULL;
-    for (; *pp; pp = &(*pp)->next)
-        if ((*pp)->cap_bytes >= need && (*pp)->cap_n >= n) {
-            a = *pp;
-            *pp = a->next;
-            g_udpdk.arena_free_n--;
-            break;
-        }
-    const uint32_t cn = n < 4096 ? 4096 : n;
-    const uint64_t cb = need < ((uint64_t)cn * 64) ? (uint64_t)cn * 64 : need;
+    /* the smallest free slab that fits (a pipelined poll asks for one slab per chunk, of
+     * similar sizes: first fit handed a chunk a larger one that a later chunk then missed) */
+    struct h_arena **best = NULL, *a = NULL;
+    for (struct h_arena **pp = &g_udpdk.arena_free; *pp; pp = &(*pp)->next)
+        if ((*pp)->cap_bytes >= need && (*pp)->cap_n >= n && (!best || (*pp)->cap_bytes < (*best)->cap_bytes))
+            best = pp;
+    if (best) {
+        a = *best;
+        *best = a->next;
+        g_udpdk.arena_free_n--;
+    }
+    /* a new slab's capacity rounded up to 1/8 of its power of two (<= 12.5 % more), so the next
+     * poll's slightly larger chunk still fits it */
+    const uint32_t cn0 = n < 4096 ? 4096 : n;
+    const uint32_t cn = cn0 > (1u << 16) ? (cn0 + 8191u) & ~8191u : cn0;
+    uint64_t cb = need < ((uint64_t)cn * 64) ? (uint64_t)cn * 64 : need;
+    if (cb > (1ull << 20)) {
+        uint64_t p2 = 1ull << 20;
+        while (p2 <= cb / 2) p2 <<= 1;
+        const uint64_t g = p2 / 8;
+        cb = (cb + g - 1) / g * g;
+    }
     if (!a) {
         const uint64_t fp = h_arena_footprint(cb, cn);
         /* release free slabs (none fits) until the new one fits the budget */

@@ -891,8 +891,9 @@ int enqueue_host(udpdk_gpu_ctx *c, int pipe, const uint8_t *frames_host, uint64_
     int rc;
     // The frames are expected in pinned memory (DPDK hugepage mbufs registered with the
     // runtime); pageable input is copied into a pinned staging buffer first.
+    // (a chunk of a larger buffer: the allocation is looked up by the buffer's own start)
     hipPointerAttribute_t attr;
-    const bool pinned = n && hipPointerGetAttributes(&attr, frames_host) == hipSuccess &&
+    const bool pinned = n && hipPointerGetAttributes(&attr, frames_host - offset_base) == hipSuccess &&
                         attr.type == hipMemoryTypeHost;
     (void)hipGetLastError();
     if ((rc = ensure_dev(c, (void **)&P.st_frames_d, &P.st_frames_dcap, fb))) return rc;
@@ -1119,13 +1120,25 @@ int udpdk_gpu_pipe_batch(udpdk_gpu_ctx *c, int pipe, udpdk_rx_batch_t *batch, co
     return 0;
 }
 
-int udpdk_gpu_pipe_copy(udpdk_gpu_ctx *c, int pipe, void *dst, const void *src, size_t bytes)
+// (explicit directions: hipMemcpyDefault made the runtime block the caller on these D2H copies
+// into pinned slabs, 8-10 ms of a pipelined poll's issue time)
+static int pipe_copy(udpdk_gpu_ctx *c, int pipe, void *dst, const void *src, size_t bytes, hipMemcpyKind kind)
 {
     if (!c || pipe < 1 || pipe >= MAX_PIPES || ((!dst || !src) && bytes)) return -EINVAL;
     HIPC(c, hipSetDevice(c->device));
     c->pipes[pipe].dirty = true;
-    if (bytes) HIPC(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, c->pipes[pipe].stream));
+    if (bytes) HIPC(c, hipMemcpyAsync(dst, src, bytes, kind, c->pipes[pipe].stream));
     return 0;
+}
+
+int udpdk_gpu_pipe_h2d(udpdk_gpu_ctx *c, int pipe, void *dev, const void *host, size_t bytes)
+{
+    return pipe_copy(c, pipe, dev, host, bytes, hipMemcpyHostToDevice);
+}
+
+int udpdk_gpu_pipe_d2h(udpdk_gpu_ctx *c, int pipe, void *host, const void *dev, size_t bytes)
+{
+    return pipe_copy(c, pipe, host, dev, bytes, hipMemcpyDeviceToHost);
 }
 
 int udpdk_gpu_pipe_gather_packed(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt,
