@@ -422,6 +422,9 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
     }
 }
 
+__device__ __forceinline__ void run_insert(const ReasmArgs &a, unsigned long long *hset, uint32_t hmask,
+                                           uint32_t id, uint32_t src, uint32_t dst);
+
 // Over the fragment list (arrival order; F = counts[0], from the select): whether every flow key
 // forms a single run, and each position's record as reasm_prep writes it for that case (sorted
 // position = arrival position), so a grouped batch needs no reasm_prep pass over the frame
@@ -442,19 +445,46 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned lon
     for (uint32_t pb = blockIdx.x * RS_BLOCK + (threadIdx.x & ~63u); pb < F; pb += gridDim.x * RS_BLOCK) {
         const uint32_t p = pb + lane;
         const bool valid = p < F;
+        // lane 0's previous position (the wave before's last) is read beside its own, each level
+        // of the two chains (list, offset, header) in the same round trip: after the record's
+        // stores, those reads had three dependent round trips of their own
+        const bool prev = lane == 0u && valid && p > 0u;
         const uint32_t i = valid ? a.frag_list[p] : 0u;
-        const FragHdr h = frag_hdr(a, fr, i);
+        const uint32_t ip = prev ? a.frag_list[p - 1u] : 0u;
+        const uint32_t o = a.offset[i];
+        const uint32_t op = prev ? a.offset[ip] : 0u;
+        constexpr uint32_t OOR = 0x80000000u;
+        const uint32_t w16 = ld32(fr, o + 16), w20 = ld32(fr, o + 20);
+        FragHdr h;
+        h.src = ld32(fr, o + 26);
+        h.dst = ld32(fr, o + 30);
+        h.flen = a.length[i];
+        const uint32_t pw16 = ld32(fr, prev ? op + 16 : OOR), pws = ld32(fr, prev ? op + 26 : OOR),
+                       pwd = ld32(fr, prev ? op + 30 : OOR);
+        h.tl = bswap16(w16 & 0xFFFFu);
+        h.id = w16 >> 16;
+        h.ff = bswap16(w20 & 0xFFFFu);
         const uint32_t id = h.id, src = h.src, dst = h.dst;
-        if (valid) prep_record(a, crc_tab, p, i, h, false);
         uint32_t pid = __shfl_up(id, 1, 64), psrc = __shfl_up(src, 1, 64), pdst = __shfl_up(dst, 1, 64);
-        if (lane == 0u && valid && p > 0u) {
-            const uint32_t op = a.offset[a.frag_list[p - 1]];
-            pid = ld32(fr, op + 16) >> 16;
-            psrc = ld32(fr, op + 26);
-            pdst = ld32(fr, op + 30);
+        if (prev) {
+            pid = pw16 >> 16;
+            psrc = pws;
+            pdst = pwd;
         }
         const bool start = p == 0u || pid != id || psrc != src || pdst != dst;
-        if (!valid || !start) continue;
+        // the record's stores after the run test: its atomics' round trips would otherwise wait
+        // for them too (vmcnt counts stores, in order)
+        if (valid && start) run_insert(a, hset, hmask, id, src, dst);
+        if (valid) prep_record(a, crc_tab, p, i, h, false);
+    }
+}
+
+// A run's first fragment inserts its key's 64-bit fingerprint into the per-call set; meeting
+// the same fingerprint again marks the batch not grouped (counts[4]).
+__device__ __forceinline__ void run_insert(const ReasmArgs &a, unsigned long long *hset, uint32_t hmask,
+                                           uint32_t id, uint32_t src, uint32_t dst)
+{
+    {
         unsigned long long fp = ((unsigned long long)dst << 32 | src) * 0x9E3779B97F4A7C15ull;
         fp ^= (unsigned long long)(id + 1u) * 0xC2B2AE3D27D4EB4Full;
         fp ^= fp >> 29;
