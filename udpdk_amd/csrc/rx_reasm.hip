@@ -1410,13 +1410,15 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_count(const uint32_t *dk
     const uint32_t p0 = blockIdx.x * RS_CL + tid * (RS_CL / RS_BLOCK);
     uint32_t c = 0, by = 0;
     bool refuse = false;
+    // (every position's check, not only until the first refusal: a check that depended on the
+    // one before it serialised the positions' dependent loads, three round trips each)
 #pragma unroll
     for (uint32_t j = 0; j < RS_CL / RS_BLOCK; ++j) {
         const uint32_t q = p0 + j;
         if (q < F && dk[q] != RS_NONE) {
             ++c;
             by += done_bytes(done, q);
-            if (g.inplace && !refuse) refuse = !inplace_ok(g, done[q]);
+            if (g.inplace) refuse |= !inplace_ok(g, done[q]);
         }
     }
     if (__ballot(refuse) && lane == 0) atomicOr(g.refuse, 1u);    // rare: one atomic per wave
