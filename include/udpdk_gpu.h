@@ -64,8 +64,9 @@ enum udpdk_verdict {
     UDPDK_V_NOT_UDP   = 3, /* next_proto_id != 17 (poller.c:368-371)                             */
     UDPDK_V_NO_BIND   = 4, /* empty bind list for the raw dst port (poller.c:376-380)            */
     UDPDK_V_NO_MATCH  = 5, /* bind list present, no IP matched (poller.c:406-411)                */
-    UDPDK_V_TRUNC     = 6, /* IPv4 by ptype but shorter than the 42 B Eth/IPv4/UDP header
-                              (the reference would read past data_len; divergence)   */
+    UDPDK_V_TRUNC     = 6, /* IPv4 by ptype but shorter than the 42 B Eth/IPv4/UDP header, and
+                              not a fragment of >= 34 B (those are FRAG: a fragment needs only
+                              its IPv4 header); the reference would read past data_len        */
     UDPDK_V_BAD_DESC  = 7  /* offset + length beyond frames_bytes: nothing was read              */
 };
 #define UDPDK_N_VERDICTS 8

@@ -272,7 +272,14 @@ static uint32_t o_reassemble(const oracle_btable *bt, const uint8_t *frames,
     if (ptype) pt = ptype[i];
     else pt = len >= 14 ? ((f[12] == 0x08 && f[13] == 0x00) ? 0x211u : 0x1u) : 0u;
     if (!(pt & 0x10u)) { cnt[V_NOT_IPV4]++; return V_NOT_IPV4; }          /* :362-366 */
-    if (len < 42) { cnt[V_TRUNC]++; return V_TRUNC; }
+    /* a fragment needs only its IPv4 header to go to rte_ipv4_frag_reassemble_packet
+     * (poller.c:338-361): an unpadded frame of 34-41 B (a last fragment of 1-7 data bytes) is
+     * reassembled; any other frame shorter than the 42-byte Eth/IPv4/UDP header is TRUNC */
+    if (len < 34) { cnt[V_TRUNC]++; return V_TRUNC; }
+    /* rte_ipv4_frag_pkt_is_fragmented, poller.c:338 (MF flag or fragment offset) */
+    const uint16_t fo = (uint16_t)((f[20] << 8) | f[21]);
+    const int fragd = (fo & 0x2000u) || (fo & 0x1FFFu);
+    if (len < 42 && !fragd) { cnt[V_TRUNC]++; return V_TRUNC; }
 
     uint32_t w = 0;
     /* ip = (eth_hdr + 1): fixed 14 B offset, IHL never read (poller.c:336) */
@@ -281,9 +288,7 @@ static uint32_t o_reassemble(const oracle_btable *bt, const uint8_t *frames,
         if (o_fold(o_sum16(f + 14, 20)) == 0xFFFFu) w |= 1u << 4;
         else cnt[9]++;
     }
-    /* rte_ipv4_frag_pkt_is_fragmented, poller.c:338 (MF flag or fragment offset) */
-    uint16_t fo = (uint16_t)((f[20] << 8) | f[21]);
-    if ((fo & 0x2000u) || (fo & 0x1FFFu)) { cnt[V_FRAG]++; return w | V_FRAG; }
+    if (fragd) { cnt[V_FRAG]++; return w | V_FRAG; }
     /* is_udp_pkt, poller.c:300-303, :368-371 */
     if (f[23] != 17) { cnt[V_NOT_UDP]++; return w | V_NOT_UDP; }
 

@@ -43,9 +43,10 @@ def wire(f):
     return f if len(f) >= 60 else f + bytes(60 - len(f))
 
 
-def batch(frames, align=1):
-    """Pack frames back to back: (buffer u8 with tailroom, offset u32, length u16)."""
-    frames = [wire(f) for f in frames]
+def batch(frames, align=1, pad=True):
+    """Pack frames back to back: (buffer u8 with tailroom, offset u32, length u16). pad=False keeps
+    short frames as they are (a 1-7 byte last fragment is a 35-41 B frame)."""
+    frames = [wire(f) if pad else f for f in frames]
     off, pos = [], 0
     for f in frames:
         off.append(pos)

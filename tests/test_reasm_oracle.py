@@ -9,14 +9,15 @@ import numpy as np
 import pytest
 
 import oracle as O
+from udpdk_amd import abi
 from reasm_util import batch, frames_of, ip_frame, raw_ip, split, udp_datagram, verdicts
 
 SRC = raw_ip("172.31.100.2")
 DST = raw_ip("172.31.100.1")
 
 
-def _run(t, frames, tms=0):
-    buf, off, ln = batch(frames)
+def _run(t, frames, tms=0, pad=True):
+    buf, off, ln = batch(frames, pad=pad)
     meta = verdicts(buf, off, ln)
     out, oo, ol, og, st = t.reassemble(buf, off, ln, meta, tms)
     return frames_of(out, oo, ol), og.tolist(), st
@@ -57,6 +58,31 @@ def test_tx_fragments_reassemble_to_the_sent_frame(mtu):
 
 
 O_MAC = (bytes.fromhex("6805ca95f8ec"), bytes.fromhex("6805ca95fa64"))
+
+
+def test_short_fragment_frames():
+    """An unpadded frame of 34-41 B holds a whole IPv4 header but not a UDP one: a fragment is
+    handed to reassembly on its IPv4 header alone (poller.c:338-361: rte_ipv4_frag_pkt_is_fragmented
+    before any UDP field is read), anything else is TRUNC, and a 33 B frame is TRUNC either way.
+    Datagrams whose last fragment carries 1-7 bytes then come back whole."""
+    d = udp_datagram(0x1027, 0x1127, bytes(range(19)))          # 27 B: fragments of 8, 8, 8 + 3
+    fs = split(SRC, DST, 7, d, [8, 8, 11])
+    assert [len(f) for f in fs] == [42, 42, 45]
+    fs = split(SRC, DST, 7, d, [8, 16, 3])
+    assert len(fs[2]) == 37
+    whole = ip_frame(SRC, DST, 8, 0, b"\0" * 5, False)           # 39 B, not a fragment
+    buf, off, ln = batch(fs + [whole, fs[2][:33]], pad=False)
+    v = verdicts(buf, off, ln) & 0xF
+    assert v.tolist() == [abi.V_FRAG] * 3 + [abi.V_TRUNC, abi.V_TRUNC]
+    got, _, st = _run(O.FragTable(), fs, pad=False)
+    assert st["done"] == 1 and got[0][34:] == d
+    for L in (1473, 1474, 1479, 2953, 2959):                     # last pieces of 1-7 bytes
+        pay = bytes(range(256)) * (L // 256) + bytes(L % 256)
+        fr = O.tx_frame(O_MAC[0], O_MAC[1], SRC, 1, 0, 0x1027, DST, 0x1127, pay)
+        pieces = O.tx_fragment(fr, 1500)
+        assert 35 <= len(pieces[-1]) <= 41
+        got, _, st = _run(O.FragTable(), pieces, pad=False)
+        assert st["done"] == 1 and _same_but_cksum(got[0], fr)
 
 
 def test_in_and_out_of_order_and_across_calls():

@@ -842,6 +842,9 @@ rx_classify(RxArgs a)
             const uint32_t frag = ((g[2] & 0xFFu) << 8) | ((g[2] >> 8) & 0xFFu);
             const bool l3 = ipv4 && len >= 42u;
             const bool fragd = (frag & 0x3FFFu) != 0u;                // udpdk_poller.c:338
+            // a fragment needs only its IPv4 header (poller.c:338-361): 34-41 B fragments reassemble
+            const bool l3h = ipv4 && len >= 34u;
+            const bool hdr = l3 || (l3h && fragd);                    // IPv4 flags and counters
             const bool not_udp = (g[2] >> 24) != 17u;                 // udpdk_poller.c:368-371
             const bool is_udp = l3 && !fragd && !not_udp;
             const uint32_t dport = g[6] & 0xFFFFu;                   // poller.c:372
@@ -900,13 +903,14 @@ rx_classify(RxArgs a)
                                                                        : UDPDK_UDP_CSUM_OK;
             const uint32_t pre = !good ? UDPDK_V_BAD_DESC
                                : !ipv4 ? UDPDK_V_NOT_IPV4
-                               : !l3 ? UDPDK_V_TRUNC
+                               : !l3h ? UDPDK_V_TRUNC
                                : fragd ? UDPDK_V_FRAG
+                               : !l3 ? UDPDK_V_TRUNC
                                : not_udp ? UDPDK_V_NOT_UDP : 0xFFu;       // 0xFF: UDP, demux pending
-            const uint32_t l3f = l3 ? ((ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8) : 0u;
+            const uint32_t l3f = hdr ? ((ip_ok ? 1u : 0u) << 4 | (ihl_ne5 ? 1u : 0u) << 8) : 0u;
             const uint32_t udpf = is_udp ? (state << 5 | (len_bad ? 1u : 0u) << 7) : 0u;
             // (pending frames count their UDP state in the tail pass)
-            acc_f0 += (l3 && !ip_ok ? 1u : 0u) | (l3 && ihl_ne5 ? 0x100u : 0u) |
+            acc_f0 += (hdr && !ip_ok ? 1u : 0u) | (hdr && ihl_ne5 ? 0x100u : 0u) |
                       (is_udp && state == UDPDK_UDP_CSUM_OK ? 0x10000u : 0u) |
                       (is_udp && state == UDPDK_UDP_CSUM_BAD ? 0x1000000u : 0u);
             acc_f1 += (is_udp && state == UDPDK_UDP_CSUM_NONE ? 1u : 0u) | (is_udp && len_bad ? 0x100u : 0u);
