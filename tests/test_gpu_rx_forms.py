@@ -170,3 +170,37 @@ def test_configs_forms(form_ctx, cfg):
     for _ in range(2):
         want, got = _run(form_ctx, w.batch, w.port_lists(), w.n_sockets)
         _same(want, got, w.name)
+
+
+@pytest.mark.parametrize("group,hist_cap", [(1, 0), (2048, 0), (4096, 1 << 16), (8192, 1 << 16),
+                                            (16384, 1 << 16), (16384, 0)])
+def test_scatter_groups(group, hist_cap):
+    """rx_scatterw taking G consecutive classify tiles per workgroup (UDPDK_SCATTER_GROUP_FRAMES
+    frames at most; UDPDK_SCATTER_MIN_WG = 1 so small batches group too), with the 16-wave form
+    past 8192 frames and the column scan writing only the groups' base rows; small histogram caps
+    give many 1024-frame tiles and ragged last groups. Multi-lane batches (IMIX over 1024 ports,
+    Zipf over 4096, a mixed batch with every verdict) equal the oracle bit for bit."""
+    env = {"UDPDK_SCATTER_GROUP_FRAMES": str(group), "UDPDK_SCATTER_MIN_WG": "1"}
+    if hist_cap:
+        env["UDPDK_RX_HIST_CAP"] = str(hist_cap)
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        ctx = abi.GpuContext(0, max_frames=1 << 20, max_lanes=4096)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        for cfg, n in ((4, 50001), (5, 300000), (5, 1 << 20)):
+            w = F.config_batch(cfg, n=n)
+            _same(*_run(ctx, w.batch, w.port_lists(), w.n_sockets, cap=n), f"group {group} {w.name}")
+        b = F.mixed_batch(7, 30000, [10001, 10002, 10003, 10004, 10005], [9, 20000, 65535],
+                          ["172.31.100.1", "172.31.100.9"])
+        lists = {abi.raw_port(10001): [(0, 0, 0)], abi.raw_port(10002): [(abi.raw_ip("172.31.100.1"), 1, 0)],
+                 abi.raw_port(10003): [(abi.raw_ip("172.31.100.9"), 3, 0)], abi.raw_port(10004): [(0, 4, 0)]}
+        _same(*_run(ctx, b, lists, 8, cap=4 * b.n), f"group {group} mixed")
+    finally:
+        ctx.close()

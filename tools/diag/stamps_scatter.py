@@ -10,14 +10,15 @@ sys.path.insert(0, ROOT)
 import numpy as np
 from udpdk_amd import abi, frames as F
 
-PH = ["lane_cursors", "woff zero", "pass0 count", "slice offsets", "pass1 place (ranks)", "staged key-order write-out"]
+PH = ["lane_cursors", "woff zero", "pass0 count", "slice offsets", "pass1 place (ranks)", "staged: global stores",
+      "staged: key starts into LDS", "staged: key-order index + position", "staged: pairs into LDS"]
 L = abi.lib()
 L.udpdk_gpu_debug_buffer.argtypes = [C.c_void_p, C.c_void_p]
 ctx = abi.GpuContext(0, max_frames=1 << 22, max_lanes=4096)
 NB = (2 * 8192 + 8192) * 16 * 8
-dbg = ctx.alloc(NB)
-L.udpdk_gpu_debug_buffer(ctx.handle, C.c_void_p(dbg.ptr))
 for cfg in (5, 4):
+    dbg = ctx.upload(np.zeros(NB // 8, np.uint64))
+    L.udpdk_gpu_debug_buffer(ctx.handle, C.c_void_p(dbg.ptr))
     w = F.config_batch(cfg)
     ctx.upload_snapshot(abi.snapshot_from_lists(w.port_lists(), w.n_sockets))
     db = abi.rx_upload(ctx, w.batch.frames, w.batch.offset, w.batch.length)
@@ -28,6 +29,10 @@ for cfg in (5, 4):
     abi.rx_stats(ctx)
     _, tiles = abi.geometry(w.batch.n, w.n_sockets)
     raw = ctx.download(dbg, np.uint64, (2 * 8192 + tiles) * 16)[2 * 8192 * 16:].reshape(tiles, 16)
+    # a scatter workgroup may take several classify tiles: keep the rows its workgroups wrote
+    # (row = scatter tile; the rows past the scatter grid stay zero in the fresh buffer)
+    raw = raw[raw[:, 13] != 0]
+    tiles = len(raw)
     d = raw.astype(np.float64)
     print(f"{w.name} tiles={tiles}")
     for k, name in enumerate(PH):

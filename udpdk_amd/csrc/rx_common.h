@@ -203,6 +203,7 @@ struct ScanArgs {
     uint32_t *ticket;
     uint32_t epoch;
     uint32_t hist16;
+    uint32_t row_mask;    // rx_scan_cols: base rows written only for tiles t with t & row_mask == 0
 };
 
 // rx_scan_cols: one launch, workgroup = a block of 2^lb lanes x every tile; each thread keeps up
@@ -227,6 +228,7 @@ struct ScatterArgs {
     uint32_t lane_mask;
     uint32_t key_bits;
     uint32_t lane_cap;
+    uint32_t row_step;         // base row of scatter tile s: s x row_step (classify tiles per scatter tile)
     unsigned long long *dbg;   // diagnostic stamps (UDPDK_STAMPS builds), may be null
 };
 
@@ -300,17 +302,28 @@ __global__ void rx_scan_reduce(ScanArgs a);
 __global__ void rx_scan_top(ScanArgs a, uint32_t n_part);
 __global__ void rx_scan_down(ScanArgs a);
 __global__ void rx_scatter(ScatterArgs a);
-__global__ void rx_scatterw(ScatterArgs a);
+template <uint32_t W> __global__ void rx_scatterw(ScatterArgs a);
 #ifndef UDPDK_SCATTER_WAVES
 #define UDPDK_SCATTER_WAVES 8
 #endif
 constexpr uint32_t SCATTER_WAVES = UDPDK_SCATTER_WAVES;   // rx_scatterw workgroup: waves per tile
 constexpr uint32_t SCATTERW_MAX_LANES = 4096;   // rx_scatterw LDS: (4 + 2 x 8) x lanes bytes
-__host__ __device__ constexpr uint32_t scatterw_lds_bytes(uint32_t n_lanes)
+constexpr uint32_t SCATTERW_MV = RX_TILE_MAX / (64 * SCATTER_WAVES);   // verdict words per lane
+// rx_scatterw takes G consecutive classify tiles as one scatter tile (the base row of its first):
+// fewer (tile, lane) pieces, so fewer partly written lane_pkt lines (config 5: 1.07 M line
+// touches at 8192 frames, 0.80 M at 16384), up to this many frames, 16 waves past 8192
+#ifndef UDPDK_SCATTER_GROUP_FRAMES
+#define UDPDK_SCATTER_GROUP_FRAMES 16384u
+#endif
+#ifndef UDPDK_SCATTER_MIN_WG
+#define UDPDK_SCATTER_MIN_WG 256u               // ... while the grid keeps this many workgroups
+#endif
+__host__ __device__ constexpr uint32_t scatterw_lds_bytes(uint32_t n_lanes, uint32_t waves = SCATTER_WAVES)
 {
-    // cursors + per-wave slice offsets (u16): 80 KiB at 4096 lanes, so two workgroups share a
-    // CU's 160 KiB
-    return 4u * n_lanes + 2u * SCATTER_WAVES * n_lanes;
+    // cursors (at least one word per wave: the key scan's wave totals) + per-wave slice offsets
+    // (u16): 80 KiB at 4096 lanes and 8 waves, so two workgroups share a CU's 160 KiB; 144 KiB at
+    // 16 waves (one per CU)
+    return 4u * (n_lanes > waves ? n_lanes : waves) + 2u * waves * n_lanes;
 }
 constexpr int SCATTER1_BLOCK = 256;             // rx_scatter: prologue by 4 waves, walk by wave 0
 __host__ __device__ constexpr uint32_t scatter1_lds_bytes(uint32_t n_lanes)

@@ -47,15 +47,17 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_wave_barrier();
 }
 
-// Inclusive prefix sum across the wave.
+// Inclusive prefix sum across the wave, on the DPP network (row shifts + row broadcasts: six
+// VALU ops; the __shfl_up form was six ds_bpermute round trips through the LDS pipeline, which
+// the LDS-bound scatter paid for in every scan). Every lane must be active.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
 {
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(v, d, 64);
-        if (lane >= (uint32_t)d) v += y;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
     return v;
 }
 
@@ -186,17 +188,8 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi, int base)
     return hm & ~lm;
 }
 
-// Inclusive wave64 prefix sum on the DPP network (row shifts + row broadcasts; no LDS traffic).
-__device__ __forceinline__ uint32_t scan_dpp(uint32_t v)
-{
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
-    return v;
-}
+// Inclusive wave64 prefix sum on the DPP network (no LDS traffic).
+__device__ __forceinline__ uint32_t scan_dpp(uint32_t v) { return wave_incl_scan(v); }
 
 // Inclusive wave64 prefix maximum on the DPP network (same shifts as scan_dpp).
 __device__ __forceinline__ uint32_t max_scan_dpp(uint32_t v)
@@ -1476,7 +1469,7 @@ rx_scan_cols(ScanArgs a, uint32_t lb)
     uint32_t *out = a.base + lanei;
 #pragma unroll
     for (uint32_t k = 0; k < SCAN_COLS_TPT; ++k) {
-        if (ok && t0 + k < t1) out[(size_t)(t0 + k) * S] = run;
+        if (ok && t0 + k < t1 && ((t0 + k) & a.row_mask) == 0u) out[(size_t)(t0 + k) * S] = run;
         run += v[k];
     }
 }
@@ -1563,7 +1556,7 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n)
 __device__ __forceinline__ void lane_cursors(const ScatterArgs &a, uint32_t tile, uint32_t *cur)
 {
     const uint32_t tid = threadIdx.x, NT = blockDim.x, S = a.n_lanes;
-    const uint32_t *base = a.base + (size_t)tile * S;
+    const uint32_t *base = a.base + (size_t)tile * a.row_step * S;
     constexpr uint32_t CU = 8;
     for (uint32_t k0 = tid; k0 < S; k0 += NT * CU) {
         uint32_t vy[CU];
@@ -1588,18 +1581,22 @@ __device__ __forceinline__ void lane_cursors(const ScatterArgs &a, uint32_t tile
 // program order, so the returns number a key's frames of the slice in arrival order. (The first
 // form ranked lanes by a wave multi-split over the key bits, 12 ballots per 64 frames at 4096
 // lanes: 11 us per pass at config 5, instruction-bound; the atomics make a pass a few
-// instructions per 64 frames.) Counters hold two waves each, 16 bits per wave (a tile has
-// <= 8192 frames, so neither half can carry into the other).
+// instructions per 64 frames.) Counters hold two waves each, 16 bits per wave (a scatter tile
+// has <= 16384 frames, so neither half can carry into the other).
 // LDS: 4 x n_lanes (cursors) + 2 x SCATTER_WAVES x n_lanes bytes.
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64 * SCATTER_WAVES)
+template <uint32_t W>
+__global__ void __launch_bounds__(64 * W)
 rx_scatterw(ScatterArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t smw[];
     const uint32_t S = a.n_lanes;
-    constexpr uint32_t W = SCATTER_WAVES;
-    uint32_t *cur = smw;                                               // [S]
-    uint32_t *cnt = smw + S;                                           // [W / 2][S] packed pairs
+    // cursors [max(S, W)]: the first W words carry the key scan's wave totals until pass 2 (their
+    // cursors wait in registers), so the LDS stays at 80 KiB for 8 waves at 4096 lanes (two
+    // workgroups per CU)
+    const uint32_t SC = S > W ? S : W;
+    uint32_t *cur = smw;
+    uint32_t *cnt = smw + SC;                                          // [W / 2][S] packed pairs
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t tile = xcd_tile(blockIdx.x, a.n_tiles);
     const uint32_t t1 = min(a.n, (tile + 1) * a.tile_frames);
@@ -1608,10 +1605,11 @@ rx_scatterw(ScatterArgs a)
     const uint32_t plast = a.n - 1u;
     uint32_t *mine = cnt + (w >> 1) * S;
     const uint32_t inc = (w & 1u) ? 0x10000u : 1u, sh = (w & 1u) * 16u;
-    // the wave's whole slice of verdict words in registers (<= RX_TILE_MAX / W frames = 16 per
-    // lane), loaded once for both passes (no load in the counting or the placing loop) and
-    // issued first, so they are in flight during the cursor prologue
-    constexpr uint32_t MV = RX_TILE_MAX / (64 * SCATTER_WAVES);
+    // the wave's whole slice of verdict words in registers (<= 16 per lane: tile_frames <=
+    // 64 W SCATTERW_MV, checked by the host), loaded once for both passes (no load in the
+    // counting or the placing loop) and issued first, so they are in flight during the cursor
+    // prologue
+    constexpr uint32_t MV = SCATTERW_MV;
     uint32_t mv[MV];
 #pragma unroll
     for (uint32_t i = 0; i < MV; ++i) {
@@ -1634,14 +1632,15 @@ rx_scatterw(ScatterArgs a)
 #endif
     // the cursors' loads (up to 8 per thread) in flight while the counters are zeroed (16-byte
     // LDS stores), then one barrier (the zeroing waited behind the cursor round trip before)
+    uint32_t cur_lo;
     {
-        const uint32_t *brow = a.base + (size_t)tile * S;
+        const uint32_t *brow = a.base + (size_t)tile * a.row_step * S;
         constexpr uint32_t CU = 8;
         const uint32_t NT = 64 * W;
         uint32_t vy[CU];
 #pragma unroll
         for (uint32_t u = 0; u < CU; ++u) vy[u] = brow[min(tid + u * NT, S - 1u)];
-        if ((S & 3u) == 0u) {                     // cnt = smw + S is 16-byte aligned
+        if ((SC & 3u) == 0u) {                    // cnt = smw + SC is 16-byte aligned
             uint4 *c4 = reinterpret_cast<uint4 *>(cnt);
             for (uint32_t k = tid; k < (W / 2) * S / 4; k += NT) c4[k] = make_uint4(0, 0, 0, 0);
         } else {
@@ -1649,7 +1648,8 @@ rx_scatterw(ScatterArgs a)
         }
 #pragma unroll
         for (uint32_t u = 0; u < CU; ++u)
-            if (tid + u * NT < S) cur[tid + u * NT] = vy[u];
+            if (tid + u * NT < S && (u > 0 || tid >= W)) cur[tid + u * NT] = vy[u];
+        cur_lo = vy[0];
         for (uint32_t k0 = tid + NT * CU; k0 < S; k0 += NT) cur[k0] = brow[k0];   // S > 4096: none
     }
     SSTAMP(0);
@@ -1665,31 +1665,85 @@ rx_scatterw(ScatterArgs a)
     }
     __syncthreads();
     SSTAMP(2);
-    // slice offsets: each wave's counts become the sum of the earlier slices' counts
-    for (uint32_t k = tid; k < S; k += 64 * W) {
-        uint32_t c = 0;
+    // slice offsets: each wave's counts become the sum of the earlier slices' counts. Wave w
+    // takes the contiguous keys [w KW, (w + 1) KW), lane l the keys w KW + 64 j + l (conflict-
+    // free LDS rows), and keeps each key's tile total: their exclusive scan in key order (a wave
+    // scan per j plus the earlier waves' totals) is each key's start in the tile's key-ordered
+    // staging, held in registers until pass 2 has released the counter region. (The former
+    // separate pass re-read the last pair's totals with 8 consecutive keys per thread: 8-way bank
+    // conflicts and two more barriers, 6000 cycles of a 16-wave workgroup at config 5.)
+    constexpr uint32_t KPT = SCATTERW_MAX_LANES / (64 * W);           // keys per lane
+    const uint32_t KW = (S + 64 * W - 1) / (64 * W) * 64;               // keys per wave
+    uint32_t *wtot = cur;                                               // [W] wave totals
+    uint32_t kt[KPT] = {};
+    {
+        // every count the lane needs in flight at once (clamped addresses, masked values): one
+        // LDS round trip instead of one per (key, wave pair). The j loops end at the wave's keys
+        // (uniform), so the reads of one j are straight-line code.
+        uint32_t cv[KPT][W / 2];
 #pragma unroll
-        for (uint32_t j = 0; j < W / 2; ++j) {
-            const uint32_t v = cnt[j * S + k];
-            const uint32_t lo = c, hi = c + (v & 0xFFFFu);
-            cnt[j * S + k] = lo | (hi << 16);
-            c = hi + (v >> 16);
+        for (uint32_t j = 0; j < KPT; ++j) {
+            if (j * 64 >= KW) break;
+            const uint32_t k = min(w * KW + j * 64 + lane, S - 1u);
+#pragma unroll
+            for (uint32_t jj = 0; jj < W / 2; ++jj) cv[j][jj] = cnt[jj * S + k];
         }
+        __builtin_amdgcn_sched_barrier(0);         // all reads issued before the first use
+        uint32_t run = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; ++j) {
+            if (j * 64 >= KW) break;
+            const uint32_t k = w * KW + j * 64 + lane;
+            const bool in = k < S;
+            uint32_t c = 0;
+#pragma unroll
+            for (uint32_t jj = 0; jj < W / 2; ++jj) {
+                const uint32_t v = in ? cv[j][jj] : 0u;
+                const uint32_t lo = c, hi = c + (v & 0xFFFFu);
+                cv[j][jj] = lo | (hi << 16);
+                c = hi + (v >> 16);
+            }
+            if (in) {
+#pragma unroll
+                for (uint32_t jj = 0; jj < W / 2; ++jj) cnt[jj * S + k] = cv[j][jj];
+            }
+            const uint32_t incl = wave_incl_scan(c);
+            kt[j] = run + incl - c;
+            run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        if (lane == 0) wtot[w] = run;
     }
     __syncthreads();
+    uint32_t nd = 0;                                                    // the tile's deliveries
+    {
+        uint32_t before = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < W; ++j) {
+            const uint32_t t = wtot[j];
+            before += j < w ? t : 0u;
+            nd += t;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < KPT; ++j) kt[j] += before;
+    }
     SSTAMP(3);
     // pass 2: placement. Staged when the tile's (frame, position) pairs fit the counter region:
     // every delivery's rank within its key comes from the atomics; the tile's deliveries are then
-    // laid out in LDS in key order (a block scan of the per-key totals gives each key's start)
-    // and written out linearly, so a wave's 64 stores fill runs of consecutive lane_pkt words (one
-    // run per key of the tile) instead of 64 scattered words (config 5: rx_scatterw 24.5 -> 22.5
-    // us). Otherwise each delivery stores its own word.
+    // laid out in LDS in key order (each key's start from the scan above) and written out
+    // linearly, so a wave's 64 stores fill runs of consecutive lane_pkt words (one run per key of
+    // the tile) instead of 64 scattered words (config 5: rx_scatterw 24.5 -> 22.5 us). Otherwise
+    // each delivery stores its own word (and needs every cursor now).
     const uint32_t T = a.tile_frames;
 #ifdef UDPDK_DIAG_SCATTER_DIRECT
     const bool staged = false;
 #else
     const bool staged = (S & 1u) == 0u && 8u * T <= 4u * (W / 2) * S;   // 8-byte pairs in cnt
 #endif
+    if (!staged) {
+        __syncthreads();                                               // wave totals read
+        if (tid < W && tid < S) cur[tid] = cur_lo;
+        __syncthreads();
+    }
     uint32_t kr[MV];                                                   // rank | key << 16
 #pragma unroll
     for (uint32_t i = 0; i < MV; ++i) {
@@ -1710,38 +1764,17 @@ rx_scatterw(ScatterArgs a)
     }
     SSTAMP(4);
     if (staged) {
-        // the tile's per-key totals: the last wave pair's upper cursors (its end = the tile's)
+        // every wave's pass 2 is done with the counters: the key starts go where they were
         __syncthreads();
-        constexpr uint32_t KPT = 8;                                   // keys per thread per pass
         uint32_t *lex = cnt;                                           // [S] key start in the tile
-        uint32_t *wsum = cnt + S;                                      // [W] wave totals
-        uint32_t carry = 0;
-        for (uint32_t k0 = 0; k0 < S; k0 += KPT * 64 * W) {
-            uint32_t tc[KPT], sum = 0;
-            const uint32_t kb = k0 + tid * KPT;
 #pragma unroll
-            for (uint32_t j = 0; j < KPT; ++j) {
-                tc[j] = kb + j < S ? cnt[(W / 2 - 1) * S + kb + j] >> 16 : 0u;
-                sum += tc[j];
-            }
-            const uint32_t winc = wave_incl_scan(sum);
-            if (lane == 63) wsum[w] = winc;
-            __syncthreads();                                           // (every tc read is done)
-            uint32_t before = carry + winc - sum, all = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < W; ++j) {
-                before += j < w ? wsum[j] : 0u;
-                all += wsum[j];
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < KPT; ++j) {
-                if (kb + j < S) lex[kb + j] = before;
-                before += tc[j];
-            }
-            carry += all;
-            __syncthreads();
+        for (uint32_t j = 0; j < KPT; ++j) {
+            const uint32_t k = w * KW + j * 64 + lane;
+            if (j * 64 < KW && k < S) lex[k] = kt[j];
         }
-        const uint32_t nd = carry;                                     // the tile's deliveries
+        if (tid < W && tid < S) cur[tid] = cur_lo;                     // wave totals read long ago
+        __syncthreads();
+        SSTAMP(6);
         // each delivery's place in key order and its lane position into registers first (lex
         // is read), then (frame, position) pairs into LDS over the whole counter region
         uint32_t li[MV], ps[MV];
@@ -1756,6 +1789,7 @@ rx_scatterw(ScatterArgs a)
             }
         }
         __syncthreads();
+        SSTAMP(7);
         uint2 *pp = reinterpret_cast<uint2 *>(cnt);                    // [T] (frame, position)
 #pragma unroll
         for (uint32_t i = 0; i < MV; ++i) {
@@ -1763,6 +1797,7 @@ rx_scatterw(ScatterArgs a)
             if (li[i] != 0xFFFFFFFFu) pp[li[i]] = make_uint2(wb + i * 64 + lane, ps[i]);
         }
         __syncthreads();
+        SSTAMP(8);
         for (uint32_t i = tid; i < nd; i += 64 * W) {
             const uint2 e = pp[i];
             if (e.y < a.lane_cap) a.lane_pkt[e.y] = e.x;
@@ -1778,6 +1813,9 @@ rx_scatterw(ScatterArgs a)
 #endif
 #undef SSTAMP
 }
+
+template __global__ void rx_scatterw<SCATTER_WAVES>(ScatterArgs a);
+template __global__ void rx_scatterw<2 * SCATTER_WAVES>(ScatterArgs a);
 
 // ------------------------------------------------------------------------------------------
 // rx_scatter: stable per-lane compaction, one wave per tile

@@ -117,6 +117,8 @@ struct udpdk_gpu_ctx {
     int force_mr = -1;             // UDPDK_RX_MR=0/1 (tests, A/B): the round-ahead descriptor form
     bool trace = false;            // UDPDK_RX_TRACE (diagnostic): the form of every call on stderr
     bool no_inline = false;        // UDPDK_RX_NO_INLINE (tests, A/B): always the port-table loads
+    uint32_t scatter_group_frames = UDPDK_SCATTER_GROUP_FRAMES;   // UDPDK_SCATTER_GROUP_FRAMES (tests, A/B)
+    uint32_t scatter_min_wg = UDPDK_SCATTER_MIN_WG;               // UDPDK_SCATTER_MIN_WG (tests, A/B)
     bool have_snapshot = false;
 
     // RX workspace, one set per pipe
@@ -306,6 +308,8 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
     c->trace = getenv("UDPDK_RX_TRACE") != nullptr;
     c->no_inline = getenv("UDPDK_RX_NO_INLINE") != nullptr;
     if (const char *e = getenv("UDPDK_RX_MR")) c->force_mr = atoi(e) ? 1 : 0;
+    if (const char *e = getenv("UDPDK_SCATTER_GROUP_FRAMES")) c->scatter_group_frames = (uint32_t)atoi(e);
+    if (const char *e = getenv("UDPDK_SCATTER_MIN_WG")) c->scatter_min_wg = (uint32_t)atoi(e);
     if (const char *e = getenv("UDPDK_RX_TAILG")) {
         const int g = atoi(e);
         if (g == 1 || g == 2) c->force_tailg = g;
@@ -364,8 +368,11 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
                                 cls_lds) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)scatter1_lds_bytes(UDPDK_GPU_MAX_LANES)) != hipSuccess) break;
-        if (hipFuncSetAttribute((const void *)rx_scatterw, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void *)rx_scatterw<SCATTER_WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 scatterw_lds_bytes(SCATTERW_MAX_LANES)) != hipSuccess) break;
+        if (hipFuncSetAttribute((const void *)rx_scatterw<2 * SCATTER_WAVES>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                scatterw_lds_bytes(SCATTERW_MAX_LANES, 2 * SCATTER_WAVES)) != hipSuccess) break;
         // rx_scan_top's lane totals: 4 B per lane, up to UDPDK_GPU_MAX_LANES (64 KiB)
         if (hipFuncSetAttribute((const void *)rx_scan_top, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 4 * UDPDK_GPU_MAX_LANES) != hipSuccess) break;
@@ -746,8 +753,25 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
         return 0;
     }
 
+    // rx_scatterw: G classify tiles per scatter workgroup while the scatter tile stays within
+    // UDPDK_SCATTER_GROUP_FRAMES, its (frame, position) pairs fit the LDS counter region (8 B each
+    // in 2 W S bytes) and the grid keeps UDPDK_SCATTER_MIN_WG workgroups; the column scan then
+    // writes only the base rows of each group's first tile
+    const bool scatterw = c->max_fanout <= 1 && S <= SCATTERW_MAX_LANES;
+    uint32_t G = 1, W = SCATTER_WAVES;
+    while (scatterw && G < tiles) {
+        const uint32_t g2 = 2 * G, f2 = g2 * T;
+        const uint32_t w2 = f2 > 64u * SCATTER_WAVES * SCATTERW_MV ? 2 * SCATTER_WAVES : SCATTER_WAVES;
+        if (f2 > c->scatter_group_frames || f2 > 64u * w2 * SCATTERW_MV || 8ull * f2 > 2ull * w2 * S ||
+            (S & 1u) || ceil_div(tiles, g2) < c->scatter_min_wg)
+            break;
+        G = g2;
+        W = w2;
+    }
+
     ScanArgs sa;
     memset(&sa, 0, sizeof(sa));
+    sa.row_mask = cols ? G - 1u : 0u;
     sa.hist = P.hist;
     sa.partial = P.partial;
     sa.lane_off = o->lane_off_dev;
@@ -796,11 +820,19 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     xa.lane_mask = c->lane_mask;
     xa.key_bits = c->key_bits;
     xa.lane_cap = o->lane_cap;
+    xa.row_step = 1;
     xa.dbg = c->dbg;
-    if (c->max_fanout <= 1 && S <= SCATTERW_MAX_LANES)
-        HIPC(c, launch(st, ts, 2, true, true, rx_scatterw, dim3(tiles), dim3(64 * SCATTER_WAVES),
-                       scatterw_lds_bytes(S), xa));
-    else
+    if (scatterw) {
+        xa.tile_frames = G * T;
+        xa.n_tiles = ceil_div(tiles, G);
+        xa.row_step = G;
+        if (W == SCATTER_WAVES)
+            HIPC(c, launch(st, ts, 2, true, true, rx_scatterw<SCATTER_WAVES>, dim3(xa.n_tiles),
+                           dim3(64 * SCATTER_WAVES), scatterw_lds_bytes(S), xa));
+        else
+            HIPC(c, launch(st, ts, 2, true, true, rx_scatterw<2 * SCATTER_WAVES>, dim3(xa.n_tiles),
+                           dim3(128 * SCATTER_WAVES), scatterw_lds_bytes(S, 2 * SCATTER_WAVES), xa));
+    } else
         HIPC(c, launch(st, ts, 2, true, true, rx_scatter, dim3(tiles), dim3(SCATTER1_BLOCK),
                        scatter1_lds_bytes(S), xa));
     return 0;
