@@ -19,7 +19,7 @@ constexpr uint32_t RX_TILE_MAX = 8192;   // classify LDS: <= 143 KiB at 16384 la
 #endif
 constexpr uint32_t RX_HIST_CAP = UDPDK_RX_HIST_CAP;  // target bound on lanes x tiles
 #ifndef UDPDK_SCAN_MIN_WG
-#define UDPDK_SCAN_MIN_WG 64u                 // rx_scan_cols: fewest workgroups before narrowing columns
+#define UDPDK_SCAN_MIN_WG 128u                // rx_scan_cols: fewest workgroups before narrowing columns
 #endif
 #ifndef UDPDK_CLS_BLOCK
 #define UDPDK_CLS_BLOCK 256
@@ -204,13 +204,14 @@ struct ScanArgs {
     uint32_t epoch;
     uint32_t hist16;
     uint32_t row_mask;    // rx_scan_cols: base rows written only for tiles t with t & row_mask == 0
+    unsigned long long *dbg;   // diagnostic stamps (UDPDK_STAMPS builds), may be null
 };
 
-// rx_scan_cols: one launch, workgroup = a block of 2^lb lanes x every tile; each thread keeps up
-// to SCAN_COLS_TPT tiles of one lane in registers, so tiles <= SCAN_COLS_TPT * (256 >> lb).
-constexpr int SCAN_COLS_BLOCK = 256;
-constexpr uint32_t SCAN_COLS_TPT = 64;
-constexpr uint32_t SCAN_COLS_MAX_TILES = SCAN_COLS_TPT * SCAN_COLS_BLOCK;
+// rx_scan_cols<B>: one launch, workgroup = a block of 2^lb lanes x every tile (B = 512 or 1024
+// threads); each thread keeps up to scan_cols_tpt(B) tiles of one lane in registers, so tiles <=
+// scan_cols_tpt(B) * (B >> lb): 16384 tiles at one lane per workgroup, whatever B.
+__host__ __device__ constexpr uint32_t scan_cols_tpt(uint32_t block) { return 16384u / block; }
+constexpr uint32_t SCAN_COLS_MAX_TILES = 16384;
 
 struct ScatterArgs {
     const uint32_t *meta;
@@ -297,7 +298,7 @@ struct GatherArgs {
 // descriptors are loaded a round ahead (in registers) instead of when they are staged
 template <int G, int MR> __global__ void rx_classify(RxArgs a);
 __global__ void rx_gather(GatherArgs a);
-__global__ void rx_scan_cols(ScanArgs a, uint32_t lb);
+template <uint32_t B> __global__ void rx_scan_cols(ScanArgs a, uint32_t lb);
 __global__ void rx_scan_reduce(ScanArgs a);
 __global__ void rx_scan_top(ScanArgs a, uint32_t n_part);
 __global__ void rx_scan_down(ScanArgs a);

@@ -1368,8 +1368,8 @@ __device__ __forceinline__ void scan_lane_totals(const uint32_t *tot, uint32_t n
 }
 
 // rx_scan_cols: the whole scan in one launch. Workgroup = a block of LB = 2^lb lanes x every
-// tile; thread (c, l) holds lane l's counts of the c-th of 256 / LB contiguous tile chunks
-// (<= SCAN_COLS_TPT tiles) in registers, all loaded at once (LB lanes x 2 or 4 B contiguous per
+// tile; thread (c, l) holds lane l's counts of the c-th of B / LB contiguous tile chunks
+// (<= scan_cols_tpt(B) tiles) in registers, all loaded at once (LB lanes x 2 or 4 B contiguous per
 // tile row). The chunk sums meet in LDS and give the lane totals; the lane offsets (the exclusive
 // scan of the totals over ALL lanes, which other workgroups hold) come from a decoupled look-back
 // over the lane blocks: blocks take tickets in dispatch order, publish their total (A) at once
@@ -1389,13 +1389,22 @@ __device__ __forceinline__ unsigned long long lb_poll(unsigned long long *p, uin
     }
 }
 
-__global__ void __launch_bounds__(SCAN_COLS_BLOCK)
+template <uint32_t B>
+__global__ void __launch_bounds__(B)
 rx_scan_cols(ScanArgs a, uint32_t lb)
 {
-    __shared__ uint32_t part[SCAN_COLS_BLOCK];
+    constexpr uint32_t TPT = scan_cols_tpt(B);
+#ifdef UDPDK_STAMPS
+    // diagnostic: memtime at start, loads summed, look-back done, stores issued; memrealtime at
+    // start and end (rows RX_TILE_MAX * 3 + ticket of a.dbg)
+    unsigned long long sst[6];
+    sst[0] = __builtin_amdgcn_s_memtime();
+    sst[4] = __builtin_amdgcn_s_memrealtime();
+#endif
+    __shared__ uint32_t part[B];
     __shared__ uint32_t loff_sh[64];
     __shared__ uint32_t jb;
-    const uint32_t LB = 1u << lb, C = (uint32_t)SCAN_COLS_BLOCK >> lb;
+    const uint32_t LB = 1u << lb, C = B >> lb;
     const uint32_t l = threadIdx.x & (LB - 1u), c = threadIdx.x >> lb;
     if (threadIdx.x == 0) {
         const uint32_t j = atomicAdd(a.ticket, 1u);
@@ -1411,18 +1420,21 @@ rx_scan_cols(ScanArgs a, uint32_t lb)
     const uint32_t hs = a.hist16 ? ((S + 1u) & ~1u) : S;   // row stride in counts
     const uint16_t *col16 = reinterpret_cast<const uint16_t *>(a.hist) + lanei;
     const uint32_t *col32 = a.hist + lanei;
-    uint32_t v[SCAN_COLS_TPT];
+    uint32_t v[TPT];
 #pragma unroll
-    for (uint32_t k = 0; k < SCAN_COLS_TPT; ++k) {
+    for (uint32_t k = 0; k < TPT; ++k) {
         const bool in = ok && t0 + k < t1;
         const size_t o = (size_t)(in ? t0 + k : 0u) * hs;
         v[k] = !in ? 0u : a.hist16 ? (uint32_t)col16[o] : col32[o];
     }
     uint32_t sum = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < SCAN_COLS_TPT; ++k) sum += v[k];
+    for (uint32_t k = 0; k < TPT; ++k) sum += v[k];
     part[c * LB + l] = sum;
     __syncthreads();
+#ifdef UDPDK_STAMPS
+    sst[1] = __builtin_amdgcn_s_memtime();
+#endif
     uint32_t run = 0, tot = 0;
     for (uint32_t i = 0; i < C; ++i) {
         const uint32_t x = part[i * LB + l];
@@ -1465,14 +1477,33 @@ rx_scan_cols(ScanArgs a, uint32_t lb)
         }
     }
     __syncthreads();
+#ifdef UDPDK_STAMPS
+    sst[2] = __builtin_amdgcn_s_memtime();
+#endif
     run += loff_sh[l];
     uint32_t *out = a.base + lanei;
 #pragma unroll
-    for (uint32_t k = 0; k < SCAN_COLS_TPT; ++k) {
+    for (uint32_t k = 0; k < TPT; ++k) {
         if (ok && t0 + k < t1 && ((t0 + k) & a.row_mask) == 0u) out[(size_t)(t0 + k) * S] = run;
         run += v[k];
     }
+#ifdef UDPDK_STAMPS
+    sst[3] = __builtin_amdgcn_s_memtime();
+    sst[5] = __builtin_amdgcn_s_memrealtime();
+    if (a.dbg && threadIdx.x == 0 && j < RX_TILE_MAX) {
+        unsigned long long *d = a.dbg + (size_t)(RX_TILE_MAX * 3 + j) * 16;
+        d[0] = sst[1] - sst[0];
+        d[1] = sst[2] - sst[1];
+        d[2] = sst[3] - sst[2];
+        d[3] = sst[4];
+        d[4] = sst[5];
+        d[5] = j;
+    }
+#endif
 }
+
+template __global__ void rx_scan_cols<512>(ScanArgs a, uint32_t lb);
+template __global__ void rx_scan_cols<1024>(ScanArgs a, uint32_t lb);
 
 // Pass 1, grid (chunks, ceil(lanes / SCAN_BLOCK)): partial[c][l] = column sum of chunk c.
 __global__ void __launch_bounds__(SCAN_BLOCK)

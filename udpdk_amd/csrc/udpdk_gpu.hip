@@ -335,8 +335,10 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
             ok = ok && hipMalloc((void **)&P.hist, e_cap * 4) == hipSuccess;
             ok = ok && hipMalloc((void **)&P.partial, c->partial_cap * 4) == hipSuccess;
             ok = ok && hipMalloc((void **)&P.base, e_cap * 4) == hipSuccess;
-            ok = ok && hipMalloc((void **)&P.agg, ((size_t)max_lanes / 8 + 1) * 8) == hipSuccess;
-            ok = ok && hipMemset(P.agg, 0, ((size_t)max_lanes / 8 + 1) * 8) == hipSuccess;
+            // one look-back word per lane block: down to one lane per block when a batch has so
+            // many tiles that a column chunk holds a single lane (rx_scan_cols' lb = 0)
+            ok = ok && hipMalloc((void **)&P.agg, ((size_t)max_lanes + 1) * 8) == hipSuccess;
+            ok = ok && hipMemset(P.agg, 0, ((size_t)max_lanes + 1) * 8) == hipSuccess;
             ok = ok && hipMalloc((void **)&P.ticket, 64) == hipSuccess;
             ok = ok && hipMemset(P.ticket, 0, 64) == hipSuccess;
             ok = ok && hipMalloc((void **)&P.tile_cnt, c->tiles_cap * UDPDK_N_COUNTERS * 4) == hipSuccess;
@@ -772,6 +774,7 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     ScanArgs sa;
     memset(&sa, 0, sizeof(sa));
     sa.row_mask = cols ? G - 1u : 0u;
+    sa.dbg = c->dbg;
     sa.hist = P.hist;
     sa.partial = P.partial;
     sa.lane_off = o->lane_off_dev;
@@ -789,12 +792,25 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
         // until the grid has >= UDPDK_SCAN_MIN_WG workgroups, never under 8 lanes (32 B row
         // segments). Wider rows beat more workgroups: at 1024 lanes x 1024 tiles, 16-lane
         // columns (64 workgroups) take 8.0 us, 8-lane (128) 11.9 us, 4-lane (256) 13.0 us.
-        const uint32_t cmin = ceil_div(tiles, SCAN_COLS_TPT);
-        uint32_t lb = 0;
-        while ((2u << lb) <= std::min<uint32_t>(64u, SCAN_COLS_BLOCK / cmin)) ++lb;
-        while (lb > 3 && ceil_div(S, 1u << lb) < UDPDK_SCAN_MIN_WG) --lb;
-        HIPC(c, launch(st, ts, 1, true, true, rx_scan_cols, dim3(ceil_div(S, 1u << lb)),
-                       dim3(SCAN_COLS_BLOCK), 0u, sa, lb));
+        // Workgroups of 1024 threads when that still leaves >= 16-lane columns (config 5: 11.2-11.8
+        // -> 7.3-7.7 us against 256 threads; more waves per CU for the column loads' latency),
+        // else 512 (config 4's 1024 lanes x 1024 tiles: 10.3-10.4 -> 8.9-9.1 us)
+        auto pick_lb = [&](uint32_t block) {
+            const uint32_t cmin = ceil_div(tiles, scan_cols_tpt(block));
+            uint32_t lb = 0;
+            while ((2u << lb) <= std::min<uint32_t>(64u, block / cmin)) ++lb;
+            while (lb > 3 && ceil_div(S, 1u << lb) < UDPDK_SCAN_MIN_WG) --lb;
+            return lb;
+        };
+        const uint32_t lb1 = pick_lb(1024u);
+        if (lb1 >= 4) {
+            HIPC(c, launch(st, ts, 1, true, true, rx_scan_cols<1024>, dim3(ceil_div(S, 1u << lb1)),
+                           dim3(1024), 0u, sa, lb1));
+        } else {
+            const uint32_t lb = pick_lb(512u);
+            HIPC(c, launch(st, ts, 1, true, true, rx_scan_cols<512>, dim3(ceil_div(S, 1u << lb)),
+                           dim3(512), 0u, sa, lb));
+        }
     } else {
         const uint32_t nc = ceil_div(tiles, SCAN_COL_CHUNK);
         if ((uint64_t)nc * S > c->partial_cap) return -EINVAL;
