@@ -1686,13 +1686,20 @@ rx_scatterw(ScatterArgs a)
     SSTAMP(0);
     __syncthreads();
     SSTAMP(1);
-    // pass 1: per-wave counts
+    // pass 1: per-wave counts; each atomic's return is the delivery's rank within its key in the
+    // wave's slice (kept with the key: the placement adds the slice's offset, a plain LDS read,
+    // where it made a second atomic per delivery)
+    uint32_t kr[MV];                                                   // rank | key << 16
 #pragma unroll
     for (uint32_t i = 0; i < MV; ++i) {
+        kr[i] = 0xFFFFFFFFu;
         if (i * 64 >= q) break;                                        // uniform
         const uint32_t p = wb + i * 64 + lane;
-        if (p < we && UDPDK_META_VERDICT(mv[i]) == UDPDK_V_DELIVERED)
-            atomicAdd(&mine[UDPDK_META_SOCKFD(mv[i]) & a.lane_mask], inc);
+        if (p < we && UDPDK_META_VERDICT(mv[i]) == UDPDK_V_DELIVERED) {
+            const uint32_t key = UDPDK_META_SOCKFD(mv[i]) & a.lane_mask;
+            const uint32_t o = atomicAdd(&mine[key], inc);
+            kr[i] = ((o >> sh) & 0xFFFFu) | key << 16;
+        }
     }
     __syncthreads();
     SSTAMP(2);
@@ -1775,21 +1782,17 @@ rx_scatterw(ScatterArgs a)
         if (tid < W && tid < S) cur[tid] = cur_lo;
         __syncthreads();
     }
-    uint32_t kr[MV];                                                   // rank | key << 16
 #pragma unroll
     for (uint32_t i = 0; i < MV; ++i) {
-        kr[i] = 0xFFFFFFFFu;
         if (i * 64 >= q) break;                                        // uniform
-        const uint32_t p = wb + i * 64 + lane;
-        const uint32_t key = UDPDK_META_SOCKFD(mv[i]) & a.lane_mask;
-        if (p < we && UDPDK_META_VERDICT(mv[i]) == UDPDK_V_DELIVERED) {
-            const uint32_t o = atomicAdd(&mine[key], inc);
-            const uint32_t rank = (o >> sh) & 0xFFFFu;
+        if (kr[i] != 0xFFFFFFFFu) {
+            const uint32_t key = kr[i] >> 16;
+            const uint32_t rank = (kr[i] & 0xFFFFu) + ((mine[key] >> sh) & 0xFFFFu);
             if (staged) {
                 kr[i] = rank | key << 16;
             } else {
                 const uint32_t pos = cur[key] + rank;
-                if (pos < a.lane_cap) a.lane_pkt[pos] = p;
+                if (pos < a.lane_cap) a.lane_pkt[pos] = wb + i * 64 + lane;
             }
         }
     }
