@@ -536,16 +536,19 @@ __device__ __forceinline__ void wave_sync_rs()
 // Every store this wave issued has completed (CDNA counts stores in vmcnt).
 __device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Exclusive prefix sum of v over the wave's lanes; *total gets the wave's sum. Wave-uniform.
+// Exclusive prefix sum of v over the wave's lanes; *total gets the wave's sum. Called with every
+// lane active (wave-uniform control flow). On the DPP network: six VALU ops and a readlane, where
+// the __shfl_up form made seven ds_bpermute round trips through the LDS pipeline.
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total)
 {
-    const uint32_t lane = __lane_id();
     uint32_t x = v;
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    *total = __shfl(x, 63, 64);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
     return x - v;
 }
 
