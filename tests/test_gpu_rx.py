@@ -132,6 +132,25 @@ def test_lane_counts_no_fanout(gpu_ctx, n_lanes):
     _assert_same(want, got, f"lanes={n_lanes}")
 
 
+def test_many_tiles_narrow_scan_columns():
+    """8 M frames over 64 lanes in a context sized for 64 lanes: 8192 tiles, so rx_scan_cols
+    narrows its columns to 2 lanes per workgroup (32 lane blocks, each with a look-back word;
+    words for only max_lanes / 8 blocks were allocated before round 5). Exact against the
+    oracle."""
+    n, n_lanes = 1 << 23, 64
+    ctx = abi.GpuContext(0, max_frames=n, max_lanes=n_lanes)
+    try:
+        assert abi.geometry(n, n_lanes) == (1024, 8192)
+        lists = {abi.raw_port(30000 + i): [(0, i, 0)] for i in range(n_lanes)}
+        rng = np.random.default_rng(64)
+        ports = 30000 + rng.integers(0, n_lanes, n)
+        b = F.build_frames(np.full(n, 64, np.uint32), ports, 11)
+        want, got = _rx_both(ctx, b, lists, n_lanes, lane_cap=n)
+        _assert_same(want, got, "8M x 64 lanes")
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("cfg,n", [(2, 70001), (3, 20000), (4, 50000), (5, 100000), (1, 4096)])
 def test_configs_reduced(gpu_ctx, cfg, n):
     w = F.config_batch(cfg, n=n)
