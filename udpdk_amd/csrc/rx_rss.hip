@@ -35,6 +35,19 @@ __device__ __forceinline__ void wsync()
 }
 
 // Lanes of the wave holding the same key (key < 2^bits), from one ballot per key bit.
+// Inclusive wave64 prefix sum on the DPP network (every lane active): six VALU ops where the
+// __shfl_up chain made six ds_bpermute round trips
+__device__ __forceinline__ uint32_t rss_scan_dpp(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return v;
+}
+
 __device__ __forceinline__ unsigned long long peers_of(uint32_t key, uint32_t bits, bool active)
 {
     unsigned long long peers = __ballot(active);
@@ -69,11 +82,7 @@ __device__ void rss_scan_last(uint32_t *hist, uint32_t n, uint32_t T, uint32_t *
 #pragma unroll
         for (uint32_t i = 0; i < PER; ++i) sum += v[i];
         uint32_t incl = sum;
-#pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t u = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += u;
-        }
+        incl = rss_scan_dpp(incl);
         if (lane == 63) wsum[w] = incl;
         __syncthreads();
         uint32_t run = carry + incl - sum, grand = 0;
@@ -246,11 +255,7 @@ rss_base(uint32_t *hist, uint32_t n, uint32_t T, uint32_t *queue_off, uint32_t *
 #pragma unroll
     for (uint32_t i = 0; i < PER; ++i) sum += v[i];
     uint32_t incl = sum;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t u = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += u;
-    }
+    incl = rss_scan_dpp(incl);
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
     uint32_t run = incl - sum, grand = 0;
