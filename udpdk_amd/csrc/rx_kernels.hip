@@ -1601,10 +1601,12 @@ __device__ __forceinline__ void lane_cursors(const ScatterArgs &a, uint32_t tile
 }
 
 // ------------------------------------------------------------------------------------------
-// rx_scatterw: stable per-lane compaction without fan-out, SCATTER_WAVES waves per tile. Wave w
-// owns the w-th contiguous slice of the tile. Pass 1 counts each wave's deliveries per lane key
-// with LDS atomics; each key's wave offsets become the exclusive prefix over the earlier slices;
-// pass 2 places every delivery at cursor + atomicAdd's return on its wave's counter.
+// rx_scatterw: stable per-lane compaction without fan-out, W waves per scatter tile (one or
+// several consecutive classify tiles, ScatterArgs::row_step). Wave w owns the w-th contiguous
+// slice of the tile. Pass 1 counts each wave's deliveries per lane key with LDS atomics, whose
+// returns are each delivery's rank within its key in the slice; each key's wave offsets then
+// become the exclusive prefix over the earlier slices (and the keys' starts in the tile, for
+// the staged write-out); the placement puts every delivery at cursor + slice offset + rank.
 //
 // Stability comes from the order in which a ds_add_rtn_u32 resolves lanes of one instruction
 // that hit the same word: lane order on gfx950 (tools/probe/lds_order_probe.hip: 1.3e10 same-key
@@ -1614,7 +1616,7 @@ __device__ __forceinline__ void lane_cursors(const ScatterArgs &a, uint32_t tile
 // lanes: 11 us per pass at config 5, instruction-bound; the atomics make a pass a few
 // instructions per 64 frames.) Counters hold two waves each, 16 bits per wave (a scatter tile
 // has <= 16384 frames, so neither half can carry into the other).
-// LDS: 4 x n_lanes (cursors) + 2 x SCATTER_WAVES x n_lanes bytes.
+// LDS: 4 x max(n_lanes, W) (cursors) + 2 x W x n_lanes bytes (scatterw_lds_bytes).
 // ------------------------------------------------------------------------------------------
 template <uint32_t W>
 __global__ void __launch_bounds__(64 * W)
