@@ -2,7 +2,8 @@
 context creation) and compared with the oracle bit for bit: the fused completion (the last
 workgroup writes lane_off and the total; with a tile before the last not full it rewrites the
 later tiles' entries from the verdict words) against rx_classify + rx_compact1, and
-rx_classify<1> (one tail chunk group in flight) against <2>, and a bind table of at most 8 ports
+rx_classify<1> (one tail chunk group in flight) against <2> (with and without the span sweep of
+steps of long back-to-back frames), and a bind table of at most 8 ports
 passed in the kernel arguments against the port-table loads. The automatic choice between them
 (kernel hints, udpdk_gpu.hip) only picks the faster of two exact forms."""
 import os
@@ -15,17 +16,20 @@ from udpdk_amd import abi, frames as F
 
 pytestmark = pytest.mark.gpu
 
-# (fused completion, tail chunk groups, bind table of <= 8 ports in the kernel arguments)
-FORMS = [(1, 1, 1), (1, 2, 1), (0, 1, 1), (0, 2, 1), (1, 1, 0), (0, 2, 0)]
-ENV = ("UDPDK_RX_FUSE", "UDPDK_RX_TAILG", "UDPDK_RX_NO_INLINE")
+# (fused completion, tail chunk groups, bind table of <= 8 ports in the kernel arguments, span
+# sweep of long-frame steps allowed)
+FORMS = [(1, 1, 1, 1), (1, 2, 1, 1), (1, 2, 1, 0), (0, 1, 1, 1), (0, 2, 1, 1), (1, 1, 0, 1), (0, 2, 0, 1),
+         (0, 2, 0, 0)]
+ENV = ("UDPDK_RX_FUSE", "UDPDK_RX_TAILG", "UDPDK_RX_NO_INLINE", "UDPDK_RX_SPAN")
 
 
-@pytest.fixture(scope="module", params=FORMS, ids=lambda f: f"fuse{f[0]}-g{f[1]}-inl{f[2]}")
+@pytest.fixture(scope="module", params=FORMS, ids=lambda f: f"fuse{f[0]}-g{f[1]}-inl{f[2]}-span{f[3]}")
 def form_ctx(request):
-    fuse, g, inl = request.param
+    fuse, g, inl, span = request.param
     old = {k: os.environ.get(k) for k in ENV}
     os.environ["UDPDK_RX_FUSE"] = str(fuse)
     os.environ["UDPDK_RX_TAILG"] = str(g)
+    os.environ["UDPDK_RX_SPAN"] = str(span)
     if not inl:
         os.environ["UDPDK_RX_NO_INLINE"] = "1"
     else:

@@ -24,12 +24,6 @@ constexpr uint32_t RX_HIST_CAP = UDPDK_RX_HIST_CAP;  // target bound on lanes x 
 #ifndef UDPDK_CLS_BLOCK
 #define UDPDK_CLS_BLOCK 256
 #endif
-#ifndef UDPDK_CLS_EARLY
-#define UDPDK_CLS_EARLY 0                    // rx_classify<1>: next window issued at the step's top
-#endif
-#ifndef UDPDK_CLS_K2
-#define UDPDK_CLS_K2 0                       // rx_classify<1>: two windows ahead (W, W1 + one in flight)
-#endif
 #ifndef UDPDK_CLS_WPE
 #define UDPDK_CLS_WPE 4                      // rx_classify minimum waves per SIMD (VGPR budget)
 #endif
@@ -81,6 +75,13 @@ __host__ __device__ constexpr uint32_t classify_lds_bytes(uint32_t n_lanes, uint
            4u * classify_hist_words(n_lanes, hist16) + 4u * classify_stage_frames(tile_frames) +
            4u * RX_ROUND + 8u * RX_ROUND;
 }
+// Span sweep (rx_classify<2, 0>, RxArgs::span): per wave a ring of two 1 KiB blocks of the step's
+// byte span plus a 64-byte copy of the even block's first pieces (a window that wraps the ring
+// reads on into it), after the classify carve
+constexpr uint32_t SPAN_RING_DW = 2u * 256u + 16u;
+constexpr uint32_t SPAN_LDS_BYTES = (uint32_t)CLS_WAVES * SPAN_RING_DW * 4u;
+constexpr uint32_t SPAN_MIN_AVG = 96;        // a step sweeps its span when its frames average this
+constexpr uint32_t SPAN_MAX_GAP = 128;       // ... and each frame starts < this after the previous ends
 
 // Port table entry (16 B per raw port): x = bindings on the port, y = index of the first in the
 // binding array, z/w = the first binding itself (ip, sockfd | reuse << 31), so single-binding
@@ -129,6 +130,12 @@ struct RxArgs {
     uint32_t n_inl;
     uint32_t inl_port[8];
     uint4 inl_ent[8];
+    // rx_classify<2, 0> with one-round tiles: a step whose frames lie in ascending order, each
+    // within SPAN_MAX_GAP bytes of the previous one's end, reads its whole byte span once on a
+    // line grid (header windows taken from the sweep through an LDS ring, UDP checksums from
+    // prefix sums over the span) instead of per-frame windows and tail chunks. The ring follows
+    // the classify carve (SPAN_LDS_BYTES more dynamic LDS)
+    uint32_t span;
 };
 #define UDPDK_INLINE_PORTS 8u
 #define UDPDK_FUSE_SHARDS 8u

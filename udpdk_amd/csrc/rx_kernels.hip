@@ -415,17 +415,18 @@ struct Win {
 // 8 % slower at G = 1, so the host picks G by whether recent calls had tail passes).
 template <int G, int MR>
 __global__ void __launch_bounds__(CLS_BLOCK)
-__attribute__((amdgpu_waves_per_eu(MR ? 2 : G == 1 && !UDPDK_CLS_K2 ? 5 : UDPDK_CLS_WPE, 8)))
+__attribute__((amdgpu_waves_per_eu(MR ? 2 : G == 1 ? 5 : UDPDK_CLS_WPE, 8)))
 rx_classify(RxArgs a)
 {
     static_assert(G == 1 || G == 2, "one or two tail chunk groups in flight");
+    // the span sweep (RxArgs::span) is compiled into the long-frame form of one-round tiles only
+    constexpr bool SPAN = G == 2 && MR == 0;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t steps = a.tile_frames / 64;
     constexpr uint32_t RSTEPS = RX_ROUND / 64;              // steps per staging round
     constexpr uint32_t SPR = RSTEPS / CLS_WAVES;            // steps per wave per staging round
     static_assert(SPR >= 2, "round staging needs two steps per wave per round");
-    static_assert(!(G == 1 && UDPDK_CLS_K2) || SPR >= 3, "two windows ahead stage the next round a step earlier");
 #ifdef UDPDK_STAMPS
     // (in LDS: a register array indexed by lane at the end went to scratch, and the scratch
     // allocation held workgroups back from starting)
@@ -517,10 +518,12 @@ rx_classify(RxArgs a)
     // funnels them to frame-relative words by offset & 3. Bytes past the frame are never used
     // (parse and sums mask by length); lanes without a frame read the buffer's first bytes
     // (cached, never used).
-    auto load_win = [&](uint32_t s, uint32_t o, uint32_t l) -> Win {
+    // (a step that sweeps its span takes its windows from the sweep: nothing loaded here)
+    constexpr uint32_t OOR = 0xFFFFFFF0u;   // past any batch's range (< 4 GiB - 16)
+    auto load_win = [&](uint32_t s, uint32_t o, uint32_t l, bool swept = false) -> Win {
         const uint32_t p = t0 + s * 64 + lane;
         const bool ok = s < steps && p < t1 && l >= 14u && l <= a.frames_bytes && o <= a.frames_bytes - l;
-        const uint32_t b = ok ? (o + 12u) & ~3u : 0u;
+        const uint32_t b = swept ? OOR : ok ? (o + 12u) & ~3u : 0u;
         Win r;
         r.a = load16(fr, b);
         r.b = load16(fr, b + 16u);
@@ -540,11 +543,35 @@ rx_classify(RxArgs a)
     uint32_t st = __builtin_amdgcn_readfirstlane(w);             // wave-uniform step (SGPR)
     uint32_t c_off, c_lp;
     Win W;
-    // K2 (G = 1, UDPDK_CLS_K2): two windows ahead; W1 / c1_* hold the next step's window and
-    // descriptor while the step after it is in flight
-    constexpr bool K2 = G == 1 && UDPDK_CLS_K2;
-    Win W1;
-    uint32_t c1_off = 0, c1_lp = 0;
+
+    // ---- span sweep (SPAN forms, a.span): is step s's span [A, Ep) sweepable? ----
+    // Every frame of the step in range, each starting within SPAN_MAX_GAP bytes after the previous
+    // one's end (ascending, disjoint: what a NIC's back-to-back mbuf images are), and on average
+    // at least SPAN_MIN_AVG bytes long (shorter frames are all window: the per-frame windows read
+    // the same lines). A = the 128-byte line holding the first frame, Ep = the end of the last
+    // frame or of the furthest window (windows read 56 bytes from the dword at or below offset +
+    // 12). Wave-uniform.
+    auto span_check = [&](uint32_t s, uint32_t o, uint32_t l, uint32_t &A, uint32_t &Ep) -> bool {
+        if (!SPAN || !a.span || s >= steps) return false;
+        const uint32_t p = t0 + s * 64u + lane;
+        const bool v = p < t1;
+        const unsigned long long vm = __ballot(v);
+        if (vm == 0ull) return false;
+        const uint32_t on = (uint32_t)__shfl_down((int)o, 1, 64);    // the next frame's offset
+        const bool nv = lane < 63u && p + 1u < t1;
+        const bool good = l <= a.frames_bytes && o <= a.frames_bytes - l;
+        const bool bad = v && (!good || (nv && on - (o + l) >= SPAN_MAX_GAP));
+        if (__ballot(bad)) return false;
+        const uint32_t ee = v ? max(o + l, ((o + 12u) & ~3u) + 56u) : 0u;
+        const uint32_t em = (uint32_t)__builtin_amdgcn_readlane((int)max_scan_dpp(ee), 63);
+        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)o) & ~127u;
+        if (em - a0 < SPAN_MIN_AVG * (uint32_t)__popcll(vm)) return false;
+        A = a0;
+        Ep = em;
+        return true;
+    };
+    bool span_cur = false;                  // the current step sweeps its span (wave-uniform)
+    uint32_t span_A = 0, span_E = 0;
     {
         uint32_t o[SPT], l[SPT], t[SPT];
         stage_load(0, o, l, t);
@@ -552,12 +579,8 @@ rx_classify(RxArgs a)
         const uint4 ie = a.inl_ent[min(tid, UDPDK_INLINE_PORTS - 1u)];
         c_off = o[0];
         c_lp = l[0] | (has_ptype ? (t[0] & 0x10u) << 12 : 0u);
-        W = load_win(st, c_off, c_lp & 0xFFFFu);
-        if constexpr (K2) {                 // step w + 4: this thread's second staged descriptor
-            c1_off = o[1];
-            c1_lp = l[1] | (has_ptype ? (t[1] & 0x10u) << 12 : 0u);
-            W1 = load_win(st + CLS_WAVES, c1_off, c1_lp & 0xFFFFu);
-        }
+        span_cur = span_check(st, c_off, c_lp & 0xFFFFu, span_A, span_E);
+        W = load_win(st, c_off, c_lp & 0xFFFFu, span_cur);
         __builtin_amdgcn_sched_barrier(0);
         const bool inl = a.inl && tid <= UDPDK_INLINE_PORTS;
         if (tid == 0) tail_any = 0u;        // (ordered by the staging barrier)
@@ -596,7 +619,6 @@ rx_classify(RxArgs a)
     uint32_t *l_own = l_B + 128;            // [64] frame + 1 whose chunks start at k0 + slot, else 0
     l_own[lane] = 0;
     bool tailed = false;                    // this wave ran a tail pass (the host's kernel hint)
-    constexpr uint32_t OOR = 0xFFFFFFF0u;   // past any batch's range (< 4 GiB - 16)
     auto tail_step = [&](uint32_t s2) {
             const uint32_t i = s2 * 64 + lane;
             const uint32_t m = mstage[i & (RX_ROUND - 1u)];
@@ -702,6 +724,109 @@ rx_classify(RxArgs a)
             }
     };
 
+    // ---- span sweep: the step's bytes [A, Ep) read once, each 128-byte line by one load ----
+    // (tools/probe/sweep_probe.hip: loads that each cover 1 KiB of consecutive 16-byte pieces read
+    // 1.004x the span's bytes from HBM; one 64-byte chunk per lane, 1.030x; the per-frame windows
+    // and tail chunks, 1.13x.) Blocks of 64 pieces, four per group, two groups in flight. Per
+    // block: the pieces' RFC 1071 sums (buffer-aligned words, whole pieces) and their prefix sum
+    // on the DPP network give Q(k), the sum of pieces [0, k) of the span, at each frame's two
+    // piece indices (the piece holding its tail start, offset + 64, and the first piece past its
+    // end); the block goes to a two-block LDS ring, from which a frame takes its header window
+    // (the same 14 dwords load_win reads) when the block holding its last window byte arrives,
+    // and the piece holding its end. Then a frame's tail sum over [offset + 64, offset + length)
+    // = Q(end) - Q(start) - the lead bytes of the start piece (in its window) - the bytes of the
+    // end piece past the frame (span_tail). Sums of 16-bit words up to 65535 bytes stay below
+    // 2^32, so the differences of the wrapping prefix sums are exact.
+    uint32_t *ring = reinterpret_cast<uint32_t *>(
+        smem + classify_lds_bytes(a.n_lanes, a.tile_frames, a.hist16 != 0u)) + w * SPAN_RING_DW;
+    uint32_t sp_Qs = 0, sp_Qe = 0;          // Q at the frame's tail-start piece and past its end
+    uint4 sp_EP = make_uint4(0, 0, 0, 0);   // the piece holding the frame's end
+    auto span_sweep = [&](uint32_t s, uint32_t A, uint32_t Ep, uint32_t o, uint32_t l) -> Win {
+        const bool v = t0 + s * 64u + lane < t1;
+        const uint32_t w0 = (o + 12u) & ~3u;
+        const uint32_t s_idx = v ? (o + 64u - A) >> 4 : 0u;
+        const uint32_t e_idx = v ? (o + l - A + 15u) >> 4 : 0u;
+        const uint32_t wblk = v ? (w0 + 52u - A) >> 10 : 0xFFFFFFFFu;
+        const uint32_t eblk = v && l > 64u && ((o + l) & 15u) != 0u ? (o + l - A) >> 10 : 0xFFFFFFFFu;
+        const uint32_t ep = ((o + l - A) >> 4) & 127u;     // ring piece of the frame's end
+        const uint32_t rb = ((w0 - A) >> 2) & 511u;         // ring dword of the window's first
+        const uint32_t nb = (Ep - A + 1023u) >> 10;          // blocks
+        const uint32_t ng = (nb + 3u) >> 2;                  // groups
+        uint32_t C = 0, Qs = 0, Qe = 0;
+        uint32_t Dw[14];
+#pragma unroll
+        for (int k = 0; k < 14; ++k) Dw[k] = 0;
+        uint4 EP = make_uint4(0, 0, 0, 0);
+        uint4 *rq = reinterpret_cast<uint4 *>(ring);
+        auto block = [&](uint32_t b, const uint4 &R) {
+            const uint32_t ps = sad16(R.x, sad16(R.z, 0u)) + sad16(R.y, sad16(R.w, 0u));
+            const uint32_t P = scan_dpp(ps);
+            const uint32_t ds = s_idx - 64u * b - 1u, de = e_idx - 64u * b - 1u;
+            const uint32_t Ps = (uint32_t)__shfl((int)P, (int)(ds & 63u), 64);
+            const uint32_t Pe = (uint32_t)__shfl((int)P, (int)(de & 63u), 64);
+            Qs = ds < 64u ? C + Ps : Qs;
+            Qe = de < 64u ? C + Pe : Qe;
+            C += (uint32_t)__builtin_amdgcn_readlane((int)P, 63);
+            wave_sync();                                     // the previous block's ring reads first
+            rq[(b & 1u) * 64u + lane] = R;
+            if ((b & 1u) == 0u && lane < 4u) rq[128u + lane] = R;
+            wave_sync();
+            if (__ballot(wblk == b)) {
+                if (wblk == b) {
+#pragma unroll
+                    for (int k = 0; k < 14; ++k) Dw[k] = ring[rb + k];
+                }
+            }
+            if (__ballot(eblk == b)) {
+                if (eblk == b) EP = rq[ep];
+            }
+        };
+        auto issue = [&](uint32_t g, uint4 (&R)[4]) {
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c) {
+                const uint32_t x = A + 4096u * g + 1024u * c + 16u * lane;
+                R[c] = load16(fr, x < Ep ? x : OOR);
+            }
+        };
+        auto consume = [&](uint32_t g, const uint4 (&R)[4]) {
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c)
+                if (4u * g + c < nb) block(4u * g + c, R[c]);
+        };
+        uint4 Ra[4], Rb[4];
+        issue(0, Ra);
+        for (uint32_t g = 0;; g += 2) {
+            issue(g + 1u, Rb);
+            consume(g, Ra);
+            issue(g + 2u, Ra);
+            consume(g + 1u, Rb);
+            if (g + 2u >= ng) break;
+        }
+        sp_Qs = Qs;
+        sp_Qe = Qe;
+        sp_EP = EP;
+        Win r;
+        r.a = make_uint4(Dw[0], Dw[1], Dw[2], Dw[3]);
+        r.b = make_uint4(Dw[4], Dw[5], Dw[6], Dw[7]);
+        r.c = make_uint4(Dw[8], Dw[9], Dw[10], Dw[11]);
+        r.d = make_uint2(Dw[12], Dw[13]);
+        return r;
+    };
+    // the swept frame's tail sum over buffer bytes [o + 64, o + l) (buffer-aligned 16-bit words):
+    // D = the window's raw dwords (buffer dwords from w0 = (o + 12) & ~3)
+    auto span_tail = [&](uint32_t o, uint32_t l, const uint32_t (&D)[14]) -> uint32_t {
+        const int hi = (int)(o + 64u - ((o + 12u) & ~3u)), lo = hi - (int)((o + 64u) & 15u);
+        uint32_t lead = 0;
+#pragma unroll
+        for (int k = 9; k < 14; ++k) lead = sad16(D[k] & byte_mask(lo, hi, 4 * k), lead);
+        const int r = (int)((o + l) & 15u);
+        const uint32_t ev[4] = {sp_EP.x, sp_EP.y, sp_EP.z, sp_EP.w};
+        uint32_t over = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) over = sad16(ev[d] & byte_mask(r, 16, 4 * d), over);
+        return sp_Qe - sp_Qs - lead - (r != 0 ? over : 0u);
+    };
+
     // ---- demux of one frame: btable_get_bindings + list walk, udpdk_poller.c:376-405 ----
     // i: the frame's index in the tile, m: its verdict word so far (verdict field 0xF: UDP, port
     // lookup pending), Sv: {raw dst port | is-UDP << 16, raw dst IPv4}, Ev: the port's 16-byte
@@ -745,11 +870,7 @@ rx_classify(RxArgs a)
         // aggregated with a wave multi-split first (all 64 lanes may share one lane)
         // (one lane: the tile's count is its delivery counter, written at the tile end)
         const uint32_t key = first & a.lane_mask;
-#ifdef UDPDK_DIAG_NO_HIST
-        if (true) {                           // timing only: histogram skipped
-#else
         if (a.n_lanes == 1u) {
-#endif
         } else if (a.key_bits <= 4u) {
             unsigned long long peers = __ballot(delivered);
             for (uint32_t bit = 0; bit < a.key_bits; ++bit) {
@@ -792,12 +913,6 @@ rx_classify(RxArgs a)
             const bool valid = p < t1;
             const uint32_t off = c_off, len = c_lp & 0xFFFFu;
             const bool good = valid && len <= a.frames_bytes && off <= a.frames_bytes - len;
-            // Early issue (G = 1, a step of the round with a successor in the same round): the
-            // next step's window goes out before this step's arithmetic, so its load overlaps the
-            // whole step instead of the last quarter; the scheduler barriers keep the compiler
-            // from sinking the loads back to their use (it does, to hold occupancy:
-            // tools/probe/chain_probe.hip). A step that needs a tail pass then runs it with that
-            // window in flight.
             // MR: the next round's descriptors go out at the round's first step, into registers,
             // and are stored to LDS at its staging step: the staging no longer waits a round trip
             // (config 5: a descriptor round trip per round was a fifth of each workgroup's time)
@@ -808,17 +923,10 @@ rx_classify(RxArgs a)
             const uint32_t nst = st + CLS_WAVES;
             uint32_t n_off, n_lp;
             Win NW;
-            const bool early = K2 || (UDPDK_CLS_EARLY && G == 1 && jstep + 1u < SPR);
-            if (K2) {
-                // the window two steps ahead (its round's descriptors are staged by then: the
-                // next round is staged at the round's second step, below)
-                read_desc(nst + CLS_WAVES, n_off, n_lp);
-                NW = load_win(nst + CLS_WAVES, n_off, n_lp & 0xFFFFu);
-                __builtin_amdgcn_sched_barrier(0);
-            } else if (early) {
-                read_desc(nst, n_off, n_lp);
-                NW = load_win(nst, n_off, n_lp & 0xFFFFu);
-                __builtin_amdgcn_sched_barrier(0);
+            // a step that sweeps its span reads its window from the sweep (no window was loaded)
+            if (SPAN && span_cur) {
+                W = span_sweep(st, span_A, span_E, off, len);
+                tailed = true;
             }
 
             // ---- header fields from the window registers (lane = frame) ----
@@ -861,7 +969,11 @@ rx_classify(RxArgs a)
             // datagram is never summed.
             const bool need_cs = is_udp && ucks != 0u && !len_bad;
             const uint32_t dge = 34u + ulen;                          // datagram end (<= len)
-            const bool pend = need_cs && dge > 64u;
+            // a swept step has every frame's tail sum over [64, len): a datagram that ends there
+            // (no padding) is complete now, any other pending one goes to the tail pass
+            const bool swept = SPAN && span_cur && dge == len;
+            const bool pend = need_cs && dge > 64u && !swept;
+            const bool pend_sw = need_cs && dge > 64u && swept;
             uint32_t ws = 0, ws2 = 0;
 #pragma unroll
             for (int i = 6; i < 13; i += 2) ws = sad16(g[i], ws);
@@ -877,6 +989,13 @@ rx_classify(RxArgs a)
             const uint32_t us = ws + (g[5] >> 16) + (g[3] >> 16) + (g[4] & 0xFFFFu) + (dip & 0xFFFFu) +
                                 (dip >> 16) + 0x1100u + ulen_raw;
             dgl[(st * 64 + lane) & (RX_ROUND - 1u)] = dge | fold32(us) << 16;
+            // the swept datagrams' checksums (buffer-aligned tail words: swapped back at odd offsets)
+            bool sw_ok = false;
+            if (SPAN && __ballot(pend_sw)) {
+                uint32_t t = fold32(span_tail(off, len, D));
+                if (off & 1u) t = ((t & 0xFFu) << 8) | (t >> 8);
+                sw_ok = fold32(t + fold32(us)) == 0xFFFFu;
+            }
             STAMP(2);
 
             // ---- next step of this wave: window loads stay in flight across the rest of this step.
@@ -884,14 +1003,17 @@ rx_classify(RxArgs a)
             // (the one it shares with the frame's first tail chunk, and the one the previous
             // frame's tail ends in) are then still in L2 when that step's tail reads them, where a
             // window loaded a whole step earlier had left L2 by then (IMIX fetched 1.29x its bytes).
-            if (!early)
-                read_desc(nst, n_off, n_lp);  // in range of the buffers for any s (unused past the tile)
+            // A next step that sweeps its span loads no window.
+            read_desc(nst, n_off, n_lp);      // in range of the buffers for any s (unused past the tile)
+            uint32_t n_A = 0, n_E = 0;
+            const bool span_n = span_check(nst, n_off, n_lp & 0xFFFFu, n_A, n_E);
             const bool tail_now = __ballot(pend) != 0ull;
-            if (!early && !tail_now) NW = load_win(nst, n_off, n_lp & 0xFFFFu);
+            if (!tail_now) NW = load_win(nst, n_off, n_lp & 0xFFFFu, span_n);
 
             // ---- what does not need the port entry: UDP state, flags, flag counters ----
             const uint32_t state = ucks == 0u ? UDPDK_UDP_CSUM_NONE
                                  : pend ? 3u
+                                 : pend_sw ? (sw_ok ? UDPDK_UDP_CSUM_OK : UDPDK_UDP_CSUM_BAD)
                                  : (len_bad || fold32(us) != 0xFFFFu) ? UDPDK_UDP_CSUM_BAD
                                                                        : UDPDK_UDP_CSUM_OK;
             const uint32_t pre = !good ? UDPDK_V_BAD_DESC
@@ -924,7 +1046,7 @@ rx_classify(RxArgs a)
             }
             if (tail_now) {
                 tail_step(st);
-                if (!early) NW = load_win(nst, n_off, n_lp & 0xFFFFu);
+                NW = load_win(nst, n_off, n_lp & 0xFFFFu, span_n);
             }
             STAMP(6);
             // next round's descriptors into the other buffer at the wave's next-to-last step of a
@@ -932,10 +1054,7 @@ rx_classify(RxArgs a)
             // buffer were before the previous round's barrier, and the next round is first read at
             // j = SPR - 1.
             // Uniform across the workgroup (every wave has steps / 4 steps).
-            // With K2 the next round is staged one step earlier (its first step is read two steps
-            // ahead, at the round's third step); the buffer's last reads were then at the
-            // previous round's second step, before that round's barrier.
-            if ((st / CLS_WAVES) % SPR == SPR - (K2 ? 3u : 2u) && st / RSTEPS + 1u < steps / RSTEPS) {
+            if ((st / CLS_WAVES) % SPR == SPR - 2u && st / RSTEPS + 1u < steps / RSTEPS) {
                 if constexpr (MR != 0)
                     stage_store(st / RSTEPS + 1u, pf_o, pf_l, pf_t);
                 else
@@ -943,18 +1062,12 @@ rx_classify(RxArgs a)
                 __syncthreads();
                 STAMP(5);
             }
-            if constexpr (K2) {
-                W = W1;
-                W1 = NW;
-                c_off = c1_off;
-                c_lp = c1_lp;
-                c1_off = n_off;
-                c1_lp = n_lp;
-            } else {
-                W = NW;
-                c_off = n_off;
-                c_lp = n_lp;
-            }
+            W = NW;
+            c_off = n_off;
+            c_lp = n_lp;
+            span_cur = span_n;
+            span_A = n_A;
+            span_E = n_E;
             st = nst;
         }
         // ---- demux pass (not step_demux): the round's port-table lookups of this wave, all SPR
@@ -1774,11 +1887,7 @@ rx_scatterw(ScatterArgs a)
     // the tile) instead of 64 scattered words (config 5: rx_scatterw 24.5 -> 22.5 us). Otherwise
     // each delivery stores its own word (and needs every cursor now).
     const uint32_t T = a.tile_frames;
-#ifdef UDPDK_DIAG_SCATTER_DIRECT
-    const bool staged = false;
-#else
     const bool staged = (S & 1u) == 0u && 8u * T <= 4u * (W / 2) * S;   // 8-byte pairs in cnt
-#endif
     if (!staged) {
         __syncthreads();                                               // wave totals read
         if (tid < W && tid < S) cur[tid] = cur_lo;

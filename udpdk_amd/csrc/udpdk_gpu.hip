@@ -115,6 +115,7 @@ struct udpdk_gpu_ctx {
     int force_fuse = -1;           // UDPDK_RX_FUSE=0/1 (tests, A/B): fused completion off / always
     int force_tailg = 0;           // UDPDK_RX_TAILG=1/2 (tests, A/B): rx_classify<G> always
     int force_mr = -1;             // UDPDK_RX_MR=0/1 (tests, A/B): the round-ahead descriptor form
+    bool no_span = false;          // UDPDK_RX_SPAN=0 (tests, A/B): no span sweep (RxArgs::span)
     bool trace = false;            // UDPDK_RX_TRACE (diagnostic): the form of every call on stderr
     bool no_inline = false;        // UDPDK_RX_NO_INLINE (tests, A/B): always the port-table loads
     uint32_t scatter_group_frames = UDPDK_SCATTER_GROUP_FRAMES;   // UDPDK_SCATTER_GROUP_FRAMES (tests, A/B)
@@ -308,6 +309,7 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
     c->trace = getenv("UDPDK_RX_TRACE") != nullptr;
     c->no_inline = getenv("UDPDK_RX_NO_INLINE") != nullptr;
     if (const char *e = getenv("UDPDK_RX_MR")) c->force_mr = atoi(e) ? 1 : 0;
+    if (const char *e = getenv("UDPDK_RX_SPAN")) c->no_span = atoi(e) == 0;
     if (const char *e = getenv("UDPDK_SCATTER_GROUP_FRAMES")) c->scatter_group_frames = (uint32_t)atoi(e);
     if (const char *e = getenv("UDPDK_SCATTER_MIN_WG")) c->scatter_min_wg = (uint32_t)atoi(e);
     if (const char *e = getenv("UDPDK_RX_TAILG")) {
@@ -358,8 +360,11 @@ int udpdk_gpu_ctx_create(int device, uint32_t max_frames, uint32_t max_lanes, ud
         }
         if (!ok) break;
         // rx_classify needs up to 141 KiB of dynamic LDS (16384 lanes, 8192-frame tiles)
-        const int cls_lds = (int)std::min<uint32_t>(classify_lds_bytes(UDPDK_GPU_MAX_LANES, RX_TILE_MAX),
-                                                    160u * 1024u - 1024u);   // static LDS besides
+        // (+ the span sweep's ring, one-round tiles only)
+        const int cls_lds = (int)std::min<uint32_t>(
+            std::max(classify_lds_bytes(UDPDK_GPU_MAX_LANES, RX_TILE_MAX),
+                     classify_lds_bytes(UDPDK_GPU_MAX_LANES, RX_ROUND) + SPAN_LDS_BYTES),
+            160u * 1024u - 1024u);   // static LDS besides
         if (hipFuncSetAttribute((const void *)rx_classify<2, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 cls_lds) != hipSuccess) break;
         if (hipFuncSetAttribute((const void *)rx_classify<1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -719,8 +724,12 @@ int rx_on_pipe(udpdk_gpu_ctx *c, int pipe, const udpdk_rx_batch_t *bt, const udp
     // each next round's descriptors a round ahead
     const bool mr = c->force_mr >= 0 ? c->force_mr == 1 : T > (uint32_t)RX_ROUND;
     auto cls = tailg == 1 ? (mr ? rx_classify<1, 1> : rx_classify<1, 0>) : (mr ? rx_classify<2, 1> : rx_classify<2, 0>);
+    // the span sweep: the long-frame form of one-round tiles (its LDS ring after the carve)
+    const uint32_t cls_lds = classify_lds_bytes(S, T, hist16);
+    ra.span = tailg == 2 && !mr && T == (uint32_t)RX_ROUND && !c->no_span &&
+              cls_lds + SPAN_LDS_BYTES <= 160u * 1024u - 1024u ? 1u : 0u;
     HIPC(c, launch(st, ts, 0, true, true, cls, dim3(tiles),
-                   dim3(CLS_BLOCK), classify_lds_bytes(S, T, hist16), ra));
+                   dim3(CLS_BLOCK), cls_lds + (ra.span ? SPAN_LDS_BYTES : 0u), ra));
     if (fuse) return 0;                        // the last workgroup completed the lane
     if (one_lane) {
         Compact1Args ca;
