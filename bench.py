@@ -788,16 +788,27 @@ def socket_path_lines(specs=((1 << 20, 64, 1024, 5), (1 << 20, 0, 1024, 3), (1 <
                 "[port0_dst]\nmac_addr = 68:05:ca:95:fa:64\n"
                 "[gpu]\ndevice = 0\nmax_frames = 1048576\nmax_lanes = 1024\n" + gpu_extra)
         ini = f.name
+    # the 1500 B batch once more polled in one piece ([gpu] poll_chunk_mb = 0): the pipelined
+    # poll's gain against its recvfrom cost on the same box
+    ini1 = ini + ".onepiece.ini"
+    with open(ini1, "w") as f:
+        f.write(open(ini).read() + "\n[gpu]\npoll_chunk_mb = 0\n")
     try:
-        for n, fb, socks, reps in specs:
-            r = subprocess.run([exe, ini, str(n), str(fb), str(socks), str(reps)], capture_output=True,
-                               text=True, timeout=300)
+        for spec in list(specs) + [(1 << 20, 1500, 1024, 3, "one_piece")]:
+            n, fb, socks, reps = spec[:4]
+            tag = spec[4] if len(spec) > 4 else None
+            r = subprocess.run([exe, ini1 if tag else ini, str(n), str(fb), str(socks), str(reps)],
+                               capture_output=True, text=True, timeout=300)
             if r.returncode:
                 out.append({"frames": n, "frame_bytes": fb, "error": r.stderr[-300:]})
             else:
-                out.append(json.loads(r.stdout.strip().splitlines()[-1]))
+                d = json.loads(r.stdout.strip().splitlines()[-1])
+                if tag:
+                    d["poll"] = "one piece (poll_chunk_mb = 0)"
+                out.append(d)
     finally:
         os.unlink(ini)
+        os.unlink(ini1)
     return out
 
 

@@ -84,7 +84,11 @@ void udpdk_dump_payload(const char *payload, int len);
  * whose datagrams do not fit the ring is dropped, later bursts may still fit. Reassembled
  * datagrams count at the index of the fragment that completed them. Safe to call from a poller
  * thread while application threads call the socket functions. stats may be NULL. Returns 0 or
- * -1 with errno. */
+ * -1 with errno. A batch polled in one piece publishes nothing when it fails; a large batch of
+ * long frames polled in chunks ([gpu] poll_chunk_mb) may fail after its first chunks' bursts were
+ * published (each chunk's bursts go to the rings before the next chunk is admitted, as the
+ * reference's burst loop publishes each burst): a caller that retries such a batch receives those
+ * datagrams twice, so retry only what the rings did not get, or poll with poll_chunk_mb = 0. */
 int udpdk_poll_rx(const uint8_t *frames, uint64_t frames_bytes, const uint32_t *offset,
                   const uint16_t *length, const uint32_t *ptype, uint32_t n,
                   udpdk_rx_stats_t *stats);

@@ -367,3 +367,61 @@ def test_tx_datagram_larger_than_any_drain_is_dropped(api):
     frames = api.tx_drain(max_frames=4, cap=1 << 16)
     assert api.tx_dropped() == 1 and api.tx_pending() == 0
     assert len(frames) == 1 and frames[0][42:] == small
+
+
+@pytest.mark.parametrize("api", ["poll_chunk_mb = 1\npoll_chunk_min_avg = 0\nslab_count_max = 3\n"], indirect=True)
+def test_chunked_poll_slab_budget_keeps_payloads(api):
+    """The pipelined poll (1 MiB chunks) over direct datagrams to 8 sockets and 2-fragment ones
+    to a ninth, with the slab budget at three: the first chunk holds two slabs (direct and
+    reassembled payloads), so a later chunk gets at most one of its two and is dropped whole
+    (it used to drop after queueing its direct gather, which then raced the next
+    chunk's use of the same buffers). Every datagram a socket receives is byte-identical to one
+    sent to it, in send order; the dropped ones are counted in rx_nobufs."""
+    ports = list(range(10002, 10010))
+    socks = {p: api.socket() for p in [10001] + ports}
+    for p, s in socks.items():
+        assert api.bind(s, "0.0.0.0", p) == 0
+    rng = np.random.default_rng(61)
+    nd, nfr, L = 3000, 700, 2910
+    direct = F.build_frames(np.full(nd, 1000, np.uint32), rng.choice(ports, nd).astype(np.uint32), 62)
+    frag = F.frag_batch(nfr, L, 1500, seed=63)
+    whole = F.build_frames(np.full(nfr, L + 42, np.uint32), np.full(nfr, 10001, np.uint32), 63)
+    order = rng.permutation(np.r_[np.zeros(nd, int), np.ones(nfr, int)])
+    buf, offs, lens = bytearray(), [], []
+    sent = {p: [] for p in socks}
+    di = fi = 0
+    for kind in order:
+        if kind == 0:
+            o, ln = int(direct.offset[di]), int(direct.length[di])
+            port = int(direct.frames[o + 36]) << 8 | int(direct.frames[o + 37])
+            sent[port].append(bytes(direct.frames[o + 42:o + ln]))
+            offs.append(len(buf)), lens.append(ln)
+            buf += bytes(direct.frames[o:o + ln])
+            di += 1
+        else:
+            for j in (2 * fi, 2 * fi + 1):
+                o, ln = int(frag.offset[j]), int(frag.length[j])
+                offs.append(len(buf)), lens.append(ln)
+                buf += bytes(frag.frames[o:o + ln])
+            sent[10001].append(bytes(whole.frames[fi * (L + 42) + 42:(fi + 1) * (L + 42)]))
+            fi += 1
+    fr = np.zeros(len(buf) + 256, np.uint8)
+    fr[:len(buf)] = np.frombuffer(bytes(buf), np.uint8)
+    b = F.Batch(fr, np.array(offs, np.uint32), np.array(lens, np.uint16), len(buf))
+    _poll(b)
+    dropped = api.rx_nobufs()
+    assert dropped > 0
+    abi.lib().udpdk_interrupt(0)                       # recvfrom returns -1 once a ring is empty
+    got = 0
+    for p, s in socks.items():
+        want = {d: i for i, d in enumerate(sent[p])}
+        last = -1
+        while True:
+            n, data, _ = api.recvfrom(s, 4096)
+            if n < 0:
+                break
+            assert data in want, (p, n)
+            assert want[data] > last, p
+            last = want[data]
+            got += 1
+    assert got + dropped == nd + nfr

@@ -35,7 +35,15 @@ LINES = {
 }
 
 
+def split_env(name: str):
+    """'base@UDPDK_RX_SPAN=0' -> ('base', {'UDPDK_RX_SPAN': '0'}): a library variant run with extra
+    environment (the library reads its form switches at context creation)."""
+    lib, *kv = name.split("@")
+    return lib, dict(x.split("=", 1) for x in kv)
+
+
 def lib_path(name: str) -> str:
+    name = split_env(name)[0]
     if name == "base":
         return os.path.join(ROOT, "udpdk_amd", "libudpdk_amd.so")
     return os.path.join(ROOT, "tools", "var", name + ".so")
@@ -90,17 +98,17 @@ def main():
             raise SystemExit(f"missing {lib_path(n)}")
     if a.tests:
         for n in libs:
-            if n == "base":
+            if split_env(n)[0] == "base":
                 continue
-            env = dict(os.environ, UDPDK_LIB_OVERRIDE=lib_path(n), TMPDIR="/tmp")
+            env = dict(os.environ, UDPDK_LIB_OVERRIDE=lib_path(n), TMPDIR="/tmp", **split_env(n)[1])
             log = os.path.join(ROOT, "gpurun_out", f"ab_test_{n}.log")
             run([sys.executable, "-u", "-m", "pytest", *a.tests.split(), "-m", "gpu", "-x", "-q",
                  "--timeout", "120", "--timeout-method", "thread"], env, 600, log)
             print(f"tests {n}: {open(log).read().strip().splitlines()[-1]}", flush=True)
     for rep in range(a.reps):
         for n in libs:
-            env = dict(os.environ, UDPDK_LIB_OVERRIDE=lib_path(n))
-            log = os.path.join(ROOT, "gpurun_out", f"ab_{n}_r{rep}.log")
+            env = dict(os.environ, UDPDK_LIB_OVERRIDE=lib_path(n), **split_env(n)[1])
+            log = os.path.join(ROOT, "gpurun_out", f"ab_{n.replace('@', '_').replace('=', '')}_r{rep}.log")
             if a.line:
                 res = run([sys.executable, os.path.abspath(__file__), "--_line", a.line], env, a.timeout, log)
             else:

@@ -15,6 +15,10 @@
  * the rings (the first 1023 x S frames: <= 1023 datagrams per socket per batch, two batches fit a
  * 2047-entry ring), and the rate is
  * the datagrams the application received over the wall time of all reps ("overlap_mdgram_s").
+ * "host_copy_gbps": this box's rate for recvfrom's own work with no library in between: one
+ * thread copying the batch's payloads (each datagram's size, in arrival order) out of pinned
+ * memory the GPU did not touch into one small buffer, the bound of the recvfrom loop; boxes
+ * differ here by 2x, so recv_mdgram_s is read against it ("recv_over_copy").
  */
 #include <arpa/inet.h>
 #include <errno.h>
@@ -144,6 +148,37 @@ int main(int argc, char **argv)
     if (udpdk_gpu_host_alloc(udpdk_gpu_context(), bytes + 64, (void **)&fr)) { perror("host_alloc"); return 1; }
     for (uint32_t i = 0; i < n; i++) make_frame(fr + off[i], len[i], (uint16_t)(10000 + i % (uint32_t)S), i);
     static char buf[65536];                    /* up to the largest UDP payload */
+    /* the host's copy rate in recvfrom's shape: the payloads back to back in a pinned buffer as
+     * large as the batch's payloads (>= 256 MiB, beyond the caches), each copied into buf */
+    double copy_gbps = 0;
+    {
+        uint64_t pay = 0;
+        for (uint32_t i = 0; i < n; i++) pay += len[i] > 42 ? len[i] - 42u : 0u;
+        const uint64_t cb = pay > (256ull << 20) ? pay : (256ull << 20);
+        uint8_t *src = NULL;
+        if (!udpdk_gpu_host_alloc(udpdk_gpu_context(), cb, (void **)&src)) {
+            memset(src, 1, cb);
+            double best = 1e30;
+            volatile uint8_t sink = 0;
+            for (int r = 0; r < 3; r++) {
+                uint64_t o = 0, moved = 0;
+                const double c0 = now();
+                for (uint32_t i = 0; moved < cb; i = (i + 1) % n) {
+                    const uint32_t m = len[i] > 42 ? len[i] - 42u : 0u;
+                    if (o + m > cb) o = 0;
+                    memcpy(buf, src + o, m);
+                    sink ^= buf[0];
+                    o += m;
+                    moved += m ? m : 1;
+                }
+                const double dt = now() - c0;
+                if (dt < best) best = dt;
+            }
+            (void)sink;
+            copy_gbps = (double)cb / best / 1e9;
+            udpdk_gpu_host_free(udpdk_gpu_context(), src);
+        }
+    }
     double t_poll = 0, t_recv = 0;
     uint64_t got = 0, pbytes = 0;
     for (int r = 0; r < reps + 1; r++) {                        /* rep 0 warms up */
@@ -205,10 +240,11 @@ int main(int argc, char **argv)
     printf("{\"overlap_mdgram_s\": %.2f, \"overlap_batches\": %d, \"frames\": %u, \"frame_bytes\": %s, \"sockets\": %d, \"reps\": %d, "
            "\"poll_ms\": %.3f, \"recv_ms\": %.3f, \"poll_mdgram_s\": %.2f, \"recv_mdgram_s\": %.2f, "
            "\"end_to_end_mdgram_s\": %.2f, \"end_to_end_frame_gbps\": %.2f, \"delivered_per_batch\": %.0f, "
-           "\"payload_bytes_per_batch\": %.0f}\n",
+           "\"payload_bytes_per_batch\": %.0f, \"host_copy_gbps\": %.2f, \"recv_gbps\": %.2f, \"recv_over_copy\": %.3f}\n",
            oreps ? (double)ogot / (o1 - o0) / 1e6 : 0.0, oreps, n, fsz ? argv[3] : "\"IMIX\"", S, reps, 1e3 * t_poll / reps, 1e3 * t_recv / reps,
            dg / (t_poll / reps) / 1e6, dg / (t_recv / reps) / 1e6, dg / ((t_poll + t_recv) / reps) / 1e6,
-           (double)bytes / ((t_poll + t_recv) / reps) / 1e9, dg, (double)pbytes / reps);
+           (double)bytes / ((t_poll + t_recv) / reps) / 1e9, dg, (double)pbytes / reps, copy_gbps,
+           (double)pbytes / t_recv / 1e9, copy_gbps > 0 ? (double)pbytes / t_recv / 1e9 / copy_gbps : 0.0);
     udpdk_gpu_host_free(udpdk_gpu_context(), fr);
     udpdk_cleanup();
     return 0;

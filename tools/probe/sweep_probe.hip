@@ -58,6 +58,55 @@ __global__ void __launch_bounds__(256) k_span(const uint8_t *fr, uint32_t bytes,
     if (s == 0x9E3779B9u) out[threadIdx.x] = s;
 }
 
+
+// timing variants of the piece-major sweep: IF groups of 4 KiB in flight per wave; JOINT: the 4
+// waves of a workgroup sweep the span of its 4 consecutive steps together (wave w takes 1 KiB
+// block 4 k + w); XCD: tiles remapped so each XCD streams one contiguous eighth of the batch
+template <int IF, int JOINT, int XCD>
+__global__ void __launch_bounds__(256) k_var(const uint8_t *fr, uint32_t bytes, const uint32_t *off,
+                                             const uint32_t *len, uint32_t n, uint32_t *out)
+{
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(fr, bytes);
+    const uint32_t nt = gridDim.x;
+    const uint32_t tile = XCD ? (blockIdx.x % 8u) * (nt / 8u) + blockIdx.x / 8u : blockIdx.x;
+    uint32_t s = 0;
+    if (JOINT) {
+        for (uint32_t st = 0; st < 16; st += 4) {
+            const uint32_t f0 = tile * 1024 + st * 64;
+            const uint32_t fl = min(n, f0 + 256) - 1;
+            const uint32_t A = off[f0] & ~127u, E = off[fl] + len[fl];
+            for (uint32_t g = A + 1024u * w; g < E; g += 4096u * IF) {
+                __attribute__((ext_vector_type(4))) uint32_t v[IF];
+#pragma unroll
+                for (int c = 0; c < IF; ++c) {
+                    const uint32_t a = g + 4096u * c + 16u * lane;
+                    v[c] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(a < E ? a : 0xFFFFFFF0u), 0, 0);
+                }
+#pragma unroll
+                for (int c = 0; c < IF; ++c) s = sum4(v[c], s);
+            }
+        }
+    } else {
+        for (uint32_t st = w; st < 16; st += 4) {
+            const uint32_t f0 = tile * 1024 + st * 64;
+            const uint32_t fl = min(n, f0 + 64) - 1;
+            const uint32_t A = off[f0] & ~127u, E = off[fl] + len[fl];
+            for (uint32_t g = A; g < E; g += 4096u * IF) {
+                __attribute__((ext_vector_type(4))) uint32_t v[4 * IF];
+#pragma unroll
+                for (int c = 0; c < 4 * IF; ++c) {
+                    const uint32_t a = g + 1024u * c + 16u * lane;
+                    v[c] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(a < E ? a : 0xFFFFFFF0u), 0, 0);
+                }
+#pragma unroll
+                for (int c = 0; c < 4 * IF; ++c) s = sum4(v[c], s);
+            }
+        }
+    }
+    if (s == 0x9E3779B9u) out[threadIdx.x] = s;
+}
+
 __global__ void __launch_bounds__(256) k_flat(const uint4 *p, uint32_t n16, uint32_t *out)
 {
     uint32_t s = 0;
@@ -117,6 +166,25 @@ int main(int argc, char **argv)
         float ms;
         (void)hipEventElapsedTime(&ms, e0, e1);
         if (rep == 4) printf("k_flat %.1f us\n", 1e3 * ms);
+    }
+    {
+        struct V { const char *nm; void (*k)(const uint8_t *, uint32_t, const uint32_t *, const uint32_t *, uint32_t, uint32_t *); };
+        const V vs[] = {{"if1", k_var<1, 0, 0>}, {"if2", k_var<2, 0, 0>}, {"if3", k_var<3, 0, 0>},
+                        {"if2_xcd", k_var<2, 0, 1>}, {"joint2", k_var<2, 1, 0>}, {"joint4", k_var<4, 1, 0>},
+                        {"joint2_xcd", k_var<2, 1, 1>}};
+        for (const V &v : vs) {
+            float best = 1e9f;
+            for (int rep = 0; rep < 5; ++rep) {
+                (void)hipEventRecord(e0, 0);
+                hipLaunchKernelGGL(v.k, dim3(N / 1024), dim3(256), 0, 0, fr, bytes, doff, dlen, N, out);
+                (void)hipEventRecord(e1, 0);
+                (void)hipEventSynchronize(e1);
+                float ms;
+                (void)hipEventElapsedTime(&ms, e0, e1);
+                best = ms < best ? ms : best;
+            }
+            printf("k_var %-10s %.1f us (best of 5)\n", v.nm, 1e3 * best);
+        }
     }
     (void)hipDeviceSynchronize();
     printf("%s frames %u bytes %.1f MB; FETCH_SIZE (KiB) expected at x2: %.0f\n", imix ? "IMIX" : "1500B", N,

@@ -1022,14 +1022,23 @@ static int h_gather_chunk(udpdk_gpu_ctx *g, int pipe, const udpdk_rx_batch_t *b,
     const udpdk_rx_gather_t go = {gb->pay, 16u, gb->len, gb->sip, gb->spt};
     uint32_t *dacc = gb->acc;
     uint32_t *hl = g_udpdk.pc_acc;
+    /* both slabs before any GPU work is queued: a chunk dropped for want of a slab (ENOBUFS)
+     * leaves nothing in flight on its pipe that could still write gb or pc_acc, or the slab it
+     * got, while the next chunk uses them */
+    if (nad && !(*ad = h_arena_get(nad, bd))) return -1;     /* ENOBUFS (budget) or ENOMEM */
+    if (naf && !(*af = h_arena_get(naf, bf))) {
+        const int e = errno;
+        if (*ad) h_arena_put(*ad);
+        *ad = NULL;
+        errno = e;
+        return -1;
+    }
     for (int part = 0; part < 2; part++) {
         const uint32_t cnt = part ? naf : nad;
         if (!cnt) continue;
         const uint32_t *acc = part ? g_udpdk.acc_f : g_udpdk.acc_d, *offs = part ? g_udpdk.acc_fo : g_udpdk.acc_do;
         const uint64_t bytes = part ? bf : bd;
-        struct h_arena *a = h_arena_get(cnt, bytes);
-        if (!a) return -1;                             /* ENOBUFS (budget) or ENOMEM */
-        *(part ? af : ad) = a;
+        struct h_arena *a = part ? *af : *ad;
         memcpy(hl, acc, 4ull * cnt);
         memcpy(hl + cnt, offs, 4ull * cnt + 4);
         int rc;
@@ -1090,10 +1099,11 @@ static int h_poll_chunked(const uint8_t *frames, uint64_t frames_bytes, const ui
     }
     if (K < 2) return 1;
     const uint32_t L1 = lanes + 1, SL = lanes < UDPDK_MAX_SOCKETS ? lanes : UDPDK_MAX_SOCKETS;
+    /* (pinned staging that cannot be had: the one-piece poll, which stages in pageable memory) */
     if (h_grow_pinned((void **)&g_udpdk.pc_meta, &g_udpdk.pc_meta_cap, 4ull * n + 4) ||
         h_grow_pinned((void **)&g_udpdk.pc_loff, &g_udpdk.pc_loff_cap, 4ull * L1 * K) ||
         h_grow_pinned((void **)&g_udpdk.pc_lpkt, &g_udpdk.pc_lpkt_cap, 4ull * n * maxfan + 4))
-        return -1;
+        return 1;
     int rc, err = 0;
     struct h_arena *ad = NULL, *af = NULL;       /* slabs of the chunk whose gather is in flight */
     uint32_t pnad = 0, pnaf = 0;
@@ -1174,7 +1184,10 @@ static int h_poll_chunked(const uint8_t *frames, uint64_t frames_bytes, const ui
         CPROF_T(t1); CPROF_ADD(5, t0, t1); t0 = t1;
         if (nad + naf && h_gather_chunk(g, h_pipe_of(k), &staged, nad, &rb, naf, &ad, &af)) {
             if (errno != ENOBUFS) { err = errno; break; }
-            /* slab budget exhausted by datagrams still queued: this chunk's bursts are dropped */
+            /* slab budget exhausted by datagrams still queued: this chunk's bursts are dropped
+             * (h_gather_chunk queued nothing; the wait only orders the chunk's own reassembly
+             * work before the next chunk reuses the pipe's buffers) */
+            if ((rc = udpdk_gpu_pipe_wait(g, h_pipe_of(k)))) { err = -rc; break; }
             if (ad) h_arena_put(ad);
             if (af) h_arena_put(af);
             ad = af = NULL;

@@ -259,6 +259,7 @@ void h_sockets_reset(void)
     g_udpdk.txp_bytes = g_udpdk.txp_cap = 0;
     g_udpdk.tx_queued = 0;
     g_udpdk.tx_dropped = 0;
+    __atomic_store_n(&g_udpdk.rx_nobufs, 0, __ATOMIC_RELAXED);   /* per library session */
     g_udpdk.version++;
 }
 

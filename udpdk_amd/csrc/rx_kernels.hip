@@ -923,6 +923,21 @@ rx_classify(RxArgs a)
             const uint32_t nst = st + CLS_WAVES;
             uint32_t n_off, n_lp;
             Win NW;
+#ifndef UDPDK_NO_PRIO
+            // Fairness between the workgroups sharing a CU: the instruction arbiter favours higher
+            // priority, then age, so the workgroups dispatched first kept winning the memory
+            // pipeline and the launch waited for the last ones (config 3 stamps: workgroup
+            // durations 168 / 227 / 299 us at p0 / p50 / p100, all resident from the start). A wave
+            // drops a priority level each quarter of its steps, so the ones behind catch up.
+            // (Long-frame forms only: config 2's G = 1 form measured even to slightly slower.)
+            if constexpr (G == 2) {
+                const uint32_t lv = (4u * (st / CLS_WAVES)) / (steps / CLS_WAVES);
+                if (lv == 0u) __builtin_amdgcn_s_setprio(3);
+                else if (lv == 1u) __builtin_amdgcn_s_setprio(2);
+                else if (lv == 2u) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+#endif
             // a step that sweeps its span reads its window from the sweep (no window was loaded)
             if (SPAN && span_cur) {
                 W = span_sweep(st, span_A, span_E, off, len);

@@ -1002,11 +1002,15 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_process(ReasmArgs a, uint32_t 
 // TAILQ_FIRST(&tbl->lru): the valid entry with the smallest (E_LRU_CALL, E_LRU_IDX). The wave keeps
 // one minimum per lane, over the entries x with x % 64 == lane (its partition), built by one scan
 // of the table (eight entries per lane in flight per round) the first time a call needs the head.
-// A lane's minimum can only go stale one way: the entry it names is invalidated or moved to the
-// list's tail (a new key is larger than every key in the table, so no entry can appear below it).
-// A cached minimum is therefore never above its partition's true one, and the head is the
-// smallest cached minimum once that one is checked against its entry; a stale one costs a scan
-// of its own partition (entries / 64, spread over the wave), not of the table.
+// A lane's minimum goes stale in two ways. (1) The entry it names is invalidated or moved to the
+// list's tail: the head is the smallest cached minimum once that one is checked against its
+// entry, and a stale one costs a scan of its own partition (entries / 64, spread over the wave),
+// not of the table. (2) An entry is inserted into a partition whose cache holds a larger key or
+// none (~0: empty when scanned): the cache then misses it. Such an entry was created in this call
+// (a new key is larger than every key already in the table), so its start is this call's time
+// and it cannot be the expired head ip_frag_find would evict; nor can it be the head ahead of an
+// older cached entry. So the head found this way is the true head whenever an eviction needs it;
+// a rule that could evict an entry of the current call would have to refresh the cache on insert.
 struct LruMin {
     unsigned long long key;                  // this lane's partition minimum, ~0 when none
     uint32_t idx;
