@@ -19,8 +19,7 @@
 //       tile's per-lane delivery histogram (tile-major row hist[tile][lane]) and counter row;
 //       single-lane calls also write speculative lane entries and, fused, complete the lane in
 //       the last workgroup (repairing tiles that were not full). MR = 1: multi-round tiles with
-//       the next round's descriptors loaded a round ahead; MR = 2: the same with two windows
-//       in flight per wave.
+//       the next round's descriptors loaded a round ahead.
 //   rx_compact1  the single-lane completion as a second launch (fused form not taken): keeps the
 //       speculative entries up to the first tile that was not full, rewrites the rest.
 //   rx_scan_cols + rx_scatterw  general case: per-lane column scan of the tile-major histogram
@@ -428,18 +427,12 @@ rx_classify(RxArgs a)
     static_assert(G == 1 || G == 2, "one or two tail chunk groups in flight");
     // the span sweep (RxArgs::span) is compiled into the long-frame form of one-round tiles only
     constexpr bool SPAN = G == 2 && MR == 0;
-    // MR == 2: tiles of several rounds with two windows in flight per wave (W1 holds the next
-    // step's window while the one after it loads). For grids of at most a few workgroups per CU
-    // (config 5: 512 tiles, two per CU), where the registers it takes cost no occupancy and one
-    // window of prefetch per wave left the memory pipeline idle between steps.
-    constexpr bool AHEAD2 = MR == 2;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const uint32_t steps = a.tile_frames / 64;
     constexpr uint32_t RSTEPS = RX_ROUND / 64;              // steps per staging round
     constexpr uint32_t SPR = RSTEPS / CLS_WAVES;            // steps per wave per staging round
     static_assert(SPR >= 2, "round staging needs two steps per wave per round");
-    static_assert(!AHEAD2 || SPR >= 3, "two windows ahead stage the next round a step earlier");
 #ifdef UDPDK_STAMPS
     // (in LDS: a register array indexed by lane at the end went to scratch, and the scratch
     // allocation held workgroups back from starting)
@@ -583,8 +576,6 @@ rx_classify(RxArgs a)
         Ep = em;
         return true;
     };
-    Win W1;                                 // AHEAD2: the next step's window
-    uint32_t c1_off = 0, c1_lp = 0;
     bool span_cur = false;                  // the current step sweeps its span (wave-uniform)
     uint32_t span_A = 0, span_E = 0;
     {
@@ -596,11 +587,6 @@ rx_classify(RxArgs a)
         c_lp = l[0] | (has_ptype ? (t[0] & 0x10u) << 12 : 0u);
         span_cur = span_check(st, c_off, c_lp & 0xFFFFu, span_A, span_E);
         W = load_win(st, c_off, c_lp & 0xFFFFu, span_cur);
-        if constexpr (AHEAD2) {             // step w + 4: this thread's second staged descriptor
-            c1_off = o[1];
-            c1_lp = l[1] | (has_ptype ? (t[1] & 0x10u) << 12 : 0u);
-            W1 = load_win(st + CLS_WAVES, c1_off, c1_lp & 0xFFFFu);
-        }
         __builtin_amdgcn_sched_barrier(0);
         const bool inl = a.inl && tid <= UDPDK_INLINE_PORTS;
         if (tid == 0) tail_any = 0u;        // (ordered by the staging barrier)
@@ -943,13 +929,6 @@ rx_classify(RxArgs a)
             const uint32_t nst = st + CLS_WAVES;
             uint32_t n_off, n_lp;
             Win NW;
-            if constexpr (AHEAD2) {
-                // the window two steps ahead, before this step's work (its round is staged by
-                // then: the next round is staged at the round's second step, below)
-                read_desc(nst + CLS_WAVES, n_off, n_lp);
-                NW = load_win(nst + CLS_WAVES, n_off, n_lp & 0xFFFFu);
-                __builtin_amdgcn_sched_barrier(0);
-            }
 #ifndef UDPDK_NO_PRIO
             // Fairness between the workgroups sharing a CU: the instruction arbiter favours higher
             // priority, then age, so the workgroups dispatched first kept winning the memory
@@ -1046,14 +1025,11 @@ rx_classify(RxArgs a)
             // frame's tail ends in) are then still in L2 when that step's tail reads them, where a
             // window loaded a whole step earlier had left L2 by then (IMIX fetched 1.29x its bytes).
             // A next step that sweeps its span loads no window.
+            read_desc(nst, n_off, n_lp);      // in range of the buffers for any s (unused past the tile)
             uint32_t n_A = 0, n_E = 0;
-            bool span_n = false;
-            if constexpr (!AHEAD2) {
-                read_desc(nst, n_off, n_lp);  // in range of the buffers for any s (unused past the tile)
-                span_n = span_check(nst, n_off, n_lp & 0xFFFFu, n_A, n_E);
-            }
+            const bool span_n = span_check(nst, n_off, n_lp & 0xFFFFu, n_A, n_E);
             const bool tail_now = __ballot(pend) != 0ull;
-            if (!AHEAD2 && !tail_now) NW = load_win(nst, n_off, n_lp & 0xFFFFu, span_n);
+            if (!tail_now) NW = load_win(nst, n_off, n_lp & 0xFFFFu, span_n);
 
             // ---- what does not need the port entry: UDP state, flags, flag counters ----
             const uint32_t state = ucks == 0u ? UDPDK_UDP_CSUM_NONE
@@ -1091,18 +1067,15 @@ rx_classify(RxArgs a)
             }
             if (tail_now) {
                 tail_step(st);
-                if constexpr (!AHEAD2) NW = load_win(nst, n_off, n_lp & 0xFFFFu, span_n);
+                NW = load_win(nst, n_off, n_lp & 0xFFFFu, span_n);
             }
             STAMP(6);
             // next round's descriptors into the other buffer at the wave's next-to-last step of a
             // round (its steps of round r are 16 r + w + CLS_WAVES j, j < SPR): the last reads of that
             // buffer were before the previous round's barrier, and the next round is first read at
             // j = SPR - 1.
-            // Uniform across the workgroup (every wave has steps / 4 steps). AHEAD2 stages a step
-            // earlier (the round's first step is read two steps ahead, at its predecessor's third);
-            // that buffer's last reads were then at the previous round's second step, before that
-            // round's staging barrier.
-            if ((st / CLS_WAVES) % SPR == SPR - (AHEAD2 ? 3u : 2u) && st / RSTEPS + 1u < steps / RSTEPS) {
+            // Uniform across the workgroup (every wave has steps / 4 steps).
+            if ((st / CLS_WAVES) % SPR == SPR - 2u && st / RSTEPS + 1u < steps / RSTEPS) {
                 if constexpr (MR != 0)
                     stage_store(st / RSTEPS + 1u, pf_o, pf_l, pf_t);
                 else
@@ -1110,18 +1083,9 @@ rx_classify(RxArgs a)
                 __syncthreads();
                 STAMP(5);
             }
-            if constexpr (AHEAD2) {
-                W = W1;
-                W1 = NW;
-                c_off = c1_off;
-                c_lp = c1_lp;
-                c1_off = n_off;
-                c1_lp = n_lp;
-            } else {
-                W = NW;
-                c_off = n_off;
-                c_lp = n_lp;
-            }
+            W = NW;
+            c_off = n_off;
+            c_lp = n_lp;
             span_cur = span_n;
             span_A = n_A;
             span_E = n_E;
@@ -1326,7 +1290,6 @@ template __global__ void rx_classify<1, 0>(RxArgs a);
 template __global__ void rx_classify<2, 0>(RxArgs a);
 template __global__ void rx_classify<1, 1>(RxArgs a);
 template __global__ void rx_classify<2, 1>(RxArgs a);
-template __global__ void rx_classify<2, 2>(RxArgs a);
 
 
 // ------------------------------------------------------------------------------------------
