@@ -125,27 +125,23 @@ def test_reassembly_inplace_scenarios_exact(gpu_ctx, seed, buckets, entries, gro
     assert tot["done"] > 0, tot
 
 
-@pytest.mark.parametrize("payload", [2952, 2951, 4001, 5900])
-def test_reassembly_inplace_in_order(gpu_ctx, payload):
-    """Fragments of each datagram back to back and in order (frames.frag_batch, the bench's
-    workload: 2, 3 and 4 fragments, odd frame sizes so later datagrams start at odd offsets): the
-    call reassembles every datagram in place (the output batch is the input buffer) and the
-    datagrams, origins, counts and their demux equal the oracle's."""
-    from udpdk_amd import frames as FR
-    b = FR.frag_batch(3000, payload)
+def _check_frag_batch(gpu_ctx, b, n_dgrams, inplace, expect_inplace):
+    """One batch of frames.frag_batch through the GPU and the oracle at the bench's table
+    geometry: counts, datagrams, origins and their demux equal; in place when expected."""
     geometry = dict(bucket_num=0x1000, bucket_entries=16, max_cycles=1 << 40)
     abi.frag_table_create(gpu_ctx, geometry["bucket_num"], geometry["bucket_entries"], geometry["max_cycles"], 65515)
     t = O.FragTable(**geometry)
+    from udpdk_amd import frames as FR
     gpu_ctx.upload_snapshot(abi.snapshot_from_lists({abi.raw_port(FR.PORT_RECV): [(0, 0, 0)]}, 4))
     db = abi.rx_upload(gpu_ctx, b.frames, b.offset, b.length)
     db.frames_bytes = b.frames_bytes
     out = abi.rx_alloc_out(gpu_ctx, b.n, 4, 4 * b.n)
     gm = abi.rx_run(gpu_ctx, db, out)[0]
-    rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, out.meta, 0, inplace=True)
+    rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, out.meta, 0, inplace=inplace)
     wout, woo, wol, wog, wst = t.reassemble(b.frames, b.offset, b.length, gm, 0)
     gst.pop("serial"), gst.pop("sorted")
-    assert gst == wst and gst["done"] == 3000, (gst, wst)
-    assert rb.frames.ptr == db.frames.ptr                 # reassembled in place
+    assert gst == wst and gst["done"] == n_dgrams, (gst, wst)
+    assert (rb.frames.ptr == db.frames.ptr) == expect_inplace
     gbuf, goff, gln = _frames(gpu_ctx, rb)
     gorg = abi.download_ptr(gpu_ctx, origin.ptr, np.uint32, rb.n)
     assert np.array_equal(gorg, wog) and np.array_equal(gln, wol)
@@ -157,6 +153,41 @@ def test_reassembly_inplace_in_order(gpu_ctx, payload):
     for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt, out2.meta,
               out2.lane_off, out2.lane_pkt):
         x.free()
+
+
+@pytest.mark.parametrize("payload", [2952, 2951, 4001, 5900])
+def test_reassembly_inplace_in_order(gpu_ctx, payload):
+    """Fragments of each datagram back to back and in order (frames.frag_batch, the bench's
+    workload: 2, 3 and 4 fragments, odd frame sizes so later datagrams start at odd offsets): the
+    call reassembles every datagram in place (the output batch is the input buffer) and the
+    datagrams, origins, counts and their demux equal the oracle's."""
+    from udpdk_amd import frames as FR
+    _check_frag_batch(gpu_ctx, FR.frag_batch(3000, payload), 3000, True, True)
+
+
+@pytest.mark.parametrize("run,inplace", [(150, True), (150, False), (700, True), (700, False)])
+def test_reassembly_long_same_key_runs(gpu_ctx, run, inplace):
+    """`run` consecutive datagrams share one flow key (each completes before the next one's first
+    fragment, so ip_frag_find gives the next a fresh entry): one flow segment of 2 x run positions,
+    walked past its wave's and its block's positions, with completions in the next completion-list
+    chunk (150: the speculative tail counts them; in place) or in several (700: the host counts
+    again; the batch is copied). Datagrams, origins and counts equal the oracle's."""
+    from udpdk_amd import frames as FR
+    b = FR.frag_batch(3000, 2952)
+    fr = b.frames
+    for a0 in (200, 1500):                            # positions 400.. and 3000..: across 512, 3072
+        for k in range(a0, a0 + run):
+            for j in range(2):
+                o = int(b.offset[2 * k + j])
+                fr[o + 18], fr[o + 19] = a0 & 0xFF, a0 >> 8      # datagram a0's IPv4 id
+                fr[o + 24] = fr[o + 25] = 0
+                h = fr[o + 14:o + 34].astype(np.uint64)
+                c = int(h[0::2].sum() + 256 * h[1::2].sum())
+                while c >> 16:
+                    c = (c & 0xFFFF) + (c >> 16)
+                c = ~c & 0xFFFF
+                fr[o + 24], fr[o + 25] = c & 0xFF, c >> 8
+    _check_frag_batch(gpu_ctx, b, 3000, inplace, inplace and run == 150)
 
 
 @pytest.mark.parametrize("seed,buckets,entries", [(11, 4, 4), (12, 8, 2), (13, 16, 4), (14, 1, 8)])

@@ -20,19 +20,21 @@
 //   reasm_fsel_*    FRAG verdicts -> fragment list in arrival order (+ the stats block zeroed);
 //                   the count launch's extra blocks make the bucket summary: valid entries per
 //                   bucket, any expired (the table is unchanged until the analysis reads it)
-//   reasm_runs      (id << ib | index) sort keys; does every flow key form one run? (grouped)
+//   reasm_scan      does every flow key form one run (grouped)? The per-position records and,
+//                   as if grouped, each flow's walk: its completions (counted per chunk of the
+//                   completion list), whether it is complex, its outcome (see the kernel)
 //   [not grouped]   radix sort 1 by (id, index); reasm_keys: src|dst keys in that order; radix
-//                   sort 2 (stable). Grouped batches skip both: the list is already grouped
-//   reasm_prep      per sorted position: frame, key, crc32c signature, length class
-//   reasm_flows     per flow: span, pending or not, key in the table, overlap records
-//   [not grouped]   radix sort 4 + max scan + reasm_overlap: flows whose spans overlap on a
-//                   shared bucket (grouped: no two spans overlap)
+//                   sort 2 (stable); reasm_prep: the records in sorted order; reasm_flows: per
+//                   flow its span, pending or not, key in the table, overlap records; radix sort
+//                   4 + max scan + reasm_overlap: flows whose spans overlap on a shared bucket
+//                   (grouped: no two spans overlap)
 //   reasm_ec        a free entry guaranteed for every parallel flow, else all go serial
-//   reasm_process   parallel flows without the table; the rest -> serial list
+//   reasm_process   parallel flows without the table; the rest -> serial list (grouped with no
+//                   complex flow: both add up reasm_scan's results)
 //   radix sort 5    serial list by arrival; reasm_serial (one wave, the table in arrival order)
 //   radix sort 3    completions by origin (the arrival index of the completing fragment: where
 //                   the reference delivers the datagram; grouped: a select of the positions
-//                   holding one) + exclusive scan of frame sizes
+//                   holding one, reasm_clist_*) + exclusive scan of frame sizes
 //   reasm_emit      one wave per datagram: first fragment's header (total length, DF only, IPv4
 //                   checksum) + every fragment's data at its offset, from the batch or the table
 //   reasm_store     one wave per fragment left pending: its data (and header, for offset 0) into
@@ -62,13 +64,18 @@ constexpr uint32_t RS_BLOCK = 256;
 constexpr uint32_t RS_WAVES = RS_BLOCK / 64;
 constexpr uint32_t RS_HELD = 0xFFFFFFFFu;       // fragment data lives in the entry buffer
 constexpr uint32_t RS_NONE = 0xFFFFFFFFu;
-// per-call device block: stats [UDPDK_RS_N], out_bytes [1], counts [8 x u32] (u64 words)
-constexpr uint32_t RS_ZERO_WORDS = UDPDK_RS_N + 1 + 4;
+// per-call device block: stats [UDPDK_RS_N], out_bytes [1], counts [10 x u32] (u64 words)
+constexpr uint32_t RS_ZERO_WORDS = UDPDK_RS_N + 1 + 5;
 constexpr uint32_t RS_MAX_FRAG = 4;             // RTE_LIBRTE_IP_FRAG_MAX_FRAG
 #ifndef UDPDK_RS_FLOW_CHUNK
 #define UDPDK_RS_FLOW_CHUNK 512
 #endif
 constexpr uint32_t RS_FLOW_CHUNK = UDPDK_RS_FLOW_CHUNK;   // sorted positions per reasm_flows block step (1024: +7 us per call)
+// Positions per completion-list chunk (reasm_clist_*, and one reasm_scan block), 2 per thread
+// (8: +6 us per call)
+constexpr uint32_t RS_CL = 512;
+constexpr uint32_t RS_PB = 6;         // reasm_scan's outcome words per block (pblk): DROP_LEN,
+                                      // DROP_SHORT, DONE, HOLES, ERRORS, completed bytes
 
 // Bits to hold every value in [0, v]
 inline uint32_t bits_for(uint32_t v) { return v ? 32u - (uint32_t)__builtin_clz(v) : 1u; }
@@ -95,7 +102,7 @@ constexpr uint32_t PF_COMPLEX = 2;    // pending after its last fragment, key in
                                       // expired entry in one of its buckets
 constexpr uint32_t PF_SHARED = 4;     // its span overlaps another flow's on a shared bucket
 constexpr uint32_t PF_START = 8;      // the first sorted position of a flow segment
-// A flow's outcome as reasm_flows found it walking the flow on its own (reasm_process uses it
+// A flow's outcome as reasm_flows (or reasm_scan) found it walking the flow on its own (reasm_process uses it
 // for a flow that runs without the table): 6-bit counts of length-class drops, completions,
 // holes and errors, OC_OVF when a count or the completed bytes did not fit (the flow is then
 // walked again by reasm_process).
@@ -123,7 +130,10 @@ struct ReasmArgs {
     // per sorted position (reasm_prep): frame index, key, crc32c signature, and
     // len | (fragment offset / 8) << 16 | MF << 29 | class << 30 (0 ok, 1 no data, 2 too long)
     uint32_t *s_i, *s_src, *s_dst, *s_id, *s_sig, *s_meta;
-    uint32_t *counts;                  // [0] F, [1] completions, [2] store jobs
+    // [0] F, [1] overlap records, [2] serial list, [3] fallback (every flow serial), [4] not
+    // grouped, [5] in-place refused, [6] max_entries test, [7] flows the bound counts, [8] complex
+    // flows (reasm_scan), [9] a completion reasm_scan could not count (the host tail then recounts)
+    uint32_t *counts;
     unsigned long long *stats;         // [UDPDK_RS_N]
     unsigned long long *out_bytes;
     uint32_t *tab;                     // [entries][E_WORDS]
@@ -150,8 +160,20 @@ struct ReasmArgs {
     // counts (reasm_flows)
     uint32_t entries, max_entries;
     uint32_t *tab_used;
-    uint32_t hset_tag;                 // reasm_runs' run-key set tag, 1..65535
+    // The run test (grouped or not): reasm_scan writes each run's first position into its key's
+    // slot of rtab, reasm_ec reads the slots back; a run that lost its slot to another key goes
+    // into hset, an exact set (run_insert)
+    uint32_t *rtab;
+    uint32_t rmask;
+    unsigned long long *hset;
+    uint32_t hmask;
+    uint32_t hset_tag;                 // hset's tag for this call, 1..65535
     uint32_t grouped;                  // every key one run in arrival order: no span overlaps
+    uint32_t inplace;                  // udpdk_gpu_rx_reassemble_inplace: reasm_scan checks each completion
+    // reasm_scan: per completion-list chunk its completions and their bytes ([2 x chunks], zeroed
+    // by reasm_fsel_count_bsum), per block its outcome totals ([RS_PB x chunks])
+    uint32_t *cblk;
+    unsigned long long *pblk;
 };
 
 template <typename T>
@@ -191,7 +213,7 @@ __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) <<
 
 // crc32c (reflected, poly 0x82F63B78) of one dword, a byte at a time from a 256-entry table of
 // the byte steps in LDS (crc_table_init): 4 lookups instead of 32 dependent bit steps (the
-// bit-serial form was ~450 VALU instructions per fragment, a sixth of reasm_runs).
+// bit-serial form was ~450 VALU instructions per fragment, a sixth of the run test's kernel).
 __device__ __forceinline__ uint32_t crc32c_u32(const uint32_t *tab, uint32_t crc, uint32_t v)
 {
     crc ^= v;
@@ -385,29 +407,40 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_keys(ReasmArgs a, uint32_t F)
 // dv (the identity permutation the origin sort of an ungrouped batch starts from) is written by
 // reasm_prep only; the store jobs are reset by the host right before reasm_serial, the only
 // kernel that sets them (a grouped batch with no serial fragment never reads either).
-__device__ __forceinline__ void prep_record(const ReasmArgs &a, const uint32_t *crc_tab, uint32_t p, uint32_t i,
-                                            const FragHdr &h, bool with_dv)
+// len | (fragment offset / 8) << 16 | MF << 29 | class << 30 (0 ok, 1 no data, 2 too long)
+__device__ __forceinline__ uint32_t rec_meta(const ReasmArgs &a, const FragHdr &h)
 {
-        const int32_t ip_len = (int32_t)h.tl - 20;                    // l3_len = 20
-        const uint32_t ofs = (h.ff & 0x1FFFu) * 8u;
-        uint32_t cls = 0, len = 0;
-        if (ip_len <= 0) {
-            cls = 1;
-        } else {
-            len = (uint32_t)ip_len;
-            if (34u + len > h.flen || ofs + len > a.max_dgram) cls = 2;
-        }
-        uint32_t v = crc32c_u32(crc_tab, 0xeaad8405u, h.src);
-        v = crc32c_u32(crc_tab, v, h.dst);
-        v = crc32c_u32(crc_tab, v, h.id);
-        a.s_i[p] = i;
-        a.s_src[p] = h.src;
-        a.s_dst[p] = h.dst;
-        a.s_id[p] = h.id;
-        a.s_sig[p] = v;
-        a.s_meta[p] = (cls ? 0u : len) | ((h.ff & 0x1FFFu) << 16) | ((h.ff & 0x2000u) << 16) | (cls << 30);
-        if (with_dv) a.dv[p] = p;
-        a.dk[p] = RS_NONE;                                           // no completion yet
+    const int32_t ip_len = (int32_t)h.tl - 20;                        // l3_len = 20
+    const uint32_t ofs = (h.ff & 0x1FFFu) * 8u;
+    uint32_t cls = 0, len = 0;
+    if (ip_len <= 0) {
+        cls = 1;
+    } else {
+        len = (uint32_t)ip_len;
+        if (34u + len > h.flen || ofs + len > a.max_dgram) cls = 2;
+    }
+    return (cls ? 0u : len) | ((h.ff & 0x1FFFu) << 16) | ((h.ff & 0x2000u) << 16) | (cls << 30);
+}
+
+// the key's crc32c signature (ipv4_frag_hash's first hash)
+__device__ __forceinline__ uint32_t rec_sig(const uint32_t *crc_tab, const FragHdr &h)
+{
+    uint32_t v = crc32c_u32(crc_tab, 0xeaad8405u, h.src);
+    v = crc32c_u32(crc_tab, v, h.dst);
+    return crc32c_u32(crc_tab, v, h.id);
+}
+
+__device__ __forceinline__ void prep_record(const ReasmArgs &a, const uint32_t *crc_tab, uint32_t p, uint32_t i,
+                                            const FragHdr &h)
+{
+    a.s_i[p] = i;
+    a.s_src[p] = h.src;
+    a.s_dst[p] = h.dst;
+    a.s_id[p] = h.id;
+    a.s_sig[p] = rec_sig(crc_tab, h);
+    a.s_meta[p] = rec_meta(a, h);
+    a.dv[p] = p;
+    a.dk[p] = RS_NONE;                                           // no completion yet
 }
 
 __global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
@@ -418,81 +451,36 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_prep(ReasmArgs a, uint32_t F)
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
     for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
         const uint32_t i = a.order[p];
-        prep_record(a, crc_tab, p, i, frag_hdr(a, fr, i), true);
+        prep_record(a, crc_tab, p, i, frag_hdr(a, fr, i));
     }
 }
 
-__device__ __forceinline__ void run_insert(const ReasmArgs &a, unsigned long long *hset, uint32_t hmask,
-                                           uint32_t id, uint32_t src, uint32_t dst);
-
-// Over the fragment list (arrival order; F = counts[0], from the select): whether every flow key
-// forms a single run, and each position's record as reasm_prep writes it for that case (sorted
-// position = arrival position), so a grouped batch needs no reasm_prep pass over the frame
-// headers; a batch that is not grouped gets its sort keys from reasm_keys1 and its records
-// rewritten by reasm_prep after the sorts. A run's first fragment inserts a
-// 64-bit fingerprint of its key into an open-addressing set; meeting it again (the key has
-// another run, or two keys share a fingerprint) sets counts[4] and the batch takes the sorts.
-__global__ void __launch_bounds__(RS_BLOCK) reasm_runs(ReasmArgs a, unsigned long long *hset, uint32_t hmask)
+// The exact half of the run test: a run's first fragment inserts its key's 64-bit fingerprint
+// into the per-call set; meeting the same fingerprint again marks the batch not grouped
+// (counts[4]).
+// The key's slot word and its home slot. Slot word: the call's 16-bit tag above a 48-bit
+// fingerprint; a word with another tag is free (left by an earlier call), so the set needs no
+// clearing between calls (the host clears it once every 65535 calls, when the tags come round).
+__device__ __forceinline__ unsigned long long run_fp(uint32_t id, uint32_t src, uint32_t dst)
 {
-    __shared__ uint32_t crc_tab[256];
-    crc_table_init(crc_tab);
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
-    const uint32_t F = a.counts[0];
-    const uint32_t lane = __lane_id();
-    // wave-uniform loop: lane l holds position p = wave base + l, so the previous position's key
-    // comes from lane l - 1 by a shuffle (each frame header read once), lane 0 reads its own
-    for (uint32_t pb = blockIdx.x * RS_BLOCK + (threadIdx.x & ~63u); pb < F; pb += gridDim.x * RS_BLOCK) {
-        const uint32_t p = pb + lane;
-        const bool valid = p < F;
-        // lane 0's previous position (the wave before's last) is read beside its own, each level
-        // of the two chains (list, offset, header) in the same round trip: after the record's
-        // stores, those reads had three dependent round trips of their own
-        const bool prev = lane == 0u && valid && p > 0u;
-        const uint32_t i = valid ? a.frag_list[p] : 0u;
-        const uint32_t ip = prev ? a.frag_list[p - 1u] : 0u;
-        const uint32_t o = a.offset[i];
-        const uint32_t op = prev ? a.offset[ip] : 0u;
-        constexpr uint32_t OOR = 0x80000000u;
-        const uint32_t w16 = ld32(fr, o + 16), w20 = ld32(fr, o + 20);
-        FragHdr h;
-        h.src = ld32(fr, o + 26);
-        h.dst = ld32(fr, o + 30);
-        h.flen = a.length[i];
-        const uint32_t pw16 = ld32(fr, prev ? op + 16 : OOR), pws = ld32(fr, prev ? op + 26 : OOR),
-                       pwd = ld32(fr, prev ? op + 30 : OOR);
-        h.tl = bswap16(w16 & 0xFFFFu);
-        h.id = w16 >> 16;
-        h.ff = bswap16(w20 & 0xFFFFu);
-        const uint32_t id = h.id, src = h.src, dst = h.dst;
-        uint32_t pid = __shfl_up(id, 1, 64), psrc = __shfl_up(src, 1, 64), pdst = __shfl_up(dst, 1, 64);
-        if (prev) {
-            pid = pw16 >> 16;
-            psrc = pws;
-            pdst = pwd;
-        }
-        const bool start = p == 0u || pid != id || psrc != src || pdst != dst;
-        // the record's stores after the run test: its atomics' round trips would otherwise wait
-        // for them too (vmcnt counts stores, in order)
-        if (valid && start) run_insert(a, hset, hmask, id, src, dst);
-        if (valid) prep_record(a, crc_tab, p, i, h, false);
-    }
+    unsigned long long fp = ((unsigned long long)dst << 32 | src) * 0x9E3779B97F4A7C15ull;
+    fp ^= (unsigned long long)(id + 1u) * 0xC2B2AE3D27D4EB4Full;
+    return fp ^ (fp >> 29);
 }
 
-// A run's first fragment inserts its key's 64-bit fingerprint into the per-call set; meeting
-// the same fingerprint again marks the batch not grouped (counts[4]).
-__device__ __forceinline__ void run_insert(const ReasmArgs &a, unsigned long long *hset, uint32_t hmask,
-                                           uint32_t id, uint32_t src, uint32_t dst)
+// the key's slot in rtab
+__device__ __forceinline__ uint32_t run_slot(const ReasmArgs &a, uint32_t id, uint32_t src, uint32_t dst)
+{
+    return (uint32_t)(run_fp(id, src, dst) >> 32) & a.rmask;
+}
+
+__device__ __forceinline__ void run_insert(const ReasmArgs &a, uint32_t id, uint32_t src, uint32_t dst)
 {
     {
-        unsigned long long fp = ((unsigned long long)dst << 32 | src) * 0x9E3779B97F4A7C15ull;
-        fp ^= (unsigned long long)(id + 1u) * 0xC2B2AE3D27D4EB4Full;
-        fp ^= fp >> 29;
-        // slot word: the call's 16-bit tag above a 48-bit fingerprint; a word with another tag is
-        // free (left by an earlier call), so the set needs no clearing between calls (the host
-        // clears it once every 65535 calls, when the tags come round)
-        const unsigned long long tag = (unsigned long long)a.hset_tag << 48;
-        const unsigned long long val = tag | (fp >> 16);
+        unsigned long long *hset = a.hset;
+        const uint32_t hmask = a.hmask;
+        const unsigned long long fp = run_fp(id, src, dst);
+        const unsigned long long val = ((unsigned long long)a.hset_tag << 48) | (fp >> 16);
         uint32_t slot = (uint32_t)fp & hmask, k = 0;
         unsigned long long cur = ld_a(&hset[slot]);
         while (k <= hmask) {
@@ -686,14 +674,18 @@ __device__ __forceinline__ void bsum_rows(const ReasmArgs &a, uint32_t blk, uint
 }
 
 // The fragment count per select block (blocks [0, nfs)) and, in the blocks after them, the
-// bucket summary (reasm_bsum's rows): one launch at the start of a call, the table being
-// unchanged until the flow analysis reads the summary.
+// bucket summary (reasm_bsum's rows) and reasm_scan's zeroed chunk counts: one launch at the
+// start of a call, the table being unchanged until the flow analysis reads the summary.
 __global__ void __launch_bounds__(RS_BLOCK) reasm_fsel_count_bsum(ReasmArgs a, uint32_t *blk, uint32_t nfs)
 {
-    if (blockIdx.x < nfs)
+    if (blockIdx.x < nfs) {
         fsel_count_block(a.meta, a.n, blk, a.stats, blockIdx.x);
-    else
+    } else {
         bsum_rows(a, blockIdx.x - nfs, gridDim.x - nfs);
+        const uint32_t cw = 2u * ((a.n + RS_CL - 1u) / RS_CL);     // reasm_scan's chunk counts
+        for (uint32_t x = (blockIdx.x - nfs) * RS_BLOCK + threadIdx.x; x < cw; x += (gridDim.x - nfs) * RS_BLOCK)
+            a.cblk[x] = 0u;
+    }
 }
 
 // One thread per flow segment (at its first sorted position p). The flow is walked on its own,
@@ -701,10 +693,11 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_fsel_count_bsum(ReasmArgs a, u
 // indices of its first and last fragment that reaches ip_frag_find) and whether it is still
 // pending after its last one. PF_COMPLEX when it is pending, its key is in the table, or one of
 // its buckets holds an expired entry; complex flows are counted per bucket. Each flow adds one
-// (bucket << ib | tf) record per distinct bucket of its pair for the overlap test.
-// F = RS_F_DEV: a speculative launch of the grouped path, made before the host knows F or
-// whether the batch is grouped: F comes from counts[0], and the kernel does nothing when
-// reasm_runs found a key in two runs (counts[4]).
+// (bucket << ib | tf) record per distinct bucket of its pair for the overlap test. (A grouped
+// batch's flows are walked by reasm_scan.)
+// F = RS_F_DEV (reasm_ec, reasm_process): a speculative launch of the grouped path, made before
+// the host knows F or whether the batch is grouped: F comes from counts[0], and the kernel does
+// nothing when reasm_scan found a key in two runs (counts[4]).
 constexpr uint32_t RS_F_DEV = 0xFFFFFFFFu;
 __device__ __forceinline__ bool spec_f(const ReasmArgs &a, uint32_t &F)
 {
@@ -870,6 +863,8 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_overlap(ReasmArgs a, const uns
 // that could hold one of them. Otherwise every flow of the batch takes the serial path.
 __global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
 {
+    __shared__ unsigned long long s_sum[RS_WAVES][RS_PB];
+    __shared__ uint32_t s_quick;
     if (!spec_f(a, F)) return;
     // ip_frag_find's max_entries test (rte_ip_frag_table_create's max_entries, NUM_FLOWS_MAX in
     // the reference): before any add in the call, use_entries <= the entries valid at call start
@@ -884,9 +879,53 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
             a.counts[6] = 1u;
         }
     }
+    // Grouped with no complex flow: no entry is held by another flow of the call, and reasm_scan
+    // made the free-entry test (with no complex counts) for every simple flow. With no fallback
+    // either, every flow runs without the table and reasm_scan has the call's outcome: workgroup 0
+    // adds up its per-block totals, and reasm_process is not launched (the host launches it after
+    // the read-back otherwise; the words added here are cleared if the batch is not grouped).
+    const bool quick = a.grouped && a.counts[8] == 0u;
+    if (blockIdx.x == 0 && quick) {
+        if (threadIdx.x == 0) s_quick = a.counts[3] == 0u;       // after the max_entries test above
+        __syncthreads();
+        if (s_quick) {
+            const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+            unsigned long long v[RS_PB] = {0, 0, 0, 0, 0, 0};
+            for (uint32_t x = threadIdx.x; x < (F + RS_CL - 1u) / RS_CL; x += RS_BLOCK)
+#pragma unroll
+                for (uint32_t k = 0; k < RS_PB; ++k) v[k] += a.pblk[(size_t)x * RS_PB + k];
+#pragma unroll
+            for (uint32_t k = 0; k < RS_PB; ++k) {
+#pragma unroll
+                for (int d = 32; d >= 1; d >>= 1) v[k] += __shfl_xor(v[k], d, 64);
+                if (lane == 0) s_sum[w][k] = v[k];
+            }
+            __syncthreads();
+            if (threadIdx.x < RS_PB) {
+                unsigned long long t = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < RS_WAVES; ++i) t += s_sum[i][threadIdx.x];
+                constexpr uint32_t word[RS_PB] = {UDPDK_RS_DROP_LEN, UDPDK_RS_DROP_SHORT, UDPDK_RS_DONE,
+                                                  UDPDK_RS_HOLES, UDPDK_RS_ERRORS, UDPDK_RS_N};
+                if (t) atomicAdd(&a.stats[word[threadIdx.x]], t);        // [UDPDK_RS_N]: out_bytes
+            }
+        }
+    }
     for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
         const uint32_t f = a.pflag[p];
-        if (!(f & PF_TOUCH) || (f & (PF_COMPLEX | PF_SHARED))) continue;
+        if (a.grouped && (f & PF_START)) {
+            // The run test's second half: a run that finds its own position in its key's slot, or
+            // another run's of the same key (then the batch is not grouped), is done; one that
+            // lost the slot to another key goes into the exact set. Two runs of one key meet:
+            // one of them holds their common slot, or another key holds it and both are in the set.
+            const uint32_t src = a.s_src[p], dst = a.s_dst[p], id = a.s_id[p];
+            const uint32_t w = a.rtab[run_slot(a, id, src, dst)];
+            if (w != p) {
+                if (a.s_src[w] == src && a.s_dst[w] == dst && a.s_id[w] == id) a.counts[4] = 1u;
+                else run_insert(a, id, src, dst);
+            }
+        }
+        if (quick || !(f & PF_TOUCH) || (f & (PF_COMPLEX | PF_SHARED))) continue;
         const uint32_t b1 = a.sb1[p], b2 = a.sb2[p];
         int32_t fr = (int32_t)a.assoc - (int32_t)(a.bsum[b1] & 0xFFFFu) - (int32_t)a.cplx[b1];
         if (b2 != b1) fr += (int32_t)a.assoc - (int32_t)(a.bsum[b2] & 0xFFFFu) - (int32_t)a.cplx[b2];
@@ -1277,13 +1316,10 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_sizes(const ReasmDone *done, c
 }
 
 // Grouped path: the completions in position (= arrival) order and their output offsets in two
-// launches (per 2048-position block: count and bytes; then each block's base from its
+// launches (per RS_CL-position block: count and bytes; then each block's base from its
 // predecessors' totals and a block scan), instead of a rocPRIM select, a size pass and a rocPRIM
-// scan (three passes, six launches with the scans' state initialisation).
-#ifndef UDPDK_RS_CL
-#define UDPDK_RS_CL 512
-#endif
-constexpr uint32_t RS_CL = UDPDK_RS_CL;           // positions per block, 2 per thread (8: +6 us per call)
+// scan (three passes, six launches with the scans' state initialisation). The speculative tail
+// takes the counts reasm_scan made and runs reasm_clist_write alone.
 
 // The grouped path's tail (completion list, offsets, emit) launched right behind reasm_process,
 // before the host has read the call's counts back (counts == nullptr: an ordinary launch). It runs
@@ -1388,7 +1424,9 @@ __device__ __forceinline__ bool inplace_ok(const SpecTail &g, const ReasmDone &r
 __device__ __forceinline__ bool spec_tail_go(const SpecTail &g, uint32_t &F, uint32_t &C)
 {
     if (!g.counts) return true;
-    if (g.counts[4] || g.counts[2]) return false;
+    // grouped, no flow through the table (reasm_ec's quick case: counts[2] stays 0 until a later
+    // reasm_process), every completion counted by reasm_scan
+    if (g.counts[4] || g.counts[8] || g.counts[3] || g.counts[9]) return false;
     const unsigned long long c = g.stats[UDPDK_RS_DONE];
     if (!c) return false;
     F = g.counts[0];
@@ -1486,6 +1524,440 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_write(const uint32_t *dk
             offs[ec] = eb;
             ++ec;
             eb += sz[j];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// reasm_scan: the grouped path's analysis in one launch (it replaced three: the run test, the
+// flow walk of reasm_flows and the grouped tail's reasm_clist_count). One block per RS_CL
+// positions of the fragment list, each wave RS_SCAN_PW consecutive ones as two slots of 64:
+//  * the run test's first half: a run's first position into its key's slot of rtab (reasm_ec
+//    reads them back);
+//  * the per-position records reasm_prep would write (reasm_process and the serial path read
+//    them), and the same records in LDS for the walk;
+//  * reasm_flows' walk of every flow from its first position, from LDS within the wave's
+//    positions and from the frames past them, under the assumption that the batch is grouped;
+//  * per completion: its chunk's count and bytes (cblk, what reasm_clist_write starts from) and,
+//    in place, whether its fragments can be joined where they lie (else counts[5]);
+//  * per block the outcome totals (pblk), which stand for reasm_process's sum when no flow is
+//    complex, and for each simple flow reasm_ec's free-entry test with no complex flow counted.
+// When the run test finds a key in two runs (counts[4], by reasm_ec) only the records are used:
+// the host clears the counters the walk touched and the batch takes the sorts.
+constexpr uint32_t RS_SCAN_PW = 128;
+static_assert(RS_WAVES * RS_SCAN_PW == RS_CL, "a scan block's positions are one completion-list chunk");
+
+// A flow's state in registers for reasm_scan's walk (the entry words frag_apply keeps in LDS:
+// E_FSIZE, E_TOTAL, E_LAST, E_FR, E_WHERE), plus each slot's frame offset and whether that frame
+// is exactly 34 header bytes + its data (the in-place test). Static indices only.
+struct FlowReg {
+    uint32_t fsize, total, last;
+    uint32_t fr[RS_MAX_FRAG], wh[RS_MAX_FRAG], fo[RS_MAX_FRAG];
+    uint32_t okm;
+};
+
+__device__ __forceinline__ void flow_reset(FlowReg &s)
+{
+    s.fsize = 0;
+    s.total = 0xFFFFFFFFu;
+    s.last = 2;
+#pragma unroll
+    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
+        s.fr[k] = 0;
+        s.wh[k] = RS_HELD;
+    }
+}
+
+// chain_ok on the registers: the same backward walk, the inner loop unrolled over slots 3..1
+__device__ __forceinline__ bool flow_chain_ok(const FlowReg &s)
+{
+    const uint32_t first_len = s.fr[0] >> 16;
+    const uint32_t n = s.last - 1u;
+    uint32_t ofs = s.fr[1] & 0xFFFFu, curr = 1;
+    for (uint32_t guard = 0; ofs != first_len && guard < 8; ++guard) {
+        const uint32_t prev = curr;
+#pragma unroll
+        for (uint32_t i = RS_MAX_FRAG - 1u; i >= 1u; --i) {
+            if (i <= n && ofs != first_len && (s.fr[i] & 0xFFFFu) + (s.fr[i] >> 16) == ofs) {
+                curr = i;
+                ofs = s.fr[i] & 0xFFFFu;
+            }
+        }
+        if (curr == prev) return false;
+    }
+    return ofs == first_len;
+}
+
+// frag_apply on the registers (same outcomes); fo/ok: the fragment's frame offset and size test
+__device__ __forceinline__ uint32_t flow_apply(FlowReg &s, uint32_t len, uint32_t ofs, uint32_t mf, uint32_t where,
+                                               uint32_t fo, bool ok)
+{
+    uint32_t idx;
+    s.fsize += len;
+    if (ofs == 0) {
+        idx = s.fr[0] == 0 ? 0u : RS_NONE;
+    } else if (!mf) {
+        s.total = ofs + len;
+        idx = s.fr[1] == 0 ? 1u : RS_NONE;
+    } else {
+        idx = s.last;
+        if (idx < RS_MAX_FRAG) s.last = idx + 1u;
+    }
+    if (idx >= RS_MAX_FRAG) return FA_NOSLOT;
+#pragma unroll
+    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
+        if (k == idx) {
+            s.fr[k] = ofs | (len << 16);
+            s.wh[k] = where;
+            s.fo[k] = fo;
+        }
+    }
+    s.okm = (s.okm & ~(1u << idx)) | (ok ? 1u << idx : 0u);
+    if (s.fsize < s.total) return FA_KEEP;
+    const bool sized = s.fsize == s.total && s.fr[0] != 0;
+    if (sized && flow_chain_ok(s)) return FA_DONE;
+    return sized ? FA_HOLE : FA_ERR;
+}
+
+// write_done from the registers
+__device__ __forceinline__ void flow_done(const ReasmArgs &a, const FlowReg &s, uint32_t q, uint32_t i)
+{
+    ReasmDone r;
+    r.origin = i;
+    r.total = s.total;
+    r.n = s.last;
+    r.entry = RS_NONE;
+#pragma unroll
+    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
+        r.fr[k] = s.fr[k];
+        r.where[k] = s.wh[k];
+    }
+    a.done[q] = r;
+    a.dk[q] = i;
+}
+
+// inplace_ok on the registers (no fragment is held: the flow never met the table)
+__device__ __forceinline__ bool flow_inplace_ok(const FlowReg &s)
+{
+    ReasmDone r;
+    r.n = s.last;
+#pragma unroll
+    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) r.fr[k] = s.fr[k];
+    uint32_t sl[RS_MAX_FRAG];
+    const uint32_t m = data_order(r, sl);
+    if (m < 2u || (pick4(r.fr, sl[0]) & 0xFFFFu) != 0u) return false;
+    uint32_t end = 0;
+    bool ok = true;
+#pragma unroll
+    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
+        if (k >= m) break;
+        const uint32_t q = sl[k], o = pick4(s.fo, q);
+        ok = ok && ((s.okm >> q) & 1u) && (k == 0u || o == end);
+        end = o + 34u + (pick4(r.fr, q) >> 16);
+    }
+    return ok;
+}
+
+__global__ void __launch_bounds__(RS_BLOCK) reasm_scan(ReasmArgs a)
+{
+    __shared__ uint32_t crc_tab[256];
+    // per wave: each position's record (frame, meta, frame offset, frame length), and per flow
+    // start by rank its position, key, signature and bucket summary words
+    __shared__ uint32_t r_i[RS_WAVES][RS_SCAN_PW], r_m[RS_WAVES][RS_SCAN_PW], r_o[RS_WAVES][RS_SCAN_PW],
+        r_l[RS_WAVES][RS_SCAN_PW];
+    __shared__ uint32_t w_pos[RS_WAVES][RS_SCAN_PW], w_src[RS_WAVES][RS_SCAN_PW], w_dst[RS_WAVES][RS_SCAN_PW],
+        w_id[RS_WAVES][RS_SCAN_PW], w_sig[RS_WAVES][RS_SCAN_PW], w_s1[RS_WAVES][RS_SCAN_PW],
+        w_s2[RS_WAVES][RS_SCAN_PW];
+    __shared__ unsigned long long s_red[RS_WAVES][RS_PB];
+    __shared__ uint32_t s_red32[RS_WAVES][4];
+    crc_table_init(crc_tab);
+    __syncthreads();
+    const uint32_t F = a.counts[0];
+    const uint32_t b = blockIdx.x;
+    if (b * RS_CL >= F) return;                                   // the whole block
+    const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
+    const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
+    const uint32_t wb = b * RS_CL + w * RS_SCAN_PW;
+    constexpr uint32_t OOR = 0x80000000u;
+    // the two slots' fragments, each level of the chains (list, offset, header) in one round trip
+    // with lane 0's previous position (the run test's left neighbour of the wave's first)
+    uint32_t i[2], o[2], w16[2], w20[2], src[2], dst[2], fl[2], id[2];
+    bool valid[2];
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        valid[k] = wb + 64u * k + lane < F;
+        i[k] = valid[k] ? a.frag_list[wb + 64u * k + lane] : 0u;
+    }
+    const bool prev = lane == 0u && valid[0] && wb > 0u;
+    const uint32_t ip = prev ? a.frag_list[wb - 1u] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) o[k] = a.offset[i[k]];
+    const uint32_t op = prev ? a.offset[ip] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        w16[k] = ld32(fr, o[k] + 16);
+        w20[k] = ld32(fr, o[k] + 20);
+        src[k] = ld32(fr, o[k] + 26);
+        dst[k] = ld32(fr, o[k] + 30);
+        fl[k] = a.length[i[k]];
+        id[k] = w16[k] >> 16;
+    }
+    const uint32_t pw16 = ld32(fr, prev ? op + 16 : OOR), pws = ld32(fr, prev ? op + 26 : OOR),
+                   pwd = ld32(fr, prev ? op + 30 : OOR);
+    bool start[2];
+    {
+        uint32_t pid = __shfl_up(id[0], 1, 64), ps = __shfl_up(src[0], 1, 64), pd = __shfl_up(dst[0], 1, 64);
+        if (prev) {
+            pid = pw16 >> 16;
+            ps = pws;
+            pd = pwd;
+        }
+        start[0] = valid[0] && (wb + lane == 0u || pid != id[0] || ps != src[0] || pd != dst[0]);
+        uint32_t qid = __shfl_up(id[1], 1, 64), qs = __shfl_up(src[1], 1, 64), qd = __shfl_up(dst[1], 1, 64);
+        const uint32_t lid = (uint32_t)__builtin_amdgcn_readlane((int)id[0], 63),
+                       ls = (uint32_t)__builtin_amdgcn_readlane((int)src[0], 63),
+                       ld = (uint32_t)__builtin_amdgcn_readlane((int)dst[0], 63);
+        if (lane == 0u) {
+            qid = lid;
+            qs = ls;
+            qd = ld;
+        }
+        start[1] = valid[1] && (qid != id[1] || qs != src[1] || qd != dst[1]);
+    }
+    // The run test's first half (each run's first position into its key's slot of rtab: plain
+    // stores, read back by reasm_ec) and the flow's bucket summary words.
+    uint32_t sig[2], s1v[2] = {0u, 0u}, s2v[2] = {0u, 0u};
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        FragHdr h;
+        h.src = src[k];
+        h.dst = dst[k];
+        h.id = id[k];
+        sig[k] = rec_sig(crc_tab, h);
+        if (start[k]) {
+            a.rtab[run_slot(a, id[k], src[k], dst[k])] = wb + 64u * k + lane;
+            s1v[k] = a.bsum[bucket_of(a, sig[k])];
+            s2v[k] = a.bsum[bucket2_of(a, sig[k])];
+        }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        FragHdr h;
+        h.src = src[k];
+        h.dst = dst[k];
+        h.id = id[k];
+        h.tl = bswap16(w16[k] & 0xFFFFu);
+        h.ff = bswap16(w20[k] & 0xFFFFu);
+        h.flen = fl[k];
+        const uint32_t m = rec_meta(a, h);
+        const uint32_t p = wb + 64u * k + lane;
+        if (valid[k]) {
+            a.s_i[p] = i[k];
+            a.s_src[p] = src[k];
+            a.s_dst[p] = dst[k];
+            a.s_id[p] = id[k];
+            a.s_sig[p] = sig[k];
+            a.s_meta[p] = m;
+        }
+        r_i[w][64u * k + lane] = i[k];
+        r_m[w][64u * k + lane] = m;
+        r_o[w][64u * k + lane] = o[k];
+        r_l[w][64u * k + lane] = fl[k];
+    }
+    const unsigned long long m0 = __ballot(start[0]), m1 = __ballot(start[1]);
+    // The wave's flows in position order, one per lane (a wave of 2-fragment flows walks once,
+    // not once per slot): each start's position, key, signature and bucket words by its rank.
+    const uint32_t n0 = (uint32_t)__popcll(m0), S = n0 + (uint32_t)__popcll(m1);
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t p = wb + 64u * k + lane;
+        if (start[k]) {
+            const uint32_t rk = (k ? n0 : 0u) + __builtin_amdgcn_mbcnt_hi((uint32_t)((k ? m1 : m0) >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)(k ? m1 : m0), 0u));
+            w_pos[w][rk] = 64u * k + lane;
+            w_src[w][rk] = src[k];
+            w_dst[w][rk] = dst[k];
+            w_id[w][rk] = id[k];
+            w_sig[w][rk] = sig[k];
+            w_s1[w][rk] = s1v[k];
+            w_s2[w][rk] = s2v[k];
+        } else if (valid[k]) {
+            a.pflag[p] = 0u;
+        }
+    }
+    wave_sync_rs();
+    unsigned long long t_len = 0, t_short = 0, t_done = 0, t_holes = 0, t_err = 0, t_bytes = 0;
+    uint32_t t_cc = 0, t_cb = 0, t_cplx = 0, t_nb = 0;
+    const bool limit = a.max_entries < a.entries;
+#pragma unroll 1
+    for (uint32_t j = lane; j < ((S + 63u) & ~63u); j += 64u) {   // wave-uniform trip count
+        if (j >= S) continue;
+        const uint32_t p = wb + w_pos[w][j];
+        const uint32_t ksrc = w_src[w][j], kdst = w_dst[w][j], kid = w_id[w][j], ksig = w_sig[w][j];
+        FlowReg s;
+        s.okm = 0;
+        s.last = 2;
+        bool live = false;
+        uint32_t tfirst = RS_NONE;
+        uint32_t c_len = 0, c_short = 0, c_done = 0, c_holes = 0, c_err = 0;
+        unsigned long long c_bytes = 0;
+        // completions in this block's chunk, in one later chunk (x_chunk), in more (x_ovf)
+        uint32_t own_c = 0, own_b = 0, x_c = 0, x_b = 0, x_chunk = 0;
+        bool x_ovf = false;
+        uint32_t q = p;
+        for (; q < F; ++q) {
+            uint32_t m, fi, fo, ffl;
+            const uint32_t d = q - wb;
+            if (d < RS_SCAN_PW) {
+                if (q != p && (((d < 64u ? m0 >> d : m1 >> (d - 64u)) & 1ull) != 0ull)) break;
+                m = r_m[w][d];
+                fi = r_i[w][d];
+                fo = r_o[w][d];
+                ffl = r_l[w][d];
+            } else {                                                 // past the wave's positions
+                fi = a.frag_list[q];
+                fo = a.offset[fi];
+                const uint32_t x16 = ld32(fr, fo + 16), x20 = ld32(fr, fo + 20), xs = ld32(fr, fo + 26),
+                               xd = ld32(fr, fo + 30);
+                if ((x16 >> 16) != kid || xs != ksrc || xd != kdst) break;
+                FragHdr h;
+                h.src = xs;
+                h.dst = xd;
+                h.id = x16 >> 16;
+                h.tl = bswap16(x16 & 0xFFFFu);
+                h.ff = bswap16(x20 & 0xFFFFu);
+                h.flen = a.length[fi];
+                m = rec_meta(a, h);
+                ffl = h.flen;
+            }
+            const uint32_t cls = m >> 30;
+            if (cls) {
+                if (cls == 1) ++c_len;
+                else ++c_short;
+                a.dk[q] = RS_NONE;
+                continue;
+            }
+            if (tfirst == RS_NONE) tfirst = fi;
+            if (!live) flow_reset(s);
+            const uint32_t len = m & 0xFFFFu;
+            const uint32_t r = flow_apply(s, len, ((m >> 16) & 0x1FFFu) * 8u, (m >> 29) & 1u, fi, fo, ffl == 34u + len);
+            live = r == FA_KEEP;
+            if (r == FA_DONE) {
+                flow_done(a, s, q, fi);
+                ++c_done;
+                const uint32_t by = (34u + s.total + 15u) & ~15u;
+                c_bytes += by;
+                const uint32_t cq = q / RS_CL;
+                if (cq == b) {
+                    ++own_c;
+                    own_b += by;
+                } else if (x_c == 0u || cq == x_chunk) {
+                    x_chunk = cq;
+                    ++x_c;
+                    x_b += by;
+                } else {
+                    x_ovf = true;
+                }
+                if (a.inplace && !flow_inplace_ok(s)) atomicOr(&a.counts[5], 1u);      // rare
+            } else {
+                a.dk[q] = RS_NONE;
+                if (r == FA_HOLE) ++c_holes;
+                else if (r != FA_KEEP) ++c_err;
+            }
+        }
+        const bool ovf = (c_len | c_short | c_done | c_holes | c_err) > 62u || c_bytes >= (1ull << 31);
+        a.oc[p] = c_len | c_short << 6 | c_done << 12 | c_holes << 18 | c_err << 24 | (ovf ? OC_OVF : 0u);
+        a.ob[p] = (uint32_t)c_bytes;
+        t_len += c_len;
+        t_short += c_short;
+        uint32_t flag = PF_START;
+        if (tfirst != RS_NONE) {
+            flag |= PF_TOUCH | (live ? PF_COMPLEX : 0u);
+            const uint32_t bk1 = bucket_of(a, ksig), bk2 = bucket2_of(a, ksig);
+            const uint32_t s1 = w_s1[w][j], s2 = w_s2[w][j];
+            if ((s1 | s2) >> 31) {
+                flag |= PF_COMPLEX;                           // an expired entry to reclaim
+            } else if ((s1 | s2) & 0xFFFFu) {                 // is the key in the table?
+                for (uint32_t h = 0; h < 2; ++h) {
+                    const uint32_t *e = a.tab + (size_t)(h ? bk2 : bk1) * a.assoc * E_WORDS;
+                    for (uint32_t x = 0; x < a.assoc; ++x, e += E_WORDS)
+                        if (ld_a(e + E_VALID) && ld_a(e + E_SRC) == ksrc && ld_a(e + E_DST) == kdst &&
+                            ld_a(e + E_ID) == kid)
+                            flag |= PF_COMPLEX;
+                }
+            }
+            a.sb1[p] = bk1;
+            a.sb2[p] = bk2;
+            if (flag & PF_COMPLEX) {
+                atomicAdd(&a.cplx[bk1], 1u);
+                if (bk2 != bk1) atomicAdd(&a.cplx[bk2], 1u);
+                ++t_cplx;
+                if (limit) ++t_nb;
+                // a complex flow goes through the table: no completion of its own
+                if (c_done)
+                    for (uint32_t v = p; v < q; ++v) a.dk[v] = RS_NONE;
+            } else {
+                // reasm_ec's test with no complex flow: a free entry in one of its buckets
+                int32_t f0 = (int32_t)a.assoc - (int32_t)(s1 & 0xFFFFu);
+                if (bk2 != bk1) f0 += (int32_t)a.assoc - (int32_t)(s2 & 0xFFFFu);
+                if (f0 < 1) a.counts[3] = 1u;
+            }
+        }
+        if (!(flag & PF_COMPLEX)) {
+            t_done += c_done;
+            t_holes += c_holes;
+            t_err += c_err;
+            t_bytes += c_bytes;
+            t_cc += own_c;
+            t_cb += own_b;
+            if (x_c) {
+                atomicAdd(&a.cblk[2u * x_chunk], x_c);
+                atomicAdd(&a.cblk[2u * x_chunk + 1u], x_b);
+            }
+            if (x_ovf) a.counts[9] = 1u;
+        }
+        a.pflag[p] = flag;
+    }
+    // the block's totals: outcome words, its chunk's completions, complex and bound-counted flows
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        t_len += __shfl_xor(t_len, d, 64);
+        t_short += __shfl_xor(t_short, d, 64);
+        t_done += __shfl_xor(t_done, d, 64);
+        t_holes += __shfl_xor(t_holes, d, 64);
+        t_err += __shfl_xor(t_err, d, 64);
+        t_bytes += __shfl_xor(t_bytes, d, 64);
+        t_cc += __shfl_xor(t_cc, d, 64);
+        t_cb += __shfl_xor(t_cb, d, 64);
+        t_cplx += __shfl_xor(t_cplx, d, 64);
+        t_nb += __shfl_xor(t_nb, d, 64);
+    }
+    if (lane == 0) {
+        s_red[w][0] = t_len;
+        s_red[w][1] = t_short;
+        s_red[w][2] = t_done;
+        s_red[w][3] = t_holes;
+        s_red[w][4] = t_err;
+        s_red[w][5] = t_bytes;
+        s_red32[w][0] = t_cc;
+        s_red32[w][1] = t_cb;
+        s_red32[w][2] = t_cplx;
+        s_red32[w][3] = t_nb;
+    }
+    __syncthreads();
+    if (threadIdx.x < RS_PB) {
+        unsigned long long v = 0;
+#pragma unroll
+        for (uint32_t x = 0; x < RS_WAVES; ++x) v += s_red[x][threadIdx.x];
+        a.pblk[(size_t)b * RS_PB + threadIdx.x] = v;
+    } else if (threadIdx.x < RS_PB + 4u) {
+        const uint32_t j = threadIdx.x - RS_PB;
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t x = 0; x < RS_WAVES; ++x) v += s_red32[x][j];
+        if (v) {
+            if (j < 2u) atomicAdd(&a.cblk[2u * b + j], v);        // with other blocks' flows' counts
+            else atomicAdd(&a.counts[j == 2u ? 8 : 7], v);
         }
     }
 }
@@ -1994,8 +2466,11 @@ struct Reasm {
     uint32_t cap = 0;                        // fragments per call (= context max_frames)
     uint32_t *frag_list = nullptr, *v1 = nullptr, *v1s = nullptr, *v2s = nullptr;
     unsigned long long *k1 = nullptr, *k1s = nullptr, *k2 = nullptr, *k2s = nullptr;
-    uint32_t *counts = nullptr;              // device [8]: F, records, serial list, fallback, not grouped
-    unsigned long long *hset = nullptr;      // [hcap] run-key fingerprints (reasm_runs)
+    uint32_t *counts = nullptr;              // device [10] (ReasmArgs::counts)
+    unsigned long long *hset = nullptr;      // [hcap] the run test's exact set (run_insert)
+    uint32_t *rtab = nullptr;                // [2 x hcap] the run test's slots (reasm_scan, reasm_ec)
+    uint32_t *cblk = nullptr;                // [2 x chunks] reasm_scan's completion counts
+    unsigned long long *pblk = nullptr;      // [RS_PB x chunks] reasm_scan's outcome per block
     uint32_t hcap = 0;
     unsigned long long *stats = nullptr;     // device [UDPDK_RS_N]
     unsigned long long *out_bytes = nullptr;
@@ -2041,7 +2516,8 @@ void reasm_destroy(Reasm *r)
                    r->k2s, r->stats, r->done, r->jobs, r->dk, r->dks,
                    r->dv, r->perm, r->sizes, r->offs, r->tmp, r->out, r->out_off, r->out_ptype,
                    r->out_origin, r->out_len, r->pflag, r->sb1, r->sb2, r->tf, r->tl, r->oc, r->ob, r->rk, r->rks,
-                   r->rx, r->rv, r->rvs, r->bsum, r->cplx, r->tpos, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs, r->hset};
+                   r->rx, r->rv, r->rvs, r->bsum, r->cplx, r->tpos, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs, r->hset,
+                   r->cblk, r->pblk, r->rtab};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (r->host) (void)hipHostFree(r->host);
@@ -2101,6 +2577,8 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
         (e = dalloc(&r->tpos, (size_t)r->entries * RS_MAX_FRAG)) != hipSuccess ||
         (e = dalloc(&r->sl_k, C)) != hipSuccess || (e = dalloc(&r->sl_ks, C)) != hipSuccess ||
         (e = dalloc(&r->sl_v, C)) != hipSuccess || (e = dalloc(&r->sl_vs, C)) != hipSuccess ||
+        (e = dalloc(&r->cblk, 2 * (C / RS_CL + 1))) != hipSuccess ||
+        (e = dalloc(&r->pblk, RS_PB * (C / RS_CL + 1))) != hipSuccess ||
         (e = hipHostMalloc((void **)&r->host, 4096)) != hipSuccess) {
         fail(e);
         reasm_destroy(r);
@@ -2128,7 +2606,7 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
     r->tmp_bytes = std::max<size_t>(*std::max_element(t, t + 7), 256);
     r->hcap = 1024;                                         // >= 2 x fragments per call, power of 2
     while (r->hcap < 2u * r->cap) r->hcap <<= 1;
-    if ((e = dalloc(&r->hset, r->hcap)) != hipSuccess) {
+    if ((e = dalloc(&r->hset, r->hcap)) != hipSuccess || (e = dalloc(&r->rtab, 2 * (size_t)r->hcap)) != hipSuccess) {
         fail(e);
         reasm_destroy(r);
         return rc;
@@ -2190,6 +2668,9 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     a.sl_k = r->sl_k;
     a.sl_v = r->sl_v;
     a.tpos = r->tpos;
+    a.cblk = r->cblk;
+    a.pblk = r->pblk;
+    a.inplace = inplace ? 1u : 0u;
     if (++r->calls == 0) r->calls = 1;          // 0 marks entries never touched
     a.call = r->calls;
     a.entries = r->entries;
@@ -2197,7 +2678,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     a.tab_used = r->tab_used;
     a.ib = bits_for(n - 1u);
     if (!n) RS_HIP(hipMemsetAsync(r->stats, 0, RS_ZERO_WORDS * sizeof(unsigned long long), st));
-    // per-position records (written by reasm_runs for a grouped batch, else by reasm_prep after
+    // per-position records (written by reasm_scan for a grouped batch, else by reasm_prep after
     // the sorts, when the sort keys sharing their buffers are dead): cap-strided halves
     a.s_i = reinterpret_cast<uint32_t *>(r->k1);
     a.s_src = a.s_i + r->cap;
@@ -2207,6 +2688,10 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     a.s_meta = a.s_sig + r->cap;
     uint32_t hsize = 1024;                   // the run-key set: >= 2 x fragments, power of 2
     while (hsize < 2u * n && hsize < r->hcap) hsize <<= 1;
+    a.hset = r->hset;
+    a.hmask = hsize - 1u;
+    a.rtab = r->rtab;
+    a.rmask = 2u * hsize - 1u;                // >= 4 x fragments: few runs lose their slot
     // the fragment list in arrival order (F to counts[0]), then its sort keys and the run test
     size_t tb = r->tmp_bytes;
     if (n) {
@@ -2220,8 +2705,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         a.hset_tag = (a.call - 1u) % 65535u + 1u;
         if (a.hset_tag == 1u)                 // the tags come round: no word may carry one
             RS_HIP(hipMemsetAsync(r->hset, 0, (size_t)r->hcap * sizeof(unsigned long long), st));
-        const uint32_t g1 = std::max<uint32_t>(1, std::min<uint32_t>((n + RS_BLOCK - 1) / RS_BLOCK, 4096));
-        hipLaunchKernelGGL(reasm_runs, dim3(g1), dim3(RS_BLOCK), 0, st, a, r->hset, hsize - 1u);
+        hipLaunchKernelGGL(reasm_scan, dim3((n + RS_CL - 1) / RS_CL), dim3(RS_BLOCK), 0, st, a);
         RS_HIP(hipGetLastError());
     }
     // Flow analysis and the parallel flows (see the top of this file). Fk = RS_F_DEV: the
@@ -2238,11 +2722,15 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
                          bt->offset_dev, bt->length_dev};
         size_t tbt = r->tmp_bytes;
         if (grp) {
+            // speculative: the chunk counts are reasm_scan's (no flow went to the table); else
+            // counted again (the serial path's completions)
             const uint32_t nb = (Fn + RS_CL - 1) / RS_CL;
-            hipLaunchKernelGGL(reasm_clist_count, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
-                               (const ReasmDone *)r->done, Fn, r->sizes, g);
+            if (!spec)
+                hipLaunchKernelGGL(reasm_clist_count, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
+                                   (const ReasmDone *)r->done, Fn, r->sizes, g);
             hipLaunchKernelGGL(reasm_clist_write, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
-                               (const ReasmDone *)r->done, Fn, (const uint32_t *)r->sizes, r->perm, r->offs, g);
+                               (const ReasmDone *)r->done, Fn, (const uint32_t *)(spec ? r->cblk : r->sizes),
+                               r->perm, r->offs, g);
             RS_HIP(hipGetLastError());
         } else {
             const uint32_t gC = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_BLOCK - 1) / RS_BLOCK, 4096));
@@ -2283,13 +2771,22 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         RS_HIP(hipGetLastError());
         return 0;
     };
+    // at most 256 workgroups: each adds its six block totals to the call's stats words with
+    // agent-scope atomics on the same six addresses, which serialise (2048 workgroups: 27 us)
+    auto process = [&](uint32_t Fk, uint32_t Fgrid) -> int {
+        const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((Fgrid + RS_BLOCK - 1) / RS_BLOCK, 256));
+        hipLaunchKernelGGL(reasm_process, dim3(gF), dim3(RS_BLOCK), 0, st, a, Fk);
+        RS_HIP(hipGetLastError());
+        return 0;
+    };
     auto analysis = [&](uint32_t Fk, uint32_t Fgrid, bool grp) -> int {
         const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((Fgrid + RS_BLOCK - 1) / RS_BLOCK, 4096));
         // (the bucket summary: made by reasm_fsel_count_bsum at the call's start; the table and
         // the complex-flow counts are untouched until here, a speculative grouped analysis that
         // found the batch not grouped having returned at once)
+        // (grouped: the flows were walked by reasm_scan)
         const uint32_t gfl = std::max<uint32_t>(1, std::min<uint32_t>((Fgrid + RS_FLOW_CHUNK - 1) / RS_FLOW_CHUNK, 2048));
-        hipLaunchKernelGGL(reasm_flows, dim3(gfl), dim3(RS_BLOCK), 0, st, a, Fk);
+        if (!grp) hipLaunchKernelGGL(reasm_flows, dim3(gfl), dim3(RS_BLOCK), 0, st, a, Fk);
         RS_HIP(hipGetLastError());
         uint32_t R = 0;                      // overlap records (none when grouped)
         if (!grp) {
@@ -2315,10 +2812,11 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         }
         hipLaunchKernelGGL(reasm_ec, dim3(gF), dim3(RS_BLOCK), 0, st, a, Fk);
         RS_HIP(hipGetLastError());
-        // at most 256 workgroups: each adds its six block totals to the call's stats words with
-        // agent-scope atomics on the same six addresses, which serialise (2048 workgroups: 27 us)
-        hipLaunchKernelGGL(reasm_process, dim3(std::min<uint32_t>(gF, 256)), dim3(RS_BLOCK), 0, st, a, Fk);
-        RS_HIP(hipGetLastError());
+        // (grouped: reasm_process only after the read-back, for a batch with a flow through the
+        // table; reasm_ec finishes the others)
+        if (!grp) {
+            if (int e = process(Fk, Fgrid)) return e;
+        }
         if (grp && (r->out || inplace))
             if (int e = tail(true, Fgrid, Fgrid, true)) return e;
         // the serial list's size comes back with the stats and counts
@@ -2344,19 +2842,31 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
         if (int e = analysis(RS_F_DEV, n, true)) return e;
         F = hc[0];
         grouped = hc[4] == 0u;
+        // reasm_ec's quick case: no complex flow, no fallback (every flow ran without the table)
+        const bool quick = hc[8] == 0u && hc[3] == 0u;
         {
             uint64_t ob0;
             memcpy(&ob0, r->host + 2 * UDPDK_RS_N, 8);
             const uint64_t c0 = reinterpret_cast<const uint64_t *>(r->host)[UDPDK_RS_DONE];
-            const bool spec_grouped = (spec_out || inplace) && grouped && hc[2] == 0u && c0;
+            const bool spec_grouped = (spec_out || inplace) && grouped && quick && hc[9] == 0u && c0;
             in_place = inplace && spec_grouped && hc[5] == 0u;
             spec_done = in_place || (spec_out && spec_grouped && ob0 + UDPDK_GPU_FRAMES_TAILROOM <= spec_cap);
+        }
+        if (F && grouped && !quick) {          // flows through the table: the serial list, outcomes
+            if (int e = process(F, F)) return e;
+            RS_HIP(hipMemcpyAsync(r->host, r->stats, RS_ZERO_WORDS * 8, hipMemcpyDeviceToHost, st));
+            RS_HIP(hipStreamSynchronize(st));
         }
         if (F && !grouped) {
             // group by key keeping arrival order: stable sorts by (id, index), then src|dst; the
             // sort keys are then dead and their buffers take the records in sorted order
             a.grouped = 0u;
             a.order = r->v2s;
+            // what reasm_scan's walk and reasm_ec (made as if grouped) left in the shared counters
+            // and the outcome words (counts[0] = F stays)
+            RS_HIP(hipMemsetAsync(r->cplx, 0, (size_t)r->nbuckets * sizeof(uint32_t), st));
+            RS_HIP(hipMemsetAsync(r->stats, 0, (UDPDK_RS_N + 1) * sizeof(unsigned long long), st));
+            RS_HIP(hipMemsetAsync(r->counts + 2, 0, 8 * sizeof(uint32_t), st));
             const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((F + RS_BLOCK - 1) / RS_BLOCK, 4096));
             hipLaunchKernelGGL(reasm_keys1, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
             RS_HIP(hipGetLastError());
