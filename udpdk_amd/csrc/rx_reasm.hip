@@ -174,6 +174,9 @@ struct ReasmArgs {
     // by reasm_fsel_count_bsum), per block its outcome totals ([RS_PB x chunks])
     uint32_t *cblk;
     unsigned long long *pblk;
+    uint32_t *cl_perm, *cl_offs;       // the grouped completion list (reasm_clist_write's perm, offs)
+    const uint32_t *fcnt;              // FRAG frames per RS_FS frames (reasm_fsel_count_bsum)
+    uint32_t nfs;
 };
 
 template <typename T>
@@ -310,11 +313,10 @@ struct HasDone {
     __device__ bool operator()(uint32_t q) const { return dk[q] != RS_NONE; }
 };
 
-// The FRAG-verdict frames in arrival order (the fragment list, F to counts[0]) in two launches:
-// per block of RS_FS frames its FRAG count, then each block's base from its predecessors'
-// counts and a block scan. Workgroup 0 of the first also zeroes the call's stats block, so a
-// call starts with two launches where it made four (a memset and rocPRIM's select: its state
-// initialisation and two passes).
+// The FRAG-verdict frames in arrival order (the fragment list, F to counts[0]): per block of
+// RS_FS frames its FRAG count (reasm_fsel_count_bsum, whose workgroup 0 also zeroes the call's
+// stats block), then reasm_scan's blocks each find and write their own positions of the list.
+// (rocPRIM's select took a memset, its state initialisation and two passes.)
 constexpr uint32_t RS_FS = 2048;                 // frames per block, 8 per thread
 
 __device__ __forceinline__ uint32_t frag_bits8(const uint32_t *meta, uint32_t i0, uint32_t n)
@@ -349,47 +351,6 @@ __device__ __forceinline__ void fsel_count_block(const uint32_t *meta, uint32_t 
         for (uint32_t i = 0; i < RS_WAVES; ++i) t += red[i];
         blk[b] = t;
     }
-}
-
-__global__ void __launch_bounds__(RS_BLOCK) reasm_fsel_count(const uint32_t *meta, uint32_t n, uint32_t *blk,
-                                                            unsigned long long *stats_block)
-{
-    fsel_count_block(meta, n, blk, stats_block, blockIdx.x);
-}
-
-__global__ void __launch_bounds__(RS_BLOCK) reasm_fsel_write(const uint32_t *meta, uint32_t n, const uint32_t *blk,
-                                                            uint32_t *frag_list, uint32_t *counts)
-{
-    __shared__ uint32_t red[2 * RS_WAVES];
-    const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6, b = blockIdx.x;
-    uint32_t pre = 0;
-    for (uint32_t i = tid; i < b; i += RS_BLOCK) pre += blk[i];
-    const uint32_t i0 = b * RS_FS + 8u * tid;
-    const uint32_t m = frag_bits8(meta, i0, n);
-    const uint32_t c = (uint32_t)__builtin_popcount(m);
-    uint32_t inc = c;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t u = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += u;
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d, 64);
-    if (lane == 63) red[w] = inc;
-    if (lane == 0) red[RS_WAVES + w] = pre;
-    __syncthreads();
-    uint32_t pos = inc - c, base = 0, tot = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < RS_WAVES; ++i) {
-        pos += i < w ? red[i] : 0u;
-        base += red[RS_WAVES + i];
-        tot += red[i];
-    }
-    pos += base;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j)
-        if ((m >> j) & 1u) frag_list[pos++] = i0 + j;
-    if (b == gridDim.x - 1u && tid == 0) counts[0] = base + tot;     // F
 }
 
 // src | dst << 32 of the fragments in (id, index) order (the second, stable, sort key).
@@ -861,7 +822,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_overlap(ReasmArgs a, const uns
 // A flow that is neither complex nor shared runs without the table only if its ip_frag_find is
 // sure to find a free entry: its buckets' free entries at call start minus the complex flows
 // that could hold one of them. Otherwise every flow of the batch takes the serial path.
-__global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
+__device__ __forceinline__ void ec_block(const ReasmArgs &a, uint32_t F, uint32_t blk, uint32_t nblk)
 {
     __shared__ unsigned long long s_sum[RS_WAVES][RS_PB];
     __shared__ uint32_t s_quick;
@@ -872,7 +833,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
     // other flow's fragment, so that is at most the complex flows; otherwise at most the other
     // touching flows. When the bound cannot stay below max_entries, the whole batch takes the
     // serial path, which applies the test (and the LRU deletion) exactly.
-    if (blockIdx.x == 0 && threadIdx.x == 0 && a.max_entries < a.entries) {
+    if (blk == 0 && threadIdx.x == 0 && a.max_entries < a.entries) {
         const uint64_t c = (uint64_t)a.counts[7] + (a.grouped ? 1u : 0u);
         if ((uint64_t)ld_a(a.tab_used) + c > a.max_entries) {
             a.counts[3] = 1u;
@@ -885,7 +846,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
     // adds up its per-block totals, and reasm_process is not launched (the host launches it after
     // the read-back otherwise; the words added here are cleared if the batch is not grouped).
     const bool quick = a.grouped && a.counts[8] == 0u;
-    if (blockIdx.x == 0 && quick) {
+    if (blk == 0 && quick) {
         if (threadIdx.x == 0) s_quick = a.counts[3] == 0u;       // after the max_entries test above
         __syncthreads();
         if (s_quick) {
@@ -911,7 +872,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
             }
         }
     }
-    for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
+    for (uint32_t p = blk * RS_BLOCK + threadIdx.x; p < F; p += nblk * RS_BLOCK) {
         const uint32_t f = a.pflag[p];
         if (a.grouped && (f & PF_START)) {
             // The run test's second half: a run that finds its own position in its key's slot, or
@@ -931,6 +892,11 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
         if (b2 != b1) fr += (int32_t)a.assoc - (int32_t)(a.bsum[b2] & 0xFFFFu) - (int32_t)a.cplx[b2];
         if (fr < 1) a.counts[3] = 1u;
     }
+}
+
+__global__ void __launch_bounds__(RS_BLOCK) reasm_ec(ReasmArgs a, uint32_t F)
+{
+    ec_block(a, F, blockIdx.x, gridDim.x);
 }
 
 // One thread per flow segment. A flow that cannot see or be seen by another flow (not complex,
@@ -1480,14 +1446,22 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_count(const uint32_t *dk
     }
 }
 
-__global__ void __launch_bounds__(RS_BLOCK) reasm_clist_write(const uint32_t *dk, const ReasmDone *done,
-                                                             uint32_t F, const uint32_t *blk,
-                                                             uint32_t *perm, uint32_t *offs, SpecTail g)
+__device__ __forceinline__ void clist_write_block(const uint32_t *dk, const ReasmDone *done, uint32_t F,
+                                                  const uint32_t *blk, uint32_t *perm, uint32_t *offs,
+                                                  const SpecTail &g, uint32_t b, bool in_ec)
 {
     __shared__ uint32_t red[4 * RS_WAVES];
     uint32_t C_unused;
-    if (!spec_tail_go(g, F, C_unused) || blockIdx.x * RS_CL >= F) return;
-    const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6, b = blockIdx.x;
+    if (in_ec) {
+        // beside reasm_ec, which may still set counts[3], [4] and the outcome words: only
+        // reasm_scan's verdicts are final here (the emit checks the rest)
+        if (g.counts[8] || g.counts[9]) return;
+        F = g.counts[0];
+    } else if (!spec_tail_go(g, F, C_unused)) {
+        return;
+    }
+    if (b * RS_CL >= F) return;
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
     // this block's base: the earlier blocks' totals
     uint32_t pc = 0, pb = 0;
     for (uint32_t i = tid; i < b; i += RS_BLOCK) { pc += blk[2 * i]; pb += blk[2 * i + 1]; }
@@ -1526,6 +1500,25 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_write(const uint32_t *dk
             eb += sz[j];
         }
     }
+}
+
+__global__ void __launch_bounds__(RS_BLOCK) reasm_clist_write(const uint32_t *dk, const ReasmDone *done,
+                                                             uint32_t F, const uint32_t *blk,
+                                                             uint32_t *perm, uint32_t *offs, SpecTail g)
+{
+    clist_write_block(dk, done, F, blk, perm, offs, g, blockIdx.x, false);
+}
+
+// The grouped path's reasm_ec (workgroups [0, nec)) with the speculative tail's completion list
+// behind it (the workgroups after them, one per chunk: reasm_clist_write from reasm_scan's chunk
+// counts). The list needs nothing reasm_ec computes: it is written while the run test may still
+// find the batch not grouped, and the emit behind it checks that first.
+__global__ void __launch_bounds__(RS_BLOCK) reasm_ec_clist(ReasmArgs a, uint32_t nec, SpecTail g)
+{
+    if (blockIdx.x < nec)
+        ec_block(a, RS_F_DEV, blockIdx.x, nec);
+    else
+        clist_write_block(a.dk, a.done, RS_F_DEV, a.cblk, a.cl_perm, a.cl_offs, g, blockIdx.x - nec, true);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1670,13 +1663,80 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_scan(ReasmArgs a)
         w_s2[RS_WAVES][RS_SCAN_PW];
     __shared__ unsigned long long s_red[RS_WAVES][RS_PB];
     __shared__ uint32_t s_red32[RS_WAVES][4];
+    __shared__ uint32_t s_fl[RS_CL + 1];                      // the frames of positions L0 .. P1 - 1
+    __shared__ uint32_t s_x[RS_WAVES], s_j0, s_pre0, s_F;
     crc_table_init(crc_tab);
+    const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
+    const uint32_t b = blockIdx.x, P0 = b * RS_CL, tgt = P0 ? P0 - 1u : 0u;
+    // The fragment list's positions of this block (and the one before them, the run test's left
+    // neighbour) from the FRAG counts per RS_FS frames: F and the count block holding position
+    // tgt by a scan of the counts, then the FRAG frames of the count blocks from there on in
+    // order (the fragment list is written here: no launch of its own)
+    {
+        uint32_t base = 0;
+        for (uint32_t j0 = 0; j0 < a.nfs; j0 += RS_BLOCK * 8u) {       // block-uniform
+            uint32_t c[8], t = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                const uint32_t j = j0 + tid * 8u + u;
+                c[u] = j < a.nfs ? a.fcnt[j] : 0u;
+                t += c[u];
+            }
+            uint32_t wt;
+            uint32_t run = wave_excl_scan(t, &wt);
+            if (lane == 0) s_x[w] = wt;
+            __syncthreads();
+            uint32_t tot = 0;
+#pragma unroll
+            for (uint32_t x = 0; x < RS_WAVES; ++x) {
+                run += x < w ? s_x[x] : 0u;
+                tot += s_x[x];
+            }
+            run += base;
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                if (c[u] && tgt >= run && tgt < run + c[u]) {
+                    s_j0 = j0 + tid * 8u + u;
+                    s_pre0 = run;
+                }
+                run += c[u];
+            }
+            base += tot;
+            __syncthreads();
+        }
+        if (tid == 0) s_F = base;
+    }
     __syncthreads();
-    const uint32_t F = a.counts[0];
-    const uint32_t b = blockIdx.x;
-    if (b * RS_CL >= F) return;                                   // the whole block
+    const uint32_t F = s_F;
+    if (b == 0 && tid == 0) a.counts[0] = F;
+    if (P0 >= F) return;                                          // the whole block
+    const uint32_t P1 = min(P0 + RS_CL, F), L0 = tgt;
+    for (uint32_t j = s_j0, pos = s_pre0; pos < P1; ++j) {          // block-uniform
+        const uint32_t i0 = j * RS_FS + 8u * tid;
+        const uint32_t m = frag_bits8(a.meta, i0, a.n);
+        uint32_t wt;
+        uint32_t q = wave_excl_scan((uint32_t)__builtin_popcount(m), &wt);
+        if (lane == 0) s_x[w] = wt;
+        __syncthreads();
+        uint32_t tot = 0;
+#pragma unroll
+        for (uint32_t x = 0; x < RS_WAVES; ++x) {
+            q += x < w ? s_x[x] : 0u;
+            tot += s_x[x];
+        }
+        q += pos;
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) {
+            if ((m >> u) & 1u) {
+                if (q >= L0 && q < P1) s_fl[q - L0] = i0 + u;
+                ++q;
+            }
+        }
+        pos += tot;
+        __syncthreads();
+    }
+    for (uint32_t x = P0 + tid; x < P1; x += RS_BLOCK) a.frag_list[x] = s_fl[x - L0];
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
-    const uint32_t lane = __lane_id(), w = threadIdx.x >> 6;
     const uint32_t wb = b * RS_CL + w * RS_SCAN_PW;
     constexpr uint32_t OOR = 0x80000000u;
     // the two slots' fragments, each level of the chains (list, offset, header) in one round trip
@@ -1686,10 +1746,10 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_scan(ReasmArgs a)
 #pragma unroll
     for (uint32_t k = 0; k < 2; ++k) {
         valid[k] = wb + 64u * k + lane < F;
-        i[k] = valid[k] ? a.frag_list[wb + 64u * k + lane] : 0u;
+        i[k] = valid[k] ? s_fl[wb + 64u * k + lane - L0] : 0u;
     }
     const bool prev = lane == 0u && valid[0] && wb > 0u;
-    const uint32_t ip = prev ? a.frag_list[wb - 1u] : 0u;
+    const uint32_t ip = prev ? s_fl[wb - 1u - L0] : 0u;
 #pragma unroll
     for (uint32_t k = 0; k < 2; ++k) o[k] = a.offset[i[k]];
     const uint32_t op = prev ? a.offset[ip] : 0u;
@@ -1804,7 +1864,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_scan(ReasmArgs a)
         // completions in this block's chunk, in one later chunk (x_chunk), in more (x_ovf)
         uint32_t own_c = 0, own_b = 0, x_c = 0, x_b = 0, x_chunk = 0;
         bool x_ovf = false;
-        uint32_t q = p;
+        uint32_t q = p, last_fi = 0;
         for (; q < F; ++q) {
             uint32_t m, fi, fo, ffl;
             const uint32_t d = q - wb;
@@ -1815,7 +1875,12 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_scan(ReasmArgs a)
                 fo = r_o[w][d];
                 ffl = r_l[w][d];
             } else {                                                 // past the wave's positions
-                fi = a.frag_list[q];
+                if (q < P1) {
+                    fi = s_fl[q - L0];
+                } else {            // past the block's: the next FRAG frame after the previous one
+                    fi = last_fi + 1u;
+                    while ((a.meta[fi] & 0xFu) != UDPDK_V_FRAG) ++fi;
+                }
                 fo = a.offset[fi];
                 const uint32_t x16 = ld32(fr, fo + 16), x20 = ld32(fr, fo + 20), xs = ld32(fr, fo + 26),
                                xd = ld32(fr, fo + 30);
@@ -1830,6 +1895,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_scan(ReasmArgs a)
                 m = rec_meta(a, h);
                 ffl = h.flen;
             }
+            last_fi = fi;
             const uint32_t cls = m >> 30;
             if (cls) {
                 if (cls == 1) ++c_len;
@@ -2670,6 +2736,8 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     a.tpos = r->tpos;
     a.cblk = r->cblk;
     a.pblk = r->pblk;
+    a.cl_perm = r->perm;
+    a.cl_offs = r->offs;
     a.inplace = inplace ? 1u : 0u;
     if (++r->calls == 0) r->calls = 1;          // 0 marks entries never touched
     a.call = r->calls;
@@ -2695,12 +2763,12 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     // the fragment list in arrival order (F to counts[0]), then its sort keys and the run test
     size_t tb = r->tmp_bytes;
     if (n) {
-        const uint32_t nfs = (n + RS_FS - 1) / RS_FS;   // blocks of the fragment select (their
+        const uint32_t nfs = (n + RS_FS - 1) / RS_FS;   // blocks of the fragment count (their
+        a.fcnt = r->sizes;
+        a.nfs = nfs;
         const uint32_t gb = std::max<uint32_t>(1, std::min<uint32_t>((r->entries + RS_BLOCK - 1) / RS_BLOCK, 4096));
         hipLaunchKernelGGL(reasm_fsel_count_bsum, dim3(nfs + gb), dim3(RS_BLOCK), 0, st, a, r->sizes,
                            nfs);                 // counts sit in sizes, dead until the completion list)
-        hipLaunchKernelGGL(reasm_fsel_write, dim3(nfs), dim3(RS_BLOCK), 0, st, meta_dev, n,
-                           (const uint32_t *)r->sizes, r->frag_list, r->counts);
         RS_HIP(hipGetLastError());
         a.hset_tag = (a.call - 1u) % 65535u + 1u;
         if (a.hset_tag == 1u)                 // the tags come round: no word may carry one
@@ -2715,22 +2783,23 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     // Completion list + output offsets + emit (the grouped path's list by clist_count/write, else a
     // sort by origin + sizes + scan). spec: launched before the read-back (grids from the batch
     // size, counts from the device, see SpecTail).
+    const SpecTail g_spec{r->counts, r->stats, (unsigned long long)r->out_cap, inplace ? 1u : 0u, r->counts + 5,
+                          bt->offset_dev, bt->length_dev};
     auto tail = [&](bool grp, uint32_t Fn, uint32_t Cn, bool spec) -> int {
         SpecTail g{nullptr, nullptr, 0, 0u, nullptr, nullptr, nullptr};
-        if (spec)
-            g = SpecTail{r->counts, r->stats, (unsigned long long)r->out_cap, inplace ? 1u : 0u, r->counts + 5,
-                         bt->offset_dev, bt->length_dev};
+        if (spec) g = g_spec;
         size_t tbt = r->tmp_bytes;
         if (grp) {
-            // speculative: the chunk counts are reasm_scan's (no flow went to the table); else
-            // counted again (the serial path's completions)
+            // speculative: the list was written beside reasm_ec (reasm_ec_clist, from reasm_scan's
+            // chunk counts: no flow went to the table); else counted and written here (the serial
+            // path's completions)
             const uint32_t nb = (Fn + RS_CL - 1) / RS_CL;
-            if (!spec)
+            if (!spec) {
                 hipLaunchKernelGGL(reasm_clist_count, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
                                    (const ReasmDone *)r->done, Fn, r->sizes, g);
-            hipLaunchKernelGGL(reasm_clist_write, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
-                               (const ReasmDone *)r->done, Fn, (const uint32_t *)(spec ? r->cblk : r->sizes),
-                               r->perm, r->offs, g);
+                hipLaunchKernelGGL(reasm_clist_write, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
+                                   (const ReasmDone *)r->done, Fn, (const uint32_t *)r->sizes, r->perm, r->offs, g);
+            }
             RS_HIP(hipGetLastError());
         } else {
             const uint32_t gC = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_BLOCK - 1) / RS_BLOCK, 4096));
@@ -2810,7 +2879,11 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
                                (const unsigned long long *)r->rx, R);
             RS_HIP(hipGetLastError());
         }
-        hipLaunchKernelGGL(reasm_ec, dim3(gF), dim3(RS_BLOCK), 0, st, a, Fk);
+        if (grp && (r->out || inplace))
+            hipLaunchKernelGGL(reasm_ec_clist, dim3(gF + (Fgrid + RS_CL - 1) / RS_CL), dim3(RS_BLOCK), 0, st, a, gF,
+                               g_spec);
+        else
+            hipLaunchKernelGGL(reasm_ec, dim3(gF), dim3(RS_BLOCK), 0, st, a, Fk);
         RS_HIP(hipGetLastError());
         // (grouped: reasm_process only after the read-back, for a batch with a flow through the
         // table; reasm_ec finishes the others)
