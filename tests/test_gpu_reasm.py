@@ -172,10 +172,17 @@ def test_reassembly_long_same_key_runs(gpu_ctx, run, inplace):
     walked past its wave's and its block's positions, with completions in the next completion-list
     chunk (150: the speculative tail counts them; in place) or in several (700: the host counts
     again; the batch is copied). Datagrams, origins and counts equal the oracle's."""
+    b = _same_key_batch(3000, run, (200, 1500))      # positions 400.. and 3000..: across 512, 3072
+    _check_frag_batch(gpu_ctx, b, 3000, inplace, inplace and run == 150)
+
+
+def _same_key_batch(n, run, starts):
+    """frames.frag_batch(n, 2952) with datagrams a0 .. a0 + run - 1 given datagram a0's IPv4 id
+    for each a0 in starts (IPv4 header checksums redone)."""
     from udpdk_amd import frames as FR
-    b = FR.frag_batch(3000, 2952)
+    b = FR.frag_batch(n, 2952)
     fr = b.frames
-    for a0 in (200, 1500):                            # positions 400.. and 3000..: across 512, 3072
+    for a0 in starts:
         for k in range(a0, a0 + run):
             for j in range(2):
                 o = int(b.offset[2 * k + j])
@@ -187,7 +194,32 @@ def test_reassembly_long_same_key_runs(gpu_ctx, run, inplace):
                     c = (c & 0xFFFF) + (c >> 16)
                 c = ~c & 0xFFFF
                 fr[o + 24], fr[o + 25] = c & 0xFF, c >> 8
-    _check_frag_batch(gpu_ctx, b, 3000, inplace, inplace and run == 150)
+    return b
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_reassembly_sparse_fragments_long_runs(gpu_ctx, inplace):
+    """Fragments between ordinary datagrams (1-3 after each fragment), with a key reused by 300
+    consecutive datagrams: the fragment list's positions of a block come from several count
+    blocks of frames, and the long flow's walk finds its fragments past its block among the
+    other frames. Every outcome equals the oracle's; fragments that are not back to back are
+    copied, not joined in place."""
+    import types
+    from udpdk_amd import frames as FR
+    b = _same_key_batch(1200, 300, (100,))
+    other = FR.build_frames(np.full(3000, 200, np.uint32), np.full(3000, FR.PORT_RECV + 1, np.uint32), 77)
+    rng = np.random.default_rng(9)
+    fl, k = [], 0
+    for x in range(b.n):
+        o, ln = int(b.offset[x]), int(b.length[x])
+        fl.append(b.frames[o:o + ln].tobytes())
+        for _ in range(int(rng.integers(1, 4))):
+            oo, ol = int(other.offset[k % other.n]), int(other.length[k % other.n])
+            fl.append(other.frames[oo:oo + ol].tobytes())
+            k += 1
+    buf, off, ln = batch(fl)
+    sb = types.SimpleNamespace(frames=buf, offset=off, length=ln, n=len(off), frames_bytes=len(buf) - 64)
+    _check_frag_batch(gpu_ctx, sb, 1200, inplace, False)
 
 
 @pytest.mark.parametrize("seed,buckets,entries", [(11, 4, 4), (12, 8, 2), (13, 16, 4), (14, 1, 8)])
