@@ -1287,24 +1287,21 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_sizes(const ReasmDone *done, c
 // scan (three passes, six launches with the scans' state initialisation). The speculative tail
 // takes the counts reasm_scan made and runs reasm_clist_write alone.
 
-// The grouped path's tail (completion list, offsets, emit) launched right behind reasm_process,
+// The grouped path's tail (completion list and offsets beside reasm_ec, then the emit) launched
 // before the host has read the call's counts back (counts == nullptr: an ordinary launch). It runs
-// only when the batch was grouped, no fragment went to the serial list (so no fragment is held
-// or stored, and every datagram's bytes are in the batch) and the output fits the buffer; F and
+// only when the batch was grouped, no flow went through the table (so no fragment is held or
+// stored, and every datagram's bytes are in the batch) and the output fits the buffer; F and
 // the completion count then come from the device. The host re-derives the same decision from the
 // read-back and runs the tail itself otherwise, so a grouped batch makes one host round trip.
 struct SpecTail {
-    const uint32_t *counts;                      // [0] F, [2] serial list, [4] not grouped
+    const uint32_t *counts;                      // ReasmArgs::counts
     const unsigned long long *stats;             // [UDPDK_RS_DONE] completions, [UDPDK_RS_N] bytes
     unsigned long long out_cap;
-    // in place (udpdk_gpu_rx_reassemble_inplace): reasm_clist_count checks every completion's
-    // fragments (back to back in the frame buffer, in data order, no padding) and raises refuse
-    // (counts[5]) for one that is not; reasm_emit_either then moves in place if none did, and
-    // copies if one did
+    // in place (udpdk_gpu_rx_reassemble_inplace): reasm_scan checks every completion's fragments
+    // (back to back in the frame buffer, in data order, no padding) and raises refuse (counts[5])
+    // for one that is not; reasm_emit_either then moves in place if none did, and copies if one did
     uint32_t inplace;
     uint32_t *refuse;
-    const uint32_t *offset;                      // the batch's descriptors
-    const uint16_t *length;
 };
 
 // In-place emit: the header dwords of the next datagram loaded with its bytes (1), or in its own
@@ -1365,28 +1362,6 @@ __device__ __forceinline__ uint32_t data_order(const ReasmDone &r, uint32_t (&sl
     return m;
 }
 
-// Can completion r be reassembled in place? Its fragments are frames of this batch (never held:
-// the in-place tail runs only when no fragment went to the table), back to back from the first
-// in data order, each exactly 34 header bytes + its data.
-__device__ __forceinline__ bool inplace_ok(const SpecTail &g, const ReasmDone &r)
-{
-    uint32_t sl[RS_MAX_FRAG];
-    const uint32_t m = data_order(r, sl);
-    if (m < 2u || (pick4(r.fr, sl[0]) & 0xFFFFu) != 0u) return false;
-    uint32_t end = 0;
-    bool ok = true;
-#pragma unroll
-    for (uint32_t k = 0; k < RS_MAX_FRAG; ++k) {
-        if (k >= m) break;
-        const uint32_t q = sl[k], w = pick4(r.where, q);
-        if (w == RS_HELD) return false;
-        const uint32_t o = g.offset[w], ln = g.length[w];
-        ok = ok && ln == 34u + (pick4(r.fr, q) >> 16) && (k == 0u || o == end);
-        end = o + ln;
-    }
-    return ok;
-}
-
 __device__ __forceinline__ bool spec_tail_go(const SpecTail &g, uint32_t &F, uint32_t &C)
 {
     if (!g.counts) return true;
@@ -1420,19 +1395,14 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_count(const uint32_t *dk
     const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
     const uint32_t p0 = blockIdx.x * RS_CL + tid * (RS_CL / RS_BLOCK);
     uint32_t c = 0, by = 0;
-    bool refuse = false;
-    // (every position's check, not only until the first refusal: a check that depended on the
-    // one before it serialised the positions' dependent loads, three round trips each)
 #pragma unroll
     for (uint32_t j = 0; j < RS_CL / RS_BLOCK; ++j) {
         const uint32_t q = p0 + j;
         if (q < F && dk[q] != RS_NONE) {
             ++c;
             by += done_bytes(done, q);
-            if (g.inplace) refuse |= !inplace_ok(g, done[q]);
         }
     }
-    if (__ballot(refuse) && lane == 0) atomicOr(g.refuse, 1u);    // rare: one atomic per wave
     uint32_t tc, tb;
     (void)wave_excl_scan(c, &tc);
     (void)wave_excl_scan(by, &tb);
@@ -2481,7 +2451,7 @@ reasm_emit(EmitArgs a)
 }
 
 // A call that may reassemble in place: one launch takes whichever emit the device-side check
-// chose (in place unless reasm_clist_count refused it, then the copy when its buffer fits), so
+// chose (in place unless reasm_scan refused it, then the copy when its buffer fits), so
 // the call has no second, empty emit launch.
 __global__ void __launch_bounds__(RS_BLOCK) __attribute__((amdgpu_waves_per_eu(UDPDK_RS_EMIT_WPE, 8)))
 reasm_emit_either(EmitArgs a, uint8_t *frames)
@@ -2783,10 +2753,9 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     // Completion list + output offsets + emit (the grouped path's list by clist_count/write, else a
     // sort by origin + sizes + scan). spec: launched before the read-back (grids from the batch
     // size, counts from the device, see SpecTail).
-    const SpecTail g_spec{r->counts, r->stats, (unsigned long long)r->out_cap, inplace ? 1u : 0u, r->counts + 5,
-                          bt->offset_dev, bt->length_dev};
+    const SpecTail g_spec{r->counts, r->stats, (unsigned long long)r->out_cap, inplace ? 1u : 0u, r->counts + 5};
     auto tail = [&](bool grp, uint32_t Fn, uint32_t Cn, bool spec) -> int {
-        SpecTail g{nullptr, nullptr, 0, 0u, nullptr, nullptr, nullptr};
+        SpecTail g{nullptr, nullptr, 0, 0u, nullptr};
         if (spec) g = g_spec;
         size_t tbt = r->tmp_bytes;
         if (grp) {
