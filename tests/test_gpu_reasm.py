@@ -165,6 +165,44 @@ def test_reassembly_inplace_in_order(gpu_ctx, payload):
     _check_frag_batch(gpu_ctx, FR.frag_batch(3000, payload), 3000, True, True)
 
 
+def _frames_flat(buf, off, ln):
+    """The bytes of frames (off, ln) of buf, concatenated (vectorised)."""
+    off = off.astype(np.int64)
+    ln = ln.astype(np.int64)
+    starts = np.repeat(off - np.concatenate(([0], np.cumsum(ln)[:-1])), ln)
+    return buf[starts + np.arange(int(ln.sum()))]
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+def test_reassembly_at_capacity(gpu_ctx, inplace):
+    """The context's largest batch (2^22 frames: 2^21 two-fragment datagrams at MTU 68, so
+    every FRAG count block and scan block of the grouped path is full): counts, origins, lengths
+    and every datagram byte equal the oracle's; in place when asked."""
+    from udpdk_amd import frames as FR
+    n_d = 1 << 21
+    b = FR.frag_batch(n_d, 60, mtu=68)
+    assert b.n == 1 << 22
+    geometry = dict(bucket_num=0x1000, bucket_entries=16, max_cycles=1 << 40)
+    abi.frag_table_create(gpu_ctx, geometry["bucket_num"], geometry["bucket_entries"], geometry["max_cycles"], 65515)
+    t = O.FragTable(**geometry)
+    gpu_ctx.upload_snapshot(abi.snapshot_from_lists({abi.raw_port(FR.PORT_RECV): [(0, 0, 0)]}, 4))
+    db = abi.rx_upload(gpu_ctx, b.frames, b.offset, b.length)
+    db.frames_bytes = b.frames_bytes
+    out = abi.rx_alloc_out(gpu_ctx, b.n, 4, 4 * b.n)
+    gm = abi.rx_run(gpu_ctx, db, out)[0]
+    rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, out.meta, 0, inplace=inplace)
+    wout, woo, wol, wog, wst = t.reassemble(b.frames, b.offset, b.length, gm, 0)
+    gst.pop("serial"), gst.pop("sorted")
+    assert gst == wst and gst["done"] == n_d, (gst, wst)
+    assert (rb.frames.ptr == db.frames.ptr) == inplace
+    gbuf, goff, gln = _frames(gpu_ctx, rb)
+    gorg = abi.download_ptr(gpu_ctx, origin.ptr, np.uint32, rb.n)
+    assert np.array_equal(gorg, wog) and np.array_equal(gln, wol)
+    assert np.array_equal(_frames_flat(gbuf, goff, gln), _frames_flat(wout, woo, wol))
+    for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt):
+        x.free()
+
+
 @pytest.mark.parametrize("run,inplace", [(150, True), (150, False), (700, True), (700, False)])
 def test_reassembly_long_same_key_runs(gpu_ctx, run, inplace):
     """`run` consecutive datagrams share one flow key (each completes before the next one's first
