@@ -1285,7 +1285,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_sizes(const ReasmDone *done, c
 // launches (per RS_CL-position block: count and bytes; then each block's base from its
 // predecessors' totals and a block scan), instead of a rocPRIM select, a size pass and a rocPRIM
 // scan (three passes, six launches with the scans' state initialisation). The speculative tail
-// takes the counts reasm_scan made and runs reasm_clist_write alone.
+// takes the counts reasm_scan made and runs reasm_clist_write beside reasm_ec (reasm_ec_clist).
 
 // The grouped path's tail (completion list and offsets beside reasm_ec, then the emit) launched
 // before the host has read the call's counts back (counts == nullptr: an ordinary launch). It runs
@@ -1492,9 +1492,11 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_ec_clist(ReasmArgs a, uint32_t
 }
 
 // ------------------------------------------------------------------------------------------
-// reasm_scan: the grouped path's analysis in one launch (it replaced three: the run test, the
-// flow walk of reasm_flows and the grouped tail's reasm_clist_count). One block per RS_CL
-// positions of the fragment list, each wave RS_SCAN_PW consecutive ones as two slots of 64:
+// reasm_scan: the grouped path's analysis in one launch (it replaced four: the fragment list's
+// write pass, the run test, the flow walk of reasm_flows and the grouped tail's
+// reasm_clist_count). One block per RS_CL positions of the fragment list, each wave RS_SCAN_PW
+// consecutive ones as two slots of 64:
+//  * the block's positions of the fragment list, found from the FRAG counts (and written);
 //  * the run test's first half: a run's first position into its key's slot of rtab (reasm_ec
 //    reads them back);
 //  * the per-position records reasm_prep would write (reasm_process and the serial path read
