@@ -203,6 +203,52 @@ def test_reassembly_at_capacity(gpu_ctx, inplace):
         x.free()
 
 
+def _reorder(b, order):
+    """The frames of batch b in the given order, packed again (a Batch-like namespace)."""
+    import types
+    buf, off, ln = batch([b.frames[int(b.offset[x]):int(b.offset[x]) + int(b.length[x])].tobytes() for x in order])
+    return types.SimpleNamespace(frames=buf, offset=off, length=ln, n=len(off), frames_bytes=len(buf) - 64)
+
+
+@pytest.mark.parametrize("case", ["split_last", "split_first", "shuffled"])
+def test_reassembly_run_test_at_scale(gpu_ctx, case):
+    """40 000 fragments over many reasm_scan blocks with one key split into two runs far apart
+    (a datagram's last or first fragment moved to the batch's end), or the whole batch shuffled:
+    the run test must find the batch not grouped (the sorted path, "sorted" = 1) and every outcome
+    equals the oracle's."""
+    from udpdk_amd import frames as FR
+    b = FR.frag_batch(20000, 2952)
+    order = list(range(b.n))
+    if case == "split_last":
+        order.remove(2 * 12345 + 1)
+        order.append(2 * 12345 + 1)
+    elif case == "split_first":
+        order.remove(2 * 7)
+        order.append(2 * 7)
+    else:
+        order = list(np.random.default_rng(3).permutation(b.n))
+    sb = _reorder(b, order)
+    geometry = dict(bucket_num=0x1000, bucket_entries=16, max_cycles=1 << 40)
+    abi.frag_table_create(gpu_ctx, geometry["bucket_num"], geometry["bucket_entries"], geometry["max_cycles"], 65515)
+    t = O.FragTable(**geometry)
+    gpu_ctx.upload_snapshot(abi.snapshot_from_lists({abi.raw_port(FR.PORT_RECV): [(0, 0, 0)]}, 4))
+    db = abi.rx_upload(gpu_ctx, sb.frames, sb.offset, sb.length)
+    db.frames_bytes = sb.frames_bytes
+    out = abi.rx_alloc_out(gpu_ctx, sb.n, 4, 4 * sb.n)
+    gm = abi.rx_run(gpu_ctx, db, out)[0]
+    rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, out.meta, 0)
+    wout, woo, wol, wog, wst = t.reassemble(sb.frames, sb.offset, sb.length, gm, 0)
+    gst.pop("serial")
+    assert gst.pop("sorted") == 1
+    assert gst == wst and gst["done"] == 20000, (gst, wst)
+    gbuf, goff, gln = _frames(gpu_ctx, rb)
+    gorg = abi.download_ptr(gpu_ctx, origin.ptr, np.uint32, rb.n)
+    assert np.array_equal(gorg, wog) and np.array_equal(gln, wol)
+    assert np.array_equal(_frames_flat(gbuf, goff, gln), _frames_flat(wout, woo, wol))
+    for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt):
+        x.free()
+
+
 @pytest.mark.parametrize("run,inplace", [(150, True), (150, False), (700, True), (700, False)])
 def test_reassembly_long_same_key_runs(gpu_ctx, run, inplace):
     """`run` consecutive datagrams share one flow key (each completes before the next one's first
