@@ -25,9 +25,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LINES = {
     "tx": "for plen in (22, 1458): out(bench.tx_line(ctx, plen, 1 << 20, 50))",
     "txfrag": "out(bench.tx_line(ctx, 2952, 1 << 18, 50, mtu=1500))",
+    "txsize": "for n in (1 << 17, 1 << 18, 1 << 19, 1 << 20): out(bench.tx_line(ctx, 1458, n, 50))",
     "rss": "for cfg in (2, 5): out(bench.rss_line(ctx, cfg, 8, 50))",
     "reasm": "out(bench.reasm_line(ctx, 1 << 18, 2952, 10))",
     "reasmip": "out(bench.reasm_inplace_line(ctx, 1 << 18, 2952, 10))",
+    "reasmx": "import reasm_probe_x\nreasm_probe_x.run(ctx, out)",
     "gather": "for cfg in (2, 3): out(bench.gather_line(ctx, cfg, 50))\n"
               "out(bench.gather_line(ctx, 2, 50, slot=0))",
     "sporadic": "out(bench.sporadic_line(ctx, 180, 640 << 20))",

@@ -2,7 +2,7 @@
 in-place reassembly's size achieves, as the ceiling for reasm_emit_inplace's moved bytes."""
 import torch
 
-for mb in (386, 1024, 1500):
+for mb in (128, 256, 386, 512, 768, 1024, 1500):
     n = mb << 20
     x = torch.empty(n, dtype=torch.uint8, device="cuda")
     y = torch.empty_like(x)
