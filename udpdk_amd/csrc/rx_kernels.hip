@@ -929,7 +929,6 @@ rx_classify(RxArgs a)
             const uint32_t nst = st + CLS_WAVES;
             uint32_t n_off, n_lp;
             Win NW;
-#ifndef UDPDK_NO_PRIO
             // Fairness between the workgroups sharing a CU: the instruction arbiter favours higher
             // priority, then age, so the workgroups dispatched first kept winning the memory
             // pipeline and the launch waited for the last ones (config 3 stamps: workgroup
@@ -943,7 +942,6 @@ rx_classify(RxArgs a)
                 else if (lv == 2u) __builtin_amdgcn_s_setprio(1);
                 else __builtin_amdgcn_s_setprio(0);
             }
-#endif
             // a step that sweeps its span reads its window from the sweep (no window was loaded)
             if (SPAN && span_cur) {
                 W = span_sweep(st, span_A, span_E, off, len);

@@ -1304,11 +1304,8 @@ struct SpecTail {
     uint32_t *refuse;
 };
 
-// In-place emit: the header dwords of the next datagram loaded with its bytes (1), or in its own
-// step (0: 8 VGPRs fewer); waves per SIMD of the emit launches.
-#ifndef UDPDK_RS_HWPF
-#define UDPDK_RS_HWPF 1
-#endif
+// Waves per SIMD of the emit launches (the in-place emit loads the next datagram's header dwords
+// with its bytes: loaded in their own step instead, 8 VGPRs fewer, measured slower).
 #ifndef UDPDK_RS_EMIT_WPE
 #define UDPDK_RS_EMIT_WPE 7
 #endif
@@ -2256,9 +2253,7 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
         uint4 x[2];
         uint32_t hi[2];
         uint4 orig;                          // lane 0: the 16 bytes at D0 before the move
-#if UDPDK_RS_HWPF
         uint32_t hw[6];                      // lane 0: header dwords from the one at or below byte 14
-#endif
     };
     auto quick_geom = [&](const ReasmDone &x, const uint32_t (&o)[RS_MAX_FRAG], const uint32_t (&sx)[RS_MAX_FRAG],
                           uint32_t mx, bool have, Quick &g) -> bool {
@@ -2279,12 +2274,7 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
         hw[0] = h4.x; hw[1] = h4.y; hw[2] = h4.z; hw[3] = h4.w; hw[4] = h2[0]; hw[5] = h2[1];
     };
     auto quick_load = [&](Quick &g, bool on, bool have, uint32_t o0) {
-#if UDPDK_RS_HWPF
         header_load(g.hw, have, o0);
-#else
-        (void)have;
-        (void)o0;
-#endif
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t c = 64u * u + lane;
@@ -2316,12 +2306,7 @@ __device__ __forceinline__ void emit_inplace(const EmitArgs &a, uint8_t *frames,
         if (k + stride < C) mn = offsets(rn, fon, sln);
         if (k + 2u * stride < C) rnn = cload(&a.done[cload(&a.perm[k + 2u * stride])]);
         const uint32_t o0 = fo[0], hs = (o0 + 14u) & 3u;
-#if UDPDK_RS_HWPF
         const uint32_t (&hw)[6] = qc.hw;
-#else
-        uint32_t hw[6];                                          // issued with this step's loads
-        header_load(hw, true, o0);
-#endif
         const bool qn_on = quick_geom(rn, fon, sln, mn, k + stride < C, qn);
         quick_load(qn, qn_on, k + stride < C, fon[0]);             // the next datagram in flight
         // (pinned: the scheduler otherwise hoists this datagram's first uses, and their waits,
