@@ -249,6 +249,44 @@ def test_reassembly_run_test_at_scale(gpu_ctx, case):
         x.free()
 
 
+@pytest.mark.parametrize("cc", [1, 0])
+@pytest.mark.parametrize("buckets,entries", [(512, 16), (64, 4)])
+def test_reassembly_interleaved_serial_components(gpu_ctx, monkeypatch, cc, buckets, entries):
+    """Pairs of flows interleaved (A1 B1 A2 B2 over 20 000 datagrams, then a second batch with the
+    pairs' order reversed): flows whose spans overlap on a shared bucket go through the table. With
+    UDPDK_RS_CC (default) the serial fragments are split by bucket component, one wave per
+    component; without, one wave takes them all. Both equal the oracle exactly, in roomy and
+    crowded tables (entries expire, held fragments, no space)."""
+    from udpdk_amd import frames as FR
+    monkeypatch.setenv("UDPDK_RS_CC", str(cc))
+    b = FR.frag_batch(20000, 2952)
+    pairs = np.arange(b.n).reshape(-1, 2, 2)
+    geometry = dict(bucket_num=buckets, bucket_entries=entries, max_cycles=20)
+    abi.frag_table_create(gpu_ctx, geometry["bucket_num"], geometry["bucket_entries"], geometry["max_cycles"], 65515)
+    t = O.FragTable(**geometry)
+    gpu_ctx.upload_snapshot(abi.snapshot_from_lists({abi.raw_port(FR.PORT_RECV): [(0, 0, 0)]}, 4))
+    serial = 0
+    for step, order in enumerate((pairs.transpose(0, 2, 1).reshape(-1), pairs[:, ::-1, :].transpose(0, 2, 1).reshape(-1))):
+        sb = _reorder(b, list(order))
+        db = abi.rx_upload(gpu_ctx, sb.frames, sb.offset, sb.length)
+        db.frames_bytes = sb.frames_bytes
+        out = abi.rx_alloc_out(gpu_ctx, sb.n, 4, 4 * sb.n)
+        gm = abi.rx_run(gpu_ctx, db, out)[0]
+        tms = 10 * step
+        rb, origin, gst = abi.rx_reassemble(gpu_ctx, db, out.meta, tms)
+        wout, woo, wol, wog, wst = t.reassemble(sb.frames, sb.offset, sb.length, gm, tms)
+        serial += gst.pop("serial")
+        gst.pop("sorted")
+        assert gst == wst, (step, gst, wst)
+        gbuf, goff, gln = _frames(gpu_ctx, rb)
+        gorg = abi.download_ptr(gpu_ctx, origin.ptr, np.uint32, rb.n)
+        assert np.array_equal(gorg, wog) and np.array_equal(gln, wol)
+        assert np.array_equal(_frames_flat(gbuf, goff, gln), _frames_flat(wout, woo, wol))
+        for x in (db.frames, db.offset, db.length, out.meta, out.lane_off, out.lane_pkt):
+            x.free()
+    assert serial >= 64, serial                           # the component path ran
+
+
 @pytest.mark.parametrize("run,inplace", [(150, True), (150, False), (700, True), (700, False)])
 def test_reassembly_long_same_key_runs(gpu_ctx, run, inplace):
     """`run` consecutive datagrams share one flow key (each completes before the next one's first

@@ -31,7 +31,9 @@
 //   reasm_ec        a free entry guaranteed for every parallel flow, else all go serial
 //   reasm_process   parallel flows without the table; the rest -> serial list (grouped with no
 //                   complex flow: both add up reasm_scan's results)
-//   radix sort 5    serial list by arrival; reasm_serial (one wave, the table in arrival order)
+//   radix sort 5    serial list by arrival; reasm_serial (the table in arrival order: one wave, or
+//                   with the max_entries test not in play one per group of bucket components,
+//                   reasm_cc)
 //   radix sort 3    completions by origin (the arrival index of the completing fragment: where
 //                   the reference delivers the datagram; grouped: a select of the positions
 //                   holding one, reasm_clist_*) + exclusive scan of frame sizes
@@ -52,6 +54,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdlib>
 
 #include "udpdk_gpu.h"
 #include "rx_common.h"
@@ -1115,19 +1118,38 @@ __device__ uint32_t lru_head(const ReasmArgs &a, LruMin &mine)
 // invalidation. It is the only writer of the table while it runs, and keeps its count of valid
 // entries (use_entries) across calls. A fragment that stays in a pending entry gets a store job;
 // a flow that ends later in the call cancels its jobs.
-__global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *list, uint32_t K)
+// comp != nullptr (the max_entries test not in play): workgroup b of the launch takes the listed
+// fragments whose bucket component (reasm_cc) maps to it, in arrival order. Components share no
+// bucket, so their fragments commute: each one's table operations are exactly the reference's
+// sequence for its fragments, and the waves run side by side.
+__device__ __forceinline__ uint32_t cc_owner(uint32_t root, uint32_t nw)
+{
+    return (uint32_t)(((unsigned long long)(root * 0x9E3779B1u) * nw) >> 32);
+}
+
+__global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *list, uint32_t K,
+                                                   const uint32_t *comp)
 {
     __shared__ uint32_t st[E_WORDS];
     const uint32_t lane = __lane_id();
     unsigned long long c_ns = 0, c_err = 0, c_holes = 0, c_exp = 0, c_done = 0, c_bytes = 0;
     long long c_stored = 0;
     const uint32_t nslot = 2u * a.assoc;
-    const bool limit = a.counts[6] != 0u;
-    uint32_t use = ld_a(a.tab_used);
+    const bool limit = comp == nullptr && a.counts[6] != 0u;
+    const uint32_t use0 = ld_a(a.tab_used);
+    uint32_t use = use0;
     uint32_t head = RS_NONE;                 // the LRU head, while head_ok
     bool head_ok = false, lru_built = false;
     LruMin lru{~0ull, RS_NONE};              // this lane's partition minimum (lru_head)
+    unsigned long long mine = 0;             // comp: this workgroup's entries of the current 64
     for (uint32_t k = 0; k < K; ++k) {
+        if (comp) {
+            if ((k & 63u) == 0u) {
+                const uint32_t kk = k + lane;
+                mine = __ballot(kk < K && cc_owner(comp[kk], gridDim.x) == blockIdx.x);
+            }
+            if (!((mine >> (k & 63u)) & 1ull)) continue;
+        }
         const uint32_t q = list[k];
         const uint32_t i = a.s_i[q], m = a.s_meta[q];
         const uint32_t src = a.s_src[q], dst = a.s_dst[q], id = a.s_id[q], sig = a.s_sig[q];
@@ -1260,7 +1282,10 @@ __global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *
         stores_done();
         wave_sync_rs();
     }
-    if (lane == 0) st_a(a.tab_used, use);
+    if (lane == 0) {
+        if (comp) atomicAdd(a.tab_used, use - use0);     // (wraps for a net release)
+        else st_a(a.tab_used, use);
+    }
     if (lane == 0) {
         unsigned long long *s = a.stats;
         if (c_ns) atomicAdd(&s[UDPDK_RS_NO_SPACE], c_ns);
@@ -1271,6 +1296,41 @@ __global__ void __launch_bounds__(64) reasm_serial(ReasmArgs a, const uint32_t *
         if (c_stored) atomicAdd(&s[UDPDK_RS_STORED], (unsigned long long)c_stored);
         if (c_bytes) atomicAdd(a.out_bytes, c_bytes);
     }
+}
+
+// The serial fragments' bucket components: union-find over the buckets in LDS (one workgroup,
+// tables of up to RS_CC_MAX buckets), each listed fragment joining its key's two buckets; comp[k]
+// = the root of list entry k's first bucket.
+constexpr uint32_t RS_CC_MAX = 16384;
+constexpr uint32_t RS_CC_BLOCK = 1024;
+
+__global__ void __launch_bounds__(RS_CC_BLOCK) reasm_cc(ReasmArgs a, const uint32_t *list, uint32_t K, uint32_t *comp)
+{
+    __shared__ uint32_t par[RS_CC_MAX];
+    for (uint32_t b = threadIdx.x; b < a.nbuckets; b += RS_CC_BLOCK) par[b] = b;
+    __syncthreads();
+    auto find = [&](uint32_t x) {
+        for (;;) {
+            const uint32_t p = __hip_atomic_load(&par[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (p == x) return x;
+            const uint32_t g = __hip_atomic_load(&par[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (g != p) atomicCAS(&par[x], p, g);                     // path halving
+            x = p;
+        }
+    };
+    for (uint32_t k = threadIdx.x; k < K; k += RS_CC_BLOCK) {
+        const uint32_t sig = a.s_sig[list[k]];
+        uint32_t x = bucket_of(a, sig), y = bucket2_of(a, sig);
+        for (;;) {
+            x = find(x);
+            y = find(y);
+            if (x == y) break;
+            if (x < y) { const uint32_t t = x; x = y; y = t; }         // the larger root under the smaller
+            if (atomicCAS(&par[x], x, y) == x) break;
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < K; k += RS_CC_BLOCK) comp[k] = find(bucket_of(a, a.s_sig[list[k]]));
 }
 
 // Frame sizes of the completions in origin order (for the offset scan).
@@ -2492,6 +2552,7 @@ struct Reasm {
     uint32_t *counts = nullptr;              // device [10] (ReasmArgs::counts)
     unsigned long long *hset = nullptr;      // [hcap] the run test's exact set (run_insert)
     uint32_t *rtab = nullptr;                // [2 x hcap] the run test's slots (reasm_scan, reasm_ec)
+    uint32_t *ccomp = nullptr;               // [cap] the serial fragments' bucket components
     uint32_t *cblk = nullptr;                // [2 x chunks] reasm_scan's completion counts
     unsigned long long *pblk = nullptr;      // [RS_PB x chunks] reasm_scan's outcome per block
     uint32_t hcap = 0;
@@ -2514,6 +2575,7 @@ struct Reasm {
     uint32_t *out_off = nullptr, *out_ptype = nullptr, *out_origin = nullptr;
     uint16_t *out_len = nullptr;
     uint32_t calls = 0;
+    bool no_cc = false;                      // UDPDK_RS_CC=0 (tests, A/B): the serial list on one wave
 };
 
 namespace {
@@ -2540,7 +2602,7 @@ void reasm_destroy(Reasm *r)
                    r->dv, r->perm, r->sizes, r->offs, r->tmp, r->out, r->out_off, r->out_ptype,
                    r->out_origin, r->out_len, r->pflag, r->sb1, r->sb2, r->tf, r->tl, r->oc, r->ob, r->rk, r->rks,
                    r->rx, r->rv, r->rvs, r->bsum, r->cplx, r->tpos, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs, r->hset,
-                   r->cblk, r->pblk, r->rtab};
+                   r->cblk, r->pblk, r->rtab, r->ccomp};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (r->host) (void)hipHostFree(r->host);
@@ -2569,6 +2631,7 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
     r->max_cycles = cfg->max_cycles;
     r->max_dgram = cfg->max_dgram;
     r->max_entries = cfg->max_entries ? cfg->max_entries : r->entries;
+    if (const char *ev = getenv("UDPDK_RS_CC")) r->no_cc = atoi(ev) == 0;
     r->flags = cfg->flags;
     r->stride = (34u + cfg->max_dgram + 4u + 255u) & ~255u;   // + 4: dword loads of the last bytes
     r->cap = std::max<uint32_t>(max_frames, 1);
@@ -2600,7 +2663,7 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
         (e = dalloc(&r->tpos, (size_t)r->entries * RS_MAX_FRAG)) != hipSuccess ||
         (e = dalloc(&r->sl_k, C)) != hipSuccess || (e = dalloc(&r->sl_ks, C)) != hipSuccess ||
         (e = dalloc(&r->sl_v, C)) != hipSuccess || (e = dalloc(&r->sl_vs, C)) != hipSuccess ||
-        (e = dalloc(&r->cblk, 2 * (C / RS_CL + 1))) != hipSuccess ||
+        (e = dalloc(&r->cblk, 2 * (C / RS_CL + 1))) != hipSuccess || (e = dalloc(&r->ccomp, C)) != hipSuccess ||
         (e = dalloc(&r->pblk, RS_PB * (C / RS_CL + 1))) != hipSuccess ||
         (e = hipHostMalloc((void **)&r->host, 4096)) != hipSuccess) {
         fail(e);
@@ -2919,7 +2982,18 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
             tb = r->tmp_bytes;
             RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs, (size_t)K, 0,
                                              bits_for(n - 1u), st));
-            hipLaunchKernelGGL(reasm_serial, dim3(1), dim3(64), 0, st, a, (const uint32_t *)r->sl_vs, K);
+            // bucket components side by side when the max_entries test is not in play (it couples
+            // every flow through use_entries and the LRU list), else one wave in arrival order
+            const bool cc = hc[6] == 0u && r->nbuckets <= RS_CC_MAX && K >= 64u && !r->no_cc;
+            if (cc) {
+                hipLaunchKernelGGL(reasm_cc, dim3(1), dim3(RS_CC_BLOCK), 0, st, a, (const uint32_t *)r->sl_vs, K,
+                                   r->ccomp);
+                hipLaunchKernelGGL(reasm_serial, dim3(std::min<uint32_t>(K / 2u, 512u)), dim3(64), 0, st, a,
+                                   (const uint32_t *)r->sl_vs, K, (const uint32_t *)r->ccomp);
+            } else {
+                hipLaunchKernelGGL(reasm_serial, dim3(1), dim3(64), 0, st, a, (const uint32_t *)r->sl_vs, K,
+                                   (const uint32_t *)nullptr);
+            }
             RS_HIP(hipGetLastError());
         }
     }
