@@ -1693,7 +1693,8 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_scan(ReasmArgs a)
     __shared__ unsigned long long s_red[RS_WAVES][RS_PB];
     __shared__ uint32_t s_red32[RS_WAVES][4];
     __shared__ uint32_t s_fl[RS_CL + 1];                      // the frames of positions L0 .. P1 - 1
-    __shared__ uint32_t s_x[RS_WAVES], s_j0, s_pre0, s_F;
+    __shared__ uint32_t s_x[RS_WAVES], s_j0, s_pre0, s_F, s_ug;
+    __shared__ uint32_t w_ht[RS_WAVES][2 * RS_SCAN_PW];       // per wave: its run keys by start rank
     crc_table_init(crc_tab);
     const uint32_t tid = threadIdx.x, lane = __lane_id(), w = tid >> 6;
     const uint32_t b = blockIdx.x, P0 = b * RS_CL, tgt = P0 ? P0 - 1u : 0u;
@@ -1765,6 +1766,11 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_scan(ReasmArgs a)
         __syncthreads();
     }
     for (uint32_t x = P0 + tid; x < P1; x += RS_BLOCK) a.frag_list[x] = s_fl[x - L0];
+    // a block found a key in two runs already: the fragment list is all the sorts need
+    if (tid == 0) s_ug = ld_a(&a.counts[4]);
+    for (uint32_t x = lane; x < 2u * RS_SCAN_PW; x += 64u) w_ht[w][x] = 0xFFFFFFFFu;
+    __syncthreads();
+    if (s_ug) return;                                             // the whole block
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
     const uint32_t wb = b * RS_CL + w * RS_SCAN_PW;
     constexpr uint32_t OOR = 0x80000000u;
@@ -1813,6 +1819,47 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_scan(ReasmArgs a)
         }
         start[1] = valid[1] && (qid != id[1] || qs != src[1] || qd != dst[1]);
     }
+    // The wave's flows in position order, one per lane (a wave of 2-fragment flows walks once,
+    // not once per slot): each start's position and key by its rank (signature and bucket words
+    // below).
+    const unsigned long long m0 = __ballot(start[0]), m1 = __ballot(start[1]);
+    const uint32_t n0 = (uint32_t)__popcll(m0), S = n0 + (uint32_t)__popcll(m1);
+    uint32_t rank[2] = {0u, 0u};
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        if (start[k]) {
+            rank[k] = (k ? n0 : 0u) + __builtin_amdgcn_mbcnt_hi((uint32_t)((k ? m1 : m0) >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)(k ? m1 : m0), 0u));
+            w_pos[w][rank[k]] = 64u * k + lane;
+            w_src[w][rank[k]] = src[k];
+            w_dst[w][rank[k]] = dst[k];
+            w_id[w][rank[k]] = id[k];
+        }
+    }
+    wave_sync_rs();
+    // Two runs of one key in the wave's positions: the batch is not grouped (interleaved flows
+    // show it here, long before reasm_ec's run test), and nothing but the fragment list is needed
+    // from this launch. Insert-or-find of each run's key in an LDS table by rank.
+    bool dup = false;
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        if (!start[k]) continue;
+        uint32_t h = ((src[k] * 0x9E3779B1u) ^ (dst[k] * 0x85EBCA77u) ^ (id[k] * 0xC2B2AE3Du)) >> 24;
+        for (uint32_t t = 0; t < 2u * RS_SCAN_PW; ++t, h = (h + 1u) & (2u * RS_SCAN_PW - 1u)) {
+            const uint32_t old = atomicCAS(&w_ht[w][h], 0xFFFFFFFFu, rank[k]);
+            if (old == 0xFFFFFFFFu) break;
+            if (w_src[w][old] == src[k] && w_dst[w][old] == dst[k] && w_id[w][old] == id[k]) {
+                dup = true;
+                break;
+            }
+        }
+    }
+    const bool ug = __ballot(dup) != 0ull;
+    if (ug && lane == 0) a.counts[4] = 1u;
+    const bool skip = ug || __builtin_amdgcn_readfirstlane((int)ld_a(&a.counts[4])) != 0;
+    unsigned long long t_len = 0, t_short = 0, t_done = 0, t_holes = 0, t_err = 0, t_bytes = 0;
+    uint32_t t_cc = 0, t_cb = 0, t_cplx = 0, t_nb = 0;
+    if (!skip) {
     // The run test's first half (each run's first position into its key's slot of rtab: plain
     // stores, read back by reasm_ec) and the flow's bucket summary words.
     uint32_t sig[2], s1v[2] = {0u, 0u}, s2v[2] = {0u, 0u};
@@ -1852,31 +1899,15 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_scan(ReasmArgs a)
         r_m[w][64u * k + lane] = m;
         r_o[w][64u * k + lane] = o[k];
         r_l[w][64u * k + lane] = fl[k];
-    }
-    const unsigned long long m0 = __ballot(start[0]), m1 = __ballot(start[1]);
-    // The wave's flows in position order, one per lane (a wave of 2-fragment flows walks once,
-    // not once per slot): each start's position, key, signature and bucket words by its rank.
-    const uint32_t n0 = (uint32_t)__popcll(m0), S = n0 + (uint32_t)__popcll(m1);
-#pragma unroll
-    for (uint32_t k = 0; k < 2; ++k) {
-        const uint32_t p = wb + 64u * k + lane;
         if (start[k]) {
-            const uint32_t rk = (k ? n0 : 0u) + __builtin_amdgcn_mbcnt_hi((uint32_t)((k ? m1 : m0) >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)(k ? m1 : m0), 0u));
-            w_pos[w][rk] = 64u * k + lane;
-            w_src[w][rk] = src[k];
-            w_dst[w][rk] = dst[k];
-            w_id[w][rk] = id[k];
-            w_sig[w][rk] = sig[k];
-            w_s1[w][rk] = s1v[k];
-            w_s2[w][rk] = s2v[k];
+            w_sig[w][rank[k]] = sig[k];
+            w_s1[w][rank[k]] = s1v[k];
+            w_s2[w][rank[k]] = s2v[k];
         } else if (valid[k]) {
             a.pflag[p] = 0u;
         }
     }
     wave_sync_rs();
-    unsigned long long t_len = 0, t_short = 0, t_done = 0, t_holes = 0, t_err = 0, t_bytes = 0;
-    uint32_t t_cc = 0, t_cb = 0, t_cplx = 0, t_nb = 0;
     const bool limit = a.max_entries < a.entries;
 #pragma unroll 1
     for (uint32_t j = lane; j < ((S + 63u) & ~63u); j += 64u) {   // wave-uniform trip count
@@ -2013,6 +2044,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_scan(ReasmArgs a)
         }
         a.pflag[p] = flag;
     }
+    }                                                             // !skip
     // the block's totals: outcome words, its chunk's completions, complex and bound-counted flows
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
