@@ -23,8 +23,8 @@
 //   reasm_scan      does every flow key form one run (grouped)? The per-position records and,
 //                   as if grouped, each flow's walk: its completions (counted per chunk of the
 //                   completion list), whether it is complex, its outcome (see the kernel)
-//   [not grouped]   radix sort 1 by (id, index); reasm_keys: src|dst keys in that order; radix
-//                   sort 2 (stable); reasm_prep: the records in sorted order; reasm_flows: per
+//   [not grouped]   reasm_group (each key's group by an exact hash table) and one radix sort by
+//                   (group, index); reasm_prep: the records in sorted order; reasm_flows: per
 //                   flow its span, pending or not, key in the table, overlap records; radix sort
 //                   4 + max scan + reasm_overlap: flows whose spans overlap on a shared bucket
 //                   (grouped: no two spans overlap)
@@ -170,6 +170,7 @@ struct ReasmArgs {
     uint32_t rmask;
     unsigned long long *hset;
     uint32_t hmask;
+    unsigned long long *gset;          // [hmask + 1] a batch that is not grouped: key -> group (reasm_group)
     uint32_t hset_tag;                 // hset's tag for this call, 1..65535
     uint32_t grouped;                  // every key one run in arrival order: no span overlaps
     uint32_t inplace;                  // udpdk_gpu_rx_reassemble_inplace: reasm_scan checks each completion
@@ -356,16 +357,6 @@ __device__ __forceinline__ void fsel_count_block(const uint32_t *meta, uint32_t 
     }
 }
 
-// src | dst << 32 of the fragments in (id, index) order (the second, stable, sort key).
-__global__ void __launch_bounds__(RS_BLOCK) reasm_keys(ReasmArgs a, uint32_t F)
-{
-    const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
-    for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
-        const uint32_t o = a.offset[a.v1s[p]];
-        a.k2[p] = (unsigned long long)ld32(fr, o + 26) | ((unsigned long long)ld32(fr, o + 30) << 32);
-    }
-}
-
 // Per sorted position: the fragment's frame, key, signature and length class (all lanes in
 // parallel, so the flow walk below reads one coalesced record per fragment).
 // dv (the identity permutation the origin sort of an ungrouped batch starts from) is written by
@@ -465,14 +456,44 @@ __device__ __forceinline__ void run_insert(const ReasmArgs &a, uint32_t id, uint
     }
 }
 
-// The first sort's keys (id << ib | index) over the fragment list, for a batch that is not
-// grouped.
-__global__ void __launch_bounds__(RS_BLOCK) reasm_keys1(ReasmArgs a, uint32_t F)
+// A batch that is not grouped: each fragment's key (src, dst, id) to a group, the position of the
+// first fragment that claimed the key's slot in gset (insert-or-find; a slot word is the call's
+// tag << 48 | 24 fingerprint bits << 24 | position, and a fingerprint match is checked against
+// that position's frame header, so the grouping is exact), and the sort key group << ib | index:
+// one radix sort then puts every key's fragments together in arrival order (it replaced two, by
+// (id, index) then by src | dst: 38 + 64 key bits against 2 ib).
+__global__ void __launch_bounds__(RS_BLOCK) reasm_group(ReasmArgs a, uint32_t F)
 {
     const __amdgpu_buffer_rsrc_t fr = rsrc(a.frames, a.rsrc_bytes);
+    const unsigned long long tag = (unsigned long long)a.hset_tag << 48;
     for (uint32_t p = blockIdx.x * RS_BLOCK + threadIdx.x; p < F; p += gridDim.x * RS_BLOCK) {
-        const uint32_t i = a.frag_list[p];
-        a.k1[p] = ((unsigned long long)(ld32(fr, a.offset[i] + 16) >> 16) << a.ib) | i;
+        const uint32_t o = a.offset[a.frag_list[p]];
+        const uint32_t id = ld32(fr, o + 16) >> 16, src = ld32(fr, o + 26), dst = ld32(fr, o + 30);
+        const unsigned long long fp = run_fp(id, src, dst);
+        const unsigned long long fpb = ((fp >> 40) & 0xFFFFFFull) << 24;
+        const unsigned long long val = tag | fpb | p;
+        uint32_t slot = (uint32_t)fp & a.hmask, group = p;
+        unsigned long long cur = ld_a(&a.gset[slot]);
+        for (uint32_t k = 0; k <= a.hmask;) {
+            if ((cur >> 48) != a.hset_tag) {
+                const unsigned long long old = atomicCAS(&a.gset[slot], cur, val);
+                if (old == cur) break;                                  // claimed: a new group
+                cur = old;
+                continue;
+            }
+            if ((cur & (0xFFFFFFull << 24)) == fpb) {
+                const uint32_t q = (uint32_t)(cur & 0xFFFFFFull);
+                const uint32_t oq = a.offset[a.frag_list[q]];
+                if ((ld32(fr, oq + 16) >> 16) == id && ld32(fr, oq + 26) == src && ld32(fr, oq + 30) == dst) {
+                    group = q;                                         // the key's group
+                    break;
+                }
+            }
+            ++k;
+            slot = (slot + 1u) & a.hmask;
+            cur = ld_a(&a.gset[slot]);
+        }
+        a.k1[p] = ((unsigned long long)group << a.ib) | p;
     }
 }
 
@@ -2585,6 +2606,7 @@ struct Reasm {
     unsigned long long *hset = nullptr;      // [hcap] the run test's exact set (run_insert)
     uint32_t *rtab = nullptr;                // [2 x hcap] the run test's slots (reasm_scan, reasm_ec)
     uint32_t *ccomp = nullptr;               // [cap] the serial fragments' bucket components
+    unsigned long long *gset = nullptr;      // [hcap] key groups of a batch that is not grouped
     uint32_t *cblk = nullptr;                // [2 x chunks] reasm_scan's completion counts
     unsigned long long *pblk = nullptr;      // [RS_PB x chunks] reasm_scan's outcome per block
     uint32_t hcap = 0;
@@ -2634,7 +2656,7 @@ void reasm_destroy(Reasm *r)
                    r->dv, r->perm, r->sizes, r->offs, r->tmp, r->out, r->out_off, r->out_ptype,
                    r->out_origin, r->out_len, r->pflag, r->sb1, r->sb2, r->tf, r->tl, r->oc, r->ob, r->rk, r->rks,
                    r->rx, r->rv, r->rvs, r->bsum, r->cplx, r->tpos, r->sl_k, r->sl_ks, r->sl_v, r->sl_vs, r->hset,
-                   r->cblk, r->pblk, r->rtab, r->ccomp};
+                   r->cblk, r->pblk, r->rtab, r->ccomp, r->gset};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (r->host) (void)hipHostFree(r->host);
@@ -2724,7 +2746,9 @@ int reasm_create(Reasm **out, int device, uint32_t max_frames, const udpdk_frag_
     r->tmp_bytes = std::max<size_t>(*std::max_element(t, t + 7), 256);
     r->hcap = 1024;                                         // >= 2 x fragments per call, power of 2
     while (r->hcap < 2u * r->cap) r->hcap <<= 1;
-    if ((e = dalloc(&r->hset, r->hcap)) != hipSuccess || (e = dalloc(&r->rtab, 2 * (size_t)r->hcap)) != hipSuccess) {
+    if ((e = dalloc(&r->hset, r->hcap)) != hipSuccess || (e = dalloc(&r->rtab, 2 * (size_t)r->hcap)) != hipSuccess ||
+        (e = dalloc(&r->gset, r->hcap)) != hipSuccess || (e = hipMemset(r->gset, 0, r->hcap * 8)) != hipSuccess ||
+        (e = hipMemset(r->hset, 0, r->hcap * 8)) != hipSuccess) {
         fail(e);
         reasm_destroy(r);
         return rc;
@@ -2810,6 +2834,7 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     while (hsize < 2u * n && hsize < r->hcap) hsize <<= 1;
     a.hset = r->hset;
     a.hmask = hsize - 1u;
+    a.gset = r->gset;
     a.rtab = r->rtab;
     a.rmask = 2u * hsize - 1u;                // >= 4 x fragments: few runs lose their slot
     // the fragment list in arrival order (F to counts[0]), then its sort keys and the run test
@@ -2823,8 +2848,10 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
                            nfs);                 // counts sit in sizes, dead until the completion list)
         RS_HIP(hipGetLastError());
         a.hset_tag = (a.call - 1u) % 65535u + 1u;
-        if (a.hset_tag == 1u)                 // the tags come round: no word may carry one
+        if (a.hset_tag == 1u) {               // the tags come round: no word may carry one
             RS_HIP(hipMemsetAsync(r->hset, 0, (size_t)r->hcap * sizeof(unsigned long long), st));
+            RS_HIP(hipMemsetAsync(r->gset, 0, (size_t)r->hcap * sizeof(unsigned long long), st));
+        }
         hipLaunchKernelGGL(reasm_scan, dim3((n + RS_CL - 1) / RS_CL), dim3(RS_BLOCK), 0, st, a);
         RS_HIP(hipGetLastError());
     }
@@ -2992,15 +3019,11 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
             RS_HIP(hipMemsetAsync(r->stats, 0, (UDPDK_RS_N + 1) * sizeof(unsigned long long), st));
             RS_HIP(hipMemsetAsync(r->counts + 2, 0, 8 * sizeof(uint32_t), st));
             const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((F + RS_BLOCK - 1) / RS_BLOCK, 4096));
-            hipLaunchKernelGGL(reasm_keys1, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
+            hipLaunchKernelGGL(reasm_group, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
             RS_HIP(hipGetLastError());
             tb = r->tmp_bytes;
-            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k1, r->k1s, r->frag_list, r->v1s, (size_t)F, 0,
-                                             16 + a.ib, st));
-            hipLaunchKernelGGL(reasm_keys, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
-            RS_HIP(hipGetLastError());
-            tb = r->tmp_bytes;
-            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k2, r->k2s, r->v1s, r->v2s, (size_t)F, 0, 64, st));
+            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tb, r->k1, r->k1s, r->frag_list, r->v2s, (size_t)F, 0,
+                                             2 * a.ib, st));
             hipLaunchKernelGGL(reasm_prep, dim3(gF), dim3(RS_BLOCK), 0, st, a, F);
             RS_HIP(hipGetLastError());
             if (int e = analysis(F, F, false)) return e;
