@@ -34,9 +34,10 @@
 //   radix sort 5    serial list by arrival; reasm_serial (the table in arrival order: one wave, or
 //                   with the max_entries test not in play one per group of bucket components,
 //                   reasm_cc)
-//   radix sort 3    completions by origin (the arrival index of the completing fragment: where
-//                   the reference delivers the datagram; grouped: a select of the positions
-//                   holding one, reasm_clist_*) + exclusive scan of frame sizes
+//   reasm_clist_*   completions by origin (the arrival index of the completing fragment: where
+//                   the reference delivers the datagram) and their output offsets: grouped, the
+//                   positions holding one in order; else each record's position at its origin
+//                   first (reasm_by_origin), then the origins holding one in order
 //   reasm_emit      one wave per datagram: first fragment's header (total length, DF only, IPv4
 //                   checksum) + every fragment's data at its offset, from the batch or the table
 //   reasm_store     one wave per fragment left pending: its data (and header, for offset 0) into
@@ -1354,13 +1355,6 @@ __global__ void __launch_bounds__(RS_CC_BLOCK) reasm_cc(ReasmArgs a, const uint3
     for (uint32_t k = threadIdx.x; k < K; k += RS_CC_BLOCK) comp[k] = find(bucket_of(a, a.s_sig[list[k]]));
 }
 
-// Frame sizes of the completions in origin order (for the offset scan).
-__global__ void __launch_bounds__(RS_BLOCK) reasm_sizes(const ReasmDone *done, const uint32_t *perm,
-                                                       uint32_t *sizes, uint32_t C)
-{
-    for (uint32_t k = blockIdx.x * RS_BLOCK + threadIdx.x; k < C; k += gridDim.x * RS_BLOCK)
-        sizes[k] = (34u + done[perm[k]].total + 15u) & ~15u;
-}
 
 // Grouped path: the completions in position (= arrival) order and their output offsets in two
 // launches (per RS_CL-position block: count and bytes; then each block's base from its
@@ -1461,11 +1455,13 @@ __device__ __forceinline__ bool spec_copy_fits(const SpecTail &g)
 
 __device__ __forceinline__ uint32_t done_bytes(const ReasmDone *done, uint32_t q)
 {
-    return (34u + done[q].total + 15u) & ~15u;    // as reasm_sizes
+    return (34u + done[q].total + 15u) & ~15u;    // the output frame's 16-byte aligned size
 }
 
+// by_origin: dk is indexed by origin (a completion's arrival index, the position of its record
+// as the value, ~0 for none), so the list comes out in origin order (a batch that is not grouped)
 __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_count(const uint32_t *dk, const ReasmDone *done,
-                                                             uint32_t F, uint32_t *blk, SpecTail g)
+                                                             uint32_t F, uint32_t *blk, SpecTail g, uint32_t by_origin)
 {
     __shared__ uint32_t red[2 * RS_WAVES];
     uint32_t C_unused;
@@ -1478,7 +1474,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_count(const uint32_t *dk
         const uint32_t q = p0 + j;
         if (q < F && dk[q] != RS_NONE) {
             ++c;
-            by += done_bytes(done, q);
+            by += done_bytes(done, by_origin ? dk[q] : q);
         }
     }
     uint32_t tc, tb;
@@ -1496,7 +1492,7 @@ __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_count(const uint32_t *dk
 
 __device__ __forceinline__ void clist_write_block(const uint32_t *dk, const ReasmDone *done, uint32_t F,
                                                   const uint32_t *blk, uint32_t *perm, uint32_t *offs,
-                                                  const SpecTail &g, uint32_t b, bool in_ec)
+                                                  const SpecTail &g, uint32_t b, bool in_ec, bool by_origin = false)
 {
     __shared__ uint32_t red[4 * RS_WAVES];
     uint32_t C_unused;
@@ -1519,11 +1515,13 @@ __device__ __forceinline__ void clist_write_block(const uint32_t *dk, const Reas
     // the thread's positions, then a block scan of their counts and bytes
     constexpr uint32_t PT = RS_CL / RS_BLOCK;
     const uint32_t p0 = b * RS_CL + tid * PT;
-    uint32_t c = 0, by = 0, sz[PT];
+    uint32_t c = 0, by = 0, sz[PT], at[PT];
 #pragma unroll
     for (uint32_t j = 0; j < PT; ++j) {
         const uint32_t q = p0 + j;
-        sz[j] = q < F && dk[q] != RS_NONE ? done_bytes(done, q) : 0u;
+        const uint32_t d = q < F ? dk[q] : RS_NONE;
+        at[j] = by_origin ? d : q;                          // the completion record's position
+        sz[j] = d != RS_NONE ? done_bytes(done, at[j]) : 0u;
         c += sz[j] ? 1u : 0u;
         by += sz[j];
     }
@@ -1542,7 +1540,7 @@ __device__ __forceinline__ void clist_write_block(const uint32_t *dk, const Reas
 #pragma unroll
     for (uint32_t j = 0; j < PT; ++j) {
         if (sz[j]) {
-            perm[ec] = p0 + j;
+            perm[ec] = at[j];
             offs[ec] = eb;
             ++ec;
             eb += sz[j];
@@ -1552,9 +1550,18 @@ __device__ __forceinline__ void clist_write_block(const uint32_t *dk, const Reas
 
 __global__ void __launch_bounds__(RS_BLOCK) reasm_clist_write(const uint32_t *dk, const ReasmDone *done,
                                                              uint32_t F, const uint32_t *blk,
-                                                             uint32_t *perm, uint32_t *offs, SpecTail g)
+                                                             uint32_t *perm, uint32_t *offs, SpecTail g,
+                                                             uint32_t by_origin)
 {
-    clist_write_block(dk, done, F, blk, perm, offs, g, blockIdx.x, false);
+    clist_write_block(dk, done, F, blk, perm, offs, g, blockIdx.x, false, by_origin != 0u);
+}
+
+// Each completion's record position at its origin (unique: a frame completes one datagram at
+// most), for the origin-ordered list of a batch that is not grouped.
+__global__ void __launch_bounds__(RS_BLOCK) reasm_by_origin(const uint32_t *dk, uint32_t F, uint32_t *slot)
+{
+    for (uint32_t q = blockIdx.x * RS_BLOCK + threadIdx.x; q < F; q += gridDim.x * RS_BLOCK)
+        if (dk[q] != RS_NONE) slot[dk[q]] = q;
 }
 
 // The grouped path's reasm_ec (workgroups [0, nec)) with the speculative tail's completion list
@@ -2866,7 +2873,6 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
     auto tail = [&](bool grp, uint32_t Fn, uint32_t Cn, bool spec) -> int {
         SpecTail g{nullptr, nullptr, 0, 0u, nullptr};
         if (spec) g = g_spec;
-        size_t tbt = r->tmp_bytes;
         if (grp) {
             // speculative: the list was written beside reasm_ec (reasm_ec_clist, from reasm_scan's
             // chunk counts: no flow went to the table); else counted and written here (the serial
@@ -2874,21 +2880,26 @@ int reasm_run(Reasm *r, hipStream_t st, const udpdk_rx_batch_t *bt, const uint32
             const uint32_t nb = (Fn + RS_CL - 1) / RS_CL;
             if (!spec) {
                 hipLaunchKernelGGL(reasm_clist_count, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
-                                   (const ReasmDone *)r->done, Fn, r->sizes, g);
+                                   (const ReasmDone *)r->done, Fn, r->sizes, g, 0u);
                 hipLaunchKernelGGL(reasm_clist_write, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk,
-                                   (const ReasmDone *)r->done, Fn, (const uint32_t *)r->sizes, r->perm, r->offs, g);
+                                   (const ReasmDone *)r->done, Fn, (const uint32_t *)r->sizes, r->perm, r->offs, g,
+                                   0u);
             }
             RS_HIP(hipGetLastError());
         } else {
-            const uint32_t gC = std::max<uint32_t>(1, std::min<uint32_t>((Cn + RS_BLOCK - 1) / RS_BLOCK, 4096));
-            RS_HIP(rocprim::radix_sort_pairs(r->tmp, tbt, r->dk, r->dks, r->dv, r->perm, (size_t)Fn, 0,
-                                             bits_for(n), st));
-            hipLaunchKernelGGL(reasm_sizes, dim3(gC), dim3(RS_BLOCK), 0, st, (const ReasmDone *)r->done,
-                               (const uint32_t *)r->perm, r->sizes, Cn);
+            // origin order: each completion's record position at its origin, then the list over
+            // the origins as the grouped path makes it over positions (a sort by origin before)
+            const uint32_t gF = std::max<uint32_t>(1, std::min<uint32_t>((Fn + RS_BLOCK - 1) / RS_BLOCK, 4096));
+            const uint32_t nb = (n + RS_CL - 1) / RS_CL;
+            RS_HIP(hipMemsetAsync(r->dks, 0xFF, (size_t)n * sizeof(uint32_t), st));
+            hipLaunchKernelGGL(reasm_by_origin, dim3(gF), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dk, Fn,
+                               r->dks);
+            hipLaunchKernelGGL(reasm_clist_count, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dks,
+                               (const ReasmDone *)r->done, n, r->sizes, g, 1u);
+            hipLaunchKernelGGL(reasm_clist_write, dim3(nb), dim3(RS_BLOCK), 0, st, (const uint32_t *)r->dks,
+                               (const ReasmDone *)r->done, n, (const uint32_t *)r->sizes, r->perm, r->offs, g,
+                               1u);
             RS_HIP(hipGetLastError());
-            tbt = r->tmp_bytes;
-            RS_HIP(rocprim::exclusive_scan(r->tmp, tbt, r->sizes, r->offs, 0u, (size_t)Cn,
-                                           rocprim::plus<uint32_t>(), st));
         }
         EmitArgs ea;
         ea.frames = bt->frames_dev;
