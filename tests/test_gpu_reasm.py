@@ -210,14 +210,15 @@ def _reorder(b, order):
     return types.SimpleNamespace(frames=buf, offset=off, length=ln, n=len(off), frames_bytes=len(buf) - 64)
 
 
-@pytest.mark.parametrize("case", ["split_last", "split_first", "shuffled"])
+@pytest.mark.parametrize("case", ["split_last", "split_first", "shuffled", "shuffled_large"])
 def test_reassembly_run_test_at_scale(gpu_ctx, case):
     """40 000 fragments over many reasm_scan blocks with one key split into two runs far apart
-    (a datagram's last or first fragment moved to the batch's end), or the whole batch shuffled:
-    the run test must find the batch not grouped (the sorted path, "sorted" = 1) and every outcome
-    equals the oracle's."""
+    (a datagram's last or first fragment moved to the batch's end), or the whole batch shuffled
+    (also at 80 000 fragments, beyond 2^16 positions): the run test must find the batch not
+    grouped (the sorted path, "sorted" = 1) and every outcome equals the oracle's."""
     from udpdk_amd import frames as FR
-    b = FR.frag_batch(20000, 2952)
+    n_d = 40000 if case == "shuffled_large" else 20000
+    b = FR.frag_batch(n_d, 2952)
     order = list(range(b.n))
     if case == "split_last":
         order.remove(2 * 12345 + 1)
@@ -240,7 +241,7 @@ def test_reassembly_run_test_at_scale(gpu_ctx, case):
     wout, woo, wol, wog, wst = t.reassemble(sb.frames, sb.offset, sb.length, gm, 0)
     gst.pop("serial")
     assert gst.pop("sorted") == 1
-    assert gst == wst and gst["done"] == 20000, (gst, wst)
+    assert gst == wst and gst["done"] == n_d, (gst, wst)
     gbuf, goff, gln = _frames(gpu_ctx, rb)
     gorg = abi.download_ptr(gpu_ctx, origin.ptr, np.uint32, rb.n)
     assert np.array_equal(gorg, wog) and np.array_equal(gln, wol)
