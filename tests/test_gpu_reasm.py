@@ -210,14 +210,15 @@ def _reorder(b, order):
     return types.SimpleNamespace(frames=buf, offset=off, length=ln, n=len(off), frames_bytes=len(buf) - 64)
 
 
-@pytest.mark.parametrize("case", ["split_last", "split_first", "shuffled", "shuffled_large"])
+@pytest.mark.parametrize("case", ["split_last", "split_first", "shuffled", "shuffled_large", "shuffled_wide"])
 def test_reassembly_run_test_at_scale(gpu_ctx, case):
     """40 000 fragments over many reasm_scan blocks with one key split into two runs far apart
     (a datagram's last or first fragment moved to the batch's end), or the whole batch shuffled
-    (also at 80 000 fragments, beyond 2^16 positions): the run test must find the batch not
+    (also at 80 000 fragments, beyond 2^16 positions; shuffled_wide in 2^16 buckets, so the
+    overlap records' (bucket, position) keys take 33 bits): the run test must find the batch not
     grouped (the sorted path, "sorted" = 1) and every outcome equals the oracle's."""
     from udpdk_amd import frames as FR
-    n_d = 40000 if case == "shuffled_large" else 20000
+    n_d = 40000 if case in ("shuffled_large", "shuffled_wide") else 20000
     b = FR.frag_batch(n_d, 2952)
     order = list(range(b.n))
     if case == "split_last":
@@ -229,7 +230,7 @@ def test_reassembly_run_test_at_scale(gpu_ctx, case):
     else:
         order = list(np.random.default_rng(3).permutation(b.n))
     sb = _reorder(b, order)
-    geometry = dict(bucket_num=0x1000, bucket_entries=16, max_cycles=1 << 40)
+    geometry = dict(bucket_num=1 << 16 if case == "shuffled_wide" else 0x1000, bucket_entries=16, max_cycles=1 << 40)
     abi.frag_table_create(gpu_ctx, geometry["bucket_num"], geometry["bucket_entries"], geometry["max_cycles"], 65515)
     t = O.FragTable(**geometry)
     gpu_ctx.upload_snapshot(abi.snapshot_from_lists({abi.raw_port(FR.PORT_RECV): [(0, 0, 0)]}, 4))
